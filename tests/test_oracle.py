@@ -1,0 +1,155 @@
+"""CPU tests: pin the oracle against the golden vectors and the reference's rules.
+
+These run without a GPU (-m "not gpu").  The oracle is the checker for the HIP path, so it
+is pinned first: its decoders must reproduce every third-party golden vector, its encoders
+must produce streams the third-party decoders accept, and its segment-level rules must
+match the reference's device.cc / config.cc behaviour.
+"""
+import ctypes
+import hashlib
+import zlib
+
+import numpy as np
+import pytest
+
+import golden_lib
+import oracle_lib as O
+
+
+# --- Configuration::UpdateCompressedSegSize (reference src/config.cc:59-73) ------------
+# Expected values worked by hand from the reference's integer loop (highest set bit of
+# 2*seg; above 32 KiB the slot is (uint16)(seg*1.1)); 59460 -> 65406 is the demo's slot
+# (apps/app_common.h:39).
+@pytest.mark.parametrize("seg,slot", [(8, 16), (2048, 4096), (4096, 8192), (16384, 32768),
+                                      (17000, 32768), (20000, 32768), (32768, 36044),
+                                      (59460, 65406), (1000, 1024), (1025, 2048)])
+def test_slot_size_rule(seg, slot):
+    assert O.compressed_seg_size(seg) == slot
+
+
+def test_generator_is_pinned():
+    m = golden_lib.manifest()
+    for key, inp in m["inputs"].items():
+        data = O.fill(inp["kind"], inp["seed"], inp["n"]).tobytes()
+        assert hashlib.sha256(data).hexdigest() == inp["sha256"], key
+
+
+def test_oracle_lz4_decodes_all_golden():
+    n = 0
+    for e, blob, plain in golden_lib.vectors("lz4"):
+        r, out = O.lz4_decompress(blob, max(len(plain), 1))
+        assert r == 0, (e["producer"], e["input"])
+        assert out == plain, (e["producer"], e["input"])
+        n += 1
+    assert n >= 100
+
+
+def test_oracle_inflate_decodes_all_golden():
+    n = 0
+    for e, blob, plain in golden_lib.vectors("deflate"):
+        r, out = O.inflate(blob, max(len(plain), 1))
+        assert r == 0, (e["producer"], e["input"])
+        assert out == plain, (e["producer"], e["input"])
+        n += 1
+    assert n >= 300
+
+
+def _liblz4():
+    try:
+        L = ctypes.CDLL("/opt/conda/lib/liblz4.so.1.9.3")
+    except OSError:
+        return None
+    L.LZ4_decompress_safe.restype = ctypes.c_int
+    L.LZ4_decompress_safe.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                      ctypes.c_int]
+    return L
+
+
+SIZES = [0, 1, 12, 13, 14, 100, 2047, 4096, 59460, 65536]
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("n", SIZES)
+def test_oracle_lz4_roundtrip_and_liblz4_accepts(kind, n):
+    data = O.fill(kind, 7, n).tobytes()
+    r, comp = O.lz4_compress(data)
+    assert r == 0 and len(comp) <= O.lz4_bound(n)
+    r, back = O.lz4_decompress(comp, max(n, 1))
+    assert r == 0 and back == data
+    L = _liblz4()
+    if L is not None:  # third-party decoder, exact capacity (enforces MFLIMIT/LASTLITERALS)
+        dst = ctypes.create_string_buffer(max(n, 1))
+        got = L.LZ4_decompress_safe(comp, dst, len(comp), n)
+        assert got == n and dst.raw[:n] == data
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("n", SIZES)
+def test_oracle_deflate_fixed_roundtrip_and_zlib_accepts(kind, n):
+    data = O.fill(kind, 9, n).tobytes()
+    r, comp = O.deflate_fixed(data)
+    assert r == 0 and len(comp) <= O.deflate_bound(n)
+    assert zlib.decompress(comp, -15) == data
+    r, back = O.inflate(comp, max(n, 1))
+    assert r == 0 and back == data
+
+
+def test_lz4_compresses_compressible_data():
+    data = O.fill(O.KIND_MIXED, 1, 3 << 20).tobytes()
+    tot = 0
+    for off in range(0, len(data), 65536):
+        r, comp = O.lz4_compress(data[off:off + 65536])
+        tot += len(comp)
+    assert len(data) / tot > 1.5
+
+
+# --- malformed input: decoders must fail with IOError, never read/write out of bounds ---
+def test_lz4_malformed():
+    data = O.fill(O.KIND_MIXED, 3, 5000).tobytes()
+    _, comp = O.lz4_compress(data)
+    assert O.lz4_decompress(b"", 10)[0] == O.BO_ERR_IO
+    for cut in (1, 2, len(comp) // 2, len(comp) - 1):
+        r, out = O.lz4_decompress(comp[:cut], 5000)
+        # a cut that lands right after a literal run is itself a valid (shorter) block
+        assert r == O.BO_ERR_IO or (r == 0 and out == data[:len(out)] and len(out) < 5000)
+    # output larger than capacity -> OUT_OF_SPACE -> IOError (device.cc:512-520)
+    assert O.lz4_decompress(comp, 4999)[0] == O.BO_ERR_IO
+    # offset 0 and offset before the segment start
+    assert O.lz4_decompress(bytes([0x10, 0x41, 0x00, 0x00, 0x00]), 100)[0] == O.BO_ERR_IO
+    assert O.lz4_decompress(bytes([0x10, 0x41, 0x02, 0x00, 0x00]), 100)[0] == O.BO_ERR_IO
+
+
+def test_inflate_malformed():
+    comp = zlib.compress(O.fill(O.KIND_MIXED, 3, 5000).tobytes(), 6)[2:-4]
+    for cut in (0, 1, len(comp) // 2, len(comp) - 1):
+        assert O.inflate(comp[:cut], 5000)[0] == O.BO_ERR_IO
+    assert O.inflate(comp, 4999)[0] == O.BO_ERR_IO
+    assert O.inflate(bytes([0x07]), 10)[0] == O.BO_ERR_IO  # BTYPE=11 reserved
+    assert O.inflate(bytes([0x01, 0x01, 0x00, 0x00, 0x00, 0x41]), 10)[0] == O.BO_ERR_IO
+
+
+# --- segment-level rules of CompressDevice (device.cc:156-318) --------------------------
+@pytest.mark.parametrize("codec", [O.CODEC_LZ4, O.CODEC_DEFLATE])
+def test_segment_roundtrip(codec):
+    seg = 59460
+    data = O.fill(O.KIND_ARROW, 5, 3 * seg + 17)
+    stride = 65536 + 512
+    r, slab, sizes = O.compress_segments(codec, data, seg, stride, threads=4)
+    assert r == 0 and sizes.size == 4
+    blobs = [slab[i * stride:i * stride + int(sizes[i])] for i in range(sizes.size)]
+    r, out, produced = O.decompress_segments(codec, blobs, seg, 4 * seg, threads=3)
+    assert r == 0
+    assert list(produced) == [seg, seg, seg, 17]
+    assert np.array_equal(out, data)
+
+
+def test_segment_empty_and_capacity():
+    r, slab, sizes = O.compress_segments(O.CODEC_LZ4, np.zeros(0, np.uint8), 2048, 4096)
+    assert r == 0 and sizes.size == 0  # empty input -> empty BufferVector (161-164)
+    r, out, _ = O.decompress_segments(O.CODEC_LZ4, [], 2048, 0)
+    assert r == 0 and out.size == 0  # empty vector -> OK (244-246)
+    data = O.fill(0, 1, 5000)
+    r, slab, sizes = O.compress_segments(O.CODEC_LZ4, data, 2048, 4096)
+    blobs = [slab[i * 4096:i * 4096 + int(sizes[i])] for i in range(sizes.size)]
+    r, _, _ = O.decompress_segments(O.CODEC_LZ4, blobs, 2048, 3 * 2048 - 1)
+    assert r == O.BO_ERR_CAPACITY  # capacity < n*seg (248-254)
