@@ -1,0 +1,208 @@
+"""bitar_amd -- MI355X-native segment codec engine (Python host side).
+
+The product is libbitar_hip.so (C ABI in include/bitar_hip.h, HIP kernels in csrc/); the
+bitar-shaped C++ front-end lives in cpp/.  This module binds the C ABI with ctypes for the
+Python callers (tests, bench.py, __graft_entry__).  torch is used only as plumbing:
+device memory and streams.  There is no CPU fallback: if the HIP library is missing or
+no gfx950 device is visible, the calls raise.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libbitar_hip.so")
+
+CODEC_LZ4 = 1
+CODEC_DEFLATE = 2
+SEGMENT_ERROR = 0xFFFFFFFF
+MAX_SEG_SIZE = 65536
+
+# negated arrow::StatusCode (reference src/include/util.h:157-205)
+STATUS_NAMES = {0: "OK", -1: "OutOfMemory", -4: "Invalid", -5: "IOError", -6: "CapacityError",
+                -8: "Cancelled", -9: "UnknownError", -10: "NotImplemented"}
+
+
+class BitarError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def build(verbose=False):
+    """Compile libbitar_hip.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    import subprocess
+    out = None if verbose else subprocess.DEVNULL
+    subprocess.check_call(["make", "-s", "-j8", "-C", _HERE], stdout=out)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BitarError(-10, f"{LIB_PATH} is not built (run bitar_amd.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    sig = {
+        "bitar_hip_abi_version": (i32, []),
+        "bitar_hip_last_error": (ctypes.c_char_p, []),
+        "bitar_hip_device_count": (i32, [ctypes.POINTER(i32)]),
+        "bitar_hip_open": (i32, [i32, vp, ctypes.POINTER(vp)]),
+        "bitar_hip_close": (i32, [vp]),
+        "bitar_hip_stream": (i32, [vp, u32, ctypes.POINTER(vp)]),
+        "bitar_hip_device": (i32, [vp, ctypes.POINTER(i32)]),
+        "bitar_hip_slot_size": (u64, [u32, u32]),
+        "bitar_hip_alloc": (i32, [vp, u64, ctypes.POINTER(vp)]),
+        "bitar_hip_free": (i32, [vp, vp]),
+        "bitar_hip_host_alloc": (i32, [vp, u64, ctypes.POINTER(vp)]),
+        "bitar_hip_host_free": (i32, [vp, vp]),
+        "bitar_hip_memcpy": (i32, [vp, vp, vp, u64, vp]),
+        "bitar_hip_compress": (i32, [vp, vp, u32, vp, u64, u32, vp, u64, vp]),
+        "bitar_hip_decompress": (i32, [vp, vp, u32, vp, vp, u32, u32, vp, u64, vp]),
+        "bitar_hip_decompress_slab": (i32, [vp, vp, u32, vp, u64, vp, u32, u32, vp, u64, vp]),
+        "bitar_hip_sync": (i32, [vp, vp]),
+        "bitar_hip_pack": (i32, [vp, vp, vp, u64, vp, u32, vp, vp]),
+        "bitar_hip_fill": (i32, [vp, vp, i32, u64, vp, u64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+# every symbol include/bitar_hip.h declares (checked by tests/test_abi.py)
+ABI_SYMBOLS = ("bitar_hip_abi_version", "bitar_hip_last_error", "bitar_hip_device_count",
+               "bitar_hip_open", "bitar_hip_close", "bitar_hip_stream", "bitar_hip_device",
+               "bitar_hip_slot_size", "bitar_hip_alloc", "bitar_hip_free",
+               "bitar_hip_host_alloc", "bitar_hip_host_free", "bitar_hip_memcpy",
+               "bitar_hip_compress", "bitar_hip_decompress", "bitar_hip_decompress_slab",
+               "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_fill")
+
+
+def check(rc):
+    if rc != 0:
+        raise BitarError(rc, lib().bitar_hip_last_error().decode())
+    return rc
+
+
+def slot_size(codec, seg):
+    return int(lib().bitar_hip_slot_size(codec, seg))
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib().bitar_hip_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def _ptr(t):
+    """device pointer of a torch tensor (or an int address, or None)."""
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return ctypes.c_void_p(t)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class Engine:
+    """One context on one gfx950 device: the CompressDevice analogue.
+
+    Calls are asynchronous on `stream` (default: torch's current stream on that device, so
+    torch copies and our kernels stay ordered).  Buffers are torch uint8 tensors in HBM.
+    """
+
+    def __init__(self, device=0, num_streams=1):
+        import torch  # plumbing only
+        self.torch = torch
+        self.device = device
+
+        class Cfg(ctypes.Structure):
+            _fields_ = [("num_streams", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+        cfg = Cfg(num_streams, 0)
+        ctx = ctypes.c_void_p()
+        check(lib().bitar_hip_open(device, ctypes.byref(cfg), ctypes.byref(ctx)))
+        self.ctx = ctx
+
+    def close(self):
+        if self.ctx:
+            lib().bitar_hip_close(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self, stream):
+        if stream is None:
+            return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+        if isinstance(stream, int):
+            return ctypes.c_void_p(stream)
+        return ctypes.c_void_p(stream.cuda_stream)
+
+    def queue_pair_stream(self, qp):
+        s = ctypes.c_void_p()
+        check(lib().bitar_hip_stream(self.ctx, qp, ctypes.byref(s)))
+        return s.value
+
+    def empty(self, nbytes, dtype=None):
+        t = self.torch
+        return t.empty(nbytes, dtype=dtype or t.uint8, device=f"cuda:{self.device}")
+
+    # --- hot path ------------------------------------------------------------------
+    def compress_into(self, codec, data, seg, slab, stride, sizes, n=None, stream=None):
+        n = data.numel() * data.element_size() if n is None else n
+        check(lib().bitar_hip_compress(self.ctx, self._stream(stream), codec, _ptr(data), n, seg,
+                                       _ptr(slab), stride, _ptr(sizes)))
+
+    def decompress_slab_into(self, codec, slab, stride, sizes, nseg, seg, out, produced,
+                             capacity=None, stream=None):
+        cap = out.numel() if capacity is None else capacity
+        check(lib().bitar_hip_decompress_slab(self.ctx, self._stream(stream), codec, _ptr(slab),
+                                              stride, _ptr(sizes), nseg, seg, _ptr(out), cap,
+                                              _ptr(produced)))
+
+    def decompress_into(self, codec, srcs, sizes, nseg, seg, out, produced, capacity=None,
+                        stream=None):
+        """srcs: device int64 tensor of segment addresses."""
+        cap = out.numel() if capacity is None else capacity
+        check(lib().bitar_hip_decompress(self.ctx, self._stream(stream), codec, _ptr(srcs),
+                                         _ptr(sizes), nseg, seg, _ptr(out), cap, _ptr(produced)))
+
+    def pack(self, slab, stride, sizes, nseg, offsets, frame=None, stream=None):
+        check(lib().bitar_hip_pack(self.ctx, self._stream(stream), _ptr(slab), stride,
+                                   _ptr(sizes), nseg, _ptr(offsets), _ptr(frame)))
+
+    def fill(self, kind, seed, out, n=None, stream=None):
+        n = out.numel() if n is None else n
+        check(lib().bitar_hip_fill(self.ctx, self._stream(stream), kind, seed, _ptr(out), n))
+
+    def sync(self, stream=None):
+        s = self._stream(stream) if stream is not False else None
+        check(lib().bitar_hip_sync(self.ctx, s))
+
+    # --- convenience: whole-buffer round trip (the CompressDevice call pair) -----------
+    def compress(self, codec, data, seg, stream=None):
+        """-> (slab, stride, sizes) ; data: uint8 HBM tensor.  sizes stays on device."""
+        n = data.numel()
+        nseg = (n + seg - 1) // seg
+        stride = slot_size(codec, seg)
+        slab = self.empty(max(nseg * stride, 1))
+        sizes = self.empty(max(nseg, 1), dtype=self.torch.int32)
+        self.compress_into(codec, data, seg, slab, stride, sizes, n=n, stream=stream)
+        return slab, stride, sizes[:nseg]
+
+    def decompress(self, codec, slab, stride, sizes, seg, stream=None):
+        nseg = sizes.numel()
+        out = self.empty(max(nseg * seg, 1))
+        produced = self.empty(max(nseg, 1), dtype=self.torch.int32)
+        self.decompress_slab_into(codec, slab, stride, sizes, nseg, seg, out, produced,
+                                  capacity=nseg * seg, stream=stream)
+        return out, produced[:nseg]

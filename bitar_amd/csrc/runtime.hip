@@ -1,0 +1,335 @@
+// runtime.hip -- the C-ABI of libbitar_hip.so (include/bitar_hip.h).
+//
+// A context = one gfx950 device + N HIP streams (queue pairs) + a sticky device error word.
+// Every entry point validates shapes on the host before launching, so a kernel never sees a
+// grid or a size it does not assume (one wave per segment, seg <= 65536).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/bitar_hip.h"
+
+namespace bitar_hip {
+__global__ void lz4_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
+                                    uint32_t*, uint32_t*);
+__global__ void lz4_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
+                                      const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
+                                      uint32_t*);
+__global__ void deflate_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
+                                        uint32_t*, uint32_t*);
+__global__ void inflate_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
+                               const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
+                               uint32_t*);
+__global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t*);
+__global__ void pack_kernel(const uint8_t*, uint64_t, const uint32_t*, const uint64_t*, uint32_t,
+                            uint8_t*);
+__global__ void fill_kernel(int, uint64_t, uint8_t*, uint64_t);
+}  // namespace bitar_hip
+
+struct bitar_hip_ctx {
+  int device = -1;
+  std::vector<hipStream_t> streams;
+  uint32_t* d_err = nullptr;  // sticky error word (bit0 decode error, bit1 slot overflow)
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(e == hipErrorOutOfMemory ? BITAR_HIP_OUT_OF_MEMORY : BITAR_HIP_UNKNOWN_ERROR,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, what)                       \
+  do {                                            \
+    hipError_t _e = (expr);                       \
+    if (_e != hipSuccess) return hip_fail(_e, what); \
+  } while (0)
+
+int enter(bitar_hip_ctx* ctx) {
+  if (!ctx) return fail(BITAR_HIP_INVALID, "null context");
+  HIP_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+  return 0;
+}
+
+// NULL is the HIP default stream (the usual HIP convention); queue-pair streams come from
+// bitar_hip_stream().
+hipStream_t pick_stream(bitar_hip_ctx*, void* stream) {
+  return reinterpret_cast<hipStream_t>(stream);
+}
+
+constexpr uint32_t kMaxSeg = BITAR_HIP_MAX_SEG_SIZE;
+
+}  // namespace
+
+extern "C" {
+
+int bitar_hip_abi_version(void) { return BITAR_HIP_ABI_VERSION; }
+
+const char* bitar_hip_last_error(void) { return g_last_error.c_str(); }
+
+int bitar_hip_device_count(int* count) {
+  if (!count) return fail(BITAR_HIP_INVALID, "null count");
+  *count = 0;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e == hipErrorNoDevice || n == 0) return 0;
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  int gfx950 = 0;
+  for (int d = 0; d < n; ++d) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d) == hipSuccess &&
+        std::strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+      ++gfx950;
+  }
+  *count = gfx950;
+  return 0;
+}
+
+int bitar_hip_open(int device, const bitar_hip_config* cfg, bitar_hip_ctx** out) {
+  if (!out) return fail(BITAR_HIP_INVALID, "null out");
+  *out = nullptr;
+  const uint32_t nstreams = cfg && cfg->num_streams ? cfg->num_streams : 1;
+  if (nstreams > 64) return fail(BITAR_HIP_INVALID, "num_streams must be in [1, 64]");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n), "hipGetDeviceCount");
+  if (device < 0 || device >= n) return fail(BITAR_HIP_INVALID, "no such device");
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(BITAR_HIP_NOT_IMPLEMENTED,
+                std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950");
+  HIP_TRY(hipSetDevice(device), "hipSetDevice");
+  auto* ctx = new bitar_hip_ctx();
+  ctx->device = device;
+  for (uint32_t q = 0; q < nstreams; ++q) {
+    hipStream_t s;
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      bitar_hip_close(ctx);
+      return hip_fail(e, "hipStreamCreate");
+    }
+    ctx->streams.push_back(s);
+  }
+  hipError_t e = hipMalloc(&ctx->d_err, 256);
+  if (e == hipSuccess) e = hipMemset(ctx->d_err, 0, 256);
+  if (e != hipSuccess) {
+    bitar_hip_close(ctx);
+    return hip_fail(e, "error word");
+  }
+  *out = ctx;
+  return 0;
+}
+
+int bitar_hip_close(bitar_hip_ctx* ctx) {
+  if (!ctx) return 0;
+  if (hipSetDevice(ctx->device) == hipSuccess) {
+    for (auto s : ctx->streams) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+    if (ctx->d_err) (void)hipFree(ctx->d_err);
+  }
+  delete ctx;
+  return 0;
+}
+
+int bitar_hip_stream(bitar_hip_ctx* ctx, uint32_t qp, void** stream) {
+  if (!ctx || !stream) return fail(BITAR_HIP_INVALID, "null argument");
+  if (qp >= ctx->streams.size()) return fail(BITAR_HIP_INVALID, "queue pair out of range");
+  *stream = ctx->streams[qp];
+  return 0;
+}
+
+int bitar_hip_device(bitar_hip_ctx* ctx, int* device) {
+  if (!ctx || !device) return fail(BITAR_HIP_INVALID, "null argument");
+  *device = ctx->device;
+  return 0;
+}
+
+uint64_t bitar_hip_slot_size(uint32_t codec, uint32_t seg) {
+  uint64_t bound;
+  if (codec == BITAR_HIP_CODEC_LZ4)
+    bound = (uint64_t)seg + seg / 255u + 16u;           // LZ4_compressBound
+  else if (codec == BITAR_HIP_CODEC_DEFLATE)
+    bound = ((uint64_t)seg * 9 + 7) / 8 + 16u;          // fixed Huffman, 9 bits/literal
+  else
+    return 0;
+  return (bound + 255u) & ~(uint64_t)255u;
+}
+
+int bitar_hip_alloc(bitar_hip_ctx* ctx, uint64_t bytes, void** ptr) {
+  if (int r = enter(ctx)) return r;
+  if (!ptr) return fail(BITAR_HIP_INVALID, "null ptr");
+  HIP_TRY(hipMalloc(ptr, bytes ? bytes : 1), "hipMalloc");
+  return 0;
+}
+
+int bitar_hip_free(bitar_hip_ctx* ctx, void* ptr) {
+  if (int r = enter(ctx)) return r;
+  HIP_TRY(hipFree(ptr), "hipFree");
+  return 0;
+}
+
+int bitar_hip_host_alloc(bitar_hip_ctx* ctx, uint64_t bytes, void** ptr) {
+  if (int r = enter(ctx)) return r;
+  if (!ptr) return fail(BITAR_HIP_INVALID, "null ptr");
+  HIP_TRY(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault), "hipHostMalloc");
+  return 0;
+}
+
+int bitar_hip_host_free(bitar_hip_ctx* ctx, void* ptr) {
+  if (int r = enter(ctx)) return r;
+  HIP_TRY(hipHostFree(ptr), "hipHostFree");
+  return 0;
+}
+
+int bitar_hip_memcpy(bitar_hip_ctx* ctx, void* dst, const void* src, uint64_t bytes,
+                     void* stream) {
+  if (int r = enter(ctx)) return r;
+  if (!bytes) return 0;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, pick_stream(ctx, stream)),
+          "hipMemcpyAsync");
+  return 0;
+}
+
+int bitar_hip_compress(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const void* d_in,
+                       uint64_t n, uint32_t seg, void* d_slab, uint64_t slot_stride,
+                       uint32_t* d_sizes) {
+  if (int r = enter(ctx)) return r;
+  if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE)
+    return fail(BITAR_HIP_NOT_IMPLEMENTED, "unknown codec");
+  if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
+  if (n == 0) return 0;  // empty input -> no segments (reference device.cc:161-164)
+  if (!d_in || !d_slab || !d_sizes) return fail(BITAR_HIP_INVALID, "null buffer");
+  if (slot_stride < bitar_hip_slot_size(codec, seg))
+    return fail(BITAR_HIP_INVALID, "slot_stride below the worst-case bound");
+  const uint64_t nseg = (n + seg - 1) / seg;
+  if (nseg > 0x7FFFFFFFull) return fail(BITAR_HIP_INVALID, "too many segments");
+  hipStream_t s = pick_stream(ctx, stream);
+  const auto* in = static_cast<const uint8_t*>(d_in);
+  auto* slab = static_cast<uint8_t*>(d_slab);
+  if (codec == BITAR_HIP_CODEC_LZ4)
+    hipLaunchKernelGGL(bitar_hip::lz4_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
+                       n, seg, slab, slot_stride, d_sizes, ctx->d_err);
+  else
+#ifdef BITAR_HAVE_DEFLATE
+    hipLaunchKernelGGL(bitar_hip::deflate_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
+                       in, n, seg, slab, slot_stride, d_sizes, ctx->d_err);
+#else
+    return fail(BITAR_HIP_NOT_IMPLEMENTED, "DEFLATE kernels not built");
+#endif
+  HIP_TRY(hipGetLastError(), "compress launch");
+  return 0;
+}
+
+static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
+                           const void* const* d_srcs, const void* d_slab, uint64_t stride,
+                           const uint32_t* d_sizes, uint32_t nseg, uint32_t seg, void* d_out,
+                           uint64_t capacity, uint32_t* d_produced) {
+  if (int r = enter(ctx)) return r;
+  if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE)
+    return fail(BITAR_HIP_NOT_IMPLEMENTED, "unknown codec");
+  if (nseg == 0) return 0;  // reference device.cc:244-246
+  if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
+  if (capacity < (uint64_t)nseg * seg)  // reference device.cc:248-254
+    return fail(BITAR_HIP_CAPACITY_ERROR,
+                "The decompressed_buffer is required to be >= " +
+                    std::to_string((uint64_t)nseg * seg) + " bytes");
+  if (!d_sizes || !d_out || !d_produced || (!d_srcs && !d_slab))
+    return fail(BITAR_HIP_INVALID, "null buffer");
+  if (nseg > 0x7FFFFFFFu) return fail(BITAR_HIP_INVALID, "too many segments");
+  hipStream_t s = pick_stream(ctx, stream);
+  const auto* srcs = reinterpret_cast<const uint8_t* const*>(d_srcs);
+  const auto* slab = static_cast<const uint8_t*>(d_slab);
+  auto* out = static_cast<uint8_t*>(d_out);
+  if (codec == BITAR_HIP_CODEC_LZ4)
+    hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
+                       stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
+  else
+#ifdef BITAR_HAVE_DEFLATE
+    hipLaunchKernelGGL(bitar_hip::inflate_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
+                       stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
+#else
+    return fail(BITAR_HIP_NOT_IMPLEMENTED, "DEFLATE kernels not built");
+#endif
+  HIP_TRY(hipGetLastError(), "decompress launch");
+  return 0;
+}
+
+int bitar_hip_decompress(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
+                         const void* const* d_srcs, const uint32_t* d_sizes, uint32_t nseg,
+                         uint32_t seg, void* d_out, uint64_t capacity, uint32_t* d_produced) {
+  if (nseg && !d_srcs) return fail(BITAR_HIP_INVALID, "null d_srcs");
+  return decompress_impl(ctx, stream, codec, d_srcs, nullptr, 0, d_sizes, nseg, seg, d_out,
+                         capacity, d_produced);
+}
+
+int bitar_hip_decompress_slab(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
+                              const void* d_slab, uint64_t slot_stride,
+                              const uint32_t* d_sizes, uint32_t nseg, uint32_t seg,
+                              void* d_out, uint64_t capacity, uint32_t* d_produced) {
+  if (nseg && !d_slab) return fail(BITAR_HIP_INVALID, "null d_slab");
+  return decompress_impl(ctx, stream, codec, nullptr, d_slab, slot_stride, d_sizes, nseg, seg,
+                         d_out, capacity, d_produced);
+}
+
+int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream) {
+  if (int r = enter(ctx)) return r;
+  HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)), "hipStreamSynchronize");
+  if (!stream)
+    for (auto s : ctx->streams) HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  uint32_t err = 0;
+  HIP_TRY(hipMemcpy(&err, ctx->d_err, sizeof(err), hipMemcpyDeviceToHost), "read error word");
+  if (err) {
+    HIP_TRY(hipMemset(ctx->d_err, 0, sizeof(err)), "clear error word");
+    if (err & 2u)
+      return fail(BITAR_HIP_IO_ERROR, "Compress data output is larger than allocated buffer");
+    return fail(BITAR_HIP_IO_ERROR, "Some operations have failed");
+  }
+  return 0;
+}
+
+int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_t slot_stride,
+                   const uint32_t* d_sizes, uint32_t nseg, uint64_t* d_offsets, void* d_frame) {
+  if (int r = enter(ctx)) return r;
+  if (!d_sizes || !d_offsets) return fail(BITAR_HIP_INVALID, "null buffer");
+  hipStream_t s = pick_stream(ctx, stream);
+  hipLaunchKernelGGL(bitar_hip::scan_sizes_kernel, dim3(1), dim3(1024), 0, s, d_sizes, nseg,
+                     d_offsets);
+  HIP_TRY(hipGetLastError(), "scan launch");
+  if (d_frame && nseg) {
+    if (!d_slab) return fail(BITAR_HIP_INVALID, "null slab");
+    hipLaunchKernelGGL(bitar_hip::pack_kernel, dim3(nseg), dim3(64), 0, s,
+                       static_cast<const uint8_t*>(d_slab), slot_stride, d_sizes, d_offsets,
+                       nseg, static_cast<uint8_t*>(d_frame));
+    HIP_TRY(hipGetLastError(), "pack launch");
+  }
+  return 0;
+}
+
+int bitar_hip_fill(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed, void* d_out,
+                   uint64_t n) {
+  if (int r = enter(ctx)) return r;
+  if (!n) return 0;
+  if (!d_out) return fail(BITAR_HIP_INVALID, "null buffer");
+  const uint64_t lines = (n + 63) / 64;
+  uint64_t blocks = (lines + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(bitar_hip::fill_kernel, dim3((uint32_t)blocks), dim3(256), 0,
+                     pick_stream(ctx, stream), kind, seed, static_cast<uint8_t*>(d_out), n);
+  HIP_TRY(hipGetLastError(), "fill launch");
+  return 0;
+}
+
+}  // extern "C"

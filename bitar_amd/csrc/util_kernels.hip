@@ -1,0 +1,170 @@
+// util_kernels.hip -- frame packing (prefix sum + gather) and the synthetic-input generator.
+#include "wave.hip.h"
+
+namespace bitar_hip {
+
+// Exclusive prefix sum of nseg sizes -> offsets[0..nseg], one 1024-thread workgroup.
+// nseg is at most a few hundred thousand (8 GiB / 64 KiB = 131072): a single block walks
+// the array in 1024-element tiles with a carried base.
+__global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint32_t* __restrict__ sizes,
+                                                          uint32_t nseg,
+                                                          uint64_t* __restrict__ offsets) {
+  __shared__ uint64_t part[1024 / kWave];
+  __shared__ uint64_t carry;
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nseg; base += 1024) {
+    const uint32_t idx = base + t;
+    uint64_t v = idx < nseg ? (uint64_t)sizes[idx] : 0ull;
+    uint64_t incl = v;  // inclusive wave scan (Hillis-Steele over 64 lanes)
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) part[w] = incl;
+    __syncthreads();
+    if (t < 64) {
+      uint64_t pv = t < 1024 / kWave ? part[t] : 0ull;
+      uint64_t pin = pv;
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(pin, d, 64);
+        if (t >= d) pin += y;
+      }
+      if (t < 1024 / kWave) part[t] = pin - pv;  // exclusive wave bases
+    }
+    __syncthreads();
+    const uint64_t c = carry;
+    if (idx < nseg) offsets[idx] = c + part[w] + incl - v;
+    __syncthreads();
+    if (t == 1023) carry = c + part[w] + incl;
+    __syncthreads();
+  }
+  if (t == 0) offsets[nseg] = carry;
+}
+
+// Gather slot i (sizes[i] bytes at slab + i*stride) to frame + offsets[i]; one wave per slot.
+__global__ __launch_bounds__(64) void pack_kernel(const uint8_t* __restrict__ slab,
+                                                  uint64_t stride,
+                                                  const uint32_t* __restrict__ sizes,
+                                                  const uint64_t* __restrict__ offsets,
+                                                  uint32_t nseg, uint8_t* __restrict__ frame) {
+  const uint32_t i = blockIdx.x;
+  if (i >= nseg) return;
+  wave_copy_global(frame + offsets[i], slab + (uint64_t)i * stride, sizes[i]);
+}
+
+// ---- synthetic input: a device restatement-free generator; tests check it against the
+// oracle's bo_fill byte for byte.  One thread per 64-byte line.
+__device__ __forceinline__ uint64_t sm64(uint64_t seed, uint64_t k) {
+  uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ void put_dec(uint8_t* p, uint32_t v, int width) {
+  for (int i = width - 1; i >= 0; --i) { p[i] = (uint8_t)('0' + v % 10); v /= 10; }
+}
+
+__device__ __forceinline__ void put_str(uint8_t* p, const char* s, int n) {
+  for (int i = 0; i < n; ++i) p[i] = (uint8_t)s[i];
+}
+
+__device__ void log_line(uint64_t seed, uint64_t j, uint8_t* l) {
+  const char* kLevel = "INFO WARN DEBUGERROR";
+  const char* kComp = "device   driver   memory   pool     queuepairconfig   burst    dequeue  ";
+  const char* kStat = "OK    OK    EAGAINOK    ";
+  const uint64_t h = sm64(seed ^ 0x5bd1e995ull, j);
+  for (int i = 0; i < 64; ++i) l[i] = ' ';
+  const uint64_t ms = j * 7;
+  put_dec(l + 0, (uint32_t)((ms / 3600000) % 24), 2); l[2] = ':';
+  put_dec(l + 3, (uint32_t)((ms / 60000) % 60), 2); l[5] = ':';
+  put_dec(l + 6, (uint32_t)((ms / 1000) % 60), 2); l[8] = '.';
+  put_dec(l + 9, (uint32_t)(ms % 1000), 3);
+  const uint32_t lv = (uint32_t)(h & 15);
+  put_str(l + 13, kLevel + 5 * (lv < 12 ? 0 : lv < 14 ? 1 : lv < 15 ? 2 : 3), 5);
+  put_str(l + 19, kComp + 9 * ((h >> 4) & 7), 9);
+  put_str(l + 29, "qp=", 3);
+  put_dec(l + 32, (uint32_t)((h >> 8) % 32), 2);
+  put_str(l + 35, "seg=", 4);
+  put_dec(l + 39, (uint32_t)((h >> 16) % 100000), 5);
+  put_str(l + 45, "status=", 7);
+  put_str(l + 52, kStat + 6 * ((h >> 40) & 3), 6);
+  l[63] = '\n';
+}
+
+__global__ __launch_bounds__(256) void fill_kernel(int kind, uint64_t seed, uint8_t* __restrict__ out,
+                                                   uint64_t n) {
+  const uint64_t nlines = (n + 63) / 64;
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < nlines;
+       j += (uint64_t)gridDim.x * blockDim.x) {
+    __attribute__((aligned(16))) uint8_t line[64];
+    uint64_t w[8];
+    const uint64_t k0 = j * 8;
+    bool text = false;
+    uint64_t tseed = seed;
+    switch (kind) {
+      case 0:
+        for (int i = 0; i < 8; ++i) w[i] = sm64(seed, k0 + i);
+        break;
+      case 1: {
+        const uint64_t region = ((j * 64) >> 20) % 3;
+        if (region == 0) {
+          for (int i = 0; i < 8; ++i) w[i] = sm64(seed ^ 0x1111ull, k0 + i) % 1000;
+        } else if (region == 1) {
+          text = true;
+        } else {
+          for (int i = 0; i < 8; ++i) w[i] = sm64(seed ^ 0x2222ull, k0 + i);
+        }
+        break;
+      }
+      case 2: {
+        const uint64_t col = ((j * 64) >> 20) & 3;
+        if (col == 3) { text = true; tseed = seed ^ 0x4444ull; break; }
+        for (int i = 0; i < 8; ++i) {
+          const uint64_t r = sm64(seed ^ (0x3333ull + col), k0 + i);
+          if (col == 0) {
+            w[i] = r % 1000;
+          } else if (col == 1) {
+            const int64_t s = (int64_t)(r & 0xFFFF) + (int64_t)((r >> 16) & 0xFFFF) +
+                              (int64_t)((r >> 32) & 0xFFFF) + (int64_t)(r >> 48) - 131070;
+            const double d = (double)s / 37837.0;
+            w[i] = (uint64_t)__double_as_longlong(d);
+          } else {
+            w[i] = (r & 63) | (((r >> 32) & 63) << 32);
+          }
+        }
+        break;
+      }
+      case 3:
+        for (int i = 0; i < 8; ++i) w[i] = 0x6161616161616161ull;
+        break;
+      default:
+        for (int b = 0; b < 64; ++b) line[b] = (uint8_t)(((j * 64 + b) % 251) * 7);
+        break;
+    }
+    if (text) {
+      log_line(tseed, j, line);
+    } else if (kind >= 0 && kind <= 3) {
+      for (int i = 0; i < 8; ++i)
+        for (int b = 0; b < 8; ++b) line[i * 8 + b] = (uint8_t)(w[i] >> (8 * b));
+    }
+    const uint64_t base = j * 64;
+    if (base + 64 <= n) {
+      uint4* d = reinterpret_cast<uint4*>(out + base);
+      const uint4* s = reinterpret_cast<const uint4*>(line);
+      if (((uintptr_t)d & 15) == 0) {
+        for (int q = 0; q < 4; ++q) d[q] = s[q];
+      } else {
+        for (int b = 0; b < 64; ++b) out[base + b] = line[b];
+      }
+    } else {
+      for (uint64_t b = 0; base + b < n; ++b) out[base + b] = line[b];
+    }
+  }
+}
+
+}  // namespace bitar_hip

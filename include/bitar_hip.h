@@ -1,0 +1,146 @@
+/*
+ * bitar_hip.h -- the C-ABI boundary of the MI355X segment codec engine (libbitar_hip.so).
+ *
+ * Plain pointers and sizes only; no Arrow, torch or HIP types in the signatures
+ * (hipStream_t travels as void*).  Every entry point returns 0 or a negated
+ * arrow::StatusCode, the convention the reference carries in an int
+ * (reference src/include/util.h:157-205).
+ *
+ * Each function names the reference interface it replaces.  The reference drives a
+ * BlueField-2 DEFLATE engine through DPDK compressdev; here one HIP kernel launch
+ * replaces a whole enqueue/dequeue burst loop, and a HIP stream replaces a queue pair.
+ */
+#ifndef BITAR_HIP_H_
+#define BITAR_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BITAR_HIP_ABI_VERSION 1
+
+/* negated arrow::StatusCode */
+enum bitar_hip_status {
+  BITAR_HIP_OK = 0,
+  BITAR_HIP_OUT_OF_MEMORY = -1,
+  BITAR_HIP_INVALID = -4,
+  BITAR_HIP_IO_ERROR = -5,
+  BITAR_HIP_CAPACITY_ERROR = -6,
+  BITAR_HIP_CANCELLED = -8,
+  BITAR_HIP_UNKNOWN_ERROR = -9,
+  BITAR_HIP_NOT_IMPLEMENTED = -10
+};
+
+/* Codec of one segment op.  DEFLATE = raw RFC 1951 stream per segment, the reference's
+ * frame (reference src/config.cc:83-105, memory.cc:110).  LZ4 = raw LZ4 block per segment
+ * (the north-star codec). */
+enum bitar_hip_codec { BITAR_HIP_CODEC_LZ4 = 1, BITAR_HIP_CODEC_DEFLATE = 2 };
+
+/* Per-segment marker written into sizes[] / produced[] when that segment's op failed
+ * (malformed stream, or output larger than its slot: the reference's
+ * RTE_COMP_OP_STATUS_OUT_OF_SPACE_*, device.cc:512-520). */
+#define BITAR_HIP_SEGMENT_ERROR 0xFFFFFFFFu
+
+/* Largest segment a kernel accepts (LZ4 offsets are 16-bit; the reference caps segments
+ * at kMaxSegSize = 59460, config.h:41-47). */
+#define BITAR_HIP_MAX_SEG_SIZE 65536u
+
+typedef struct bitar_hip_ctx bitar_hip_ctx;
+
+typedef struct {
+  uint32_t num_streams; /* queue pairs: one HIP stream each (driver.cc:100-157 lcore map) */
+  uint32_t flags;       /* reserved, 0 */
+} bitar_hip_config;
+
+/* Number of visible gfx950 devices.  Replaces rte_compressdev_devices_get() in
+ * CompressDriver::ListAvailableDeviceIds (reference src/driver.cc:173-190). */
+int bitar_hip_device_count(int* count);
+
+/* Open a device context with cfg->num_streams streams.  Replaces
+ * CompressDevice::Initialize: configure + queue_pair_setup + start
+ * (reference src/device.cc:114-154). */
+int bitar_hip_open(int device, const bitar_hip_config* cfg, bitar_hip_ctx** out);
+
+/* Release streams and device state.  Replaces ~CompressDevice (device.cc:329-343). */
+int bitar_hip_close(bitar_hip_ctx* ctx);
+
+/* The hipStream_t behind queue pair `qp` (returned as void*). */
+int bitar_hip_stream(bitar_hip_ctx* ctx, uint32_t qp, void** stream);
+
+/* Device ordinal of the context. */
+int bitar_hip_device(bitar_hip_ctx* ctx, int* device);
+
+/* Worst-case compressed bytes of one segment of `seg` bytes (LZ4_compressBound /
+ * fixed-Huffman bound), rounded up to 256 B.  Plays the role of compressed_seg_size
+ * (reference src/config.cc:59-73): the stride of output slots in a slab. */
+uint64_t bitar_hip_slot_size(uint32_t codec, uint32_t seg);
+
+/* HBM / pinned-host allocations on the context's device.  Replace the memzone reservation
+ * of RtememzoneAllocator::AllocateAligned / rte_malloc (reference src/memory_pool.cc:70-188).
+ * Device allocations are 256-B aligned. */
+int bitar_hip_alloc(bitar_hip_ctx* ctx, uint64_t bytes, void** ptr);
+int bitar_hip_free(bitar_hip_ctx* ctx, void* ptr);
+int bitar_hip_host_alloc(bitar_hip_ctx* ctx, uint64_t bytes, void** ptr);
+int bitar_hip_host_free(bitar_hip_ctx* ctx, void* ptr);
+
+/* Asynchronous copy in any direction on `stream`.  In every call `stream` is a hipStream_t;
+ * NULL is the HIP default stream, queue-pair streams come from bitar_hip_stream(). */
+int bitar_hip_memcpy(bitar_hip_ctx* ctx, void* dst, const void* src, uint64_t bytes,
+                     void* stream);
+
+/* Compress n bytes at d_in (device memory) as ceil(n/seg) independent segments.
+ * Segment i is written to d_slab + i*slot_stride and d_sizes[i] receives its compressed
+ * size.  Asynchronous on `stream`.  n == 0 launches nothing.
+ * Replaces one CompressDevice::Compress call: the AssembleFrom / EnqueueBurst /
+ * DequeueBurst loop over bursts of segments (reference src/device.cc:156-238,
+ * src/memory.cc:350-430).  slot_stride must be >= bitar_hip_slot_size(codec, seg). */
+int bitar_hip_compress(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const void* d_in,
+                       uint64_t n, uint32_t seg, void* d_slab, uint64_t slot_stride,
+                       uint32_t* d_sizes);
+
+/* Decompress nseg segments.  d_srcs[i] (a device array of device pointers) holds
+ * d_sizes[i] compressed bytes; segment i inflates into d_out + i*seg and d_produced[i]
+ * receives its size.  Requires capacity >= nseg*seg, else BITAR_HIP_CAPACITY_ERROR
+ * (reference device.cc:248-254).  Asynchronous on `stream`.
+ * Replaces one CompressDevice::Decompress call (reference src/device.cc:240-318,
+ * src/memory.cc:432-505). */
+int bitar_hip_decompress(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
+                         const void* const* d_srcs, const uint32_t* d_sizes, uint32_t nseg,
+                         uint32_t seg, void* d_out, uint64_t capacity, uint32_t* d_produced);
+
+/* Same, with segment i at d_slab + i*slot_stride (the layout bitar_hip_compress writes). */
+int bitar_hip_decompress_slab(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
+                              const void* d_slab, uint64_t slot_stride,
+                              const uint32_t* d_sizes, uint32_t nseg, uint32_t seg,
+                              void* d_out, uint64_t capacity, uint32_t* d_produced);
+
+/* Wait for `stream` (NULL = the default stream and every queue-pair stream).  Returns BITAR_HIP_IO_ERROR if
+ * any segment op launched on this context failed since the last sync (the sticky
+ * device-side error word), which it then clears.  Replaces the completion polling of
+ * DequeueBurst + GetErrorCount (reference src/device.cc:84-110, 490-535). */
+int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream);
+
+/* Exclusive prefix sum of d_sizes (nseg entries) into d_offsets (nseg+1 entries), then
+ * gather each slot into one contiguous frame at d_frame (d_frame may be NULL to compute
+ * offsets only).  Builds the packed frame / global frame index. */
+int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_t slot_stride,
+                   const uint32_t* d_sizes, uint32_t nseg, uint64_t* d_offsets, void* d_frame);
+
+/* Deterministic synthetic input (SplitMix64-based; kinds as in the oracle's bo_fill:
+ * 0 random, 1 Silesia-style mix, 2 Arrow record-batch body, 3 constant, 4 periodic). */
+int bitar_hip_fill(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed, void* d_out,
+                   uint64_t n);
+
+/* Thread-local text of the last error returned on this thread. */
+const char* bitar_hip_last_error(void);
+
+/* ABI version (BITAR_HIP_ABI_VERSION). */
+int bitar_hip_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BITAR_HIP_H_ */

@@ -76,14 +76,15 @@ int bo_lz4_decompress_block(const uint8_t* src, uint32_t csize, uint8_t* dst, ui
 
 /* ---- the bitar window-scan parse (shared by the LZ4 and fixed-DEFLATE encoders) --- *
  * Restated exactly as the HIP kernels run it (DESIGN.md "Window-scan parse"):
- *   positions are scanned in windows of 64 (one per wavefront lane);
- *   every window position i <= n-12 looks up hash(read32(i)) in a 4096-entry table of
- *   the most recent position seen in an EARLIER window, then all window positions are
- *   inserted (the largest position wins a shared slot);
- *   greedily, from the current position, the first window position with a verified
- *   4-byte match (distance <= max_dist) starts a match, extended forward while bytes
- *   agree, never past n-5; the next search starts at the match end;
- *   the next window starts at max(match end, window start + 64).                      */
+ *   positions 0..n-12 (legal match starts) are visited in FIXED windows of 64, one per
+ *   wavefront lane: window w covers [64w, 64w+64);
+ *   every window position looks up hash(read32(p)) in a 4096-entry table holding the most
+ *   recent position inserted by an EARLIER window, then all window positions are inserted
+ *   (the largest position wins a shared slot) -- the table never depends on the parse;
+ *   greedily, from the current position, the first window position whose candidate c
+ *   satisfies c < p, p - c <= max_dist and read32(c) == read32(p) starts a match,
+ *   extended forward while bytes agree, never past n-5 nor max_mlen; the search resumes
+ *   at the match end (possibly several windows later).                                  */
 #define BO_HASH_LOG 12
 #define BO_WIN 64
 #define BO_MINMATCH 4
@@ -105,10 +106,10 @@ static void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist,
   if (n >= BO_MFLIMIT + 1) {
     static __thread uint32_t table[1u << BO_HASH_LOG];
     memset(table, 0, sizeof(table));
-    const uint32_t last_start = n - BO_MFLIMIT; /* match start must be <= n-12 */
-    const uint32_t match_limit = n - BO_LASTLITERALS; /* match end must be <= n-5 */
-    uint32_t x = 0;
-    while (x <= last_start) {
+    const uint32_t last_start = n - BO_MFLIMIT;        /* match start must be <= n-12 */
+    const uint32_t match_limit = n - BO_LASTLITERALS;  /* match end must be <= n-5 */
+    uint32_t pos = 0;
+    for (uint32_t x = 0; x <= last_start; x += BO_WIN) {
       uint32_t cnt = last_start - x + 1;
       if (cnt > BO_WIN) cnt = BO_WIN;
       uint32_t cand[BO_WIN], h[BO_WIN];
@@ -117,7 +118,6 @@ static void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist,
         cand[l] = table[h[l]];
       }
       for (uint32_t l = 0; l < cnt; ++l) table[h[l]] = x + l; /* ascending: max wins */
-      uint32_t pos = x;
       for (;;) {
         uint32_t i = 0, found = 0;
         for (uint32_t l = (pos > x ? pos - x : 0); l < cnt; ++l) {
@@ -137,9 +137,7 @@ static void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist,
         emit(ctx, anchor, i - anchor, i - c, len);
         pos = i + len;
         anchor = pos;
-        if (pos >= x + cnt) break;
       }
-      x = (pos > x + BO_WIN) ? pos : x + BO_WIN;
     }
   }
   emit(ctx, anchor, n - anchor, 0, 0); /* last sequence: literals only */
