@@ -32,6 +32,7 @@ def parse():
     p.add_argument("--bytes", type=int, default=1 << 30, help="bytes per rank")
     p.add_argument("--seg", type=int, default=65536)
     p.add_argument("--kind", type=int, default=1, help="0 random, 1 mixed, 2 arrow")
+    p.add_argument("--codec", default="lz4", choices=["lz4", "deflate"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=256 << 20)
     p.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
@@ -108,7 +109,7 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
     eng = bitar_amd.Engine(dev)
-    codec = bitar_amd.CODEC_LZ4
+    codec = bitar_amd.CODEC_LZ4 if args.codec == "lz4" else bitar_amd.CODEC_DEFLATE
     n, seg = args.bytes, args.seg
     nseg = (n + seg - 1) // seg
     stride = bitar_amd.slot_size(codec, seg)
@@ -185,8 +186,9 @@ def main():
     value = world * U * args.steps / elapsed / GIB
     comp_bytes = U + C + 4.0 * nseg        # algorithmic bytes of one compress launch
     dec_bytes = U + C                      # algorithmic bytes of one decompress launch
-    dominant = ("lz4_compress_kernel", comp_bytes, t_comp) if t_comp >= t_dec else \
-        ("lz4_decompress_kernel", dec_bytes, t_dec)
+    kc, kd = (("lz4_compress_kernel", "lz4_decompress_kernel") if args.codec == "lz4"
+              else ("deflate_compress_kernel", "inflate_kernel"))
+    dominant = (kc, comp_bytes, t_comp) if t_comp >= t_dec else (kd, dec_bytes, t_dec)
     achieved = dominant[1] / dominant[2] / 1e9
     traffic = None
     try:
@@ -210,9 +212,11 @@ def main():
         "data": "synthetic (deterministic SplitMix64 generator, generated in HBM)",
         "config": {"workload": "LZ4 block compress + decompress round trip, 1 GiB per GPU, "
                                "64 KiB segments, Silesia-style mix (BASELINE configs[2])"
-                               if args.kind == 1 else f"LZ4 round trip, kind {args.kind}",
+                               if (args.kind == 1 and args.codec == "lz4")
+                               else f"{args.codec} round trip, kind {args.kind}, seg {seg}",
                    "bytes_per_gpu": n, "segment_bytes": seg, "segments_per_gpu": nseg,
-                   "codec": "lz4-block", "input_kind": args.kind,
+                   "codec": "lz4-block" if args.codec == "lz4" else "deflate-raw-fixed",
+                   "input_kind": args.kind,
                    "parallelism": f"{world} independent shards (round-robin segments), "
                                   "RCCL all-gather of sizes" if world > 1 else "1 GPU"},
         "compression_ratio": round(U / C, 4),
@@ -224,12 +228,12 @@ def main():
                      "traffic": traffic,
                      "algorithmic_bytes_per_launch": dominant[1],
                      "avg_launch_ms": round(dominant[2] * 1e3, 4)},
-        "kernels": {"lz4_compress_kernel": {"avg_ms": round(t_comp * 1e3, 4),
-                                            "alg_GBs": round(comp_bytes / t_comp / 1e9, 2)},
-                    "lz4_decompress_kernel": {"avg_ms": round(t_dec * 1e3, 4),
-                                              "alg_GBs": round(dec_bytes / t_dec / 1e9, 2)}},
+        "kernels": {kc: {"avg_ms": round(t_comp * 1e3, 4),
+                         "alg_GBs": round(comp_bytes / t_comp / 1e9, 2)},
+                    kd: {"avg_ms": round(t_dec * 1e3, 4),
+                         "alg_GBs": round(dec_bytes / t_dec / 1e9, 2)}},
     }
-    if not args.no_cpu_baseline and world == 1:
+    if not args.no_cpu_baseline and world == 1 and args.codec == "lz4":
         res["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(res), flush=True)
     if world > 1:

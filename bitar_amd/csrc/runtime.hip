@@ -214,6 +214,8 @@ int bitar_hip_compress(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const v
   if (!d_in || !d_slab || !d_sizes) return fail(BITAR_HIP_INVALID, "null buffer");
   if (slot_stride < bitar_hip_slot_size(codec, seg))
     return fail(BITAR_HIP_INVALID, "slot_stride below the worst-case bound");
+  if (((uintptr_t)d_slab & 15u) != 0 || (slot_stride & 15u) != 0)
+    return fail(BITAR_HIP_INVALID, "d_slab and slot_stride must be 16-B aligned");
   const uint64_t nseg = (n + seg - 1) / seg;
   if (nseg > 0x7FFFFFFFull) return fail(BITAR_HIP_INVALID, "too many segments");
   hipStream_t s = pick_stream(ctx, stream);
@@ -223,12 +225,8 @@ int bitar_hip_compress(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const v
     hipLaunchKernelGGL(bitar_hip::lz4_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
                        n, seg, slab, slot_stride, d_sizes, ctx->d_err);
   else
-#ifdef BITAR_HAVE_DEFLATE
     hipLaunchKernelGGL(bitar_hip::deflate_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
                        in, n, seg, slab, slot_stride, d_sizes, ctx->d_err);
-#else
-    return fail(BITAR_HIP_NOT_IMPLEMENTED, "DEFLATE kernels not built");
-#endif
   HIP_TRY(hipGetLastError(), "compress launch");
   return 0;
 }
@@ -257,12 +255,8 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
     hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
                        stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
   else
-#ifdef BITAR_HAVE_DEFLATE
     hipLaunchKernelGGL(bitar_hip::inflate_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
                        stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
-#else
-    return fail(BITAR_HIP_NOT_IMPLEMENTED, "DEFLATE kernels not built");
-#endif
   HIP_TRY(hipGetLastError(), "decompress launch");
   return 0;
 }

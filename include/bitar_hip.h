@@ -96,7 +96,8 @@ int bitar_hip_memcpy(bitar_hip_ctx* ctx, void* dst, const void* src, uint64_t by
  * size.  Asynchronous on `stream`.  n == 0 launches nothing.
  * Replaces one CompressDevice::Compress call: the AssembleFrom / EnqueueBurst /
  * DequeueBurst loop over bursts of segments (reference src/device.cc:156-238,
- * src/memory.cc:350-430).  slot_stride must be >= bitar_hip_slot_size(codec, seg). */
+ * src/memory.cc:350-430).  slot_stride must be >= bitar_hip_slot_size(codec, seg); d_slab
+ * and slot_stride must be 16-B aligned. */
 int bitar_hip_compress(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const void* d_in,
                        uint64_t n, uint32_t seg, void* d_slab, uint64_t slot_stride,
                        uint32_t* d_sizes);
