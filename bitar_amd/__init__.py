@@ -61,6 +61,8 @@ def lib():
         "bitar_hip_host_free": (i32, [vp, vp]),
         "bitar_hip_memcpy": (i32, [vp, vp, vp, u64, vp]),
         "bitar_hip_compress": (i32, [vp, vp, u32, vp, u64, u32, vp, u64, vp]),
+        "bitar_hip_compress_scattered": (i32, [vp, vp, u32, vp, u64, u32, vp, u64, vp]),
+        "bitar_hip_pointer_info": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "bitar_hip_decompress": (i32, [vp, vp, u32, vp, vp, u32, u32, vp, u64, vp]),
         "bitar_hip_decompress_slab": (i32, [vp, vp, u32, vp, u64, vp, u32, u32, vp, u64, vp]),
         "bitar_hip_sync": (i32, [vp, vp]),
@@ -80,7 +82,8 @@ ABI_SYMBOLS = ("bitar_hip_abi_version", "bitar_hip_last_error", "bitar_hip_devic
                "bitar_hip_open", "bitar_hip_close", "bitar_hip_stream", "bitar_hip_device",
                "bitar_hip_slot_size", "bitar_hip_alloc", "bitar_hip_free",
                "bitar_hip_host_alloc", "bitar_hip_host_free", "bitar_hip_memcpy",
-               "bitar_hip_compress", "bitar_hip_decompress", "bitar_hip_decompress_slab",
+               "bitar_hip_compress", "bitar_hip_compress_scattered", "bitar_hip_pointer_info",
+               "bitar_hip_decompress", "bitar_hip_decompress_slab",
                "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_fill")
 
 

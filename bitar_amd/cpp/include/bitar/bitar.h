@@ -1,0 +1,10 @@
+// bitar/bitar.h -- umbrella header of the MI355X bitar front-end.
+#pragma once
+
+#include "bitar/config.h"
+#include "bitar/device.h"
+#include "bitar/driver.h"
+#include "bitar/hip_device.h"
+#include "bitar/memory_pool.h"
+#include "bitar/type_fwd.h"
+#include "bitar/util.h"

@@ -1,0 +1,499 @@
+// device.cc -- CompressDevice on an MI355X (reference src/device.cc + src/memory.cc).
+//
+// Reference flow per call: AssembleFrom (mbufs per segment, memzone slots) -> EnqueueBurst
+// -> DequeueBurst (busy-poll) -> callback, repeated per burst of <= 32 ops
+// (device.cc:156-318, memory.cc:350-505).  Here: take one slot per segment from the HBM slot
+// pool, upload the slot-address table, launch ONE kernel over every segment on the queue
+// pair's stream, read back the per-segment sizes, sync.  Errors map as in the reference:
+// per-op failure / OUT_OF_SPACE -> IOError, busy queue pair -> Cancelled, capacity ->
+// CapacityError, bad state/range -> Invalid.
+#include "bitar/device.h"
+
+#include <arrow/buffer.h>
+#include <arrow/util/logging.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stack>
+
+#include "bitar/hip_device.h"
+#include "bitar_hip.h"
+#include "hip_ctx.h"
+
+namespace bitar {
+
+namespace internal {
+
+static constexpr std::uint32_t kMinPreallocateSlots = 20;  // reference memory.h:51
+
+// Pool of compressed-output slots (DeviceMemory, reference memory.cc:120-228): a LIFO free
+// stack of slot addresses carved from HBM chunks, an occupied set, growth on demand.
+class DeviceMemory {
+ public:
+  DeviceMemory(bitar_hip_ctx* ctx, std::uint64_t slot_size) : ctx_(ctx), slot_size_(slot_size) {}
+  ~DeviceMemory() {
+    for (void* c : chunks_) (void)bitar_hip_free(ctx_, c);
+  }
+
+  arrow::Status Preallocate(std::uint32_t n) { return Grow(n); }
+
+  // n slots (the reference takes one memzone per segment, memory.cc:405-425)
+  arrow::Status Take(std::uint32_t n, std::vector<std::uint8_t*>* out) {
+    const std::lock_guard<std::mutex> lock(mutex_);
+    if (free_.size() < n) {
+      ARROW_RETURN_NOT_OK(GrowLocked(std::max<std::uint32_t>(
+          n - static_cast<std::uint32_t>(free_.size()), kGrowSlots)));
+    }
+    out->resize(n);
+    for (std::uint32_t i = 0; i < n; ++i) {
+      (*out)[i] = free_.back();
+      free_.pop_back();
+      occupied_.insert((*out)[i]);
+    }
+    return arrow::Status::OK();
+  }
+
+  // 1 if addr is the start of an occupied slot (returned to the pool), else 0
+  std::size_t Put(const std::uint8_t* addr) {
+    const std::lock_guard<std::mutex> lock(mutex_);
+    auto it = occupied_.find(addr);
+    if (it == occupied_.end()) return 0;
+    occupied_.erase(it);
+    free_.push_back(const_cast<std::uint8_t*>(addr));
+    return 1;
+  }
+
+  void PutAll(const std::vector<std::uint8_t*>& slots) {
+    for (auto* s : slots) Put(s);
+  }
+
+ private:
+  static constexpr std::uint32_t kGrowSlots = 256;
+
+  arrow::Status Grow(std::uint32_t n) {
+    const std::lock_guard<std::mutex> lock(mutex_);
+    return GrowLocked(n);
+  }
+  arrow::Status GrowLocked(std::uint32_t n) {
+    if (!chunks_.empty())
+      ARROW_LOG(WARNING) << "Allocating output slots in the critical path (" << n << " slots)";
+    void* p = nullptr;
+    BITAR_ABI(bitar_hip_alloc(ctx_, slot_size_ * n, &p), "slot pool");
+    chunks_.push_back(p);
+    auto* base = static_cast<std::uint8_t*>(p);
+    for (std::uint32_t i = n; i-- > 0;) free_.push_back(base + slot_size_ * i);
+    return arrow::Status::OK();
+  }
+
+  bitar_hip_ctx* ctx_;
+  const std::uint64_t slot_size_;
+  std::vector<void*> chunks_;
+  std::vector<std::uint8_t*> free_;
+  std::unordered_set<const std::uint8_t*> occupied_;
+  std::mutex mutex_;
+};
+
+// Per-queue-pair stream and staging (QueuePairMemory, reference memory.cc:237-348): pinned
+// host tables of slot addresses / sizes, their device copies, and an HBM staging area for
+// host-resident inputs and outputs.
+struct QueuePairMemory {
+  bitar_hip_ctx* ctx = nullptr;
+  void* stream = nullptr;
+  std::atomic<bool> busy{false};
+  std::uint64_t* h_ptrs = nullptr;
+  std::uint32_t* h_sizes = nullptr;
+  std::uint64_t* d_ptrs = nullptr;
+  std::uint32_t* d_sizes = nullptr;
+  std::uint32_t* d_prod = nullptr;
+  std::size_t table_cap = 0;
+  void* d_stage = nullptr;
+  std::uint64_t stage_cap = 0;
+
+  ~QueuePairMemory() {
+    if (!ctx) return;
+    if (h_ptrs) (void)bitar_hip_host_free(ctx, h_ptrs);
+    if (h_sizes) (void)bitar_hip_host_free(ctx, h_sizes);
+    if (d_ptrs) (void)bitar_hip_free(ctx, d_ptrs);
+    if (d_sizes) (void)bitar_hip_free(ctx, d_sizes);
+    if (d_prod) (void)bitar_hip_free(ctx, d_prod);
+    if (d_stage) (void)bitar_hip_free(ctx, d_stage);
+  }
+
+  arrow::Status Tables(std::size_t n) {
+    if (n <= table_cap) return arrow::Status::OK();
+    std::size_t cap = std::max<std::size_t>(n, 2 * table_cap);
+    if (h_ptrs) (void)bitar_hip_host_free(ctx, h_ptrs);
+    if (h_sizes) (void)bitar_hip_host_free(ctx, h_sizes);
+    if (d_ptrs) (void)bitar_hip_free(ctx, d_ptrs);
+    if (d_sizes) (void)bitar_hip_free(ctx, d_sizes);
+    if (d_prod) (void)bitar_hip_free(ctx, d_prod);
+    h_ptrs = nullptr;
+    h_sizes = nullptr;
+    d_ptrs = nullptr;
+    d_sizes = nullptr;
+    d_prod = nullptr;
+    table_cap = 0;
+    void* p = nullptr;
+    BITAR_ABI(bitar_hip_host_alloc(ctx, cap * 8, &p), "qp tables");
+    h_ptrs = static_cast<std::uint64_t*>(p);
+    BITAR_ABI(bitar_hip_host_alloc(ctx, cap * 4, &p), "qp tables");
+    h_sizes = static_cast<std::uint32_t*>(p);
+    BITAR_ABI(bitar_hip_alloc(ctx, cap * 8, &p), "qp tables");
+    d_ptrs = static_cast<std::uint64_t*>(p);
+    BITAR_ABI(bitar_hip_alloc(ctx, cap * 4, &p), "qp tables");
+    d_sizes = static_cast<std::uint32_t*>(p);
+    BITAR_ABI(bitar_hip_alloc(ctx, cap * 4, &p), "qp tables");
+    d_prod = static_cast<std::uint32_t*>(p);
+    table_cap = cap;
+    return arrow::Status::OK();
+  }
+
+  arrow::Status Stage(std::uint64_t bytes) {
+    if (bytes <= stage_cap) return arrow::Status::OK();
+    if (d_stage) (void)bitar_hip_free(ctx, d_stage);
+    d_stage = nullptr;
+    stage_cap = 0;
+    BITAR_ABI(bitar_hip_alloc(ctx, bytes, &d_stage), "qp staging");
+    stage_cap = bytes;
+    return arrow::Status::OK();
+  }
+};
+
+namespace {
+
+// true if `addr` is HBM of `device` (buffers of our memory manager short-cut the query)
+bool OnDevice(const arrow::Buffer& b, int device) {
+  const auto& mm = b.memory_manager();
+  if (mm && !mm->is_cpu() && mm->device()->device_type() == arrow::DeviceAllocationType::kROCM)
+    return mm->device()->device_id() == device;
+  int kind = 0, dev = -1;
+  if (bitar_hip_pointer_info(reinterpret_cast<const void*>(b.address()), &kind, &dev) != 0)
+    return false;
+  return kind == 2 && dev == device;
+}
+
+bool OnDevice(std::uint64_t address, int device) {
+  int kind = 0, dev = -1;
+  if (bitar_hip_pointer_info(reinterpret_cast<const void*>(address), &kind, &dev) != 0)
+    return false;
+  return kind == 2 && dev == device;
+}
+
+std::uint32_t AbiCodec(Codec c) {
+  return c == Codec::LZ4 ? BITAR_HIP_CODEC_LZ4 : BITAR_HIP_CODEC_DEFLATE;
+}
+
+}  // namespace
+
+}  // namespace internal
+
+template <typename Class, typename Enable>
+arrow::Status CompressDevice<Class, Enable>::Initialize(
+    std::unique_ptr<Configuration<Class>> configuration) {
+  if (state_ != internal::DeviceState::kUndefined)
+    return arrow::Status::Invalid("Compress device ", +device_id_, " is already initialized");
+  ARROW_RETURN_NOT_OK(set_configuration(std::move(configuration)));
+  ARROW_RETURN_NOT_OK(ValidateConfiguration());
+  ARROW_RETURN_NOT_OK(PreAllocateMemory());
+  set_state(internal::DeviceState::kStarted);
+  return arrow::Status::OK();
+}
+
+template <typename Class, typename Enable>
+arrow::Status CompressDevice<Class, Enable>::PreAllocateMemory() {
+  bitar_hip_config cfg{num_qps(), 0};
+  BITAR_ABI(bitar_hip_open(device_id_, &cfg, &ctx_), "Device configuration failed");
+  set_state(internal::DeviceState::kConfigured);
+  const auto codec = internal::AbiCodec(configuration_->codec());
+  const std::uint32_t seg = configuration_->decompressed_seg_size();
+  slot_size_ = std::max<std::uint64_t>(bitar_hip_slot_size(codec, seg),
+                                       (configuration_->compressed_seg_size() + 255u) & ~255u);
+  device_memory_ = std::make_unique<internal::DeviceMemory>(ctx_, slot_size_);
+  ARROW_RETURN_NOT_OK(device_memory_->Preallocate(configuration_->max_preallocate_memzones()));
+  for (std::uint16_t qp = 0; qp < num_qps(); ++qp) {
+    auto m = std::make_unique<internal::QueuePairMemory>();
+    m->ctx = ctx_;
+    BITAR_ABI(bitar_hip_stream(ctx_, qp, &m->stream), "queue pair stream");
+    ARROW_RETURN_NOT_OK(m->Tables(1024));
+    qp_memory_.push_back(std::move(m));
+  }
+  return arrow::Status::OK();
+}
+
+template <typename Class, typename Enable>
+arrow::Status CompressDevice<Class, Enable>::EntryGuard(std::uint16_t queue_pair_id) {
+  if (ARROW_PREDICT_FALSE(state_ != internal::DeviceState::kStarted)) {
+    return arrow::Status::Invalid("Compress device ", +device_id_,
+                                  " has not started. [Current state: ",
+                                  static_cast<int>(state_), "]");
+  }
+  if (ARROW_PREDICT_FALSE(queue_pair_id >= num_qps())) {
+    return arrow::Status::Invalid("queue_pair_id must be in the range of [0, ", num_qps(), ")");
+  }
+  bool expected = false;  // atomic, unlike the reference's pending-ops hint (device.cc:456)
+  if (!qp_memory_[queue_pair_id]->busy.compare_exchange_strong(expected, true)) {
+    return arrow::Status::Cancelled("Queue pair ", queue_pair_id, " of compress device ",
+                                    +device_id_, " is busy");
+  }
+  return arrow::Status::OK();
+}
+
+template <typename Class, typename Enable>
+void CompressDevice<Class, Enable>::Leave(std::uint16_t queue_pair_id) {
+  qp_memory_[queue_pair_id]->busy.store(false);
+}
+
+template <typename Class, typename Enable>
+void* CompressDevice<Class, Enable>::stream(std::uint16_t queue_pair_id) const {
+  return queue_pair_id < qp_memory_.size() ? qp_memory_[queue_pair_id]->stream : nullptr;
+}
+
+template <typename Class, typename Enable>
+arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
+    std::uint16_t queue_pair_id, const std::shared_ptr<arrow::Buffer>& decompressed_buffer) {
+  BufferVector compressed_buffers;
+  if (ARROW_PREDICT_FALSE(decompressed_buffer == nullptr || decompressed_buffer->size() == 0)) {
+    return compressed_buffers;  // reference device.cc:161-164
+  }
+  ARROW_RETURN_NOT_OK(EntryGuard(queue_pair_id));
+  auto* m = qp_memory_[queue_pair_id].get();
+  struct Guard {
+    CompressDevice* d;
+    std::uint16_t qp;
+    ~Guard() { d->Leave(qp); }
+  } guard{this, queue_pair_id};
+
+  const std::uint32_t seg = configuration_->decompressed_seg_size();
+  const auto n = static_cast<std::uint64_t>(decompressed_buffer->size());
+  const auto nseg = static_cast<std::uint32_t>((n + seg - 1) / seg);
+  const auto codec = internal::AbiCodec(configuration_->codec());
+
+  // input: read HBM in place, else stage it (the reference attaches it zero-copy, 380-399)
+  const void* d_in = reinterpret_cast<const void*>(decompressed_buffer->address());
+  if (!internal::OnDevice(*decompressed_buffer, device_id_)) {
+    ARROW_RETURN_NOT_OK(m->Stage(n));
+    BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_stage, d_in, n, m->stream), "stage input");
+    d_in = m->d_stage;
+  }
+
+  std::vector<std::uint8_t*> slots;
+  ARROW_RETURN_NOT_OK(device_memory_->Take(nseg, &slots));
+  auto release = [&](const arrow::Status& st) {  // ReleaseAll (device.cc:537-542)
+    device_memory_->PutAll(slots);
+    return st;
+  };
+  auto st = m->Tables(nseg);
+  if (!st.ok()) return release(st);
+  for (std::uint32_t i = 0; i < nseg; ++i)
+    m->h_ptrs[i] = static_cast<std::uint64_t>(reinterpret_cast<uintptr_t>(slots[i]));
+  int rc = bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 8ull * nseg, m->stream);
+  if (rc == 0)
+    rc = bitar_hip_compress_scattered(ctx_, m->stream, codec, d_in, n, seg,
+                                      reinterpret_cast<void* const*>(m->d_ptrs), slot_size_,
+                                      m->d_sizes);
+  if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sizes, m->d_sizes, 4ull * nseg, m->stream);
+  if (rc == 0) rc = bitar_hip_sync(ctx_, m->stream);
+  if (rc != 0) {
+    return release(internal::FromAbi(
+        rc, "Failed to compress via queue pair " + std::to_string(queue_pair_id) +
+                " of compress device " + std::to_string(device_id_)));
+  }
+  auto mm = hip_memory_manager(device_id_);
+  compressed_buffers.reserve(nseg);
+  for (std::uint32_t i = 0; i < nseg; ++i) {
+    if (m->h_sizes[i] == BITAR_HIP_SEGMENT_ERROR)
+      return release(arrow::Status::IOError("Compress data output is larger than allocated buffer"));
+    compressed_buffers.emplace_back(std::make_unique<arrow::Buffer>(slots[i], m->h_sizes[i], mm));
+  }
+  return compressed_buffers;
+}
+
+template <typename Class, typename Enable>
+arrow::Status CompressDevice<Class, Enable>::Decompress(
+    std::uint16_t queue_pair_id, const BufferVector& compressed_buffers,
+    const std::unique_ptr<arrow::ResizableBuffer>& decompressed_buffer) {
+  if (ARROW_PREDICT_FALSE(compressed_buffers.empty())) return arrow::Status::OK();
+  const std::uint32_t seg = configuration_->decompressed_seg_size();
+  const auto min_capacity = static_cast<std::int64_t>(compressed_buffers.size() * seg);
+  if (decompressed_buffer == nullptr || decompressed_buffer->capacity() < min_capacity) {
+    return arrow::Status::CapacityError("The decompressed_buffer is required to be >= ",
+                                        min_capacity, " bytes");  // device.cc:248-254
+  }
+  ARROW_RETURN_NOT_OK(EntryGuard(queue_pair_id));
+  auto* m = qp_memory_[queue_pair_id].get();
+  struct Guard {
+    CompressDevice* d;
+    std::uint16_t qp;
+    ~Guard() { d->Leave(qp); }
+  } guard{this, queue_pair_id};
+
+  const auto nseg = static_cast<std::uint32_t>(compressed_buffers.size());
+  const auto codec = internal::AbiCodec(configuration_->codec());
+  ARROW_RETURN_NOT_OK(m->Tables(nseg));
+
+  // sources: HBM buffers in place; host buffers staged behind the output area
+  std::uint64_t host_bytes = 0;
+  std::vector<bool> on_dev(nseg);
+  for (std::uint32_t i = 0; i < nseg; ++i) {
+    on_dev[i] = internal::OnDevice(*compressed_buffers[i], device_id_);
+    if (!on_dev[i]) host_bytes += (static_cast<std::uint64_t>(compressed_buffers[i]->size()) + 15) & ~15ull;
+  }
+  const auto out_addr = decompressed_buffer->mutable_address();
+  const bool out_on_dev = internal::OnDevice(out_addr, device_id_);
+  const std::uint64_t out_bytes = out_on_dev ? 0 : static_cast<std::uint64_t>(min_capacity);
+  if (host_bytes + out_bytes) ARROW_RETURN_NOT_OK(m->Stage(host_bytes + out_bytes));
+  auto* stage = static_cast<std::uint8_t*>(m->d_stage);
+  std::uint64_t off = out_bytes;
+  for (std::uint32_t i = 0; i < nseg; ++i) {
+    const auto& b = compressed_buffers[i];
+    m->h_sizes[i] = static_cast<std::uint32_t>(b->size());
+    if (on_dev[i]) {
+      m->h_ptrs[i] = b->address();
+    } else {
+      BITAR_ABI(bitar_hip_memcpy(ctx_, stage + off, reinterpret_cast<const void*>(b->address()),
+                                 static_cast<std::uint64_t>(b->size()), m->stream),
+                "stage compressed input");
+      m->h_ptrs[i] = reinterpret_cast<std::uint64_t>(stage + off);
+      off += (static_cast<std::uint64_t>(b->size()) + 15) & ~15ull;
+    }
+  }
+  void* d_out = out_on_dev ? reinterpret_cast<void*>(out_addr) : m->d_stage;
+  BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 8ull * nseg, m->stream), "tables");
+  BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_sizes, m->h_sizes, 4ull * nseg, m->stream), "tables");
+  int rc = bitar_hip_decompress(ctx_, m->stream, codec,
+                                reinterpret_cast<const void* const*>(m->d_ptrs), m->d_sizes,
+                                nseg, seg, d_out, static_cast<std::uint64_t>(min_capacity),
+                                m->d_prod);
+  if (rc == 0)
+    rc = bitar_hip_memcpy(ctx_, m->h_sizes, m->d_prod, 4ull * nseg, m->stream);
+  if (rc == 0 && !out_on_dev)
+    rc = bitar_hip_memcpy(ctx_, reinterpret_cast<void*>(out_addr), d_out,
+                          static_cast<std::uint64_t>(min_capacity), m->stream);
+  if (rc == 0) rc = bitar_hip_sync(ctx_, m->stream);
+  if (rc != 0) {
+    return internal::FromAbi(rc, "Failed to decompress via queue pair " +
+                                     std::to_string(queue_pair_id) + " of compress device " +
+                                     std::to_string(device_id_));
+  }
+  std::int64_t total = 0;
+  for (std::uint32_t i = 0; i < nseg; ++i) {
+    if (m->h_sizes[i] == BITAR_HIP_SEGMENT_ERROR)
+      return arrow::Status::IOError("Some operations have failed");
+    total += m->h_sizes[i];
+  }
+  // Don't shrink the buffer (reference device.cc:312-315)
+  ARROW_UNUSED(decompressed_buffer->Resize(total, false));
+  return arrow::Status::OK();
+}
+
+template <typename Class, typename Enable>
+std::size_t CompressDevice<Class, Enable>::Recycle(const BufferVector& buffers) {
+  std::size_t count = 0;
+  if (!device_memory_) return 0;
+  for (auto it = std::crbegin(buffers); it != std::crend(buffers); ++it)
+    count += device_memory_->Put(reinterpret_cast<const std::uint8_t*>((*it)->address()));
+  return count;
+}
+
+template <typename Class, typename Enable>
+CompressDevice<Class, Enable>::~CompressDevice() {
+  qp_memory_.clear();
+  device_memory_.reset();
+  if (ctx_) bitar_hip_close(ctx_);
+  ctx_ = nullptr;
+  set_state(internal::DeviceState::kUndefined);
+}
+
+template <typename Class, typename Enable>
+CompressDevice<Class, Enable>::CompressDevice(std::uint8_t device_id,
+                                              std::vector<std::uint32_t> worker_lcores)
+    : device_id_(device_id), worker_lcores_(std::move(worker_lcores)) {}
+
+template <typename Class, typename Enable>
+arrow::Status CompressDevice<Class, Enable>::ValidateConfiguration() {
+  // device capabilities: <= 64 queue pairs, no chained segments, window 2^15 (DEFLATE) or
+  // 2^16 (LZ4), fixed Huffman (reference device.cc:352-415)
+  constexpr std::uint16_t kMaxQueuePairs = 64;
+  if (num_qps() == 0 || num_qps() > kMaxQueuePairs) {
+    return arrow::Status::Invalid("The requested number of queue pairs (", num_qps(),
+                                  ") exceeds the maximum (", kMaxQueuePairs,
+                                  ") allowed for device ", +device_id_);
+  }
+  if (configuration_->burst_size() == 0)
+    return arrow::Status::Invalid("Burst size must be greater than 0");
+  if (configuration_->codec() != Codec::DEFLATE && configuration_->codec() != Codec::LZ4)
+    return arrow::Status::NotImplemented("Compress device ", +device_id_,
+                                         " does not support the codec");
+  if (configuration_->max_sgl_segs() < 1) configuration_->set_max_sgl_segs(1);
+  if (configuration_->max_sgl_segs() > 1)
+    return arrow::Status::Invalid("Compress device does not support chained mbufs.");
+  if (configuration_->decompressed_seg_size() < internal::kMinSegSize ||
+      configuration_->decompressed_seg_size() > internal::kMaxSegSize32) {
+    return arrow::Status::Invalid("decompressed_seg_size is not in the range of [",
+                                  internal::kMinSegSize, ", ", internal::kMaxSegSize32, "]");
+  }
+  const std::uint8_t window = configuration_->codec() == Codec::LZ4 ? 16 : 15;
+  if (configuration_->window_size() == 0) {
+    configuration_->set_window_size(window);
+  } else if (configuration_->window_size() != window) {
+    return arrow::Status::Invalid("window_size is not in the range of [", +window, ", ",
+                                  +window, "]");
+  }
+  if (configuration_->codec() == Codec::DEFLATE &&
+      configuration_->huffman_enc() == HuffmanEncoding::DYNAMIC) {
+    return arrow::Status::Invalid("Compress device does not supported dynamic Huffman");
+  }
+  if (configuration_->max_preallocate_memzones() < internal::kMinPreallocateSlots) {
+    return arrow::Status::Invalid("max_preallocate_memzones (",
+                                  configuration_->max_preallocate_memzones(),
+                                  ") is not in the range of [", internal::kMinPreallocateSlots,
+                                  ", ", internal::kMaxPreallocateSlots, "]");
+  }
+  return arrow::Status::OK();
+}
+
+template <typename Class, typename Enable>
+arrow::Status CompressDevice<Class, Enable>::set_configuration(
+    std::unique_ptr<Configuration<Class>> configuration) {
+  if (!configuration) return arrow::Status::Invalid("null configuration");
+  configuration_ = std::move(configuration);
+  return arrow::Status::OK();
+}
+
+template class CompressDevice<Class_HIP_GFX950>;
+
+DeviceManager* DeviceManager::Instance() {
+  static DeviceManager instance;
+  return &instance;
+}
+
+template <>
+arrow::Result<HipGfx950CompressDevice*> DeviceManager::Create<Class_HIP_GFX950>(
+    std::uint8_t device_id, std::vector<std::uint32_t> worker_lcores) {
+  return new HipCompressDevice(device_id, std::move(worker_lcores));
+}
+
+arrow::Status HipCompressDevice::ValidateConfiguration() {
+  const auto* hip_configuration = dynamic_cast<HipConfiguration*>(configuration().get());
+  if (ARROW_PREDICT_FALSE(hip_configuration == nullptr))
+    return arrow::Status::Invalid("Invalid configuration for HipCompressDevice");
+  if (hip_configuration->checksum_type() != ChecksumType::NONE)
+    return arrow::Status::NotImplemented("checksum type ",
+                                         ToString(hip_configuration->checksum_type()),
+                                         " is not supported by compress device of type ",
+                                         kHipConfigurationTypeName);
+  return HipGfx950CompressDevice::ValidateConfiguration();
+}
+
+arrow::Status HipCompressDevice::set_configuration(
+    std::unique_ptr<Configuration<Class_HIP_GFX950>> configuration) {
+  if (!configuration) return arrow::Status::Invalid("null configuration");
+  if (configuration->type_name() != kHipConfigurationTypeName) {
+    return arrow::Status::Invalid("Configuration of type ", configuration->type_name(),
+                                  " cannot be applied to compress device of type ",
+                                  kHipConfigurationTypeName);
+  }
+  return HipGfx950CompressDevice::set_configuration(std::move(configuration));
+}
+
+}  // namespace bitar

@@ -373,8 +373,8 @@ __device__ __forceinline__ void parse(const uint8_t* in, uint32_t n, const uint8
 
 __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
-    uint8_t* __restrict__ slab, uint64_t slot_stride, uint32_t* __restrict__ sizes,
-    uint32_t* __restrict__ err) {
+    uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
+    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
   using namespace cmp;
   __shared__ __attribute__((aligned(16))) uint32_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf];
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
   Lz4Out o;
   o.ring = obuf;
-  o.dst = slab + (uint64_t)i_seg * slot_stride;
+  o.dst = dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride;
   o.cap = slot_stride;
   o.op = 0;
   o.flushed = 0;
@@ -399,8 +399,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
 
 __global__ __launch_bounds__(64) void deflate_compress_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
-    uint8_t* __restrict__ slab, uint64_t slot_stride, uint32_t* __restrict__ sizes,
-    uint32_t* __restrict__ err) {
+    uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
+    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
   using namespace cmp;
   __shared__ __attribute__((aligned(16))) uint32_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint32_t stage[kBitWords];
@@ -411,7 +411,7 @@ __global__ __launch_bounds__(64) void deflate_compress_kernel(
   for (uint32_t k = lane_id(); k < kBitWords; k += kWave) stage[k] = 0;
   DflOut o;
   o.stage = stage;
-  o.dst = reinterpret_cast<uint32_t*>(slab + (uint64_t)i_seg * slot_stride);
+  o.dst = reinterpret_cast<uint32_t*>(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
   o.cap = slot_stride;
   o.bits = 0;
   o.wflushed = 0;

@@ -15,12 +15,12 @@
 
 namespace bitar_hip {
 __global__ void lz4_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
-                                    uint32_t*, uint32_t*);
+                                    uint8_t* const*, uint32_t*, uint32_t*);
 __global__ void lz4_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                       const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
                                       uint32_t*);
 __global__ void deflate_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
-                                        uint32_t*, uint32_t*);
+                                        uint8_t* const*, uint32_t*, uint32_t*);
 __global__ void inflate_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
                                uint32_t*);
@@ -203,31 +203,68 @@ int bitar_hip_memcpy(bitar_hip_ctx* ctx, void* dst, const void* src, uint64_t by
   return 0;
 }
 
-int bitar_hip_compress(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const void* d_in,
-                       uint64_t n, uint32_t seg, void* d_slab, uint64_t slot_stride,
-                       uint32_t* d_sizes) {
+static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const void* d_in,
+                         uint64_t n, uint32_t seg, void* d_slab, uint64_t slot_stride,
+                         void* const* d_dsts, uint32_t* d_sizes) {
   if (int r = enter(ctx)) return r;
   if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE)
     return fail(BITAR_HIP_NOT_IMPLEMENTED, "unknown codec");
   if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
   if (n == 0) return 0;  // empty input -> no segments (reference device.cc:161-164)
-  if (!d_in || !d_slab || !d_sizes) return fail(BITAR_HIP_INVALID, "null buffer");
+  if (!d_in || (!d_slab && !d_dsts) || !d_sizes) return fail(BITAR_HIP_INVALID, "null buffer");
   if (slot_stride < bitar_hip_slot_size(codec, seg))
-    return fail(BITAR_HIP_INVALID, "slot_stride below the worst-case bound");
-  if (((uintptr_t)d_slab & 15u) != 0 || (slot_stride & 15u) != 0)
+    return fail(BITAR_HIP_INVALID, "slot size below the worst-case bound");
+  if (d_slab && (((uintptr_t)d_slab & 15u) != 0 || (slot_stride & 15u) != 0))
     return fail(BITAR_HIP_INVALID, "d_slab and slot_stride must be 16-B aligned");
   const uint64_t nseg = (n + seg - 1) / seg;
   if (nseg > 0x7FFFFFFFull) return fail(BITAR_HIP_INVALID, "too many segments");
   hipStream_t s = pick_stream(ctx, stream);
   const auto* in = static_cast<const uint8_t*>(d_in);
   auto* slab = static_cast<uint8_t*>(d_slab);
+  auto* dsts = reinterpret_cast<uint8_t* const*>(d_dsts);
   if (codec == BITAR_HIP_CODEC_LZ4)
     hipLaunchKernelGGL(bitar_hip::lz4_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
-                       n, seg, slab, slot_stride, d_sizes, ctx->d_err);
+                       n, seg, slab, slot_stride, dsts, d_sizes, ctx->d_err);
   else
     hipLaunchKernelGGL(bitar_hip::deflate_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
-                       in, n, seg, slab, slot_stride, d_sizes, ctx->d_err);
+                       in, n, seg, slab, slot_stride, dsts, d_sizes, ctx->d_err);
   HIP_TRY(hipGetLastError(), "compress launch");
+  return 0;
+}
+
+int bitar_hip_compress(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const void* d_in,
+                       uint64_t n, uint32_t seg, void* d_slab, uint64_t slot_stride,
+                       uint32_t* d_sizes) {
+  if (n && !d_slab) return fail(BITAR_HIP_INVALID, "null d_slab");
+  return compress_impl(ctx, stream, codec, d_in, n, seg, d_slab, slot_stride, nullptr, d_sizes);
+}
+
+int bitar_hip_compress_scattered(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
+                                 const void* d_in, uint64_t n, uint32_t seg,
+                                 void* const* d_dsts, uint64_t slot_capacity, uint32_t* d_sizes) {
+  if (n && !d_dsts) return fail(BITAR_HIP_INVALID, "null d_dsts");
+  return compress_impl(ctx, stream, codec, d_in, n, seg, nullptr, slot_capacity, d_dsts,
+                       d_sizes);
+}
+
+int bitar_hip_pointer_info(const void* ptr, int* kind, int* device) {
+  if (!kind || !device) return fail(BITAR_HIP_INVALID, "null argument");
+  *kind = 0;
+  *device = -1;
+  if (!ptr) return 0;
+  hipPointerAttribute_t a;
+  hipError_t e = hipPointerGetAttributes(&a, ptr);
+  if (e != hipSuccess) {  // unknown to HIP: ordinary pageable host memory
+    (void)hipGetLastError();
+    return 0;
+  }
+  if (a.type == hipMemoryTypeDevice) {
+    *kind = 2;
+    *device = a.device;
+  } else if (a.type == hipMemoryTypeHost) {
+    *kind = 1;
+    *device = a.device;
+  }
   return 0;
 }
 

@@ -102,6 +102,14 @@ int bitar_hip_compress(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const v
                        uint64_t n, uint32_t seg, void* d_slab, uint64_t slot_stride,
                        uint32_t* d_sizes);
 
+/* Same, but segment i goes to its own slot d_dsts[i] (a device array of device pointers,
+ * each 16-B aligned with room for slot_capacity >= bitar_hip_slot_size(codec, seg) bytes).
+ * The form the slot pool of the C++ front-end uses: its free slots are not contiguous
+ * (DeviceMemory::Take, reference src/memory.cc:160-189). */
+int bitar_hip_compress_scattered(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
+                                 const void* d_in, uint64_t n, uint32_t seg,
+                                 void* const* d_dsts, uint64_t slot_capacity, uint32_t* d_sizes);
+
 /* Decompress nseg segments.  d_srcs[i] (a device array of device pointers) holds
  * d_sizes[i] compressed bytes; segment i inflates into d_out + i*seg and d_produced[i]
  * receives its size.  Requires capacity >= nseg*seg, else BITAR_HIP_CAPACITY_ERROR
@@ -134,6 +142,10 @@ int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_
  * 0 random, 1 Silesia-style mix, 2 Arrow record-batch body, 3 constant, 4 periodic). */
 int bitar_hip_fill(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed, void* d_out,
                    uint64_t n);
+
+/* Where `ptr` lives: *kind = 0 pageable host, 1 pinned host, 2 device memory (then *device
+ * is its ordinal).  Replaces rte_mem_virt2iova() residency assumptions (memory.cc:388). */
+int bitar_hip_pointer_info(const void* ptr, int* kind, int* device);
 
 /* Thread-local text of the last error returned on this thread. */
 const char* bitar_hip_last_error(void);

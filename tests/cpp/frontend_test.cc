@@ -1,0 +1,240 @@
+// frontend_test.cc -- tests of the bitar C++ front-end (namespace bitar) on MI355X.
+//
+// Modes: `cpu` (no GPU needed: configuration rules, discovery errors) and `gpu <in> <outdir>`
+// (Compress/Decompress/Recycle/async through real devices; compressed segments are written
+// to <outdir> so the Python side can check them with zlib / liblz4).  Mirrors the reference's
+// only behavioural checks (apps/demo_app.cc:288-290, 500-501, 534-543, 671-686).
+#include <arrow/buffer.h>
+#include <arrow/memory_pool.h>
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "bitar/bitar.h"
+
+namespace {
+
+int g_failures = 0;
+#define CHECK(cond)                                                           \
+  do {                                                                        \
+    if (!(cond)) {                                                            \
+      std::cerr << __FILE__ << ":" << __LINE__ << " CHECK failed: " #cond "\n"; \
+      ++g_failures;                                                           \
+    }                                                                         \
+  } while (0)
+#define CHECK_OK(expr)                                                                 \
+  do {                                                                                 \
+    auto _s = (expr);                                                                  \
+    if (!_s.ok()) {                                                                    \
+      std::cerr << __FILE__ << ":" << __LINE__ << " not OK: " << _s.ToString() << "\n"; \
+      ++g_failures;                                                                    \
+    }                                                                                  \
+  } while (0)
+
+std::unique_ptr<bitar::HipConfiguration> MakeConfig(bitar::Codec codec, std::uint32_t seg) {
+  auto c = std::make_unique<bitar::HipConfiguration>(bitar::HipConfiguration::Defaults());
+  c->set_codec(codec);
+  c->set_decompressed_seg_size32(seg);
+  c->set_burst_size(32);
+  c->set_max_preallocate_memzones(64);
+  return c;
+}
+
+void CpuTests() {
+  // slot sizing rule of the reference (config.cc:59-73)
+  bitar::HipConfiguration c;
+  c.set_decompressed_seg_size(2048);
+  CHECK(c.compressed_seg_size() == 4096);
+  c.set_decompressed_seg_size(59460);
+  CHECK(c.compressed_seg_size() == 65406);
+  c.set_decompressed_seg_size(32768);
+  CHECK(c.compressed_seg_size() == 36044);
+  c.set_decompressed_seg_size(16384);
+  CHECK(c.compressed_seg_size() == 32768);
+  CHECK(bitar::internal::kMaxSegSize == 59460);
+  CHECK(c.ToString().find("checksum_type: NONE") != std::string::npos);
+  CHECK(c.type_name() == bitar::kHipConfigurationTypeName);
+  // memory pools exist and the reference names alias the HIP ones
+  CHECK(bitar::GetMemoryPool(bitar::MemoryPoolBackend::Rtememzone) ==
+        bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipDevice));
+  CHECK(bitar::GetMemoryPool(bitar::MemoryPoolBackend::System) != nullptr);
+  uint8_t* p = nullptr;
+  CHECK_OK(bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipDevice)->Allocate(0, 64, &p));
+  CHECK(p != nullptr);  // zero-size sentinel, no device needed
+}
+
+std::vector<uint8_t> ReadFile(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  return std::vector<uint8_t>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+void WriteSegments(const std::string& path, const bitar::BufferVector& bufs) {
+  // [u32 size][bytes]... via Arrow's device -> CPU copy
+  std::ofstream f(path, std::ios::binary);
+  for (const auto& b : bufs) {
+    auto view = std::make_shared<arrow::Buffer>(reinterpret_cast<const uint8_t*>(b->address()),
+                                                b->size(), b->memory_manager());
+    auto copied = arrow::Buffer::Copy(view, arrow::default_cpu_memory_manager());
+    if (!copied.ok()) {
+      std::cerr << "copy failed: " << copied.status().ToString() << "\n";
+      ++g_failures;
+      return;
+    }
+    const uint32_t sz = static_cast<uint32_t>(b->size());
+    f.write(reinterpret_cast<const char*>(&sz), 4);
+    f.write(reinterpret_cast<const char*>((*copied)->data()), sz);
+  }
+}
+
+void GpuTests(const std::string& input_path, const std::string& outdir) {
+  auto* driver = bitar::CompressDriver<bitar::Class_HIP_GFX950>::Instance();
+  auto ids = driver->ListAvailableDeviceIds();
+  CHECK_OK(ids.status());
+  if (!ids.ok()) return;
+  driver->set_num_workers(2);
+  auto devs = driver->GetDevices({(*ids)[0]});
+  CHECK_OK(devs.status());
+  if (!devs.ok()) return;
+  CHECK(devs->size() == 1 && (*devs)[0]->num_qps() == 2);
+  CHECK((*devs)[0]->LcoreOf(0) == 1 && (*devs)[0]->LcoreOf(1) == 2);
+  auto bad = driver->GetDevices({200});
+  CHECK(bad.status().IsInvalid());
+
+  const auto data = ReadFile(input_path);
+  CHECK(data.size() > 100000);
+  auto host_in = std::make_shared<arrow::Buffer>(data.data(), static_cast<int64_t>(data.size()));
+
+  for (auto codec : {bitar::Codec::DEFLATE, bitar::Codec::LZ4}) {
+    const std::uint32_t seg = codec == bitar::Codec::DEFLATE ? 59460 : 65536;
+    auto& dev = (*devs)[0];
+    // not initialized yet -> Invalid (EntryGuard, device.cc:446-451)
+    if (codec == bitar::Codec::DEFLATE) CHECK(dev->Compress(0, host_in).status().IsInvalid());
+    // wrong configuration type is rejected
+    // (a fresh device per codec: the reference initializes a device once)
+    auto fresh = driver->GetDevices({(*ids)[0]});
+    CHECK_OK(fresh.status());
+    auto& d = (*fresh)[0];
+    auto cfg = MakeConfig(codec, seg);
+    if (codec == bitar::Codec::DEFLATE) {
+      auto dyn = MakeConfig(codec, seg);
+      dyn->set_huffman_enc(bitar::HuffmanEncoding::DYNAMIC);
+      auto tmp = driver->GetDevices({(*ids)[0]});
+      CHECK((*tmp)[0]->Initialize(std::move(dyn)).IsInvalid());
+    }
+    CHECK_OK(d->Initialize(std::move(cfg)));
+    CHECK(d->Compress(5, host_in).status().IsInvalid());  // qp out of range
+
+    // sync round trip from a HOST buffer (staged to HBM by the device)
+    auto comp = d->Compress(0, host_in);
+    CHECK_OK(comp.status());
+    if (!comp.ok()) continue;
+    const auto nseg = (data.size() + seg - 1) / seg;
+    CHECK(comp->size() == nseg);
+    for (const auto& b : *comp) CHECK(!b->is_cpu());
+    WriteSegments(outdir + (codec == bitar::Codec::DEFLATE ? "/deflate.segs" : "/lz4.segs"), *comp);
+
+    auto out = arrow::AllocateResizableBuffer(static_cast<int64_t>(nseg * seg));
+    CHECK_OK(out.status());
+    std::unique_ptr<arrow::ResizableBuffer> host_out = std::move(*out);
+    CHECK_OK(d->Decompress(1, *comp, host_out));
+    CHECK(host_out->size() == static_cast<int64_t>(data.size()));
+    CHECK(std::memcmp(host_out->data(), data.data(), data.size()) == 0);
+
+    // capacity rule (device.cc:248-254)
+    // (Arrow pads capacities to 64 B, so stay a full pad below the requirement)
+    auto small = arrow::AllocateResizableBuffer(static_cast<int64_t>(nseg * seg - 128));
+    std::unique_ptr<arrow::ResizableBuffer> small_out = std::move(*small);
+    CHECK(d->Decompress(0, *comp, small_out).IsCapacityError());
+
+    // HBM-resident input and output (no staging), via the Arrow device API
+    auto dev_in = arrow::Buffer::Copy(host_in, bitar::hip_memory_manager(0));
+    CHECK_OK(dev_in.status());
+    auto comp2 = d->Compress(0, *dev_in);
+    CHECK_OK(comp2.status());
+    auto dev_out = bitar::AllocateResizableDeviceBuffer(static_cast<int64_t>(nseg * seg), 0);
+    CHECK_OK(dev_out.status());
+    std::unique_ptr<arrow::ResizableBuffer> dout = std::move(*dev_out);
+    CHECK_OK(d->Decompress(0, *comp2, dout));
+    CHECK(!dout->is_cpu() && dout->size() == static_cast<int64_t>(data.size()));
+    auto back = arrow::Buffer::Copy(std::shared_ptr<arrow::Buffer>(std::move(dout)),
+                                    arrow::default_cpu_memory_manager());
+    CHECK_OK(back.status());
+    if (back.ok()) CHECK(std::memcmp((*back)->data(), data.data(), data.size()) == 0);
+
+    // corrupted stream -> IOError (per-op status, device.cc:512-520)
+    {
+      auto bogus = std::make_shared<arrow::Buffer>(reinterpret_cast<const uint8_t*>("\x07\x07\x07\x07"), 4);
+      bitar::BufferVector bv;
+      bv.emplace_back(std::make_unique<arrow::Buffer>(bogus->data(), 4));
+      auto o = arrow::AllocateResizableBuffer(seg);
+      std::unique_ptr<arrow::ResizableBuffer> ob = std::move(*o);
+      if (codec == bitar::Codec::DEFLATE) CHECK(d->Decompress(0, bv, ob).IsIOError());
+    }
+
+    // async on both queue pairs (CompressAsync / WaitLcore, util.h:216-236)
+    int calls = 0;
+    bitar::BufferVector async_out[2];
+    auto cb = [&](std::uint8_t, std::uint16_t qp, arrow::Result<bitar::BufferVector>&& r) {
+      ++calls;
+      if (!r.ok()) return 1;
+      async_out[qp] = std::move(r).ValueUnsafe();
+      return bitar::kAsyncReturnOK;
+    };
+    using Param = bitar::CompressParam<bitar::Class_HIP_GFX950, decltype(cb)>;
+    auto p0 = std::make_unique<Param>(d, 0, host_in, cb);
+    auto p1 = std::make_unique<Param>(d, 1, *dev_in, cb);
+    CHECK(bitar::CompressAsync(p0) == 0);
+    CHECK(bitar::CompressAsync(p1) == 0);
+    CHECK(bitar::WaitLcore(d->LcoreOf(0)) == bitar::kAsyncReturnOK);
+    CHECK(bitar::WaitLcore(d->LcoreOf(1)) == bitar::kAsyncReturnOK);
+    CHECK(calls == 2);
+    auto dcb = [&](std::uint8_t, std::uint16_t, const arrow::Status& s) {
+      return s.ok() ? bitar::kAsyncReturnOK : 1;
+    };
+    auto o2 = arrow::AllocateResizableBuffer(static_cast<int64_t>(nseg * seg));
+    std::unique_ptr<arrow::ResizableBuffer> aout = std::move(*o2);
+    using DParam = bitar::DecompressParam<bitar::Class_HIP_GFX950, decltype(dcb)>;
+    auto dp = std::make_unique<DParam>(d, 1, async_out[0], aout, dcb);
+    CHECK(bitar::DecompressAsync(dp) == 0);
+    CHECK(bitar::WaitLcore(d->LcoreOf(1)) == bitar::kAsyncReturnOK);
+    CHECK(aout->size() == static_cast<int64_t>(data.size()) &&
+          std::memcmp(aout->data(), data.data(), data.size()) == 0);
+
+    // Recycle returns every slot exactly once (demo_app.cc:288-290)
+    CHECK(d->Recycle(*comp) == comp->size());
+    CHECK(d->Recycle(*comp) == 0);
+    CHECK(d->Recycle(*comp2) == comp2->size());
+    CHECK(d->Recycle(async_out[0]) == async_out[0].size());
+    CHECK(d->Recycle(async_out[1]) == async_out[1].size());
+  }
+  // empty input -> empty vector (device.cc:161-164); empty vector -> OK
+  auto& d0 = (*devs)[0];
+  CHECK_OK(d0->Initialize(MakeConfig(bitar::Codec::LZ4, 65536)));
+  auto empty = d0->Compress(0, std::make_shared<arrow::Buffer>(nullptr, 0));
+  CHECK(empty.ok() && empty->empty());
+  std::unique_ptr<arrow::ResizableBuffer> none;
+  CHECK_OK(d0->Decompress(0, bitar::BufferVector{}, none));
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::string mode = argc > 1 ? argv[1] : "cpu";
+  CpuTests();
+  if (mode == "cpu") {
+    // no GPU in the build container: discovery must fail cleanly, not crash
+    auto ids = bitar::CompressDriver<bitar::Class_HIP_GFX950>::Instance()->ListAvailableDeviceIds();
+    if (!ids.ok()) CHECK(ids.status().IsInvalid());
+  } else if (argc >= 4) {
+    GpuTests(argv[2], argv[3]);
+  } else {
+    std::cerr << "usage: frontend_test cpu | gpu <input> <outdir>\n";
+    return 2;
+  }
+  std::cout << (g_failures ? "FAILED " : "PASSED ") << g_failures << " failures\n";
+  return g_failures ? 1 : 0;
+}
