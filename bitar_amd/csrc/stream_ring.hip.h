@@ -36,10 +36,11 @@ struct State {
   uint32_t wlen;       // bytes of the stream covered by win: [wb, wb + wlen) ∩ segment
 };
 
-// Stage stream bytes around absolute position `pos` into win.  Blocks that hold no byte of
-// the segment are skipped (never read: every read is bounds-checked against csize first).
-__device__ __forceinline__ void refill(State& s, uint8_t* win, uint32_t pos) {
-  const uint64_t a = (uint64_t)(uintptr_t)(s.src + pos) & ~(uint64_t)15;
+// Stage the stream bytes starting at absolute address `abs` (rounded down to 16 B) into
+// win.  Blocks that hold no byte of the segment are skipped (never read: every read is
+// bounds-checked against csize first).
+__device__ __forceinline__ void refill_abs(State& s, uint8_t* win, uint64_t abs) {
+  const uint64_t a = abs & ~(uint64_t)15;
   const uint64_t lo = (uint64_t)(uintptr_t)s.src, hi = lo + s.csize;
   const uint32_t lane = lane_id();
 #pragma unroll
@@ -54,11 +55,20 @@ __device__ __forceinline__ void refill(State& s, uint8_t* win, uint32_t pos) {
   s.wb = a;
 }
 
+__device__ __forceinline__ void refill(State& s, uint8_t* win, uint32_t pos) {
+  refill_abs(s, win, (uint64_t)(uintptr_t)(s.src + pos));
+}
+
+// window index of absolute address abs, refilling so that [abs, abs+need) is staged
+// (need <= kWin - 15)
+__device__ __forceinline__ uint32_t win_at_abs(State& s, uint8_t* win, uint64_t abs, uint32_t need) {
+  if (abs < s.wb || abs + need > s.wb + kWin) refill_abs(s, win, abs);
+  return (uint32_t)(abs - s.wb);
+}
+
 // window-relative index of stream position pos, refilling so that [pos, pos+need) is staged
 __device__ __forceinline__ uint32_t win_at(State& s, uint8_t* win, uint32_t pos, uint32_t need) {
-  const uint64_t abs = (uint64_t)(uintptr_t)(s.src + pos);
-  if (abs < s.wb || abs + need > s.wb + kWin) refill(s, win, pos);
-  return (uint32_t)((uint64_t)(uintptr_t)(s.src + pos) - s.wb);
+  return win_at_abs(s, win, (uint64_t)(uintptr_t)(s.src + pos), need);
 }
 
 __device__ __forceinline__ uint32_t byte_u(State& s, uint8_t* win, uint32_t pos) {

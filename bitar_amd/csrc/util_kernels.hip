@@ -142,13 +142,19 @@ __global__ __launch_bounds__(256) void fill_kernel(int kind, uint64_t seed, uint
       case 3:
         for (int i = 0; i < 8; ++i) w[i] = 0x6161616161616161ull;
         break;
+      case 5:
+        for (int i = 0; i < 8; ++i) w[i] = sm64(seed ^ 0x1111ull, k0 + i) % 1000;
+        break;
+      case 6:
+        text = true;
+        break;
       default:
         for (int b = 0; b < 64; ++b) line[b] = (uint8_t)(((j * 64 + b) % 251) * 7);
         break;
     }
     if (text) {
       log_line(tseed, j, line);
-    } else if (kind >= 0 && kind <= 3) {
+    } else if ((kind >= 0 && kind <= 3) || kind == 5) {
       for (int i = 0; i < 8; ++i)
         for (int b = 0; b < 8; ++b) line[i * 8 + b] = (uint8_t)(w[i] >> (8 * b));
     }

@@ -66,10 +66,56 @@ __device__ __forceinline__ void wave_copy_global(uint8_t* d, const uint8_t* s, u
   const uint4* sa = reinterpret_cast<const uint4*>((uintptr_t)s & ~(uintptr_t)15);
   uint4* da = reinterpret_cast<uint4*>(d);
   if (sh == 0) {
-    for (uint64_t b = lane; b < nb; b += kWave) da[b] = sa[b];
+    uint64_t b = lane;
+    for (; b + 3 * kWave < nb; b += 4 * kWave) {  // 4 KiB per wave in flight
+      const uint4 x0 = sa[b], x1 = sa[b + kWave], x2 = sa[b + 2 * kWave], x3 = sa[b + 3 * kWave];
+      da[b] = x0;
+      da[b + kWave] = x1;
+      da[b + 2 * kWave] = x2;
+      da[b + 3 * kWave] = x3;
+    }
+    for (; b < nb; b += kWave) da[b] = sa[b];
   } else {
     const uint32_t q = sh >> 2, r = sh & 3u;
-    for (uint64_t base = 0; base < nb; base += kWave) {
+    // funnel one 16-B output block from its source block x and the next one y
+    auto emit = [&](uint64_t b, uint4 x, uint4 y) {
+      const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+      uint4 o;
+      switch (q) {  // q is wave-uniform: a scalar branch
+        case 0: o = make_uint4(funnel(w[0], w[1], r), funnel(w[1], w[2], r), funnel(w[2], w[3], r), funnel(w[3], w[4], r)); break;
+        case 1: o = make_uint4(funnel(w[1], w[2], r), funnel(w[2], w[3], r), funnel(w[3], w[4], r), funnel(w[4], w[5], r)); break;
+        case 2: o = make_uint4(funnel(w[2], w[3], r), funnel(w[3], w[4], r), funnel(w[4], w[5], r), funnel(w[5], w[6], r)); break;
+        default: o = make_uint4(funnel(w[3], w[4], r), funnel(w[4], w[5], r), funnel(w[5], w[6], r), funnel(w[6], w[7], r)); break;
+      }
+      da[b] = o;
+    };
+    uint64_t base = 0;
+    // main body: 4 wave-contiguous 1 KiB rows per step (4 KiB in flight per wave); a lane's
+    // next source block comes from lane+1, lane 63 takes lane 0 of the next row
+    auto next = [&](uint4 x, uint4 row_after) {
+      uint4 y;
+      y.x = shfl_down1(x.x);
+      y.y = shfl_down1(x.y);
+      y.z = shfl_down1(x.z);
+      y.w = shfl_down1(x.w);
+      if (lane == kWave - 1) {
+        y.x = readlane(row_after.x, 0);
+        y.y = readlane(row_after.y, 0);
+        y.z = readlane(row_after.z, 0);
+        y.w = readlane(row_after.w, 0);
+      }
+      return y;
+    };
+    for (; base + 4 * kWave <= nb; base += 4 * kWave) {
+      const uint64_t b = base + lane;
+      const uint4 x0 = sa[b], x1 = sa[b + kWave], x2 = sa[b + 2 * kWave], x3 = sa[b + 3 * kWave];
+      const uint4 x4 = lane == 0 ? sa[base + 4 * kWave] : make_uint4(0, 0, 0, 0);  // in bounds
+      emit(b, x0, next(x0, x1));
+      emit(b + kWave, x1, next(x1, x2));
+      emit(b + 2 * kWave, x2, next(x2, x3));
+      emit(b + 3 * kWave, x3, next(x3, x4));
+    }
+    for (; base < nb; base += kWave) {
       const uint64_t b = base + lane;
       const bool act = b < nb;
       uint4 x = act ? sa[b] : make_uint4(0, 0, 0, 0);
@@ -79,16 +125,7 @@ __device__ __forceinline__ void wave_copy_global(uint8_t* d, const uint8_t* s, u
       y.z = shfl_down1(x.z);
       y.w = shfl_down1(x.w);
       if (act && (lane == kWave - 1 || b + 1 == nb)) y = sa[b + 1];  // holds s+16b+15
-      const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-      uint4 o;
-      // q is wave-uniform: the switch is a scalar branch
-      switch (q) {
-        case 0: o = make_uint4(funnel(w[0], w[1], r), funnel(w[1], w[2], r), funnel(w[2], w[3], r), funnel(w[3], w[4], r)); break;
-        case 1: o = make_uint4(funnel(w[1], w[2], r), funnel(w[2], w[3], r), funnel(w[3], w[4], r), funnel(w[4], w[5], r)); break;
-        case 2: o = make_uint4(funnel(w[2], w[3], r), funnel(w[3], w[4], r), funnel(w[4], w[5], r), funnel(w[5], w[6], r)); break;
-        default: o = make_uint4(funnel(w[3], w[4], r), funnel(w[4], w[5], r), funnel(w[5], w[6], r), funnel(w[6], w[7], r)); break;
-      }
-      if (act) da[b] = o;
+      if (act) emit(b, x, y);
     }
   }
   const uint64_t done = nb << 4;

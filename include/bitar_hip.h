@@ -139,7 +139,8 @@ int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_
                    const uint32_t* d_sizes, uint32_t nseg, uint64_t* d_offsets, void* d_frame);
 
 /* Deterministic synthetic input (SplitMix64-based; kinds as in the oracle's bo_fill:
- * 0 random, 1 Silesia-style mix, 2 Arrow record-batch body, 3 constant, 4 periodic). */
+ * 0 random, 1 Silesia-style mix, 2 Arrow record-batch body, 3 constant, 4 periodic,
+ * 5 int64 small-range only, 6 log text only). */
 int bitar_hip_fill(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed, void* d_out,
                    uint64_t n);
 

@@ -643,6 +643,12 @@ static void bo_line(int kind, uint64_t seed, uint64_t j, uint8_t* out) {
       if (col == 3) { log_line(seed ^ 0x4444ull, j, out); return; }
       break;
     }
+    case 5: /* int64 in [0, 1000) only (region 0 of kind 1) */
+      for (int i = 0; i < 8; ++i) w[i] = sm64(seed ^ 0x1111ull, k0 + (uint64_t)i) % 1000;
+      break;
+    case 6: /* log text only (region 1 of kind 1) */
+      log_line(seed, j, out);
+      return;
     case 3: /* constant */
       for (int i = 0; i < 8; ++i) w[i] = 0x6161616161616161ull;
       break;

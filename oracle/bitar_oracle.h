@@ -89,7 +89,7 @@ int bo_decompress(int codec, const uint8_t* const* srcs, const uint32_t* sizes, 
 /* ---- deterministic synthetic inputs ------------------------------ */
 /* kind: 0 = random (SplitMix64), 1 = "Silesia-style" 3 MiB period mix, 2 = Arrow-like
  * record-batch body (int64 small range | float64 | dictionary-index int32 | utf8),
- * 3 = constant, 4 = periodic. */
+ * 3 = constant, 4 = periodic, 5 = int64 small-range only, 6 = log text only. */
 void bo_fill(int kind, uint64_t seed, uint8_t* out, uint64_t n);
 
 #ifdef __cplusplus

@@ -41,7 +41,7 @@ def down(t, n=None):
     return a if n is None else a[:n]
 
 
-@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 4096 + 7, (3 << 20) + 129])
 def test_fill_matches_oracle(eng, kind, n):
     d = eng.empty(n)
@@ -83,7 +83,7 @@ def test_decode_all_golden_lz4(eng):
         assert out[k * seg:k * seg + len(plain)].tobytes() == plain, (e["producer"], e["input"])
 
 
-@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("seg", [65536, 59460, 2048, 13, 8])
 def test_compress_bit_exact_vs_oracle(eng, kind, seg):
     import bitar_amd
