@@ -64,6 +64,10 @@ struct SVec {
   }
 };
 
+__device__ __forceinline__ uint32_t bpermute_lane(uint32_t v, uint32_t src_lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+
 // LZ4 length extension from the register vector; long runs (> 32 bytes of 255s) fall back
 // to the 64-byte ballot scan.
 __device__ __forceinline__ bool ext_len(State& s, uint8_t* win, SVec& sv, uint32_t& len) {
@@ -108,46 +112,87 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   sv.v = 0;
   const uint32_t lane = lane_id();
   const uint32_t base = (uint32_t)(uintptr_t)s.dst;  // ring index = absolute address & mask
+  const uint32_t src_lo = (uint32_t)(uintptr_t)s.src;
   while (ok) {
-    // ---- fast path: short sequence fully inside the register vector and the window -----
-    // token, no length extensions, not the last sequence, near match, room in the ring.
-    // Every output byte of the sequence is gathered with ONE ds_read (literal bytes from the
-    // window, match bytes from the ring -- a match byte whose source lies in this sequence's
-    // own literals is read from the window too) and stored with ONE ds_write.
-    if (s.ip + 20 <= s.csize && s.op + 64 - s.flushed <= kFlushAt) {
-      if (!sv.covers(s.ip, 20)) sv.load(s, win, s.ip);
-      const int64_t wrel = (int64_t)((uintptr_t)(s.src + s.ip) - s.wb);  // ip inside win
-      const uint32_t token = sv.byte(s.ip);
-      const uint32_t L = token >> 4, m4 = token & 15u;
-      if (L < 15 && m4 < 15 && wrel >= 0 && wrel + 20 <= (int64_t)kWin) {
-        const uint32_t off = sv.u16(s.ip + 1 + L);
-        const uint32_t M = m4 + 4;
-        const uint32_t opl = s.op + L;
-        if (off != 0 && off <= opl && off <= kNearOff && opl + M <= s.cap) {
-          const uint32_t t = lane;
-          const uint32_t lit0 = (uint32_t)wrel + 1;  // window index of the first literal
-          uint32_t addr;
-          if (t < L) {
-            addr = lit0 + t;
-          } else {
-            const uint32_t r = t - L;
-            uint32_t rel = r;
-            if (off <= r) {  // overlap: r mod off (exact for r, off < 64)
-              const float q = floorf(((float)r + 0.5f) * __builtin_amdgcn_rcpf((float)off));
-              rel = r - (uint32_t)q * off;
-            }
-            const uint32_t src = opl - off + rel;  // < opl
-            addr = src >= s.op ? lit0 + (src - s.op) : kWin + ((base + src) & kRingMask);
-          }
-          lds_order();
-          const uint32_t b = t < L + M ? (uint32_t)lds[addr] : 0u;
-          if (t < L + M) ring[(base + s.op + t) & kRingMask] = (uint8_t)b;
-          lds_order();
-          s.ip += 3 + L;
-          s.op = opl + M;
-          continue;
+    // ---- batch fast path: up to 64 output bytes of short sequences per step -------------
+    // 1. every lane l decodes "a token at stream position ip+l" from the LDS window
+    //    (token, literal count, match length, offset): a speculative parse of 64 candidates;
+    // 2. a scalar walk follows the real token chain from ip (one v_readlane per sequence)
+    //    while the sequences are short (no length extension), not last, and fit in 64 bytes;
+    // 3. each output lane t finds its sequence (recorded during the walk), and its source:
+    //    a literal byte in the window, a history byte in the ring, or -- for a match reaching
+    //    into this batch -- another lane, resolved by pointer doubling over lanes;
+    // 4. ONE ds_read gathers all 64 bytes, ONE ds_write stores them into the ring.
+    // Lanes past the batch write too: their ring slots are >= kRing - 64 behind the output,
+    // older than any near source and already flushed, and are rewritten before use.
+    for (;;) {
+      if (s.ip + 84 > s.csize || s.op + 64 - s.flushed > kFlushAt) break;
+      uint32_t wrel = src_lo + s.ip - (uint32_t)s.wb;  // window index of ip (mod 2^32)
+      if (wrel > kWin - 84) {
+        win_at(s, win, s.ip, 84);
+        wrel = src_lo + s.ip - (uint32_t)s.wb;
+      }
+      // (1) speculative parse, one candidate token per lane
+      lds_order();
+      const uint32_t wc = wrel + lane;
+      const uint32_t tok = win[wc];
+      const uint32_t cL = tok >> 4, cm4 = tok & 15u;
+      const uint32_t cb0 = win[wc + 1 + cL], cb1 = win[wc + 2 + cL];
+      const uint32_t coff = cb0 | (cb1 << 8);
+      const uint32_t colen = cL + cm4 + 4;
+      const bool csimple = cL < 15 && cm4 < 15 && coff != 0 && coff <= kNearOff;
+      // nxt (7 bits) | olen (6 bits) | simple
+      const uint32_t pack = (lane + 3 + cL) | (colen << 8) | (csimple ? 1u << 16 : 0u);
+      // (2) scalar walk over the real tokens
+      uint32_t k = 0, out = 0;
+      uint32_t seqlane = 0, ostart = 0;  // per output lane: its token lane, its out start
+      for (;;) {
+        const uint32_t e = readlane(pack, k);
+        const uint32_t ol = (e >> 8) & 0xFFu;
+        if (!(e & (1u << 16)) || out + ol > 64) break;
+        const uint32_t Lk = readlane(cL, k);
+        const uint32_t offk = readlane(coff, k);
+        const uint32_t opl = s.op + out + Lk;
+        if (offk > opl || opl + ol - Lk > s.cap) break;  // leave errors to the general path
+        if (lane >= out && lane < out + ol) { seqlane = k; ostart = out; }
+        out += ol;
+        k = e & 0xFFu;
+        if (k >= 64) break;
+      }
+      if (out == 0) break;
+      // (3) sources: window literal / ring history / alias of an earlier lane of the batch
+      const uint32_t t = lane;
+      const uint32_t jL = bpermute_lane(cL, seqlane);
+      const uint32_t joff = bpermute_lane(coff, seqlane);
+      const uint32_t r = t - ostart;
+      uint32_t addr, alias = 64;  // alias < 64: take lane `alias`'s value
+      if (r < jL) {
+        addr = wrel + seqlane + 1 + r;  // window: literal byte r of token lane seqlane
+      } else {
+        const uint32_t m = r - jL;
+        const float q = floorf(((float)(m & 63u) + 0.5f) * __builtin_amdgcn_rcpf((float)joff));
+        const uint32_t mm = joff <= m ? (m & 63u) - (uint32_t)q * joff : m;
+        const int32_t srel = (int32_t)(ostart + jL + mm) - (int32_t)joff;  // vs op
+        if (srel >= 0) {
+          alias = (uint32_t)srel;
+          addr = 0;
+        } else {
+          addr = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
         }
       }
+      // pointer doubling until no lane of the batch aliases another (chains strictly descend)
+      uint32_t st = alias < 64 ? (alias | 0x80000000u) : addr;  // bit31: alias, low bits lane
+      while (ballot((st & 0x80000000u) != 0u && t < out)) {
+        const uint32_t other = bpermute_lane(st, st & 63u);
+        if (st & 0x80000000u) st = other;
+      }
+      // (4) one gather, one store
+      lds_order();
+      const uint8_t b = lds[st & 0x3FFFu];
+      ring[(base + s.op + t) & kRingMask] = b;
+      lds_order();
+      s.ip += k;
+      s.op += out;
     }
     // ---- general path: one sequence, any shape -----------------------------------------
     if (s.ip >= s.csize) { ok = false; break; }
