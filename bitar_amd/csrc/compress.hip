@@ -10,17 +10,20 @@
 // and must match the oracle's output byte for byte.
 //
 // Per fixed window of 64 positions (one per lane):
-//   1. the 4 bytes at every position (coalesced dword loads; the previous window's
-//      registers are kept, so literal bytes come from registers via ds_bpermute);
-//   2. look up a 4096-entry LDS table of (position << 16 | upper 16 bits of the 4 bytes),
-//      then insert every position with ds_max_u32 (largest position wins: deterministic);
-//   3. lanes whose 16-bit check matches verify + measure the match on 16 bytes;
+//   1. the segment streams through an 8 KiB LDS input ring in 256-B rows loaded 2 KiB ahead
+//      (coalesced dword loads held in registers), so every byte a position, a candidate
+//      (matches are capped at 7680 B back) or a literal needs is an LDS read;
+//   2. look up a 4096-entry LDS table of u16 positions, then insert every position (the
+//      largest position wins a slot: deterministic);
+//   3. lanes with a candidate verify + measure the match on 8 bytes from the input ring;
 //   4. a scalar greedy loop picks matches in lane order (ballot + ctz), extends long ones
-//      cooperatively 1 KiB per step, and hands each sequence to the codec's emitter.
+//      cooperatively (ring first, then HBM 1 KiB per step), and hands each sequence to the
+//      codec's emitter.
 // Emitters stage output in LDS and flush it with wide stores:
-//   LZ4: a byte ring flushed in 16-B blocks; long literal runs go HBM -> HBM.
-//   DEFLATE: a bit ring; each lane's code is placed by a wave prefix sum of code lengths
-//            and OR-ed into LDS (ds_or_b32), whole dwords flushed to HBM.
+//   LZ4: one LDS write per sequence (token, length bytes, literals, offset laid out across
+//        lanes); a byte ring flushed in 16-B blocks; long literal runs go HBM -> HBM.
+//   DEFLATE: a bit ring; each lane's code (a sequence's literals and its match symbol) is
+//            placed by a wave prefix sum of code lengths and OR-ed into LDS (ds_or_b32).
 #include "wave.hip.h"
 
 namespace bitar_hip {
@@ -31,6 +34,11 @@ constexpr uint32_t kHashLog = 12;
 constexpr uint32_t kMinMatch = 4;
 constexpr uint32_t kLastLiterals = 5;
 constexpr uint32_t kMfLimit = 12;
+// Match distance cap (both codecs): the 8 KiB input ring holds [x + 128 - 8192, x + 128) at
+// window x, so every candidate of a window (>= x - 7680) is in LDS; it is also inside the
+// LZ4 decoder's 8 KiB history ring (reach 8048), so our streams decode on its LDS path.
+constexpr uint32_t kMaxDist = 7680;
+constexpr uint32_t kIn = 8192, kInMask = kIn - 1;  // LDS input ring
 
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
 
@@ -75,20 +83,35 @@ __device__ __forceinline__ uint32_t bpermute(uint32_t v, uint32_t src_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
 }
 
-// The input bytes the parse has in registers: lane l of `cur` holds the 4 bytes at x+l,
-// lane l of `prev` those at x-64+l.  A literal run inside [x-64, x+64) is read from here.
-struct Regs {
-  uint32_t prev, cur, x;
-  // byte at segment position q, x-64 <= q < x+64 (per lane)
-  __device__ __forceinline__ uint32_t byte_at(uint32_t q) const {
-    const uint32_t rel = q + 64 - x;  // 0..127
-    const uint32_t a = bpermute(prev, rel & 63), b = bpermute(cur, rel & 63);
-    return (rel >= 64 ? b : a) & 0xFFu;
+// The LDS input ring: byte of segment position q lives at ring[(in_lo + q) & kInMask]
+// (absolute-address indexing keeps aligned dwords aligned).
+struct InRing {
+  uint8_t* ring;
+  uint32_t in_lo;  // low 32 bits of the segment's input address
+  uint32_t lo;     // positions >= lo are in the ring (< the filled end)
+
+  __device__ __forceinline__ uint32_t byte(uint32_t q) const {
+    return ring[(in_lo + q) & kInMask];
+  }
+  // 8 bytes at position q (q >= lo, q + 8 <= filled end), as a little-endian 64-bit value
+  __device__ __forceinline__ uint64_t bytes8(uint32_t q) const {
+    const uint32_t a = in_lo + q;
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring);
+    const uint32_t d = a >> 2, sh = a & 3u;
+    const uint32_t w0 = r32[d & (kInMask >> 2)], w1 = r32[(d + 1) & (kInMask >> 2)],
+                   w2 = r32[(d + 2) & (kInMask >> 2)];
+    return (uint64_t)funnel(w0, w1, sh) | ((uint64_t)funnel(w1, w2, sh) << 32);
   }
 };
 
+// number of equal leading bytes of two 8-byte little-endian values (0..8)
+__device__ __forceinline__ uint32_t common8(uint64_t a, uint64_t b) {
+  const uint64_t d = a ^ b;
+  return d ? (uint32_t)(__builtin_ctzll(d) >> 3) : 8u;
+}
+
 // ---- LZ4 emitter: output staged in an LDS byte ring, flushed in aligned 16-B blocks ----
-constexpr uint32_t kObuf = 4096, kObufMask = kObuf - 1, kObufFlush = kObuf / 2;
+constexpr uint32_t kObuf = 2048, kObufMask = kObuf - 1, kObufFlush = kObuf / 2;
 
 struct Lz4Out {
   uint8_t* ring;  // LDS
@@ -141,26 +164,42 @@ struct Lz4Out {
       put(t + 1 < cnt ? 255u : v % 255u, step);
     }
   }
-  __device__ __forceinline__ void sequence(const uint8_t* in, const Regs& R, uint32_t lit_start,
+  __device__ __forceinline__ void sequence(const uint8_t* in, const InRing& I, uint32_t lit_start,
                                            uint32_t lit_len, uint32_t off, uint32_t mlen) {
     if (overflow) return;
     const uint32_t ml = mlen ? mlen - kMinMatch : 0;
     const uint32_t token = ((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15);
+    const uint32_t nlx = lit_len >= 15 ? (lit_len - 15) / 255u + 1 : 0;
+    const uint32_t nmx = mlen && ml >= 15 ? (ml - 15) / 255u + 1 : 0;
+    const uint32_t e = 1 + nlx + lit_len + (mlen ? 2 + nmx : 0);
+    if (e <= kWave && lit_start >= I.lo) {
+      // the whole sequence in one LDS write: lane t holds encoded byte t
+      if (!room(e)) return;
+      const uint32_t t = lane_id();
+      const uint32_t lit0 = 1 + nlx, offp = lit0 + lit_len;
+      lds_order();
+      const uint32_t lb = I.byte(lit_start + (t - lit0 < lit_len ? t - lit0 : 0u));
+      uint32_t v;
+      if (t == 0) v = token;
+      else if (t < lit0) v = t + 1 < lit0 ? 255u : (lit_len - 15) - 255u * (nlx - 1);
+      else if (t < offp) v = lb;
+      else if (t == offp) v = off & 0xFFu;
+      else if (t == offp + 1) v = off >> 8;
+      else v = t + 1 < e ? 255u : (ml - 15) - 255u * (nmx - 1);
+      put(v, e);
+      return;
+    }
     if (!room(1)) return;
     put(token, 1);
     if (lit_len >= 15) put_ext(lit_len - 15);
     if (overflow) return;
     if (lit_len) {
       if ((uint64_t)op + lit_len > cap) { overflow = true; return; }
-      if (lit_len <= kWave && lit_start + 64 >= R.x) {  // from registers
-        room(lit_len);
-        put(R.byte_at(lit_start + (lane_id() < lit_len ? lane_id() : 0)), lit_len);
-      } else {  // long run: drain the ring, then HBM -> HBM
-        flush(op, true);
-        wave_copy_global(dst + op, in + lit_start, lit_len);
-        op += lit_len;
-        flushed = op;
-      }
+      // long run (or not in the input ring): drain the ring, then HBM -> HBM
+      flush(op, true);
+      wave_copy_global(dst + op, in + lit_start, lit_len);
+      op += lit_len;
+      flushed = op;
     }
     if (!mlen) return;
     if (!room(2)) return;
@@ -174,7 +213,7 @@ struct Lz4Out {
 };
 
 // ---- fixed-Huffman DEFLATE emitter: LDS bit ring, lane codes placed by prefix sum -----
-constexpr uint32_t kBitWords = 1024, kBitMask = kBitWords - 1, kBitFlushWords = kBitWords / 2;
+constexpr uint32_t kBitWords = 512, kBitMask = kBitWords - 1, kBitFlushWords = kBitWords / 2;
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                       31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -242,35 +281,43 @@ struct DflOut {
   __device__ __forceinline__ void put_one(uint32_t val, uint32_t nb) {
     put_lanes(lane_id() == 0 ? val : 0u, lane_id() == 0 ? nb : 0u);
   }
-  __device__ __forceinline__ void literals(const uint8_t* in, const Regs& R, uint32_t s,
-                                           uint32_t n) {
+  // literal codes of [s, s+n) and (if mlen) the match symbol, in lane order, 63 per step
+  __device__ __forceinline__ void sequence(const uint8_t* in, const InRing& I, uint32_t s,
+                                           uint32_t n, uint32_t off, uint32_t mlen) {
+    if (overflow) return;
     const uint32_t lane = lane_id();
-    for (uint32_t k = 0; k < n && !overflow; k += kWave) {
-      const uint32_t step = n - k < kWave ? n - k : kWave;
+    uint32_t mv = 0, mb = 0;  // the match symbol: length code + extra + distance code + extra
+    if (mlen) {
+      uint32_t ls = 28;
+      while (kLenBase[ls] > mlen) --ls;
+      uint32_t ln;
+      const uint32_t lcode = fixed_code(257 + ls, ln);
+      uint32_t ds = 29;
+      while (kDistBase[ds] > off) --ds;
+      const uint32_t le = kLenExtra[ls], de = kDistExtra[ds];
+      mv = lcode | ((mlen - kLenBase[ls]) << ln) | (rev(ds, 5) << (ln + le)) |
+           ((off - kDistBase[ds]) << (ln + le + 5));
+      mb = ln + le + 5 + de;
+    }
+    const bool ring_ok = s >= I.lo;
+    uint32_t k = 0;
+    for (;;) {
+      const uint32_t step = n - k < kWave - 1 ? n - k : kWave - 1;
+      const bool last = k + step == n;
       const uint32_t q = s + k + (lane < step ? lane : 0);
       uint32_t b;
-      if (n <= kWave && s + 64 >= R.x) b = R.byte_at(q);
+      lds_order();
+      if (ring_ok) b = I.byte(q);
       else b = lane < step ? (uint32_t)in[q] : 0u;
       uint32_t nb;
       const uint32_t code = fixed_code(b, nb);
-      put_lanes(lane < step ? code : 0u, lane < step ? nb : 0u);
+      uint32_t val = lane < step ? code : 0u;
+      uint32_t bits_n = lane < step ? nb : 0u;
+      if (last && lane == step) { val = mv; bits_n = mb; }
+      put_lanes(val, bits_n);
+      if (last || overflow) return;
+      k += step;
     }
-  }
-  __device__ __forceinline__ void sequence(const uint8_t* in, const Regs& R, uint32_t lit_start,
-                                           uint32_t lit_len, uint32_t off, uint32_t mlen) {
-    if (overflow) return;
-    if (lit_len) literals(in, R, lit_start, lit_len);
-    if (!mlen || overflow) return;
-    uint32_t ls = 28;
-    while (kLenBase[ls] > mlen) --ls;
-    uint32_t ln;
-    const uint32_t lcode = fixed_code(257 + ls, ln);
-    uint32_t ds = 29;
-    while (kDistBase[ds] > off) --ds;
-    const uint32_t le = kLenExtra[ls], de = kDistExtra[ds];
-    const uint32_t v = lcode | ((mlen - kLenBase[ls]) << ln) | (rev(ds, 5) << (ln + le)) |
-                       ((off - kDistBase[ds]) << (ln + le + 5));
-    put_one(v, ln + le + 5 + de);
   }
   __device__ __forceinline__ uint32_t finish() {
     uint32_t n;
@@ -282,62 +329,130 @@ struct DflOut {
 };
 
 // The window-scan parse over one segment; calls E.sequence(...) in stream order.
+//
+// Input staging: the segment is read in 256-B rows (one aligned dword per lane, absolute-
+// address aligned) that are loaded kQ rows ahead into registers and written into the 8 KiB
+// LDS input ring one row ahead of the window scan.  At window x (row m = x / 256) the ring
+// holds positions [F - 8192, F) with F = 256 (m + 2) - (in & 3): every candidate
+// (>= x - 7680), every position's 8-byte probe (<= x + 74) and the first >= 256 B of every
+// match extension are LDS reads; HBM is only touched by the row prefetch, by extensions past
+// F and by literal runs longer than the ring.
+// Hash table: 4096 u16 positions (8 KiB).  Lookups read the previous windows' state, then
+// every position is written; a read-back loop settles same-slot writes of one window so the
+// largest position wins (the oracle's ascending insert order).
+constexpr uint32_t kQ = 8;  // rows in flight ahead of the ring (2 KiB)
+
+__device__ __forceinline__ uint32_t common4(uint32_t a, uint32_t b) {
+  const uint32_t d = a ^ b;
+  return d ? (uint32_t)(__builtin_ctz(d) >> 3) : 4u;
+}
+
 template <class E>
 __device__ __forceinline__ void parse(const uint8_t* in, uint32_t n, const uint8_t* in_end,
-                                      uint32_t* table, uint32_t max_dist, uint32_t max_mlen, E& em) {
+                                      uint16_t* table, uint8_t* inring, uint32_t max_dist,
+                                      uint32_t max_mlen, E& em) {
   const uint32_t lane = lane_id();
   uint32_t anchor = 0;
-  Regs R;
-  R.prev = 0;
-  R.cur = 0;
-  R.x = 0;
+  InRing I;
+  I.ring = inring;
+  I.in_lo = (uint32_t)(uintptr_t)in;
+  I.lo = 0xFFFFFFFFu;  // nothing staged: literal bytes come from HBM
   if (n >= kMfLimit + 1) {
-    // An empty slot means "candidate position 0" (the oracle's zeroed table): it holds
-    // position 0 with position 0's own check bits.
-    const uint32_t empty = ld32u(in, in_end) >> 16;
-    for (uint32_t k = lane; k < (1u << kHashLog); k += kWave) table[k] = empty;
-    lds_order();
+    // empty slot = candidate position 0 (the oracle's zeroed table)
+    for (uint32_t k = lane; k < (1u << kHashLog) / 8; k += kWave)
+      reinterpret_cast<uint4*>(table)[k] = make_uint4(0, 0, 0, 0);
     const uint32_t last_start = n - kMfLimit;
     const uint32_t match_limit = n - kLastLiterals;
+    const uint32_t s0 = I.in_lo & 3u;
+    const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in - s0);
+    uint32_t* r32 = reinterpret_cast<uint32_t*>(inring);
+    const uint32_t rbase = (I.in_lo - s0) >> 2;  // ring dword of in32[0]
+    // row r = dwords [64 r, 64 r + 64) of in32 = positions [256 r - s0, 256 r + 256 - s0)
+    auto load_row = [&](uint32_t r) -> uint32_t {
+      const uint32_t j = 64u * r + lane;
+      return 4u * j < n + s0 ? in32[j] : 0u;
+    };
+    auto write_row = [&](uint32_t r, uint32_t v) { r32[(rbase + 64u * r + lane) & (kInMask >> 2)] = v; };
+    uint32_t q[kQ];
+    const uint32_t r0 = load_row(0);
+#pragma unroll
+    for (uint32_t k = 0; k < kQ; ++k) q[k] = load_row(1 + k);
+    lds_order();
+    write_row(0, r0);
+    uint32_t F = 0;
     uint32_t pos = 0;
     for (uint32_t x = 0; x <= last_start; x += kWave) {
+      if ((x & 255u) == 0) {  // next row into the ring, one more row in flight
+        const uint32_t m = x >> 8;
+        lds_order();
+        write_row(m + 1, q[0]);
+#pragma unroll
+        for (uint32_t k = 0; k + 1 < kQ; ++k) q[k] = q[k + 1];
+        q[kQ - 1] = load_row(m + 1 + kQ);
+        F = 256u * (m + 2) - s0;
+        I.lo = F > kIn ? F - kIn : 0u;
+      }
+      lds_order();
       const uint32_t p = x + lane;
-      R.prev = R.cur;
-      R.cur = p < n ? ld32u(in + p, in_end) : 0u;
-      R.x = x;
       const bool act = p <= last_start;
-      const uint32_t v = R.cur;
-      const uint32_t h = hash4(v);
+      const uint64_t vp = I.bytes8(p);
+      const uint32_t h = hash4((uint32_t)vp);
+      const uint32_t cand = act ? table[h] : 0u;
       lds_order();
-      const uint32_t e = act ? table[h] : 0u;
-      lds_order();
-      if (act) atomicMax(&table[h], (p << 16) | (v >> 16));
-      const uint32_t cand = e >> 16;
-      const bool pre = act && cand < p && p - cand <= max_dist && (e & 0xFFFFu) == (v >> 16);
+      if (act) table[h] = (uint16_t)p;
+      const bool pre = act && cand < p && p - cand <= max_dist;
       uint32_t len = 0;
-      if (pre) {  // verify the 4 bytes and measure up to 16 (gathered loads)
-        const uint4 a = ld16u(in + p, in_end);
-        const uint4 b = ld16u(in + cand, in_end);
-        len = common16(a, b);
+      if (pre) {  // verify the 4 bytes and measure up to 8, from the input ring
+        len = common8(vp, I.bytes8(cand));
         uint32_t lim = match_limit - p;
         if (lim > max_mlen) lim = max_mlen;
         if (len > lim) len = lim;
+      }
+      // same-slot writes of this window: re-write until the largest position holds the slot
+      lds_order();
+      bool redo = act && table[h] < p;
+      while (ballot(redo)) {
+        lds_order();
+        if (redo) table[h] = (uint16_t)p;
+        lds_order();
+        redo = redo && table[h] < p;
       }
       const uint64_t valid = ballot(pre && len >= kMinMatch);
       while (valid) {
         const uint32_t start = pos > x ? pos - x : 0u;
         if (start >= kWave) break;
-        const uint64_t m = valid & (~0ull << start);
-        if (!m) break;
-        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        const uint64_t mk = valid & (~0ull << start);
+        if (!mk) break;
+        const uint32_t l = (uint32_t)__builtin_ctzll(mk);
         const uint32_t i = x + l;
         const uint32_t c = readlane(cand, l);
         uint32_t mlen = readlane(len, l);
         uint32_t lim = match_limit - i;
         if (lim > max_mlen) lim = max_mlen;
-        if (mlen == 16 && lim > 16) {  // cooperative extension, 16 B per lane per step
-          uint32_t k = 16;
+        if (mlen == 8 && lim > 8) {
+          // extension, first from the input ring (4 B per lane per step) up to F ...
+          const uint32_t lr = lim < F - i ? lim : F - i;
+          uint32_t k = 8;
+          bool more = true;
           for (;;) {
+            const uint32_t kk = k + 4u * lane;
+            uint32_t cl = 4;
+            if (kk < lr) {
+              cl = common4((uint32_t)I.bytes8(i + kk), (uint32_t)I.bytes8(c + kk));
+              if (cl > lr - kk) cl = lr - kk;
+            }
+            const uint64_t stop = ballot(kk >= lr || cl < 4);
+            if (stop) {
+              const uint32_t sl = (uint32_t)__builtin_ctzll(stop);
+              const uint32_t ks = k + 4u * sl;
+              k = ks >= lr ? lr : ks + readlane(cl, sl);
+              more = k == lr && lr < lim;  // stopped by the ring's end, not by a mismatch
+              break;
+            }
+            k += 4u * kWave;
+          }
+          // ... then from HBM, 16 B per lane per step
+          while (more) {
             const uint32_t kk = k + 16u * lane;
             uint32_t cl = 16;
             if (kk < lim) {
@@ -349,24 +464,21 @@ __device__ __forceinline__ void parse(const uint8_t* in, uint32_t n, const uint8
             const uint64_t stop = ballot(kk >= lim || cl < 16);
             if (stop) {
               const uint32_t sl = (uint32_t)__builtin_ctzll(stop);
-              const uint32_t kk_s = k + 16u * sl;
-              const uint32_t cl_s = readlane(cl, sl);
-              mlen = kk_s >= lim ? lim : kk_s + cl_s;
+              const uint32_t ks = k + 16u * sl;
+              k = ks >= lim ? lim : ks + readlane(cl, sl);
               break;
             }
             k += 16u * kWave;
           }
+          mlen = k;
         }
-        em.sequence(in, R, anchor, i - anchor, i - c, mlen);
+        em.sequence(in, I, anchor, i - anchor, i - c, mlen);
         pos = i + mlen;
         anchor = pos;
       }
     }
-    R.x = ~0u;  // the final run is past the register window: read it from HBM
-  } else {
-    R.x = ~0u;
   }
-  em.sequence(in, R, anchor, n - anchor, 0, 0);
+  em.sequence(in, I, anchor, n - anchor, 0, 0);
 }
 
 }  // namespace cmp
@@ -376,7 +488,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
   using namespace cmp;
-  __shared__ __attribute__((aligned(16))) uint32_t table[1u << kHashLog];
+  __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
+  __shared__ __attribute__((aligned(16))) uint8_t inring[kIn];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf];
   const uint32_t i_seg = blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
@@ -389,7 +502,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   o.op = 0;
   o.flushed = 0;
   o.overflow = false;
-  parse(input + seg_off, n, input + n_total, table, 65535u, 0xFFFFFFFFu, o);
+  parse(input + seg_off, n, input + n_total, table, inring, kMaxDist, 0xFFFFFFFFu, o);
   const uint32_t size = o.finish();
   if (lane_id() == 0) {
     sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : size;
@@ -402,7 +515,8 @@ __global__ __launch_bounds__(64) void deflate_compress_kernel(
     uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
   using namespace cmp;
-  __shared__ __attribute__((aligned(16))) uint32_t table[1u << kHashLog];
+  __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
+  __shared__ __attribute__((aligned(16))) uint8_t inring[kIn];
   __shared__ __attribute__((aligned(16))) uint32_t stage[kBitWords];
   const uint32_t i_seg = blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
@@ -417,7 +531,7 @@ __global__ __launch_bounds__(64) void deflate_compress_kernel(
   o.wflushed = 0;
   o.overflow = false;
   o.put_one(1u | (1u << 1), 3);  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
-  parse(input + seg_off, n, input + n_total, table, 32768u, 258u, o);
+  parse(input + seg_off, n, input + n_total, table, inring, kMaxDist, 258u, o);
   const uint32_t size = o.finish();
   if (lane_id() == 0) {
     sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : size;

@@ -140,21 +140,22 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t cb0 = win[wc + 1 + cL], cb1 = win[wc + 2 + cL];
       const uint32_t coff = cb0 | (cb1 << 8);
       const uint32_t colen = cL + cm4 + 4;
-      const bool csimple = cL < 15 && cm4 < 15 && coff != 0 && coff <= kNearOff;
-      // nxt (7 bits) | olen (6 bits) | simple
-      const uint32_t pack = (lane + 3 + cL) | (colen << 8) | (csimple ? 1u << 16 : 0u);
-      // (2) scalar walk over the real tokens
+      // eligible: no length extension, real offset, near, and (conservatively, as if this
+      // token opened the batch) not reaching before the segment start
+      const bool csimple = cL < 15 && cm4 < 15 && coff != 0 && coff <= kNearOff &&
+                           coff <= s.op + cL;
+      // nxt (7 bits) | olen, or 127 when not eligible (the walk's one compare then stops)
+      const uint32_t pack = (lane + 3 + cL) | ((csimple ? colen : 127u) << 8);
+      // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
+      const uint32_t room = s.cap - s.op;
+      const uint32_t lim = room < 64 ? room : 64;
       uint32_t k = 0, out = 0;
       uint32_t seqlane = 0, ostart = 0;  // per output lane: its token lane, its out start
       for (;;) {
         const uint32_t e = readlane(pack, k);
-        const uint32_t ol = (e >> 8) & 0xFFu;
-        if (!(e & (1u << 16)) || out + ol > 64) break;
-        const uint32_t Lk = readlane(cL, k);
-        const uint32_t offk = readlane(coff, k);
-        const uint32_t opl = s.op + out + Lk;
-        if (offk > opl || opl + ol - Lk > s.cap) break;  // leave errors to the general path
-        if (lane >= out && lane < out + ol) { seqlane = k; ostart = out; }
+        const uint32_t ol = e >> 8;
+        if (out + ol > lim) break;
+        if (lane - out < ol) { seqlane = k; ostart = out; }
         out += ol;
         k = e & 0xFFu;
         if (k >= 64) break;

@@ -179,11 +179,18 @@ static void lz4_emit(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t 
   if (ml >= 15) lz4_put_len(c, ml - 15);
 }
 
+/* Match distance cap of the bitar parse (both codecs): 7680 B.  The compressor keeps the
+ * last 8 KiB of input in an LDS ring (every candidate of a 64-position window is then in
+ * LDS), and the LZ4 decoder's 8 KiB LDS history ring reaches 8048 B back, so every match
+ * of our own streams decodes from LDS.  Standard LZ4 allows 65535 and DEFLATE 32768; the cap
+ * costs ~2% ratio on the mixed corpus (DESIGN.md "Window-scan parse"). */
+#define BO_MAX_DIST 7680u
+
 int bo_lz4_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
                           uint32_t* csize) {
   if (n > 65536u) return BO_ERR_INVALID;
   lz4_emit_ctx c = {src, dst, cap, 0, 0};
-  bo_window_parse(src, n, 65535u, 0xFFFFFFFFu, lz4_emit, &c);
+  bo_window_parse(src, n, BO_MAX_DIST, 0xFFFFFFFFu, lz4_emit, &c);
   if (c.err) return BO_ERR_IO;
   *csize = c.op;
   return BO_OK;
@@ -449,7 +456,7 @@ int bo_deflate_fixed_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_
                            uint32_t* csize) {
   dfl_ctx c = {src, dst, cap, 0, 0};
   put_bits(&c, 1u | (1u << 1), 3); /* BFINAL=1, BTYPE=01 */
-  bo_window_parse(src, n, 32768u, 258u, dfl_emit, &c);
+  bo_window_parse(src, n, BO_MAX_DIST, 258u, dfl_emit, &c);
   dfl_put_lit(&c, 256);
   if (c.err) return BO_ERR_IO;
   *csize = (uint32_t)((c.bitpos + 7) >> 3);
