@@ -9,21 +9,28 @@
 // They share the "window-scan parse" restated in oracle/bitar_oracle.c (bo_window_parse)
 // and must match the oracle's output byte for byte.
 //
+// Input staging.  The segment streams through an 8 KiB LDS input ring in 1 KiB rows (one
+// aligned 16-B block per lane): each row is loaded into registers a whole row of windows
+// before it is written into the ring, and the ring runs 576..1536 B ahead of the scan.
+// Every byte a position, a candidate (matches are capped at 6656 B back) or a literal needs
+// is then an LDS read.  One register block in a fixed register: a rotation between
+// blocks would make the compiler wait for every load in flight.
+//
 // Per fixed window of 64 positions (one per lane):
-//   1. the segment streams through an 8 KiB LDS input ring in 256-B rows loaded 2 KiB ahead
-//      (coalesced dword loads held in registers), so every byte a position, a candidate
-//      (matches are capped at 7680 B back) or a literal needs is an LDS read;
-//   2. look up a 4096-entry LDS table of u16 positions, then insert every position (the
-//      largest position wins a slot: deterministic);
-//   3. lanes with a candidate verify + measure the match on 8 bytes from the input ring;
-//   4. a scalar greedy loop picks matches in lane order (ballot + ctz), extends long ones
-//      cooperatively (ring first, then HBM 1 KiB per step), and hands each sequence to the
-//      codec's emitter.
-// Emitters stage output in LDS and flush it with wide stores:
-//   LZ4: one LDS write per sequence (token, length bytes, literals, offset laid out across
-//        lanes); a byte ring flushed in 16-B blocks; long literal runs go HBM -> HBM.
-//   DEFLATE: a bit ring; each lane's code (a sequence's literals and its match symbol) is
-//            placed by a wave prefix sum of code lengths and OR-ed into LDS (ds_or_b32).
+//   1. hash the 4 bytes at every position (from the ring), look up a 4096-entry LDS table of
+//      u16 positions, then insert every position (the largest position wins a slot);
+//   2. lanes with a candidate verify + measure the match on 8 bytes from the ring, and
+//      lanes still matching extend in parallel up to 32 bytes;
+//   3. a scalar chain walk picks the greedy matches in lane order (one ctz per match,
+//      cooperative extension only for matches reaching 32 bytes);
+//   4. the codec's emitter writes the whole window's output lane-parallel:
+//      LZ4: every selected match lane writes its token / length bytes / offset, every
+//           literal lane writes its own byte, placed by a wave prefix sum of sequence sizes;
+//           rare long runs fall back to a per-sequence path (long literal runs go HBM->HBM);
+//      DEFLATE: every position lane contributes its literal code or its match symbol; codes
+//           are placed by a prefix sum of bit lengths and OR-ed into an LDS bit ring.
+// Output is staged in LDS and flushed with aligned 16-B stores once per input row, right
+// before the next row's load is issued.
 #include "wave.hip.h"
 
 namespace bitar_hip {
@@ -34,32 +41,24 @@ constexpr uint32_t kHashLog = 12;
 constexpr uint32_t kMinMatch = 4;
 constexpr uint32_t kLastLiterals = 5;
 constexpr uint32_t kMfLimit = 12;
-// Match distance cap (both codecs): the 8 KiB input ring holds [x + 128 - 8192, x + 128) at
-// window x, so every candidate of a window (>= x - 7680) is in LDS; it is also inside the
-// LZ4 decoder's 8 KiB history ring (reach 8048), so our streams decode on its LDS path.
-constexpr uint32_t kMaxDist = 7680;
+// Match distance cap (both codecs): at window x the input ring holds positions
+// [F - 8192, F) with F <= x + 1536, so every candidate (>= x - 6656) is in LDS; it is also
+// inside the LZ4 decoder's 8 KiB history ring (reach 8048), so our streams decode from LDS.
+constexpr uint32_t kMaxDist = 6656;
 constexpr uint32_t kIn = 8192, kInMask = kIn - 1;  // LDS input ring
+constexpr uint32_t kRow = 1024;                   // prefetch row: one 16-B block per lane
+constexpr uint32_t kPreExt = 32;                  // parallel per-lane match extension limit
 
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
 
-// 4 bytes at p (any alignment).  The dword after the aligned one is loaded only if it
-// starts before `end`, so no load leaves the input buffer (an aligned dword holding a valid
-// byte never crosses a page).
-__device__ __forceinline__ uint32_t ld32u(const uint8_t* p, const uint8_t* end) {
-  const uintptr_t a = (uintptr_t)p & ~(uintptr_t)3;
-  const uint32_t r = (uint32_t)((uintptr_t)p & 3);
-  const uint32_t lo = *reinterpret_cast<const uint32_t*>(a);
-  const uint32_t hi = (r && a + 4 < (uintptr_t)end) ? *reinterpret_cast<const uint32_t*>(a + 4) : 0u;
-  return funnel(lo, hi, r);
-}
-
 // 16 bytes at p (any alignment); aligned blocks at or past `end` are not loaded (zeros)
-__device__ __forceinline__ uint4 ld16u(const uint8_t* p, const uint8_t* end) {
+__device__ __forceinline__ uint4 ld16u(const GMEM uint8_t* p, const GMEM uint8_t* end) {
   const uintptr_t a = (uintptr_t)p & ~(uintptr_t)15;
   const uint32_t sh = (uint32_t)((uintptr_t)p & 15);
-  const uint4 x = *reinterpret_cast<const uint4*>(a);
+  const GMEM uint4* xa = reinterpret_cast<const GMEM uint4*>(p - sh);
+  const uint4 x = xa[0];
   uint4 y = make_uint4(0, 0, 0, 0);
-  if (sh && a + 16 < (uintptr_t)end) y = *reinterpret_cast<const uint4*>(a + 16);
+  if (sh && a + 16 < (uintptr_t)end) y = xa[1];
   const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
   const uint32_t q = sh >> 2, r = sh & 3u;
   const uint32_t s0 = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : w[3];
@@ -79,12 +78,38 @@ __device__ __forceinline__ uint32_t common16(uint4 a, uint4 b) {
   return 16;
 }
 
+// number of equal leading bytes of two little-endian values
+__device__ __forceinline__ uint32_t common8(uint64_t a, uint64_t b) {
+  const uint64_t d = a ^ b;
+  return d ? (uint32_t)(__builtin_ctzll(d) >> 3) : 8u;
+}
+__device__ __forceinline__ uint32_t common4(uint32_t a, uint32_t b) {
+  const uint32_t d = a ^ b;
+  return d ? (uint32_t)(__builtin_ctz(d) >> 3) : 4u;
+}
+
 __device__ __forceinline__ uint32_t bpermute(uint32_t v, uint32_t src_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
 }
 
+// inclusive prefix sum over the wave's 64 lanes (DPP row shifts + row broadcasts)
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return (uint32_t)x;
+}
+
+// lowest set bit of a 64-bit mask (64 if none); highest set bit (mask nonzero)
+__device__ __forceinline__ uint32_t lowbit(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
+__device__ __forceinline__ uint32_t highbit(uint64_t m) { return 63u - (uint32_t)__builtin_clzll(m); }
+
 // The LDS input ring: byte of segment position q lives at ring[(in_lo + q) & kInMask]
-// (absolute-address indexing keeps aligned dwords aligned).
+// (absolute-address indexing keeps aligned blocks aligned).
 struct InRing {
   uint8_t* ring;
   uint32_t in_lo;  // low 32 bits of the segment's input address
@@ -93,7 +118,7 @@ struct InRing {
   __device__ __forceinline__ uint32_t byte(uint32_t q) const {
     return ring[(in_lo + q) & kInMask];
   }
-  // 8 bytes at position q (q >= lo, q + 8 <= filled end), as a little-endian 64-bit value
+  // 8 bytes at position q as a little-endian 64-bit value
   __device__ __forceinline__ uint64_t bytes8(uint32_t q) const {
     const uint32_t a = in_lo + q;
     const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring);
@@ -104,22 +129,30 @@ struct InRing {
   }
 };
 
-// number of equal leading bytes of two 8-byte little-endian values (0..8)
-__device__ __forceinline__ uint32_t common8(uint64_t a, uint64_t b) {
-  const uint64_t d = a ^ b;
-  return d ? (uint32_t)(__builtin_ctzll(d) >> 3) : 8u;
-}
+// One parsed window, as handed to the emitter.  Per-lane fields are meaningful on the
+// lanes the masks name.
+struct Window {
+  uint32_t x;       // window start
+  uint64_t chain;   // lanes where a selected match starts
+  uint32_t mlen;    // per lane: match length (chain lanes)
+  uint32_t off;     // per lane: match distance (chain lanes)
+  uint32_t byte;    // per lane: input byte at x + lane
+  uint32_t pos_in;  // parse position at window start: [x, pos_in) is covered by a match
+};
 
 // ---- LZ4 emitter: output staged in an LDS byte ring, flushed in aligned 16-B blocks ----
-constexpr uint32_t kObuf = 2048, kObufMask = kObuf - 1, kObufFlush = kObuf / 2;
+constexpr uint32_t kObuf = 2048, kObufMask = kObuf - 1;
 
 struct Lz4Out {
-  uint8_t* ring;  // LDS
-  uint8_t* dst;   // slot
+  uint8_t* ring;      // LDS
+  GMEM uint8_t* dst;  // slot
   uint64_t cap;
   uint32_t op, flushed;
   bool overflow;
 
+  __device__ __forceinline__ uint32_t at(uint32_t k) const {
+    return ((uint32_t)(uintptr_t)dst + k) & kObufMask;
+  }
   __device__ __forceinline__ void flush(uint32_t upto, bool final) {
     const uint32_t lane = lane_id();
     const uintptr_t base = (uintptr_t)dst;
@@ -128,30 +161,34 @@ struct Lz4Out {
     uint32_t head = (uint32_t)((16u - ((base + f) & 15u)) & 15u);
     if (head > upto - f) head = upto - f;
     if (head) {
-      if (lane < head) dst[f + lane] = ring[(base + f + lane) & kObufMask];
+      if (lane < head) dst[f + lane] = ring[at(f + lane)];
       f += head;
     }
     const uint32_t nb = (upto - f) >> 4;
     for (uint32_t b = lane; b < nb; b += kWave) {
       const uint32_t k = f + 16u * b;
-      *reinterpret_cast<uint4*>(dst + k) = *reinterpret_cast<const uint4*>(ring + ((base + k) & kObufMask));
+      *reinterpret_cast<GMEM uint4*>(dst + k) = *reinterpret_cast<const uint4*>(ring + at(k));
     }
     f += nb << 4;
     if (final && f < upto) {
-      if (lane < upto - f) dst[f + lane] = ring[(base + f + lane) & kObufMask];
+      if (lane < upto - f) dst[f + lane] = ring[at(f + lane)];
       f = upto;
     }
     flushed = f;
   }
+  // once per input row, before the next row's load is issued
+  __device__ __forceinline__ void drain() {
+    if (op - flushed >= 16) flush(op, false);
+  }
   __device__ __forceinline__ bool room(uint32_t n) {
     if ((uint64_t)op + n > cap) { overflow = true; return false; }
-    if (op + n - flushed > kObufFlush) flush(op, false);
+    if (op + n - flushed > kObuf - 64) flush(op, false);
     return true;
   }
   // lanes < n write byte `v` at op + lane
   __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
     lds_order();
-    if (lane_id() < n) ring[((uintptr_t)dst + op + lane_id()) & kObufMask] = (uint8_t)v;
+    if (lane_id() < n) ring[at(op + lane_id())] = (uint8_t)v;
     lds_order();
     op += n;
   }
@@ -164,66 +201,112 @@ struct Lz4Out {
       put(t + 1 < cnt ? 255u : v % 255u, step);
     }
   }
-  __device__ __forceinline__ void sequence(const uint8_t* in, const InRing& I, uint32_t lit_start,
-                                           uint32_t lit_len, uint32_t off, uint32_t mlen) {
+  // One sequence, general path: any literal run (long runs HBM -> HBM), any lengths.
+  __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I,
+                                           uint32_t lit_start, uint32_t lit_len, uint32_t off,
+                                           uint32_t mlen) {
     if (overflow) return;
     const uint32_t ml = mlen ? mlen - kMinMatch : 0;
     const uint32_t token = ((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15);
-    const uint32_t nlx = lit_len >= 15 ? (lit_len - 15) / 255u + 1 : 0;
-    const uint32_t nmx = mlen && ml >= 15 ? (ml - 15) / 255u + 1 : 0;
-    const uint32_t e = 1 + nlx + lit_len + (mlen ? 2 + nmx : 0);
-    if (e <= kWave && lit_start >= I.lo) {
-      // the whole sequence in one LDS write: lane t holds encoded byte t
-      if (!room(e)) return;
-      const uint32_t t = lane_id();
-      const uint32_t lit0 = 1 + nlx, offp = lit0 + lit_len;
-      lds_order();
-      const uint32_t lb = I.byte(lit_start + (t - lit0 < lit_len ? t - lit0 : 0u));
-      uint32_t v;
-      if (t == 0) v = token;
-      else if (t < lit0) v = t + 1 < lit0 ? 255u : (lit_len - 15) - 255u * (nlx - 1);
-      else if (t < offp) v = lb;
-      else if (t == offp) v = off & 0xFFu;
-      else if (t == offp + 1) v = off >> 8;
-      else v = t + 1 < e ? 255u : (ml - 15) - 255u * (nmx - 1);
-      put(v, e);
-      return;
-    }
     if (!room(1)) return;
     put(token, 1);
     if (lit_len >= 15) put_ext(lit_len - 15);
     if (overflow) return;
     if (lit_len) {
       if ((uint64_t)op + lit_len > cap) { overflow = true; return; }
-      // long run (or not in the input ring): drain the ring, then HBM -> HBM
-      flush(op, true);
-      wave_copy_global(dst + op, in + lit_start, lit_len);
-      op += lit_len;
-      flushed = op;
+      if (lit_len <= 256 && lit_start >= I.lo) {
+        for (uint32_t k = 0; k < lit_len; k += kWave) {
+          const uint32_t step = lit_len - k < kWave ? lit_len - k : kWave;
+          room(step);
+          lds_order();
+          const uint32_t b = I.byte(lit_start + k + (lane_id() < step ? lane_id() : 0u));
+          put(b, step);
+        }
+      } else {
+        // long run (or not in the input ring): drain the ring, then HBM -> HBM
+        flush(op, true);
+        wave_copy_global(dst + op, in + lit_start, lit_len);
+        op += lit_len;
+        flushed = op;
+      }
     }
     if (!mlen) return;
     if (!room(2)) return;
     put(lane_id() ? off >> 8 : off & 0xFF, 2);
     if (ml >= 15) put_ext(ml - 15);
   }
-  __device__ __forceinline__ uint32_t finish() {
-    flush(op, true);
-    return op;
+  // the tail sequence starts at the last match's end
+  __device__ __forceinline__ uint32_t pending_from(uint32_t anchor, uint32_t) const { return anchor; }
+
+  // All sequences of one window.  Fast path (every literal run < 270 bytes and in the
+  // input ring, every match < 274 bytes: at most one length byte each): each match lane
+  // writes its header bytes and each literal lane its own byte, all lanes at once, at
+  // offsets from a prefix sum of the sequence sizes.
+  __device__ __forceinline__ void window(const GMEM uint8_t* in, const InRing& I, const Window& W,
+                                         uint32_t anchor, uint32_t) {
+    if (!W.chain || overflow) return;
+    const uint32_t lane = lane_id();
+    const uint32_t q = W.x + lane;
+    const bool cl = (W.chain >> lane) & 1;
+    const uint64_t below = W.chain & ((1ull << lane) - 1);
+    const uint32_t pl = below ? highbit(below) : lane;
+    const uint32_t prev_end = bpermute(q + W.mlen, pl);
+    const uint32_t lit_start = below ? prev_end : anchor;
+    const uint32_t lit_len = q - lit_start;
+    const uint32_t ml = W.mlen - kMinMatch;
+    const bool bad = cl && (lit_len >= 270 || ml >= 270);
+    const uint32_t nlx = lit_len >= 15 ? 1u : 0u, nmx = ml >= 15 ? 1u : 0u;
+    const uint32_t e = cl ? 1 + nlx + lit_len + 2 + nmx : 0u;
+    const uint32_t incl = wave_incl_sum(e);
+    const uint32_t total = readlane(incl, 63);
+    if (ballot(bad) || anchor < I.lo || (uint64_t)op + total > cap) {
+      // general path, one sequence at a time
+      uint64_t m = W.chain;
+      uint32_t a = anchor;
+      while (m) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t i = W.x + l, mlen = readlane(W.mlen, l);
+        sequence(in, I, a, i - a, readlane(W.off, l), mlen);
+        a = i + mlen;
+      }
+      return;
+    }
+    room(total);
+    const uint32_t o = op + incl - e;  // this lane's sequence start (chain lanes)
+    // a literal lane (not a match start, not inside a match) belongs to the sequence of the
+    // lowest chain lane above it; its byte lands in that sequence's literal run
+    const uint64_t above = lane == 63 ? 0ull : W.chain & (~0ull << (lane + 1));
+    const uint32_t s = above ? lowbit(above) : lane;
+    const uint32_t s_lit = bpermute(lit_start, s);
+    const uint32_t s_dst = bpermute(o + 1 + nlx - lit_start, s);  // + position = byte slot
+    const bool lit = !cl && above && q >= s_lit;
+    lds_order();
+    if (cl) {
+      ring[at(o)] = (uint8_t)(((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15));
+      if (nlx) ring[at(o + 1)] = (uint8_t)(lit_len - 15);
+      const uint32_t h = o + 1 + nlx + lit_len;
+      ring[at(h)] = (uint8_t)W.off;
+      ring[at(h + 1)] = (uint8_t)(W.off >> 8);
+      if (nmx) ring[at(h + 2)] = (uint8_t)(ml - 15);
+    }
+    if (lit) ring[at(s_dst + q)] = (uint8_t)W.byte;
+    // literals of the first sequence that precede the window (anchor < x): from the ring
+    if (anchor < W.x) {
+      const uint32_t l0 = lowbit(W.chain);
+      const uint32_t d0 = op + 1 + (W.x + l0 - anchor >= 15 ? 1u : 0u) - anchor;
+      for (uint32_t k = anchor; k < W.x; k += kWave) {
+        const uint32_t qq = k + lane;
+        if (qq < W.x) ring[at(d0 + qq)] = (uint8_t)I.byte(qq);
+      }
+    }
+    lds_order();
+    op += total;
   }
 };
 
 // ---- fixed-Huffman DEFLATE emitter: LDS bit ring, lane codes placed by prefix sum -----
-constexpr uint32_t kBitWords = 512, kBitMask = kBitWords - 1, kBitFlushWords = kBitWords / 2;
-
-__constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
-                                      2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t kDistBase[30] = {1,    2,    3,    4,    5,    7,     9,     13,    17,  25,
-                                       33,   49,   65,   97,   129,  193,   257,   385,   513, 769,
-                                       1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  5,  5,  6,
-                                       6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+constexpr uint32_t kBitWords = 512, kBitMask = kBitWords - 1;
 
 __device__ __forceinline__ uint32_t rev(uint32_t v, uint32_t n) {
   return __builtin_bitreverse32(v) >> (32 - n);
@@ -236,11 +319,36 @@ __device__ __forceinline__ uint32_t fixed_code(uint32_t s, uint32_t& n) {
   n = 8;
   return rev(0xC0 + (s - 280), 8);
 }
+// The whole match symbol -- length code, its extra bits, distance code, its extra bits --
+// LSB first (RFC 1951 3.2.5); mlen in [3, 258], off in [1, 32768]; *n <= 31.
+__device__ __forceinline__ uint32_t match_code(uint32_t mlen, uint32_t off, uint32_t& n) {
+  const uint32_t v = mlen - 3;
+  uint32_t lc, le;  // length code (symbol - 257), extra bit count
+  if (mlen == 258) { lc = 28; le = 0; }
+  else if (v < 8) { lc = v; le = 0; }
+  else {
+    le = 29u - __builtin_clz(v);  // floor(log2 v) - 2
+    lc = 4 * le + 4 + ((v >> le) & 3u);
+  }
+  const uint32_t lx = v & ((1u << le) - 1);
+  const uint32_t d = off - 1;
+  uint32_t dc, de;  // distance code, extra bit count
+  if (d < 4) { dc = d; de = 0; }
+  else {
+    de = 30u - __builtin_clz(d);  // floor(log2 d) - 1
+    dc = 2 * de + 2 + ((d >> de) & 1u);
+  }
+  const uint32_t dx = d & ((1u << de) - 1);
+  uint32_t ln;
+  const uint32_t code = fixed_code(257 + lc, ln);
+  n = ln + le + 5 + de;
+  return code | (lx << ln) | (rev(dc, 5) << (ln + le)) | (dx << (ln + le + 5));
+}
 
 struct DflOut {
-  uint32_t* stage;  // LDS, kBitWords dwords, zero outside the pending range
-  uint32_t* dst;    // slot (16-B aligned)
-  uint64_t cap;     // bytes
+  uint32_t* stage;     // LDS, kBitWords dwords, zero outside the pending range
+  GMEM uint32_t* dst;  // slot (16-B aligned)
+  uint64_t cap;        // bytes
   uint64_t bits;
   uint32_t wflushed;
   bool overflow;
@@ -255,15 +363,15 @@ struct DflOut {
     lds_order();
     wflushed = upto;
   }
+  // once per input row, before the next row's load is issued: complete words only
+  __device__ __forceinline__ void drain() {
+    const uint32_t full = (uint32_t)(bits >> 5);
+    if (full != wflushed) flush_words(full);
+  }
   // append each lane's (val, nb) in lane order (nb <= 32; nb = 0 appends nothing)
   __device__ __forceinline__ void put_lanes(uint32_t val, uint32_t nb) {
-    const uint32_t lane = lane_id();
-    uint32_t incl = nb;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
-      if (lane >= d) incl += y;
-    }
+    if (overflow) return;
+    const uint32_t incl = wave_incl_sum(nb);
     const uint32_t total = readlane(incl, 63);
     if ((bits + total + 7) / 8 > cap) { overflow = true; return; }
     const uint64_t bp = bits + incl - nb;
@@ -276,34 +384,18 @@ struct DflOut {
     lds_order();
     bits += total;
     const uint32_t full = (uint32_t)(bits >> 5);
-    if (full - wflushed >= kBitFlushWords) flush_words(full);
+    if (full - wflushed >= kBitWords - 128) flush_words(full);
   }
   __device__ __forceinline__ void put_one(uint32_t val, uint32_t nb) {
     put_lanes(lane_id() == 0 ? val : 0u, lane_id() == 0 ? nb : 0u);
   }
-  // literal codes of [s, s+n) and (if mlen) the match symbol, in lane order, 63 per step
-  __device__ __forceinline__ void sequence(const uint8_t* in, const InRing& I, uint32_t s,
-                                           uint32_t n, uint32_t off, uint32_t mlen) {
-    if (overflow) return;
+  // literal codes of [s, s+n) (from the input ring when it holds them, else from HBM)
+  __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I, uint32_t s,
+                                           uint32_t n, uint32_t, uint32_t) {
     const uint32_t lane = lane_id();
-    uint32_t mv = 0, mb = 0;  // the match symbol: length code + extra + distance code + extra
-    if (mlen) {
-      uint32_t ls = 28;
-      while (kLenBase[ls] > mlen) --ls;
-      uint32_t ln;
-      const uint32_t lcode = fixed_code(257 + ls, ln);
-      uint32_t ds = 29;
-      while (kDistBase[ds] > off) --ds;
-      const uint32_t le = kLenExtra[ls], de = kDistExtra[ds];
-      mv = lcode | ((mlen - kLenBase[ls]) << ln) | (rev(ds, 5) << (ln + le)) |
-           ((off - kDistBase[ds]) << (ln + le + 5));
-      mb = ln + le + 5 + de;
-    }
     const bool ring_ok = s >= I.lo;
-    uint32_t k = 0;
-    for (;;) {
-      const uint32_t step = n - k < kWave - 1 ? n - k : kWave - 1;
-      const bool last = k + step == n;
+    for (uint32_t k = 0; k < n; k += kWave) {
+      const uint32_t step = n - k < kWave ? n - k : kWave;
       const uint32_t q = s + k + (lane < step ? lane : 0);
       uint32_t b;
       lds_order();
@@ -311,48 +403,39 @@ struct DflOut {
       else b = lane < step ? (uint32_t)in[q] : 0u;
       uint32_t nb;
       const uint32_t code = fixed_code(b, nb);
-      uint32_t val = lane < step ? code : 0u;
-      uint32_t bits_n = lane < step ? nb : 0u;
-      if (last && lane == step) { val = mv; bits_n = mb; }
-      put_lanes(val, bits_n);
-      if (last || overflow) return;
-      k += step;
+      put_lanes(lane < step ? code : 0u, lane < step ? nb : 0u);
+      if (overflow) return;
     }
   }
-  __device__ __forceinline__ uint32_t finish() {
-    uint32_t n;
-    const uint32_t eob = fixed_code(256, n);
-    put_one(eob, n);
-    flush_words((uint32_t)((bits + 31) >> 5));
-    return (uint32_t)((bits + 7) >> 3);
+  // literals are emitted window by window: the tail starts where output stopped
+  __device__ __forceinline__ uint32_t pending_from(uint32_t, uint32_t emitted) const { return emitted; }
+
+  // One window: each position contributes its literal code, its match symbol (a selected
+  // match starts there) or nothing (inside a match); one prefix sum places them all.
+  __device__ __forceinline__ void window(const GMEM uint8_t*, const InRing&, const Window& W,
+                                         uint32_t, uint32_t n) {
+    const uint32_t lane = lane_id();
+    const uint32_t q = W.x + lane;
+    const bool cl = (W.chain >> lane) & 1;
+    const uint64_t upto = W.chain & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+    const uint32_t pl = upto ? highbit(upto) : lane;
+    const uint32_t pend = bpermute(q + W.mlen, pl);
+    const bool covered = q < W.pos_in || (upto && !cl && q < pend);
+    uint32_t val = 0, nb = 0;
+    if (cl) val = match_code(W.mlen, W.off, nb);
+    else if (!covered && q < n) val = fixed_code(W.byte, nb);
+    put_lanes(val, nb);
   }
 };
 
-// The window-scan parse over one segment; calls E.sequence(...) in stream order.
-//
-// Input staging: the segment is read in 256-B rows (one aligned dword per lane, absolute-
-// address aligned) that are loaded kQ rows ahead into registers and written into the 8 KiB
-// LDS input ring one row ahead of the window scan.  At window x (row m = x / 256) the ring
-// holds positions [F - 8192, F) with F = 256 (m + 2) - (in & 3): every candidate
-// (>= x - 7680), every position's 8-byte probe (<= x + 74) and the first >= 256 B of every
-// match extension are LDS reads; HBM is only touched by the row prefetch, by extensions past
-// F and by literal runs longer than the ring.
-// Hash table: 4096 u16 positions (8 KiB).  Lookups read the previous windows' state, then
-// every position is written; a read-back loop settles same-slot writes of one window so the
-// largest position wins (the oracle's ascending insert order).
-constexpr uint32_t kQ = 8;  // rows in flight ahead of the ring (2 KiB)
-
-__device__ __forceinline__ uint32_t common4(uint32_t a, uint32_t b) {
-  const uint32_t d = a ^ b;
-  return d ? (uint32_t)(__builtin_ctz(d) >> 3) : 4u;
-}
-
+// The window-scan parse over one segment; hands each window to E::window and the tail to
+// E::sequence.
 template <class E>
-__device__ __forceinline__ void parse(const uint8_t* in, uint32_t n, const uint8_t* in_end,
+__device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const GMEM uint8_t* in_end,
                                       uint16_t* table, uint8_t* inring, uint32_t max_dist,
                                       uint32_t max_mlen, E& em) {
   const uint32_t lane = lane_id();
-  uint32_t anchor = 0;
+  uint32_t anchor = 0, emitted = 0;
   InRing I;
   I.ring = inring;
   I.in_lo = (uint32_t)(uintptr_t)in;
@@ -363,36 +446,27 @@ __device__ __forceinline__ void parse(const uint8_t* in, uint32_t n, const uint8
       reinterpret_cast<uint4*>(table)[k] = make_uint4(0, 0, 0, 0);
     const uint32_t last_start = n - kMfLimit;
     const uint32_t match_limit = n - kLastLiterals;
-    const uint32_t s0 = I.in_lo & 3u;
-    const uint32_t* in32 = reinterpret_cast<const uint32_t*>(in - s0);
-    uint32_t* r32 = reinterpret_cast<uint32_t*>(inring);
-    const uint32_t rbase = (I.in_lo - s0) >> 2;  // ring dword of in32[0]
-    // row r = dwords [64 r, 64 r + 64) of in32 = positions [256 r - s0, 256 r + 256 - s0)
-    auto load_row = [&](uint32_t r) -> uint32_t {
-      const uint32_t j = 64u * r + lane;
-      return 4u * j < n + s0 ? in32[j] : 0u;
+    // Rows cover the 16-B aligned span starting at in - s0: row r, lane l = the block of
+    // segment positions [kRow r + 16 l - s0, +16).  Blocks past the segment are not loaded;
+    // a block holding a byte before in_end never crosses a page.
+    const uint32_t s0 = I.in_lo & 15u;
+    const GMEM uint4* in16 = reinterpret_cast<const GMEM uint4*>(in - s0);
+    const uint64_t span = (uint64_t)(in_end - (in - s0));
+    uint4* ring16 = reinterpret_cast<uint4*>(inring);
+    const uint32_t rbase = (I.in_lo - s0) >> 4;  // ring block of in16[0]
+    auto load_row = [&](uint32_t r) __attribute__((always_inline)) -> uint4 {
+      const uint32_t o = kRow * r + 16u * lane;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (o < n + s0 && o < span) v = in16[o >> 4];
+      return v;
     };
-    auto write_row = [&](uint32_t r, uint32_t v) { r32[(rbase + 64u * r + lane) & (kInMask >> 2)] = v; };
-    uint32_t q[kQ];
-    const uint32_t r0 = load_row(0);
-#pragma unroll
-    for (uint32_t k = 0; k < kQ; ++k) q[k] = load_row(1 + k);
-    lds_order();
-    write_row(0, r0);
-    uint32_t F = 0;
+    auto write_row = [&](uint32_t r, const uint4& v) __attribute__((always_inline)) {
+      ring16[(rbase + (kRow / 16) * r + lane) & (kInMask >> 4)] = v;
+    };
     uint32_t pos = 0;
-    for (uint32_t x = 0; x <= last_start; x += kWave) {
-      if ((x & 255u) == 0) {  // next row into the ring, one more row in flight
-        const uint32_t m = x >> 8;
-        lds_order();
-        write_row(m + 1, q[0]);
-#pragma unroll
-        for (uint32_t k = 0; k + 1 < kQ; ++k) q[k] = q[k + 1];
-        q[kQ - 1] = load_row(m + 1 + kQ);
-        F = 256u * (m + 2) - s0;
-        I.lo = F > kIn ? F - kIn : 0u;
-      }
-      lds_order();
+    uint32_t F = 0;  // the ring holds positions [F - kIn, F)
+    // one window of 64 positions at x
+    auto window = [&](uint32_t x) __attribute__((always_inline)) {
       const uint32_t p = x + lane;
       const bool act = p <= last_start;
       const uint64_t vp = I.bytes8(p);
@@ -401,11 +475,11 @@ __device__ __forceinline__ void parse(const uint8_t* in, uint32_t n, const uint8
       lds_order();
       if (act) table[h] = (uint16_t)p;
       const bool pre = act && cand < p && p - cand <= max_dist;
+      uint32_t lim = match_limit - p;
+      if (lim > max_mlen) lim = max_mlen;
       uint32_t len = 0;
       if (pre) {  // verify the 4 bytes and measure up to 8, from the input ring
         len = common8(vp, I.bytes8(cand));
-        uint32_t lim = match_limit - p;
-        if (lim > max_mlen) lim = max_mlen;
         if (len > lim) len = lim;
       }
       // same-slot writes of this window: re-write until the largest position holds the slot
@@ -417,22 +491,32 @@ __device__ __forceinline__ void parse(const uint8_t* in, uint32_t n, const uint8
         lds_order();
         redo = redo && table[h] < p;
       }
+      // lanes still matching after 8 bytes extend in parallel, up to kPreExt
+      for (uint32_t k = 8; k < kPreExt; k += 8) {
+        const bool go = pre && len == k && lim > k;
+        if (!ballot(go)) break;
+        if (go) {
+          const uint32_t l2 = k + common8(I.bytes8(p + k), I.bytes8(cand + k));
+          len = l2 < lim ? l2 : lim;
+        }
+      }
       const uint64_t valid = ballot(pre && len >= kMinMatch);
-      while (valid) {
-        const uint32_t start = pos > x ? pos - x : 0u;
-        if (start >= kWave) break;
-        const uint64_t mk = valid & (~0ull << start);
-        if (!mk) break;
-        const uint32_t l = (uint32_t)__builtin_ctzll(mk);
+      const uint32_t pos_in = pos;
+      uint64_t chain = 0;
+      uint32_t mlen_v = len;
+      const uint32_t start = pos > x ? pos - x : 0u;
+      uint64_t m = start < kWave ? valid & (~0ull << start) : 0ull;
+      while (m) {  // the greedy chain: the next match is the first valid lane past the end
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
         const uint32_t i = x + l;
-        const uint32_t c = readlane(cand, l);
         uint32_t mlen = readlane(len, l);
-        uint32_t lim = match_limit - i;
-        if (lim > max_mlen) lim = max_mlen;
-        if (mlen == 8 && lim > 8) {
-          // extension, first from the input ring (4 B per lane per step) up to F ...
-          const uint32_t lr = lim < F - i ? lim : F - i;
-          uint32_t k = 8;
+        uint32_t li = match_limit - i;
+        if (li > max_mlen) li = max_mlen;
+        if (mlen == kPreExt && li > kPreExt) {
+          const uint32_t c = readlane(cand, l);
+          // cooperative extension, first from the input ring (4 B per lane per step) up to F
+          const uint32_t lr = li < F - i ? li : F - i;
+          uint32_t k = kPreExt;
           bool more = true;
           for (;;) {
             const uint32_t kk = k + 4u * lane;
@@ -446,7 +530,7 @@ __device__ __forceinline__ void parse(const uint8_t* in, uint32_t n, const uint8
               const uint32_t sl = (uint32_t)__builtin_ctzll(stop);
               const uint32_t ks = k + 4u * sl;
               k = ks >= lr ? lr : ks + readlane(cl, sl);
-              more = k == lr && lr < lim;  // stopped by the ring's end, not by a mismatch
+              more = k == lr && lr < li;  // stopped by the ring's end, not by a mismatch
               break;
             }
             k += 4u * kWave;
@@ -455,30 +539,68 @@ __device__ __forceinline__ void parse(const uint8_t* in, uint32_t n, const uint8
           while (more) {
             const uint32_t kk = k + 16u * lane;
             uint32_t cl = 16;
-            if (kk < lim) {
+            if (kk < li) {
               const uint4 a = ld16u(in + i + kk, in_end);
               const uint4 b = ld16u(in + c + kk, in_end);
               cl = common16(a, b);
-              if (cl > lim - kk) cl = lim - kk;
+              if (cl > li - kk) cl = li - kk;
             }
-            const uint64_t stop = ballot(kk >= lim || cl < 16);
+            const uint64_t stop = ballot(kk >= li || cl < 16);
             if (stop) {
               const uint32_t sl = (uint32_t)__builtin_ctzll(stop);
               const uint32_t ks = k + 16u * sl;
-              k = ks >= lim ? lim : ks + readlane(cl, sl);
+              k = ks >= li ? li : ks + readlane(cl, sl);
               break;
             }
             k += 16u * kWave;
           }
           mlen = k;
+          if (lane == l) mlen_v = mlen;
         }
-        em.sequence(in, I, anchor, i - anchor, i - c, mlen);
+        chain |= 1ull << l;
         pos = i + mlen;
-        anchor = pos;
+        const uint32_t e = l + mlen;
+        m = e < kWave ? valid & (~0ull << e) : 0ull;
       }
+      Window W;
+      W.x = x;
+      W.chain = chain;
+      W.mlen = mlen_v;
+      W.off = p - cand;
+      W.byte = (uint32_t)vp & 0xFFu;
+      W.pos_in = pos_in;
+      em.window(in, I, W, anchor, n);
+      if (chain) anchor = pos;
+      emitted = pos > x + kWave ? pos : x + kWave;
+    };
+    // Row k+1 goes into the ring at x = 1024 k + 512 (the ring then runs 576..1536 B ahead
+    // of the scan); right after, the row register block is reloaded with row k+2, which
+    // has a whole row of windows (1 KiB of scan) to land.  The output is drained just
+    // before that load, so no store queues behind it.
+    uint4 nxt = load_row(1);
+    {
+      const uint4 r0 = load_row(0);
+      lds_order();
+      write_row(0, r0);
+    }
+    F = kRow - s0;
+    I.lo = 0;
+    for (uint32_t x = 0; x <= last_start; x += kWave) {
+      if ((x & (kRow - 1)) == kRow / 2) {
+        const uint32_t k = x / kRow;
+        lds_order();
+        write_row(k + 1, nxt);
+        F = kRow * (k + 2) - s0;
+        I.lo = F > kIn ? F - kIn : 0u;
+        em.drain();
+        nxt = load_row(k + 2);
+      }
+      lds_order();
+      window(x);
     }
   }
-  em.sequence(in, I, anchor, n - anchor, 0, 0);
+  const uint32_t t0 = em.pending_from(anchor, emitted);
+  if (t0 < n) em.sequence(in, I, t0, n - t0, 0, 0);
 }
 
 }  // namespace cmp
@@ -497,15 +619,16 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
   Lz4Out o;
   o.ring = obuf;
-  o.dst = dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride;
+  o.dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
   o.cap = slot_stride;
   o.op = 0;
   o.flushed = 0;
   o.overflow = false;
-  parse(input + seg_off, n, input + n_total, table, inring, kMaxDist, 0xFFFFFFFFu, o);
-  const uint32_t size = o.finish();
+  parse(global_ptr(input + seg_off), n, global_ptr(input + n_total), table, inring, kMaxDist,
+        0xFFFFFFFFu, o);
+  o.flush(o.op, true);
   if (lane_id() == 0) {
-    sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : size;
+    sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : o.op;
     if (o.overflow) atomicOr(err, 2u);
   }
 }
@@ -525,16 +648,21 @@ __global__ __launch_bounds__(64) void deflate_compress_kernel(
   for (uint32_t k = lane_id(); k < kBitWords; k += kWave) stage[k] = 0;
   DflOut o;
   o.stage = stage;
-  o.dst = reinterpret_cast<uint32_t*>(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
+  o.dst = reinterpret_cast<GMEM uint32_t*>(
+      global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride));
   o.cap = slot_stride;
   o.bits = 0;
   o.wflushed = 0;
   o.overflow = false;
   o.put_one(1u | (1u << 1), 3);  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
-  parse(input + seg_off, n, input + n_total, table, inring, kMaxDist, 258u, o);
-  const uint32_t size = o.finish();
+  parse(global_ptr(input + seg_off), n, global_ptr(input + n_total), table, inring, kMaxDist,
+        258u, o);
+  uint32_t eb;
+  const uint32_t eob = fixed_code(256, eb);
+  o.put_one(eob, eb);
+  o.flush_words((uint32_t)((o.bits + 31) >> 5));
   if (lane_id() == 0) {
-    sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : size;
+    sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : (uint32_t)((o.bits + 7) >> 3);
     if (o.overflow) atomicOr(err, 2u);
   }
 }

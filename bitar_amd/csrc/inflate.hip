@@ -251,9 +251,9 @@ __global__ __launch_bounds__(64) void inflate_kernel(
   const uint32_t lane = lane_id();
 
   State s;
-  s.src = srcs ? srcs[i] : slab + (uint64_t)i * slot_stride;
+  s.src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
   s.csize = csizes[i];
-  s.dst = out + (uint64_t)i * seg;
+  s.dst = global_ptr(out + (uint64_t)i * seg);
   s.cap = seg;
   s.ip = 0;
   s.op = 0;

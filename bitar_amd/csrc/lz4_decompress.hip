@@ -95,9 +95,9 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   if (i >= nseg) return;
 
   State s;
-  s.src = srcs ? srcs[i] : slab + (uint64_t)i * slot_stride;
+  s.src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
   s.csize = csizes[i];
-  s.dst = out + (uint64_t)i * seg;
+  s.dst = global_ptr(out + (uint64_t)i * seg);
   s.cap = seg;
   s.ip = 0;
   s.op = 0;

@@ -24,9 +24,9 @@ constexpr uint32_t kFlushAt = kRing / 2;
 constexpr uint32_t kNearOff = kRing - 2 * kWave - 16;  // ring holds the source
 
 struct State {
-  const uint8_t* src;  // compressed segment
+  const GMEM uint8_t* src;  // compressed segment
   uint32_t csize;
-  uint8_t* dst;        // output segment base
+  GMEM uint8_t* dst;        // output segment base
   uint32_t cap;
   uint32_t ip;         // stream position
   uint32_t op;         // output position
@@ -47,7 +47,7 @@ __device__ __forceinline__ void refill_abs(State& s, uint8_t* win, uint64_t abs)
   for (uint32_t j = 0; j < kWin / (16 * kWave); ++j) {
     const uint64_t blk = a + 16ull * (lane + j * kWave);
     if (blk < hi && blk + 16 > lo) {
-      const uint4 v = *reinterpret_cast<const uint4*>((uintptr_t)blk);
+      const uint4 v = *reinterpret_cast<const GMEM uint4*>(s.src + (int64_t)(blk - lo));
       *reinterpret_cast<uint4*>(win + 16 * (lane + j * kWave)) = v;
     }
   }
@@ -117,7 +117,7 @@ __device__ __forceinline__ void flush(State& s, const uint8_t* ring, uint32_t up
   for (uint32_t b = lane; b < nb; b += kWave) {
     const uint32_t k = f + 16u * b;
     const uint4 v = *reinterpret_cast<const uint4*>(ring + ((base + k) & kRingMask));
-    *reinterpret_cast<uint4*>(s.dst + k) = v;
+    *reinterpret_cast<GMEM uint4*>(s.dst + k) = v;
   }
   f += nb << 4;
   if (final && f < upto) {

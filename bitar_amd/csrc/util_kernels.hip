@@ -53,7 +53,7 @@ __global__ __launch_bounds__(64) void pack_kernel(const uint8_t* __restrict__ sl
                                                   uint32_t nseg, uint8_t* __restrict__ frame) {
   const uint32_t i = blockIdx.x;
   if (i >= nseg) return;
-  wave_copy_global(frame + offsets[i], slab + (uint64_t)i * stride, sizes[i]);
+  wave_copy_global(global_ptr(frame + offsets[i]), global_ptr(slab + (uint64_t)i * stride), sizes[i]);
 }
 
 // ---- synthetic input: a device restatement-free generator; tests check it against the

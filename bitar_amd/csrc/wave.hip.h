@@ -28,6 +28,23 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
+// Pointers into global memory (HBM) are typed GMEM (address space 1).  A generic pointer
+// (loaded from a slot table, or rebuilt from an integer) makes the compiler emit FLAT
+// accesses: those count against both vmcnt and lgkmcnt, and every later LDS access must
+// wait for outstanding FLAT stores (they may alias LDS).  GMEM pointers give global_load /
+// global_store.  A cast back to a generic pointer loses the address space, so kernel
+// state keeps GMEM-typed pointers.
+// (The host compilation pass parses device code too; there the qualifier is dropped.)
+#ifdef __HIP_DEVICE_COMPILE__
+#define GMEM __attribute__((address_space(1)))
+#else
+#define GMEM
+#endif
+template <typename T>
+__device__ __forceinline__ GMEM T* global_ptr(T* p) {
+  return (GMEM T*)p;
+}
+
 // Compiler barrier: keeps LDS accesses in program order (the hardware already executes a
 // wave's DS instructions in order).
 __device__ __forceinline__ void lds_order() { __asm__ volatile("" ::: "memory"); }
@@ -53,7 +70,7 @@ __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t r)
 // Copy `len` bytes from global `s` to global `d` (no overlap), all 64 lanes cooperating,
 // 16 B per lane per step with aligned dwordx4 loads + stores.  Source blocks that contain
 // no byte of [s, s+len) are never loaded.  len, s, d wave-uniform.
-__device__ __forceinline__ void wave_copy_global(uint8_t* d, const uint8_t* s, uint64_t len) {
+__device__ __forceinline__ void wave_copy_global(GMEM uint8_t* d, const GMEM uint8_t* s, uint64_t len) {
   const uint32_t lane = lane_id();
   uint32_t head = (uint32_t)((16u - ((uintptr_t)d & 15u)) & 15u);
   if (head > len) head = (uint32_t)len;
@@ -63,8 +80,8 @@ __device__ __forceinline__ void wave_copy_global(uint8_t* d, const uint8_t* s, u
   len -= head;
   const uint64_t nb = len >> 4;
   const uint32_t sh = (uint32_t)((uintptr_t)s & 15u);
-  const uint4* sa = reinterpret_cast<const uint4*>((uintptr_t)s & ~(uintptr_t)15);
-  uint4* da = reinterpret_cast<uint4*>(d);
+  const GMEM uint4* sa = reinterpret_cast<const GMEM uint4*>(s - sh);
+  GMEM uint4* da = reinterpret_cast<GMEM uint4*>(d);
   if (sh == 0) {
     uint64_t b = lane;
     for (; b + 3 * kWave < nb; b += 4 * kWave) {  // 4 KiB per wave in flight
@@ -109,7 +126,8 @@ __device__ __forceinline__ void wave_copy_global(uint8_t* d, const uint8_t* s, u
     for (; base + 4 * kWave <= nb; base += 4 * kWave) {
       const uint64_t b = base + lane;
       const uint4 x0 = sa[b], x1 = sa[b + kWave], x2 = sa[b + 2 * kWave], x3 = sa[b + 3 * kWave];
-      const uint4 x4 = lane == 0 ? sa[base + 4 * kWave] : make_uint4(0, 0, 0, 0);  // in bounds
+      uint4 x4 = make_uint4(0, 0, 0, 0);
+      if (lane == 0) x4 = sa[base + 4 * kWave];  // in bounds
       emit(b, x0, next(x0, x1));
       emit(b + kWave, x1, next(x1, x2));
       emit(b + 2 * kWave, x2, next(x2, x3));
@@ -118,7 +136,8 @@ __device__ __forceinline__ void wave_copy_global(uint8_t* d, const uint8_t* s, u
     for (; base < nb; base += kWave) {
       const uint64_t b = base + lane;
       const bool act = b < nb;
-      uint4 x = act ? sa[b] : make_uint4(0, 0, 0, 0);
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (act) x = sa[b];
       uint4 y;
       y.x = shfl_down1(x.x);
       y.y = shfl_down1(x.y);
