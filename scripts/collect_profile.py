@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Copy one gpu_bench.sh PROFILE=1 run (gpurun_out/) into profiles/<round>/ and derive the
+per-launch HBM traffic that bench.py reports as roofline.traffic.
+
+usage: python scripts/collect_profile.py TAG ROUND_DIR
+  TAG        the TAG the GPU run used (gpurun_out/bench_TAG.json, prof_TAG/, pmc_TAG_*)
+  ROUND_DIR  e.g. profiles/r01
+
+Traffic per launch (MI355X_MICROARCH.md "HBM"): FETCH_SIZE and WRITE_SIZE are in KiB; on
+gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane streaming reads, which is how
+every bulk read of these kernels is issued, so it is doubled; WRITE_SIZE is exact for
+16-B-per-lane stores.  Each counter comes from its own --pmc pass; the value is averaged
+over the kernel's launches in that pass.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_kernel(path):
+    agg = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            name = r["Kernel_Name"].split("(")[0]
+            if not name.startswith("bitar_hip::"):
+                continue
+            agg.setdefault(name.split("::")[-1], []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    tag, rdir = sys.argv[1], sys.argv[2]
+    out = os.path.join(ROOT, "gpurun_out")
+    rdir = os.path.join(ROOT, rdir)
+    os.makedirs(rdir, exist_ok=True)
+    shutil.copy(os.path.join(out, f"bench_{tag}.json"), os.path.join(rdir, "bench.json"))
+    shutil.copy(os.path.join(out, f"prof_{tag}", "trace_kernel_stats.csv"),
+                os.path.join(rdir, "kernel_stats.csv"))
+    fetch = per_kernel(os.path.join(out, f"pmc_{tag}_FETCH_SIZE", "pmc_counter_collection.csv"))
+    write = per_kernel(os.path.join(out, f"pmc_{tag}_WRITE_SIZE", "pmc_counter_collection.csv"))
+    traffic, lines = {}, []
+    for k in sorted(set(fetch) | set(write)):
+        f_kib, w_kib = fetch.get(k, 0.0), write.get(k, 0.0)
+        b = (2.0 * f_kib + w_kib) * 1024.0
+        traffic[k] = round(b)
+        lines.append(f"{k:28s} FETCH_SIZE {f_kib:14.1f} KiB (x2 = {2 * f_kib * 1024:.4g} B)  "
+                     f"WRITE_SIZE {w_kib:14.1f} KiB  -> {b:.4g} B per launch")
+    with open(os.path.join(rdir, "traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1, sort_keys=True)
+    with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1, sort_keys=True)
+    with open(os.path.join(rdir, "pmc_summary.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
