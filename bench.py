@@ -98,6 +98,7 @@ def main():
     import torch
     import torch.distributed as dist
     import bitar_amd
+    from bitar_amd import dist as bd
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -121,6 +122,7 @@ def main():
     out = eng.empty(nseg * seg)
     prod = eng.empty(nseg, dtype=torch.int32)
     all_sizes = eng.empty(nseg * world, dtype=torch.int32) if world > 1 else None
+    index = [None]
     stream = torch.cuda.current_stream()
 
     ev = []  # (compress start, compress end, decompress start, decompress end)
@@ -134,6 +136,7 @@ def main():
             e[1].record(stream)
         if world > 1:  # global frame index: per-segment sizes of every rank
             dist.all_gather_into_tensor(all_sizes, sizes)
+            index[0] = bd.frame_index(all_sizes)  # rank-major = global segment order
         if timed:
             e[2].record(stream)
         eng.decompress_slab_into(codec, slab, stride, sizes, nseg, seg, out, prod,
@@ -171,6 +174,8 @@ def main():
         elapsed = float(mx[0].item())
         ok = mx[1].item() == 0.0
         csize_total = int(sm[2].item())
+        # the frame index every rank built from the all-gathered sizes spans the whole job
+        ok = ok and int(index[0][-1].item()) == csize_total
     else:
         csize_total = csize
 
