@@ -46,6 +46,7 @@ constexpr uint32_t kMfLimit = 12;
 // inside the LZ4 decoder's 8 KiB history ring (reach 8048), so our streams decode from LDS.
 constexpr uint32_t kMaxDist = 6656;
 constexpr uint32_t kIn = 8192, kInMask = kIn - 1;  // LDS input ring
+constexpr uint32_t kInPad = 64;  // mirror of ring[0, 64) after its end: probes never wrap
 constexpr uint32_t kRow = 1024;                   // prefetch row: one 16-B block per lane
 constexpr uint32_t kPreExt = 32;                  // parallel per-lane match extension limit
 
@@ -104,6 +105,22 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
   return (uint32_t)x;
 }
 
+// inclusive prefix max (unsigned) over the wave's 64 lanes
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  uint32_t x = v;
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+  return x;
+}
+// lane l gets lane l-1's value, lane 0 gets 0 (DPP wave_shr:1)
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+
 // lowest set bit of a 64-bit mask (64 if none); highest set bit (mask nonzero)
 __device__ __forceinline__ uint32_t lowbit(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
 __device__ __forceinline__ uint32_t highbit(uint64_t m) { return 63u - (uint32_t)__builtin_clzll(m); }
@@ -118,14 +135,20 @@ struct InRing {
   __device__ __forceinline__ uint32_t byte(uint32_t q) const {
     return ring[(in_lo + q) & kInMask];
   }
-  // 8 bytes at position q as a little-endian 64-bit value
-  __device__ __forceinline__ uint64_t bytes8(uint32_t q) const {
-    const uint32_t a = in_lo + q;
-    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring);
-    const uint32_t d = a >> 2, sh = a & 3u;
-    const uint32_t w0 = r32[d & (kInMask >> 2)], w1 = r32[(d + 1) & (kInMask >> 2)],
-                   w2 = r32[(d + 2) & (kInMask >> 2)];
-    return (uint64_t)funnel(w0, w1, sh) | ((uint64_t)funnel(w1, w2, sh) << 32);
+  // 4 / 16 bytes at position q (little-endian); the pad lets the dword reads run past the
+  // ring's end without wrapping
+  __device__ __forceinline__ uint32_t dword(uint32_t q) const {
+    const uint32_t a = (in_lo + q) & kInMask;
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring) + (a >> 2);
+    return funnel(r32[0], r32[1], a & 3u);
+  }
+  __device__ __forceinline__ uint4 bytes16(uint32_t q) const {
+    const uint32_t a = (in_lo + q) & kInMask;
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring) + (a >> 2);
+    const uint32_t sh = a & 3u;
+    const uint32_t w0 = r32[0], w1 = r32[1], w2 = r32[2], w3 = r32[3], w4 = r32[4];
+    return make_uint4(funnel(w0, w1, sh), funnel(w1, w2, sh), funnel(w2, w3, sh),
+                      funnel(w3, w4, sh));
   }
 };
 
@@ -248,11 +271,11 @@ struct Lz4Out {
     const uint32_t lane = lane_id();
     const uint32_t q = W.x + lane;
     const bool cl = (W.chain >> lane) & 1;
-    const uint64_t below = W.chain & ((1ull << lane) - 1);
-    const uint32_t pl = below ? highbit(below) : lane;
-    const uint32_t prev_end = bpermute(q + W.mlen, pl);
-    const uint32_t lit_start = below ? prev_end : anchor;
-    const uint32_t lit_len = q - lit_start;
+    // match ends increase along the chain, so "end of the previous match" is a prefix max
+    const uint32_t end_incl = wave_incl_max(cl ? q + W.mlen : 0u);
+    const uint32_t end_excl = wave_shr1(end_incl);
+    const uint32_t lit_start = max(anchor, cl ? end_excl : end_incl);
+    const uint32_t lit_len = q - lit_start;  // chain lanes: their literal run
     const uint32_t ml = W.mlen - kMinMatch;
     const bool bad = cl && (lit_len >= 270 || ml >= 270);
     const uint32_t nlx = lit_len >= 15 ? 1u : 0u, nmx = ml >= 15 ? 1u : 0u;
@@ -273,14 +296,15 @@ struct Lz4Out {
       return;
     }
     room(total);
-    const uint32_t o = op + incl - e;  // this lane's sequence start (chain lanes)
-    // a literal lane (not a match start, not inside a match) belongs to the sequence of the
-    // lowest chain lane above it; its byte lands in that sequence's literal run
+    // A literal lane (not a match start, not inside a match) belongs to the sequence of the
+    // lowest chain lane s above it: that sequence starts at op + incl (no chain lane lies
+    // between), its literal run at lit_start (= this lane's prefix max), and its token is
+    // followed by one length byte if the run is >= 15 bytes.
     const uint64_t above = lane == 63 ? 0ull : W.chain & (~0ull << (lane + 1));
-    const uint32_t s = above ? lowbit(above) : lane;
-    const uint32_t s_lit = bpermute(lit_start, s);
-    const uint32_t s_dst = bpermute(o + 1 + nlx - lit_start, s);  // + position = byte slot
-    const bool lit = !cl && above && q >= s_lit;
+    const uint32_t s = lowbit(above);
+    const bool lit = !cl && above && q >= lit_start;
+    const uint32_t lit_nlx = W.x + s - lit_start >= 15 ? 1u : 0u;
+    const uint32_t o = op + incl - e;  // chain lanes: sequence start
     lds_order();
     if (cl) {
       ring[at(o)] = (uint8_t)(((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15));
@@ -290,7 +314,7 @@ struct Lz4Out {
       ring[at(h + 1)] = (uint8_t)(W.off >> 8);
       if (nmx) ring[at(h + 2)] = (uint8_t)(ml - 15);
     }
-    if (lit) ring[at(s_dst + q)] = (uint8_t)W.byte;
+    if (lit) ring[at(op + incl + 1 + lit_nlx + (q - lit_start))] = (uint8_t)W.byte;
     // literals of the first sequence that precede the window (anchor < x): from the ring
     if (anchor < W.x) {
       const uint32_t l0 = lowbit(W.chain);
@@ -417,10 +441,8 @@ struct DflOut {
     const uint32_t lane = lane_id();
     const uint32_t q = W.x + lane;
     const bool cl = (W.chain >> lane) & 1;
-    const uint64_t upto = W.chain & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-    const uint32_t pl = upto ? highbit(upto) : lane;
-    const uint32_t pend = bpermute(q + W.mlen, pl);
-    const bool covered = q < W.pos_in || (upto && !cl && q < pend);
+    const uint32_t pend = wave_incl_max(cl ? q + W.mlen : 0u);  // end of the last match <= q
+    const bool covered = q < W.pos_in || (!cl && q < pend);
     uint32_t val = 0, nb = 0;
     if (cl) val = match_code(W.mlen, W.off, nb);
     else if (!covered && q < n) val = fixed_code(W.byte, nb);
@@ -461,42 +483,41 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
       return v;
     };
     auto write_row = [&](uint32_t r, const uint4& v) __attribute__((always_inline)) {
-      ring16[(rbase + (kRow / 16) * r + lane) & (kInMask >> 4)] = v;
+      const uint32_t blk = (rbase + (kRow / 16) * r + lane) & (kInMask >> 4);
+      ring16[blk] = v;
+      if (blk < kInPad / 16) ring16[kIn / 16 + blk] = v;  // the pad mirrors the ring's head
     };
     uint32_t pos = 0;
     uint32_t F = 0;  // the ring holds positions [F - kIn, F)
-    // one window of 64 positions at x
+    // one window of 64 positions at x; vp = the 16 bytes at x + lane, read during the
+    // previous window (the ring already holds them then)
+    uint4 vp = make_uint4(0, 0, 0, 0);
     auto window = [&](uint32_t x) __attribute__((always_inline)) {
       const uint32_t p = x + lane;
       const bool act = p <= last_start;
-      const uint64_t vp = I.bytes8(p);
-      const uint32_t h = hash4((uint32_t)vp);
+      const uint4 v = vp;
+      const uint32_t h = hash4(v.x);
       const uint32_t cand = act ? table[h] : 0u;
       lds_order();
       if (act) table[h] = (uint16_t)p;
+      lds_order();
+      // read back now, settle same-slot writes at the end of the window
+      const uint32_t back = act ? table[h] : 0u;
+      vp = I.bytes16(p + kWave);  // next window's bytes
       const bool pre = act && cand < p && p - cand <= max_dist;
       uint32_t lim = match_limit - p;
       if (lim > max_mlen) lim = max_mlen;
       uint32_t len = 0;
-      if (pre) {  // verify the 4 bytes and measure up to 8, from the input ring
-        len = common8(vp, I.bytes8(cand));
+      if (pre) {  // verify the 4 bytes and measure up to 16, from the input ring
+        len = common16(v, I.bytes16(cand));
         if (len > lim) len = lim;
       }
-      // same-slot writes of this window: re-write until the largest position holds the slot
-      lds_order();
-      bool redo = act && table[h] < p;
-      while (ballot(redo)) {
-        lds_order();
-        if (redo) table[h] = (uint16_t)p;
-        lds_order();
-        redo = redo && table[h] < p;
-      }
-      // lanes still matching after 8 bytes extend in parallel, up to kPreExt
-      for (uint32_t k = 8; k < kPreExt; k += 8) {
+      // lanes still matching after 16 bytes extend in parallel, up to kPreExt
+      for (uint32_t k = 16; k < kPreExt; k += 16) {
         const bool go = pre && len == k && lim > k;
         if (!ballot(go)) break;
         if (go) {
-          const uint32_t l2 = k + common8(I.bytes8(p + k), I.bytes8(cand + k));
+          const uint32_t l2 = k + common16(I.bytes16(p + k), I.bytes16(cand + k));
           len = l2 < lim ? l2 : lim;
         }
       }
@@ -522,7 +543,7 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
             const uint32_t kk = k + 4u * lane;
             uint32_t cl = 4;
             if (kk < lr) {
-              cl = common4((uint32_t)I.bytes8(i + kk), (uint32_t)I.bytes8(c + kk));
+              cl = common4(I.dword(i + kk), I.dword(c + kk));
               if (cl > lr - kk) cl = lr - kk;
             }
             const uint64_t stop = ballot(kk >= lr || cl < 4);
@@ -567,11 +588,19 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
       W.chain = chain;
       W.mlen = mlen_v;
       W.off = p - cand;
-      W.byte = (uint32_t)vp & 0xFFu;
+      W.byte = v.x & 0xFFu;
       W.pos_in = pos_in;
       em.window(in, I, W, anchor, n);
       if (chain) anchor = pos;
       emitted = pos > x + kWave ? pos : x + kWave;
+      // same-slot writes of this window: re-write until the largest position holds the slot
+      bool redo = act && back < p;
+      while (ballot(redo)) {
+        lds_order();
+        if (redo) table[h] = (uint16_t)p;
+        lds_order();
+        redo = redo && table[h] < p;
+      }
     };
     // Row k+1 goes into the ring at x = 1024 k + 512 (the ring then runs 576..1536 B ahead
     // of the scan); right after, the row register block is reloaded with row k+2, which
@@ -585,6 +614,8 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
     }
     F = kRow - s0;
     I.lo = 0;
+    lds_order();
+    vp = I.bytes16(lane);
     for (uint32_t x = 0; x <= last_start; x += kWave) {
       if ((x & (kRow - 1)) == kRow / 2) {
         const uint32_t k = x / kRow;
@@ -611,7 +642,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
   using namespace cmp;
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
-  __shared__ __attribute__((aligned(16))) uint8_t inring[kIn];
+  __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf];
   const uint32_t i_seg = blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
@@ -639,7 +670,7 @@ __global__ __launch_bounds__(64) void deflate_compress_kernel(
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
   using namespace cmp;
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
-  __shared__ __attribute__((aligned(16))) uint8_t inring[kIn];
+  __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint32_t stage[kBitWords];
   const uint32_t i_seg = blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
