@@ -70,13 +70,16 @@ __device__ __forceinline__ uint4 ld16u(const GMEM uint8_t* p, const GMEM uint8_t
   return make_uint4(funnel(s0, s1, r), funnel(s1, s2, r), funnel(s2, s3, r), funnel(s3, s4, r));
 }
 
+// number of equal leading bytes of two 16-byte little-endian values (branch-free: all four
+// dwords are compared, so the compiler cannot defer the loads behind data-dependent branches)
 __device__ __forceinline__ uint32_t common16(uint4 a, uint4 b) {
   const uint32_t d0 = a.x ^ b.x, d1 = a.y ^ b.y, d2 = a.z ^ b.z, d3 = a.w ^ b.w;
-  if (d0) return __builtin_ctz(d0) >> 3;
-  if (d1) return 4 + (__builtin_ctz(d1) >> 3);
-  if (d2) return 8 + (__builtin_ctz(d2) >> 3);
-  if (d3) return 12 + (__builtin_ctz(d3) >> 3);
-  return 16;
+  uint32_t r = 128;
+  r = d3 ? 96 + __builtin_ctz(d3) : r;
+  r = d2 ? 64 + __builtin_ctz(d2) : r;
+  r = d1 ? 32 + __builtin_ctz(d1) : r;
+  r = d0 ? __builtin_ctz(d0) : r;
+  return r >> 3;
 }
 
 // number of equal leading bytes of two little-endian values
@@ -521,19 +524,24 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
           len = l2 < lim ? l2 : lim;
         }
       }
-      const uint64_t valid = ballot(pre && len >= kMinMatch);
+      // lanes at or past the parse position holding a match, and those of them whose match
+      // reached kPreExt bytes and may go on (cooperative extension during the walk)
       const uint32_t pos_in = pos;
+      const uint32_t start = pos > x ? pos - x : 0u;
+      const bool okl = pre && len >= kMinMatch && lane >= start;
+      const uint64_t valid = ballot(okl);
+      const uint64_t extm = ballot(okl && len == kPreExt && lim > kPreExt);
       uint64_t chain = 0;
       uint32_t mlen_v = len;
-      const uint32_t start = pos > x ? pos - x : 0u;
-      uint64_t m = start < kWave ? valid & (~0ull << start) : 0ull;
+      uint64_t m = valid;
+      uint32_t e = 0;
       while (m) {  // the greedy chain: the next match is the first valid lane past the end
         const uint32_t l = (uint32_t)__builtin_ctzll(m);
-        const uint32_t i = x + l;
         uint32_t mlen = readlane(len, l);
-        uint32_t li = match_limit - i;
-        if (li > max_mlen) li = max_mlen;
-        if (mlen == kPreExt && li > kPreExt) {
+        if ((extm >> l) & 1) {
+          const uint32_t i = x + l;
+          uint32_t li = match_limit - i;
+          if (li > max_mlen) li = max_mlen;
           const uint32_t c = readlane(cand, l);
           // cooperative extension, first from the input ring (4 B per lane per step) up to F
           const uint32_t lr = li < F - i ? li : F - i;
@@ -579,10 +587,10 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
           if (lane == l) mlen_v = mlen;
         }
         chain |= 1ull << l;
-        pos = i + mlen;
-        const uint32_t e = l + mlen;
+        e = l + mlen;
         m = e < kWave ? valid & (~0ull << e) : 0ull;
       }
+      if (chain) pos = x + e;
       Window W;
       W.x = x;
       W.chain = chain;
@@ -594,7 +602,10 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
       if (chain) anchor = pos;
       emitted = pos > x + kWave ? pos : x + kWave;
       // same-slot writes of this window: re-write until the largest position holds the slot
-      bool redo = act && back < p;
+      // (the empty asm pins the read-back's use, and so its wait, here)
+      uint32_t bk = back;
+      __asm__ volatile("" : "+v"(bk));
+      bool redo = act && bk < p;
       while (ballot(redo)) {
         lds_order();
         if (redo) table[h] = (uint16_t)p;
