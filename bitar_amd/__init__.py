@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libbitar_hip.so")
+LIB_PATH = os.environ.get("BITAR_HIP_LIB") or os.path.join(_HERE, "lib", "libbitar_hip.so")
 
 CODEC_LZ4 = 1
 CODEC_DEFLATE = 2

@@ -37,7 +37,15 @@ namespace bitar_hip {
 
 namespace cmp {
 
-constexpr uint32_t kHashLog = 12;
+// Build-time knobs for tuning experiments (scripts/build_variant.sh); the defaults are the
+// shipped configuration and the one the oracle restates.
+#ifndef BITAR_CMP_HASH_LOG
+#define BITAR_CMP_HASH_LOG 12
+#endif
+#ifndef BITAR_CMP_OBUF
+#define BITAR_CMP_OBUF 2048
+#endif
+constexpr uint32_t kHashLog = BITAR_CMP_HASH_LOG;
 constexpr uint32_t kMinMatch = 4;
 constexpr uint32_t kLastLiterals = 5;
 constexpr uint32_t kMfLimit = 12;
@@ -167,10 +175,10 @@ struct Window {
 };
 
 // ---- LZ4 emitter: output staged in an LDS byte ring, flushed in aligned 16-B blocks ----
-constexpr uint32_t kObuf = 2048, kObufMask = kObuf - 1;
+constexpr uint32_t kObuf = BITAR_CMP_OBUF, kObufMask = kObuf - 1;
 
 struct Lz4Out {
-  uint8_t* ring;      // LDS
+  uint8_t* ring;      // LDS, kObuf bytes + one trash byte per lane
   GMEM uint8_t* dst;  // slot
   uint64_t cap;
   uint32_t op, flushed;
@@ -308,16 +316,17 @@ struct Lz4Out {
     const bool lit = !cl && above && q >= lit_start;
     const uint32_t lit_nlx = W.x + s - lit_start >= 15 ? 1u : 0u;
     const uint32_t o = op + incl - e;  // chain lanes: sequence start
+    // every lane stores every byte kind; lanes without one store into their trash byte
+    // past the ring (no exec-mask branches)
+    const uint32_t tr = kObuf + lane;
+    const uint32_t h = o + 1 + nlx + lit_len;
     lds_order();
-    if (cl) {
-      ring[at(o)] = (uint8_t)(((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15));
-      if (nlx) ring[at(o + 1)] = (uint8_t)(lit_len - 15);
-      const uint32_t h = o + 1 + nlx + lit_len;
-      ring[at(h)] = (uint8_t)W.off;
-      ring[at(h + 1)] = (uint8_t)(W.off >> 8);
-      if (nmx) ring[at(h + 2)] = (uint8_t)(ml - 15);
-    }
-    if (lit) ring[at(op + incl + 1 + lit_nlx + (q - lit_start))] = (uint8_t)W.byte;
+    ring[cl ? at(o) : tr] = (uint8_t)(((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15));
+    ring[cl && nlx ? at(o + 1) : tr] = (uint8_t)(lit_len - 15);
+    ring[cl ? at(h) : tr] = (uint8_t)W.off;
+    ring[cl ? at(h + 1) : tr] = (uint8_t)(W.off >> 8);
+    ring[cl && nmx ? at(h + 2) : tr] = (uint8_t)(ml - 15);
+    ring[lit ? at(op + incl + 1 + lit_nlx + (q - lit_start)) : tr] = (uint8_t)W.byte;
     // literals of the first sequence that precede the window (anchor < x): from the ring
     if (anchor < W.x) {
       const uint32_t l0 = lowbit(W.chain);
@@ -340,31 +349,25 @@ __device__ __forceinline__ uint32_t rev(uint32_t v, uint32_t n) {
 }
 // fixed literal/length code of symbol s, bit-reversed for LSB-first packing; *n = length
 __device__ __forceinline__ uint32_t fixed_code(uint32_t s, uint32_t& n) {
-  if (s < 144) { n = 8; return rev(0x30 + s, 8); }
-  if (s < 256) { n = 9; return rev(0x190 + (s - 144), 9); }
-  if (s < 280) { n = 7; return rev(s - 256, 7); }
-  n = 8;
-  return rev(0xC0 + (s - 280), 8);
+  // 0-143: 8 bits 0x30+s; 144-255: 9 bits 0x190+s-144; 256-279: 7 bits s-256;
+  // 280-287: 8 bits 0xC0+s-280 (RFC 1951 3.2.6), as selects
+  const uint32_t code = s < 144 ? 0x30 + s : s < 256 ? 0x190 + (s - 144) : s < 280 ? s - 256 : 0xC0 + (s - 280);
+  n = s < 144 ? 8u : s < 256 ? 9u : s < 280 ? 7u : 8u;
+  return __builtin_bitreverse32(code) >> (32 - n);
 }
 // The whole match symbol -- length code, its extra bits, distance code, its extra bits --
 // LSB first (RFC 1951 3.2.5); mlen in [3, 258], off in [1, 32768]; *n <= 31.
 __device__ __forceinline__ uint32_t match_code(uint32_t mlen, uint32_t off, uint32_t& n) {
   const uint32_t v = mlen - 3;
-  uint32_t lc, le;  // length code (symbol - 257), extra bit count
-  if (mlen == 258) { lc = 28; le = 0; }
-  else if (v < 8) { lc = v; le = 0; }
-  else {
-    le = 29u - __builtin_clz(v);  // floor(log2 v) - 2
-    lc = 4 * le + 4 + ((v >> le) & 3u);
-  }
+  // length code (symbol - 257) and extra bit count; distance code and extra bit count
+  const uint32_t lev = 29u - __builtin_clz(v | 8u);  // floor(log2 v) - 2 for v >= 8
+  const uint32_t le = mlen == 258 || v < 8 ? 0u : lev;
+  const uint32_t lc = mlen == 258 ? 28u : v < 8 ? v : 4 * lev + 4 + ((v >> lev) & 3u);
   const uint32_t lx = v & ((1u << le) - 1);
   const uint32_t d = off - 1;
-  uint32_t dc, de;  // distance code, extra bit count
-  if (d < 4) { dc = d; de = 0; }
-  else {
-    de = 30u - __builtin_clz(d);  // floor(log2 d) - 1
-    dc = 2 * de + 2 + ((d >> de) & 1u);
-  }
+  const uint32_t dev = 30u - __builtin_clz(d | 4u);  // floor(log2 d) - 1 for d >= 4
+  const uint32_t de = d < 4 ? 0u : dev;
+  const uint32_t dc = d < 4 ? d : 2 * dev + 2 + ((d >> dev) & 1u);
   const uint32_t dx = d & ((1u << de) - 1);
   uint32_t ln;
   const uint32_t code = fixed_code(257 + lc, ln);
@@ -403,11 +406,11 @@ struct DflOut {
     if ((bits + total + 7) / 8 > cap) { overflow = true; return; }
     const uint64_t bp = bits + incl - nb;
     const uint32_t w = (uint32_t)(bp >> 5), sh = (uint32_t)(bp & 31);
+    // every lane ORs into both words (zeros where it has nothing): no exec-mask branches
+    const uint32_t spill = sh + nb > 32 ? val >> ((32 - sh) & 31) : 0u;
     lds_order();
-    if (nb) {
-      atomicOr(&stage[w & kBitMask], val << sh);
-      if (sh + nb > 32) atomicOr(&stage[(w + 1) & kBitMask], val >> (32 - sh));
-    }
+    atomicOr(&stage[w & kBitMask], val << sh);
+    atomicOr(&stage[(w + 1) & kBitMask], spill);
     lds_order();
     bits += total;
     const uint32_t full = (uint32_t)(bits >> 5);
@@ -446,10 +449,11 @@ struct DflOut {
     const bool cl = (W.chain >> lane) & 1;
     const uint32_t pend = wave_incl_max(cl ? q + W.mlen : 0u);  // end of the last match <= q
     const bool covered = q < W.pos_in || (!cl && q < pend);
-    uint32_t val = 0, nb = 0;
-    if (cl) val = match_code(W.mlen, W.off, nb);
-    else if (!covered && q < n) val = fixed_code(W.byte, nb);
-    put_lanes(val, nb);
+    uint32_t mb, lb;
+    const uint32_t mv = match_code(cl ? W.mlen : 3u, cl ? W.off : 1u, mb);
+    const uint32_t lv = fixed_code(W.byte, lb);
+    const bool lit = !cl && !covered && q < n;
+    put_lanes(cl ? mv : lit ? lv : 0u, cl ? mb : lit ? lb : 0u);
   }
 };
 
@@ -500,29 +504,28 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
       const bool act = p <= last_start;
       const uint4 v = vp;
       const uint32_t h = hash4(v.x);
-      const uint32_t cand = act ? table[h] : 0u;
+      // Table and ring accesses are issued on all lanes (no exec-mask branches: the scalar
+      // unit is the bottleneck).  Lanes past last_start exist only in the final window;
+      // their table writes are never looked up again.
+      const uint32_t cand = table[h];
       lds_order();
-      if (act) table[h] = (uint16_t)p;
+      table[h] = (uint16_t)p;
       lds_order();
       // read back now, settle same-slot writes at the end of the window
-      const uint32_t back = act ? table[h] : 0u;
+      const uint32_t back = table[h];
       vp = I.bytes16(p + kWave);  // next window's bytes
       const bool pre = act && cand < p && p - cand <= max_dist;
       uint32_t lim = match_limit - p;
       if (lim > max_mlen) lim = max_mlen;
-      uint32_t len = 0;
-      if (pre) {  // verify the 4 bytes and measure up to 16, from the input ring
-        len = common16(v, I.bytes16(cand));
-        if (len > lim) len = lim;
-      }
+      // verify the 4 bytes and measure up to 16, from the input ring
+      const uint32_t c16 = common16(v, I.bytes16(cand));
+      uint32_t len = pre ? (c16 < lim ? c16 : lim) : 0u;
       // lanes still matching after 16 bytes extend in parallel, up to kPreExt
       for (uint32_t k = 16; k < kPreExt; k += 16) {
         const bool go = pre && len == k && lim > k;
         if (!ballot(go)) break;
-        if (go) {
-          const uint32_t l2 = k + common16(I.bytes16(p + k), I.bytes16(cand + k));
-          len = l2 < lim ? l2 : lim;
-        }
+        const uint32_t l2 = k + common16(I.bytes16(p + k), I.bytes16(cand + k));
+        len = go ? (l2 < lim ? l2 : lim) : len;
       }
       // lanes at or past the parse position holding a match, and those of them whose match
       // reached kPreExt bytes and may go on (cooperative extension during the walk)
@@ -654,7 +657,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   using namespace cmp;
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
-  __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf];
+  __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];  // + trash bytes
   const uint32_t i_seg = blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build a tuning variant of libbitar_hip.so: scripts/build_variant.sh NAME "-DKNOB=V ..."
+# -> bitar_amd/lib/variants/libbitar_hip_NAME.so (select it with BITAR_HIP_LIB=...)
+set -e
+cd "$(dirname "$0")/../bitar_amd"
+name=$1; defs=$2
+mkdir -p build_$name lib/variants
+for f in runtime lz4_decompress inflate compress util_kernels; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics $defs -c csrc/$f.hip -o build_$name/$f.o &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o lib/variants/libbitar_hip_$name.so build_$name/*.o
+rm -rf build_$name
+echo lib/variants/libbitar_hip_$name.so
