@@ -17,7 +17,7 @@
 // blocks would make the compiler wait for every load in flight.
 //
 // Per fixed window of 64 positions (one per lane):
-//   1. hash the 4 bytes at every position (from the ring), look up a 4096-entry LDS table of
+//   1. hash the 4 bytes at every position (from the ring), look up a 2048-entry LDS table of
 //      u16 positions, then insert every position (the largest position wins a slot);
 //   2. lanes with a candidate verify + measure the match on 8 bytes from the ring, and
 //      lanes still matching extend in parallel up to 32 bytes;
@@ -40,10 +40,13 @@ namespace cmp {
 // Build-time knobs for tuning experiments (scripts/build_variant.sh); the defaults are the
 // shipped configuration and the one the oracle restates.
 #ifndef BITAR_CMP_HASH_LOG
-#define BITAR_CMP_HASH_LOG 12
+#define BITAR_CMP_HASH_LOG 11
 #endif
 #ifndef BITAR_CMP_OBUF
-#define BITAR_CMP_OBUF 2048
+#define BITAR_CMP_OBUF 1024
+#endif
+#ifndef BITAR_CMP_BITWORDS
+#define BITAR_CMP_BITWORDS 256
 #endif
 constexpr uint32_t kHashLog = BITAR_CMP_HASH_LOG;
 constexpr uint32_t kMinMatch = 4;
@@ -342,7 +345,7 @@ struct Lz4Out {
 };
 
 // ---- fixed-Huffman DEFLATE emitter: LDS bit ring, lane codes placed by prefix sum -----
-constexpr uint32_t kBitWords = 512, kBitMask = kBitWords - 1;
+constexpr uint32_t kBitWords = BITAR_CMP_BITWORDS, kBitMask = kBitWords - 1;
 
 __device__ __forceinline__ uint32_t rev(uint32_t v, uint32_t n) {
   return __builtin_bitreverse32(v) >> (32 - n);
@@ -414,7 +417,7 @@ struct DflOut {
     lds_order();
     bits += total;
     const uint32_t full = (uint32_t)(bits >> 5);
-    if (full - wflushed >= kBitWords - 128) flush_words(full);
+    if (full - wflushed >= kBitWords - 80) flush_words(full);  // a window adds <= 63 words
   }
   __device__ __forceinline__ void put_one(uint32_t val, uint32_t nb) {
     put_lanes(lane_id() == 0 ? val : 0u, lane_id() == 0 ? nb : 0u);
