@@ -25,6 +25,10 @@ namespace lz4d {
 
 using namespace sr;
 
+// stream bytes the batch path may touch past ip: 64 candidate tokens, each with up to two
+// length bytes and <= 60 literals, plus its offset
+constexpr uint32_t kBatchIn = 132;
+
 // 256 stream bytes held in ONE register, dword-packed: lane l holds bytes vb+4l .. vb+4l+3
 // (vb 4-byte aligned in absolute address terms).  The parse reads tokens, extensions and
 // offsets with v_readlane instead of LDS round trips.
@@ -126,66 +130,72 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     // Lanes past the batch write too: their ring slots are >= kRing - 64 behind the output,
     // older than any near source and already flushed, and are rewritten before use.
     for (;;) {
-      if (s.ip + 84 > s.csize || s.op + 64 - s.flushed > kFlushAt) break;
+      if (s.ip + kBatchIn > s.csize || s.op + 64 - s.flushed > kFlushAt) break;
       uint32_t wrel = src_lo + s.ip - (uint32_t)s.wb;  // window index of ip (mod 2^32)
-      if (wrel > kWin - 84) {
-        win_at(s, win, s.ip, 84);
+      if (wrel > kWin - kBatchIn) {
+        win_at(s, win, s.ip, kBatchIn);
         wrel = src_lo + s.ip - (uint32_t)s.wb;
       }
-      // (1) speculative parse, one candidate token per lane
+      // (1) speculative parse, one candidate token per lane: token, optional literal
+      //     length byte, literals, offset, optional match length byte
       lds_order();
       const uint32_t wc = wrel + lane;
       const uint32_t tok = win[wc];
-      const uint32_t cL = tok >> 4, cm4 = tok & 15u;
-      const uint32_t cb0 = win[wc + 1 + cL], cb1 = win[wc + 2 + cL];
+      const uint32_t b1 = win[wc + 1];
+      const uint32_t cm4 = tok & 15u;
+      const bool lx = (tok >> 4) == 15u, mx = cm4 == 15u;
+      const uint32_t cL = lx ? 15u + b1 : tok >> 4;
+      const uint32_t ob = wc + 1 + (lx ? 1u : 0u) + cL;  // offset position
+      const uint32_t cb0 = win[ob], cb1 = win[ob + 1], b2 = win[ob + 2];
       const uint32_t coff = cb0 | (cb1 << 8);
-      const uint32_t colen = cL + cm4 + 4;
-      // eligible: no length extension, real offset, near, and (conservatively, as if this
-      // token opened the batch) not reaching before the segment start
-      const bool csimple = cL < 15 && cm4 < 15 && coff != 0 && coff <= kNearOff &&
-                           coff <= s.op + cL;
-      // nxt (7 bits) | olen, or 127 when not eligible (the walk's one compare then stops)
-      const uint32_t pack = (lane + 3 + cL) | ((csimple ? colen : 127u) << 8);
-      // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
+      const uint32_t cml = 4 + (mx ? 15u + b2 : cm4);
+      const uint32_t colen = cL + cml;
+      // eligible: at most one length byte each (< 255), <= 31 literals, fits a batch, real
+      // offset, near, and (conservatively, as if this token opened the batch) not before the
+      // segment start
+      const bool csimple = (!lx || b1 < 255u) && (!mx || b2 < 255u) && cL <= 31u &&
+                           colen <= 64u && coff != 0 && coff <= kNearOff && coff <= s.op + cL;
+      // the walk's record, one dword: next token lane (7 bits, capped at 64) | olen (7 bits:
+      // output length, 127 when not eligible -- the walk's one compare then stops) |
+      // literal count (5 bits) | offset (13 bits; eligible offsets are <= 8048)
+      const uint32_t nxt = lane + 3 + (lx ? 1u : 0u) + (mx ? 1u : 0u) + cL;
+      const uint32_t pack = (nxt < 64u ? nxt : 64u) | ((csimple ? colen : 127u) << 7) |
+                            ((cL & 31u) << 14) | (coff << 19);
+      // (2) scalar walk over the real tokens (capacity: checked once for the whole batch);
+      // every output lane keeps the record and token lane of the sequence it falls in
       const uint32_t room = s.cap - s.op;
       const uint32_t lim = room < 64 ? room : 64;
       uint32_t k = 0, out = 0;
-      uint32_t seqlane = 0, ostart = 0;  // per output lane: its token lane, its out start
+      uint32_t sel = 0, seqlane = 0, ostart = 0;
       for (;;) {
         const uint32_t e = readlane(pack, k);
-        const uint32_t ol = e >> 8;
+        const uint32_t ol = (e >> 7) & 127u;
         if (out + ol > lim) break;
-        if (lane - out < ol) { seqlane = k; ostart = out; }
+        if (lane - out < ol) { sel = e; seqlane = k; ostart = out; }
         out += ol;
-        k = e & 0xFFu;
+        k = e & 127u;
         if (k >= 64) break;
       }
       if (out == 0) break;
       // (3) sources: window literal / ring history / alias of an earlier lane of the batch
+      // (branch-free: every lane computes both forms)
       const uint32_t t = lane;
-      const uint32_t jL = bpermute_lane(cL, seqlane);
-      const uint32_t joff = bpermute_lane(coff, seqlane);
+      const uint32_t jL = (sel >> 14) & 31u;
+      const uint32_t joff = sel >> 19;
       const uint32_t r = t - ostart;
-      uint32_t addr, alias = 64;  // alias < 64: take lane `alias`'s value
-      if (r < jL) {
-        addr = wrel + seqlane + 1 + r;  // window: literal byte r of token lane seqlane
-      } else {
-        const uint32_t m = r - jL;
-        const float q = floorf(((float)(m & 63u) + 0.5f) * __builtin_amdgcn_rcpf((float)joff));
-        const uint32_t mm = joff <= m ? (m & 63u) - (uint32_t)q * joff : m;
-        const int32_t srel = (int32_t)(ostart + jL + mm) - (int32_t)joff;  // vs op
-        if (srel >= 0) {
-          alias = (uint32_t)srel;
-          addr = 0;
-        } else {
-          addr = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
-        }
-      }
+      const bool is_lit = r < jL;
+      const uint32_t m = r - jL;
+      const float qf = floorf(((float)(m & 63u) + 0.5f) * __builtin_amdgcn_rcpf((float)(joff > 1u ? joff : 1u)));
+      const uint32_t mm = joff <= m ? (m & 63u) - (uint32_t)qf * joff : m;
+      const int32_t srel = (int32_t)(ostart + jL + mm) - (int32_t)joff;  // vs op
+      const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
+      const uint32_t lit_addr = wrel + seqlane + 1 + (jL >= 15u ? 1u : 0u) + r;
+      // bit31: alias (low bits: the source lane); else an LDS byte address
+      uint32_t st = is_lit ? lit_addr : srel >= 0 ? ((uint32_t)srel | 0x80000000u) : hist;
       // pointer doubling until no lane of the batch aliases another (chains strictly descend)
-      uint32_t st = alias < 64 ? (alias | 0x80000000u) : addr;  // bit31: alias, low bits lane
       while (ballot((st & 0x80000000u) != 0u && t < out)) {
         const uint32_t other = bpermute_lane(st, st & 63u);
-        if (st & 0x80000000u) st = other;
+        st = (st & 0x80000000u) ? other : st;
       }
       // (4) one gather, one store
       lds_order();
