@@ -34,63 +34,107 @@ struct Tables {  // LDS
   uint8_t lens[320];
 };
 
-__constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t kLenExtra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
-                                      2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t kDistBase[30] = {1,    2,    3,    4,    5,    7,     9,     13,    17,  25,
-                                       33,   49,   65,   97,   129,  193,   257,   385,   513, 769,
-                                       1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  5,  5,  6,
-                                       6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+// Length and distance symbol bases and extra-bit counts (RFC 1951 3.2.5), computed rather
+// than looked up: a table indexed by a value the compiler cannot prove wave-uniform becomes a
+// per-match vector load from memory.
+__device__ __forceinline__ uint32_t len_extra(uint32_t ls) {  // ls = symbol - 257, 0..28
+  return ls < 8 || ls == 28 ? 0u : (ls - 4) >> 2;
+}
+__device__ __forceinline__ uint32_t len_base(uint32_t ls) {
+  return ls < 8 ? 3 + ls : ls == 28 ? 258u : ((4 + ((ls - 4) & 3u)) << len_extra(ls)) + 3;
+}
+__device__ __forceinline__ uint32_t dist_extra(uint32_t ds) {  // 0..29
+  return ds < 4 ? 0u : (ds - 2) >> 1;
+}
+__device__ __forceinline__ uint32_t dist_base(uint32_t ds) {
+  return ds < 4 ? ds + 1 : ((2 + (ds & 1u)) << dist_extra(ds)) + 1;
+}
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// Wave-uniform LSB-first bit reader over the staged stream.
+// Wave-uniform LSB-first bit reader.  The bit buffer lives in scalar registers; it is
+// refilled 32 bits at a time from a register vector holding 256 stream bytes (lane l:
+// bytes vb+4l .. vb+4l+3), itself reloaded from the LDS stream window every ~250 bytes --
+// no LDS round trip per refill.
+//
+// Reads past the stream's end return zero bits and are not checked per symbol: the decoder
+// checks once, at the end, that it consumed no more than csize*8 bits (a stream that runs
+// short then fails exactly as the oracle's bit-by-bit check makes it fail; zero bits decode
+// to bounded work -- every output is capped by the segment size).
 struct Bits {
   uint64_t buf;   // next bits, LSB first
   uint32_t cnt;   // valid bits in buf
   uint32_t bp;    // next stream byte to load into buf
-  uint64_t used;  // bits consumed so far
+  uint32_t v;     // register vector of stream bytes
+  uint32_t vb;    // stream position of its byte 0 (modular; may sit up to 3 below 0)
 };
 
+__device__ __forceinline__ void bits_reset(Bits& b, uint32_t pos) {
+  b.buf = 0;
+  b.cnt = 0;
+  b.bp = pos;
+  b.vb = 0xFFFFFF00u;  // nothing loaded
+  b.v = 0;
+}
+
 // 4 stream bytes at bp (zeros past csize), as one little-endian word
-__device__ __forceinline__ uint32_t peek4(State& s, uint8_t* win, uint32_t bp) {
-  const uint32_t lane = lane_id();
-  uint32_t avail = bp < s.csize ? s.csize - bp : 0;
-  if (avail > 4) avail = 4;
-  uint32_t v = 0;
-  if (avail) {
-    const uint32_t w = win_at(s, win, bp, avail);
+__device__ __forceinline__ uint32_t peek4(State& s, uint8_t* win, Bits& b, uint32_t bp) {
+  if (bp >= s.csize) return 0u;
+  if (bp - b.vb > 256u - 8u) {  // modular: also when bp < vb
+    const uint64_t abs = (uint64_t)(uintptr_t)(s.src + bp);
+    const uint32_t mis = (uint32_t)(abs & 3u);
+    uint32_t want = s.csize - bp + mis;
+    if (want > 256) want = 256;
+    const uint32_t w = win_at_abs(s, win, abs - mis, want);  // 16-B aligned window
     lds_order();
-    v = lane < avail ? (uint32_t)win[w + lane] : 0u;
+    b.v = *reinterpret_cast<const uint32_t*>(win + w + 4 * lane_id());
+    b.vb = bp - mis;
   }
-  const uint32_t b0 = readlane(v, 0), b1 = readlane(v, 1), b2 = readlane(v, 2), b3 = readlane(v, 3);
-  return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+  const uint32_t k = bp - b.vb;
+  const uint32_t d = k >> 2;
+  const uint64_t w2 = (uint64_t)readlane(b.v, d) | ((uint64_t)readlane(b.v, d + 1) << 32);
+  uint32_t w = (uint32_t)(w2 >> ((k & 3u) * 8));
+  const uint32_t avail = s.csize - bp;
+  if (avail < 4) w &= (1u << (8 * avail)) - 1;
+  return w;
+}
+
+// The reader's scalars are wave-uniform; saying so (readfirstlane of an SGPR value is free)
+// keeps them in SGPRs -- otherwise the divergent per-lane code around them (literal
+// gathering, ring copies) can make the compiler carry them in VGPRs and turn every branch
+// on them into an exec-mask branch.
+__device__ __forceinline__ void bits_uniform(Bits& b) {
+  b.buf = uniform64(b.buf);
+  b.cnt = uniform(b.cnt);
+  b.bp = uniform(b.bp);
+  b.vb = uniform(b.vb);
 }
 
 __device__ __forceinline__ void need(State& s, uint8_t* win, Bits& b, uint32_t n) {
   while (b.cnt < n) {  // n <= 32: at most two refills
-    const uint32_t w = peek4(s, win, b.bp);
+    const uint32_t w = peek4(s, win, b, b.bp);
     b.buf |= (uint64_t)w << b.cnt;
     b.cnt += 32;
     b.bp += 4;
   }
+  bits_uniform(b);
 }
 
 // take n (<= 32) bits; false if that runs past the stream (the oracle's bits_get == -1)
+__device__ __forceinline__ uint64_t used_bits(const Bits& b) { return (uint64_t)b.bp * 8 - b.cnt; }
+
 __device__ __forceinline__ bool take(State& s, uint8_t* win, Bits& b, uint32_t n, uint32_t& v) {
   if (n == 0) { v = 0; return true; }
   need(s, win, b, n);
-  if (b.used + n > (uint64_t)s.csize * 8) return false;
   v = (uint32_t)(b.buf & ((1ull << n) - 1));
   b.buf >>= n;
   b.cnt -= n;
-  b.used += n;
   return true;
 }
 
 // Build the decoding tables of one code from lens[0..n) (LDS).  Returns false if the code is
 // over-subscribed.  fast: 2^fbits entries; count/sym: canonical arrays for long codes.
+// Inlined (at two sites): an out-of-line call would make every value live across it --
+// the bit reader's state included -- sit in callee-saved VGPRs for the whole kernel.
 __device__ __forceinline__ bool build(Tables& t, const uint8_t* lens, uint32_t n, uint16_t* fast, uint32_t fbits,
                       uint16_t* count, uint16_t* sym) {
   const uint32_t lane = lane_id();
@@ -157,29 +201,64 @@ __device__ __forceinline__ bool build(Tables& t, const uint8_t* lens, uint32_t n
   return true;
 }
 
-// Decode one symbol; returns -1 if the code runs past the stream, -2 if unassigned.
-__device__ __forceinline__ int decode(State& s, uint8_t* win, Bits& b, const uint16_t* fast,
-                                      uint32_t fbits, const uint16_t* count, const uint16_t* sym) {
-  need(s, win, b, 15);
+// The literal/length and distance fast tables mirrored in registers (two 16-bit entries
+// per dword, dword d in lane d % 64 of register d / 64): a lookup is a register select and a
+// v_readlane instead of an LDS round trip.
+struct RegTables {
+  uint32_t lit[(1u << kLitFast) / 128];
+  uint32_t dist[(1u << kDistFast) / 128];
+};
+
+__device__ __forceinline__ void load_reg_tables(const Tables& t, RegTables& r) {
+  const uint32_t lane = lane_id();
+  const uint32_t* lf = reinterpret_cast<const uint32_t*>(t.lit_fast);
+  const uint32_t* df = reinterpret_cast<const uint32_t*>(t.dist_fast);
   lds_order();
-  const uint32_t e = uniform((uint32_t)fast[b.buf & ((1u << fbits) - 1)]);
+#pragma unroll
+  for (uint32_t j = 0; j < (1u << kLitFast) / 128; ++j) r.lit[j] = lf[j * kWave + lane];
+#pragma unroll
+  for (uint32_t j = 0; j < (1u << kDistFast) / 128; ++j) r.dist[j] = df[j * kWave + lane];
+}
+
+// register j of r (j uniform) by a select tree on j's bits (written out: a linear select
+// chain gets turned back into an indexed stack array)
+__device__ __forceinline__ uint32_t pick(const uint32_t (&r)[8], uint32_t j) {
+  const bool b0 = j & 1u, b1 = j & 2u, b2 = j & 4u;
+  const uint32_t a0 = b0 ? r[1] : r[0], a1 = b0 ? r[3] : r[2];
+  const uint32_t a2 = b0 ? r[5] : r[4], a3 = b0 ? r[7] : r[6];
+  const uint32_t c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
+  return b2 ? c1 : c0;
+}
+__device__ __forceinline__ uint32_t pick(const uint32_t (&r)[4], uint32_t j) {
+  const bool b0 = j & 1u, b1 = j & 2u;
+  const uint32_t a0 = b0 ? r[1] : r[0], a1 = b0 ? r[3] : r[2];
+  return b1 ? a1 : a0;
+}
+template <uint32_t N>
+__device__ __forceinline__ uint32_t reg_entry(const uint32_t (&r)[N], uint32_t idx) {
+  const uint32_t dw = idx >> 1;
+  const uint32_t v = readlane(pick(r, dw / kWave), dw % kWave);
+  return (idx & 1u) ? v >> 16 : v & 0xFFFFu;
+}
+
+// Decode one symbol; returns -1 if the code runs past the stream, -2 if unassigned.
+// `e` is the fast-table entry of the next fbits bits (0: code longer than fbits).
+__device__ __forceinline__ int decode_entry(State& s, Bits& b, uint32_t e, const uint16_t* count,
+                                            const uint16_t* sym) {
   if (e) {
     const uint32_t len = e >> 9;
-    if (b.used + len > (uint64_t)s.csize * 8) return -1;
     b.buf >>= len;
     b.cnt -= len;
-    b.used += len;
     return (int)(e & 511u);
   }
+  lds_order();
   int code = 0, first = 0, index = 0;
   for (uint32_t len = 1; len <= 15; ++len) {
-    if (b.used + len > (uint64_t)s.csize * 8) return -1;
     code |= (int)((b.buf >> (len - 1)) & 1u);
     const int cnt = (int)uniform((uint32_t)count[len]);
     if (code - cnt < first) {
       b.buf >>= len;
       b.cnt -= len;
-      b.used += len;
       return (int)uniform((uint32_t)sym[index + (code - first)]);
     }
     index += cnt;
@@ -190,14 +269,31 @@ __device__ __forceinline__ int decode(State& s, uint8_t* win, Bits& b, const uin
   return -2;
 }
 
+__device__ __forceinline__ int decode(State& s, uint8_t* win, Bits& b, const uint16_t* fast,
+                                      uint32_t fbits, const uint16_t* count, const uint16_t* sym) {
+  need(s, win, b, 15);
+  lds_order();
+  const uint32_t e = uniform((uint32_t)fast[b.buf & ((1u << fbits) - 1)]);
+  return decode_entry(s, b, e, count, sym);
+}
+template <uint32_t N>
+__device__ __forceinline__ int decode_reg(State& s, uint8_t* win, Bits& b, const uint32_t (&r)[N],
+                                          uint32_t fbits, const uint16_t* count, const uint16_t* sym) {
+  need(s, win, b, 15);
+  const uint32_t e = reg_entry(r, (uint32_t)b.buf & ((1u << fbits) - 1));
+  return decode_entry(s, b, e, count, sym);
+}
+
 // pending literals, one per lane, written to the ring 64 at a time
 struct Lits {
   uint32_t v;  // lane j: j-th pending byte
   uint32_t n;
 };
 
-__device__ __forceinline__ void lits_flush(State& s, uint8_t* ring, Lits& L) {
-  if (!L.n) return;
+// false if the literals would overflow the segment (checked here, once per 64 literals)
+__device__ __forceinline__ bool lits_flush(State& s, uint8_t* ring, Lits& L) {
+  if (!L.n) return true;
+  if (s.op + L.n > s.cap) return false;
   make_room(s, ring, L.n);
   const uintptr_t base = (uintptr_t)s.dst;
   lds_order();
@@ -205,30 +301,35 @@ __device__ __forceinline__ void lits_flush(State& s, uint8_t* ring, Lits& L) {
   lds_order();
   s.op += L.n;
   L.n = 0;
+  return true;
 }
 
 __device__ __forceinline__ int inflate_codes(State& s, uint8_t* win, uint8_t* ring, Bits& b, Tables& t,
                              Lits& L) {
+  RegTables rt;
+  load_reg_tables(t, rt);
   for (;;) {
-    const int sym = decode(s, win, b, t.lit_fast, kLitFast, t.lit_count, t.lit_sym);
+    bits_uniform(b);
+    s.op = uniform(s.op);
+    L.n = uniform(L.n);
+    const int sym = decode_reg(s, win, b, rt.lit, kLitFast, t.lit_count, t.lit_sym);
     if (sym < 0) return -1;
     if (sym < 256) {
-      if (s.op + L.n >= s.cap) return -1;
       if (lane_id() == L.n) L.v = (uint32_t)sym;
-      if (++L.n == kWave) lits_flush(s, ring, L);
+      if (++L.n == kWave && !lits_flush(s, ring, L)) return -1;
       continue;
     }
     if (sym == 256) return 0;
     const uint32_t ls = (uint32_t)sym - 257;
     if (ls >= 29) return -1;
     uint32_t e;
-    if (!take(s, win, b, kLenExtra[ls], e)) return -1;
-    const uint32_t len = kLenBase[ls] + e;
-    const int ds = decode(s, win, b, t.dist_fast, kDistFast, t.dist_count, t.dist_sym);
+    if (!take(s, win, b, len_extra(ls), e)) return -1;
+    const uint32_t len = len_base(ls) + e;
+    const int ds = decode_reg(s, win, b, rt.dist, kDistFast, t.dist_count, t.dist_sym);
     if (ds < 0 || ds >= 30) return -1;
-    if (!take(s, win, b, kDistExtra[ds], e)) return -1;
-    const uint32_t d = kDistBase[ds] + e;
-    lits_flush(s, ring, L);
+    if (!take(s, win, b, dist_extra((uint32_t)ds), e)) return -1;
+    const uint32_t d = dist_base((uint32_t)ds) + e;
+    if (!lits_flush(s, ring, L)) return -1;
     if (d > s.op) return -1;
     if (s.op + len > s.cap) return -1;
     match_copy(s, ring, d, len);
@@ -262,7 +363,8 @@ __global__ __launch_bounds__(64) void inflate_kernel(
   s.wb = ~0ull;
   s.wlen = 0;
 
-  Bits b = {0ull, 0u, 0u, 0ull};
+  Bits b;
+  bits_reset(b, 0);
   Lits L = {0u, 0u};
   bool ok = true;
   uint32_t last = 0;
@@ -273,44 +375,45 @@ __global__ __launch_bounds__(64) void inflate_kernel(
     last = hdr & 1u;
     const uint32_t type = hdr >> 1;
     if (type == 0) {  // stored: LEN, NLEN at the next byte boundary, then LEN raw bytes
-      const uint32_t drop = (uint32_t)(b.used & 7u) ? 8u - (uint32_t)(b.used & 7u) : 0u;
+      const uint32_t drop = b.cnt & 7u;  // bits up to the next byte boundary
       uint32_t junk;
       if (drop && !take(s, win, b, drop, junk)) { ok = false; break; }
-      const uint32_t p = (uint32_t)(b.used >> 3);
+      const uint32_t p = (uint32_t)(used_bits(b) >> 3);
       if ((uint64_t)p + 4 > s.csize) { ok = false; break; }
       uint32_t w0;
       take(s, win, b, 32, w0);
       const uint32_t len = w0 & 0xFFFFu, nlen = w0 >> 16;
       if (len != (~nlen & 0xFFFFu)) { ok = false; break; }
       if ((uint64_t)p + 4 + len > s.csize) { ok = false; break; }
-      lits_flush(s, ring, L);
+      if (!lits_flush(s, ring, L)) { ok = false; break; }
       if ((uint64_t)s.op + len > s.cap) { ok = false; break; }
       s.ip = p + 4;
       if (len >= kLongLit) literals_long(s, win, ring, len);
       else if (len) literals_short(s, win, ring, len);
-      b.buf = 0;  // restart the bit reader after the raw bytes
-      b.cnt = 0;
-      b.bp = s.ip;
-      b.used = (uint64_t)s.ip * 8;
-    } else if (type == 1) {
-      if (!built_fixed) {
+      bits_reset(b, s.ip);  // restart the bit reader after the raw bytes
+    } else if (type == 1 || type == 2) {
+    uint32_t nlen = 288, ndist = 30;
+    bool need_build = true;
+    if (type == 1) {
+      if (built_fixed) {
+        need_build = false;
+      } else {
         lds_order();
         for (uint32_t k = lane; k < 320; k += kWave)
           t.lens[k] = k < 144 ? 8 : k < 256 ? 9 : k < 280 ? 7 : k < 288 ? 8 : 5;
         lds_order();
-        build(t, t.lens, 288, t.lit_fast, kLitFast, t.lit_count, t.lit_sym);
-        build(t, t.lens + 288, 30, t.dist_fast, kDistFast, t.dist_count, t.dist_sym);
-        built_fixed = 1;
       }
-      if (inflate_codes(s, win, ring, b, t, L)) { ok = false; break; }
-    } else if (type == 2) {
+      built_fixed = 1;
+    } else {
       built_fixed = 0;
       uint32_t hlit, hdist, hclen;
       if (!take(s, win, b, 5, hlit) || !take(s, win, b, 5, hdist) || !take(s, win, b, 4, hclen)) {
         ok = false;
         break;
       }
-      const uint32_t nlen = hlit + 257, ndist = hdist + 1, ncode = hclen + 4;
+      nlen = hlit + 257;
+      ndist = hdist + 1;
+      const uint32_t ncode = hclen + 4;
       if (nlen > 286 || ndist > 30) { ok = false; break; }
       lds_order();
       if (lane < 19) t.lens[lane] = 0;
@@ -359,20 +462,28 @@ __global__ __launch_bounds__(64) void inflate_kernel(
       if (bad) { ok = false; break; }
       lds_order();
       if (uniform((uint32_t)t.lens[256]) == 0) { ok = false; break; }
-      // the distance lengths must not alias the scratch the literal build uses
-      if (!build(t, t.lens, nlen, t.lit_fast, kLitFast, t.lit_count, t.lit_sym)) { ok = false; break; }
-      if (!build(t, t.lens + nlen, ndist, t.dist_fast, kDistFast, t.dist_count, t.dist_sym)) {
-        ok = false;
-        break;
+    }
+    // literal/length then distance tables: one build site for fixed and dynamic blocks
+    if (need_build) {
+      for (uint32_t j = 0; j < 2 && ok; ++j) {
+        const bool d = j == 1;
+        ok = build(t, d ? t.lens + nlen : t.lens, d ? ndist : nlen, d ? t.dist_fast : t.lit_fast,
+                   d ? kDistFast : kLitFast, d ? t.dist_count : t.lit_count,
+                   d ? t.dist_sym : t.lit_sym);
       }
-      if (inflate_codes(s, win, ring, b, t, L)) { ok = false; break; }
+      if (!ok) break;
+    }
     } else {
       ok = false;
       break;
     }
+    // one call site for the Huffman-coded body of fixed and dynamic blocks
+    if (type != 0 && inflate_codes(s, win, ring, b, t, L)) { ok = false; break; }
   } while (!last);
+  // the stream must hold every bit the decode consumed (reads past its end returned zeros)
+  if (ok && used_bits(b) > (uint64_t)s.csize * 8) ok = false;
+  if (ok && !lits_flush(s, ring, L)) ok = false;
   if (ok) {
-    lits_flush(s, ring, L);
     flush(s, ring, s.op, true);
     if (lane == 0) produced[i] = s.op;
   } else if (lane == 0) {
