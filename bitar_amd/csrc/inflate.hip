@@ -304,19 +304,148 @@ __device__ __forceinline__ bool lits_flush(State& s, uint8_t* ring, Lits& L) {
   return true;
 }
 
+// Move the reader to absolute stream bit `bit` (the batch path's position).
+__device__ __forceinline__ void seek(State& s, uint8_t* win, Bits& b, uint64_t bit) {
+  b.buf = 0;
+  b.cnt = 0;
+  b.bp = (uint32_t)(bit >> 3);
+  const uint32_t skip = (uint32_t)(bit & 7u);
+  if (skip) {
+    need(s, win, b, skip);
+    b.buf >>= skip;
+    b.cnt -= skip;
+  }
+  bits_uniform(b);
+}
+
+// Batch path for Huffman-coded block bodies: up to 64 output bytes per step.
+//   1. every lane decodes, speculatively, the symbol starting at 4 candidate bit offsets
+//      (lane, lane+64, lane+128, lane+192 past the current position): literal, or length +
+//      distance with their extra bits, from the LDS fast tables -- two LDS round trips for
+//      all 256 candidates;
+//   2. a scalar walk follows the real symbol chain (one v_readlane per symbol; the walk over
+//      candidates of register j is unrolled so each register is read statically);
+//   3. each output lane takes its byte from its symbol: the literal itself, history in the
+//      ring, or (match source inside this batch) another lane, resolved by pointer doubling;
+//      one ds_read gathers, one ds_write stores.
+// Symbols it does not take (end of block, codes longer than the fast tables, matches longer
+// than 64 or farther than the ring, anything invalid) stop it; the scalar path decodes them.
+constexpr uint32_t kBatchStreamBytes = 48;  // stream bytes past the position a batch may read
+
+__device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring, Bits& b,
+                                           const Tables& t) {
+  const uint32_t lane = lane_id();
+  const uint32_t base = (uint32_t)(uintptr_t)s.dst;  // ring index = absolute address & mask
+  const uint64_t src_abs = (uint64_t)(uintptr_t)s.src;
+  uint64_t P = used_bits(b);
+  bool moved = false;
+  for (;;) {
+    const uint32_t room = s.cap - s.op;
+    const uint32_t byte0 = (uint32_t)(P >> 3);
+    if (room == 0 || byte0 + kBatchStreamBytes > s.csize) break;
+    make_room(s, ring, 64);
+    const uint64_t a0 = (src_abs + byte0) & ~3ull;
+    win_at_abs(s, win, a0, kBatchStreamBytes + 8);
+    const uint64_t absbit0 = (src_abs + byte0) * 8 + (P & 7u);
+    const uint32_t wd = (uint32_t)(s.wb >> 2);  // window base, in absolute dwords
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win);
+    // (1) speculative decode of 4 candidates per lane
+    uint32_t rec[4];
+    lds_order();
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t c = lane + kWave * j;
+      const uint64_t ab = absbit0 + c;
+      const uint32_t di = (uint32_t)(ab >> 5) - wd, sh = (uint32_t)(ab & 31u);
+      const uint32_t d0 = w32[di], d1 = w32[di + 1], d2 = w32[di + 2];
+      const uint64_t bits = (uint64_t)__builtin_amdgcn_alignbit(d1, d0, sh) |
+                            ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32);
+      const uint32_t e = t.lit_fast[(uint32_t)bits & ((1u << kLitFast) - 1)];
+      const uint32_t l1 = e >> 9, sym = e & 511u;
+      const bool is_lit = e != 0 && sym < 256;
+      const uint32_t ls = sym - 257;
+      const bool is_len = e != 0 && sym > 256 && ls < 29;
+      const uint32_t lsc = is_len ? ls : 0u;
+      const uint32_t le = len_extra(lsc);
+      const uint32_t mlen = len_base(lsc) + ((uint32_t)(bits >> l1) & ((1u << le) - 1));
+      const uint32_t o2 = l1 + le;
+      const uint32_t e2 = t.dist_fast[(uint32_t)(bits >> o2) & ((1u << kDistFast) - 1)];
+      const uint32_t dl = e2 >> 9, ds = e2 & 511u;
+      const uint32_t dsc = ds < 30 ? ds : 0u;
+      const uint32_t de = dist_extra(dsc);
+      const uint32_t dist = dist_base(dsc) + ((uint32_t)(bits >> (o2 + dl)) & ((1u << de) - 1));
+      const bool m_ok = is_len && e2 != 0 && ds < 30 && mlen <= 64 && dist <= kNearOff &&
+                        dist <= s.op;
+      const uint32_t nb = is_lit ? l1 : o2 + dl + de;
+      const uint32_t olen = is_lit ? 1u : m_ok ? mlen : 127u;
+      const uint32_t payload = is_lit ? sym : (0x8000u | dist);
+      // record: next candidate (9 bits) | olen (7 bits, 127 = stop) | payload (16 bits:
+      // literal byte, or 0x8000 | distance)
+      rec[j] = ((c + nb) & 511u) | (olen << 9) | (payload << 16);
+    }
+    // (2) scalar walk over the real symbols
+    const uint32_t lim = room < 64 ? room : 64;
+    uint32_t k = 0, out = 0, sel = 0, ostart = 0;
+    bool stop = false, taken_all = true;  // taken_all: stopped only because the batch is full
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      while (!stop && k < kWave * (j + 1)) {
+        const uint32_t e = readlane(rec[j], k & 63u);
+        const uint32_t ol = (e >> 9) & 127u;
+        if (out + ol > lim) {
+          stop = true;
+          taken_all = ol != 127u && lim == 64u;
+          break;
+        }
+        if (lane - out < ol) { sel = e; ostart = out; }
+        out += ol;
+        k = e & 511u;
+      }
+    }
+    if (out == 0) break;
+    // (3) sources: the literal / ring history / an earlier lane of this batch
+    const uint32_t payload = sel >> 16;
+    const bool lit = (payload & 0x8000u) == 0;
+    const uint32_t dist = payload & 0x1FFFu;
+    const uint32_t r = lane - ostart;
+    const float qf = floorf(((float)(r & 63u) + 0.5f) * __builtin_amdgcn_rcpf((float)(dist > 1u ? dist : 1u)));
+    const uint32_t mm = dist <= r ? (r & 63u) - (uint32_t)qf * dist : r;
+    const int32_t srel = (int32_t)(ostart + mm) - (int32_t)dist;  // vs op
+    const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
+    // bit31: alias (low bits: source lane); bit30: literal (low byte); else an LDS address
+    uint32_t st = lit ? (0x40000000u | (payload & 255u))
+                      : srel >= 0 ? ((uint32_t)srel | 0x80000000u) : hist;
+    while (ballot((st & 0x80000000u) != 0u && lane < out)) {
+      const uint32_t other = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((st & 63u) << 2), (int)st);
+      st = (st & 0x80000000u) ? other : st;
+    }
+    lds_order();
+    const uint32_t v = (st & 0x40000000u) ? (st & 255u) : (uint32_t)win[st & 0x3FFFu];
+    if (lane < out) ring[(base + s.op + lane) & kRingMask] = (uint8_t)v;
+    lds_order();
+    s.op += out;
+    P += k;
+    moved = true;
+    if (!taken_all) break;  // stopped on a symbol the batch does not take
+  }
+  if (moved) seek(s, win, b, P);
+}
+
 __device__ __forceinline__ int inflate_codes(State& s, uint8_t* win, uint8_t* ring, Bits& b, Tables& t,
                              Lits& L) {
   RegTables rt;
   load_reg_tables(t, rt);
   for (;;) {
+    if (!lits_flush(s, ring, L)) return -1;
+    huff_batch(s, win, ring, b, t);
     bits_uniform(b);
     s.op = uniform(s.op);
-    L.n = uniform(L.n);
+    // one symbol on the scalar path
     const int sym = decode_reg(s, win, b, rt.lit, kLitFast, t.lit_count, t.lit_sym);
     if (sym < 0) return -1;
     if (sym < 256) {
       if (lane_id() == L.n) L.v = (uint32_t)sym;
-      if (++L.n == kWave && !lits_flush(s, ring, L)) return -1;
+      ++L.n;
       continue;
     }
     if (sym == 256) return 0;
