@@ -99,10 +99,7 @@ static inline uint32_t rd32(const uint8_t* p) {
 }
 static inline uint32_t bo_hash(uint32_t v) { return (v * 2654435761u) >> (32 - BO_HASH_LOG); }
 
-typedef void (*bo_emit_fn)(void* ctx, uint32_t lit_start, uint32_t lit_len, uint32_t off,
-                           uint32_t mlen);
-
-static void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist,
+void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist,
                             uint32_t max_mlen, bo_emit_fn emit, void* ctx) {
   uint32_t anchor = 0;
   if (n >= BO_MFLIMIT + 1) {
@@ -188,6 +185,7 @@ static void lz4_emit(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t 
  * DEFLATE 32768; the cap costs ~1-2% ratio on the synthetic corpora (DESIGN.md
  * "Window-scan parse"). */
 #define BO_MAX_DIST 6656u
+_Static_assert(BO_MAX_DIST == BO_MAX_DIST_ALL, "one distance cap for all codecs");
 
 int bo_lz4_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
                           uint32_t* csize) {
@@ -499,6 +497,9 @@ static void* bo_worker(void* arg) {
       if (j->codec == BO_CODEC_LZ4)
         r = bo_lz4_compress_block(j->in + off, len, j->slab + (uint64_t)i * j->stride, cap,
                                   &j->sizes[i]);
+      else if (j->codec == BO_CODEC_ZSTD)
+        r = bo_zstd_compress_block(j->in + off, len, j->slab + (uint64_t)i * j->stride, cap,
+                                   &j->sizes[i]);
       else
         r = bo_deflate_fixed_block(j->in + off, len, j->slab + (uint64_t)i * j->stride, cap,
                                    &j->sizes[i]);
@@ -507,6 +508,8 @@ static void* bo_worker(void* arg) {
       if (j->codec == BO_CODEC_LZ4)
         r = bo_lz4_decompress_block(j->srcs[i], j->csizes[i], j->out + off, j->seg,
                                     &j->produced[i]);
+      else if (j->codec == BO_CODEC_ZSTD)
+        r = bo_zstd_decompress(j->srcs[i], j->csizes[i], j->out + off, j->seg, &j->produced[i]);
       else
         r = bo_inflate_raw(j->srcs[i], j->csizes[i], j->out + off, j->seg, &j->produced[i]);
     }
@@ -540,8 +543,9 @@ static int bo_run(bo_job* proto, int threads) {
 int bo_compress(int codec, const uint8_t* in, uint64_t n, uint32_t seg, uint8_t* slab,
                 uint64_t slot_stride, uint32_t* sizes, uint32_t* nseg_out, int threads) {
   if (seg == 0) return BO_ERR_INVALID;
-  if (codec == BO_CODEC_LZ4 && seg > 65536u) return BO_ERR_INVALID;
-  if (codec != BO_CODEC_LZ4 && codec != BO_CODEC_DEFLATE) return BO_ERR_NOT_IMPLEMENTED;
+  if ((codec == BO_CODEC_LZ4 || codec == BO_CODEC_ZSTD) && seg > 65536u) return BO_ERR_INVALID;
+  if (codec != BO_CODEC_LZ4 && codec != BO_CODEC_DEFLATE && codec != BO_CODEC_ZSTD)
+    return BO_ERR_NOT_IMPLEMENTED;
   uint32_t nseg = (uint32_t)((n + seg - 1) / seg); /* device.cc:169-172 */
   *nseg_out = nseg;
   if (n == 0) return BO_OK; /* empty input -> empty BufferVector (device.cc:161-164) */
@@ -558,7 +562,8 @@ int bo_decompress(int codec, const uint8_t* const* srcs, const uint32_t* sizes, 
   *out_size = 0;
   if (nseg == 0) return BO_OK; /* device.cc:244-246 */
   if (capacity < (uint64_t)nseg * seg) return BO_ERR_CAPACITY; /* device.cc:248-254 */
-  if (codec != BO_CODEC_LZ4 && codec != BO_CODEC_DEFLATE) return BO_ERR_NOT_IMPLEMENTED;
+  if (codec != BO_CODEC_LZ4 && codec != BO_CODEC_DEFLATE && codec != BO_CODEC_ZSTD)
+    return BO_ERR_NOT_IMPLEMENTED;
   bo_job j;
   memset(&j, 0, sizeof(j));
   j.codec = codec; j.mode = 1; j.seg = seg; j.srcs = srcs; j.csizes = sizes; j.out = out;

@@ -47,7 +47,7 @@ enum {
   BO_ERR_NOT_IMPLEMENTED = -10
 };
 
-enum { BO_CODEC_LZ4 = 1, BO_CODEC_DEFLATE = 2 };
+enum { BO_CODEC_LZ4 = 1, BO_CODEC_DEFLATE = 2, BO_CODEC_ZSTD = 3 };
 
 /* Configuration::UpdateCompressedSegSize (src/config.cc:59-73). */
 uint32_t bo_compressed_seg_size(uint32_t decompressed_seg_size);
@@ -72,6 +72,26 @@ int bo_inflate_raw(const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t ca
  * (the exact stream the HIP kernel emits). */
 int bo_deflate_fixed_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
                            uint32_t* csize);
+
+/* ---- Zstandard (RFC 8878), bitar_zstd.c ------------------------------------------ */
+/* Decode one Zstandard frame (no dictionary; content checksum verified). */
+int bo_zstd_decompress(const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t cap,
+                       uint32_t* produced);
+uint64_t bo_xxh64(const uint8_t* p, uint64_t len, uint64_t seed);
+/* Encode one segment as one Zstandard frame, exactly as the HIP kernel does (bitar
+ * window-scan parse; blocks of <= 512 sequences; raw literals; predefined FSE sequence
+ * codes; no repeat offsets; a block that does not shrink is stored raw).  cap must be
+ * >= bo_zstd_bound(n). */
+uint32_t bo_zstd_bound(uint32_t n);
+int bo_zstd_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
+                           uint32_t* csize);
+
+/* internal: the shared window-scan parse (bitar_oracle.c) */
+typedef void (*bo_emit_fn)(void* ctx, uint32_t lit_start, uint32_t lit_len, uint32_t off,
+                           uint32_t mlen);
+void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t max_mlen,
+                     bo_emit_fn emit, void* ctx);
+#define BO_MAX_DIST_ALL 6656u
 
 /* ---- segment-level restatement of CompressDevice ------------------------------- */
 /* Compress (device.cc:156-238): cut `in` into ceil(n/seg) segments in order, compress each

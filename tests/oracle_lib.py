@@ -14,6 +14,7 @@ ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "libbitar_oracle.so")
 
 CODEC_LZ4 = 1
 CODEC_DEFLATE = 2
+CODEC_ZSTD = 3
 
 BO_OK = 0
 BO_ERR_INVALID = -4
@@ -38,8 +39,10 @@ def lib():
         L.bo_lz4_bound.argtypes = [ctypes.c_uint32]
         L.bo_deflate_bound.restype = ctypes.c_uint32
         L.bo_deflate_bound.argtypes = [ctypes.c_uint32]
+        L.bo_zstd_bound.restype = ctypes.c_uint32
+        L.bo_zstd_bound.argtypes = [ctypes.c_uint32]
         for name in ("bo_lz4_decompress_block", "bo_lz4_compress_block", "bo_inflate_raw",
-                     "bo_deflate_fixed_block"):
+                     "bo_deflate_fixed_block", "bo_zstd_decompress", "bo_zstd_compress_block"):
             f = getattr(L, name)
             f.restype = ctypes.c_int
             f.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32,
@@ -104,6 +107,18 @@ def inflate(src, cap):
 
 def deflate_fixed(src):
     return _block(lib().bo_deflate_fixed_block, src, deflate_bound(len(src)))
+
+
+def zstd_bound(n):
+    return int(lib().bo_zstd_bound(n))
+
+
+def zstd_decompress(src, cap):
+    return _block(lib().bo_zstd_decompress, src, cap)
+
+
+def zstd_compress(src):
+    return _block(lib().bo_zstd_compress_block, src, zstd_bound(len(src)))
 
 
 def compress_segments(codec, data, seg, stride, threads=1):

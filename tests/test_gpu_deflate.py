@@ -20,7 +20,8 @@ torch = pytest.importorskip("torch")
 
 
 def test_inflate_all_golden(eng):
-    vecs = [(e, blob, plain) for e, blob, plain in golden_lib.vectors("deflate")]
+    vecs = [(e, blob, plain) for e, blob, plain in golden_lib.vectors("deflate")
+            if len(plain) <= 65536]  # one segment each (larger inputs: oracle tests)
     seg = 65536
     blobs = [blob for _, blob, _ in vecs]
     ok, out, prod = _decode_blobs(eng, O.CODEC_DEFLATE, blobs, seg)

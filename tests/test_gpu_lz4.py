@@ -73,7 +73,8 @@ def _decode_blobs(eng, codec, blobs, seg):
 
 
 def test_decode_all_golden_lz4(eng):
-    vecs = [(e, blob, plain) for e, blob, plain in golden_lib.vectors("lz4")]
+    vecs = [(e, blob, plain) for e, blob, plain in golden_lib.vectors("lz4")
+            if len(plain) <= 65536]  # one segment each (larger inputs: oracle tests)
     seg = 65536
     blobs = [blob for _, blob, _ in vecs]
     ok, out, prod = _decode_blobs(eng, O.CODEC_LZ4, blobs, seg)

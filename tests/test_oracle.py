@@ -153,3 +153,62 @@ def test_segment_empty_and_capacity():
     blobs = [slab[i * 4096:i * 4096 + int(sizes[i])] for i in range(sizes.size)]
     r, _, _ = O.decompress_segments(O.CODEC_LZ4, blobs, 2048, 3 * 2048 - 1)
     assert r == O.BO_ERR_CAPACITY  # capacity < n*seg (248-254)
+
+
+# ---- Zstandard (oracle/bitar_zstd.c) -----------------------------------------------------
+def _libzstd():
+    try:
+        L = ctypes.CDLL("/opt/conda/lib/libzstd.so.1.4.9")
+    except OSError:
+        pytest.skip("libzstd not present")
+    L.ZSTD_decompress.restype = ctypes.c_size_t
+    L.ZSTD_decompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                  ctypes.c_size_t]
+    L.ZSTD_isError.restype = ctypes.c_uint
+    L.ZSTD_isError.argtypes = [ctypes.c_size_t]
+    return L
+
+
+def test_oracle_zstd_decodes_all_golden():
+    n = 0
+    for e, blob, plain in golden_lib.vectors("zstd"):
+        r, out = O.zstd_decompress(blob, max(len(plain), 1))
+        assert r == 0, (e["producer"], e["input"])
+        assert out == plain, (e["producer"], e["input"])
+        n += 1
+    assert n >= 300
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5, 6])
+def test_libzstd_decodes_oracle_frames(kind):
+    Z = _libzstd()
+    for n in (0, 1, 12, 13, 100, 255, 256, 257, 4096, 59460, 65536):
+        data = O.fill(kind, 9, n).tobytes()
+        r, frame = O.zstd_compress(data)
+        assert r == 0 and len(frame) <= O.zstd_bound(n)
+        out = ctypes.create_string_buffer(max(n, 1))
+        rr = Z.ZSTD_decompress(out, max(n, 1), frame, len(frame))
+        assert not Z.ZSTD_isError(rr) and out.raw[:rr] == data, (kind, n)
+        r2, back = O.zstd_decompress(frame, max(n, 1))
+        assert r2 == 0 and back == data
+
+
+def test_oracle_zstd_rejects_malformed():
+    data = O.fill(O.KIND_MIXED, 3, 20000).tobytes()
+    r, frame = O.zstd_compress(data)
+    assert r == 0
+    bad = [frame[:3], frame[:len(frame) // 2], frame[:-1], frame + b"\x00",
+           b"\x28\xb5\x2f\xfe" + frame[4:],               # magic
+           frame[:4] + bytes([frame[4] | 8]) + frame[5:]]  # reserved header bit
+    for b in bad:
+        r, _ = O.zstd_decompress(b, 20000)
+        assert r != 0
+    # capacity: a frame larger than the segment slot is an error, not a truncation
+    r, _ = O.zstd_decompress(frame, 19999)
+    assert r != 0
+    # content checksum: flip one checksum bit in a libzstd +checksum vector
+    for e, blob, plain in golden_lib.vectors("zstd"):
+        if "checksum" in e["producer"] and len(plain) > 100:
+            r, _ = O.zstd_decompress(blob[:-1] + bytes([blob[-1] ^ 1]), len(plain))
+            assert r != 0
+            break
