@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("BITAR_HIP_LIB") or os.path.join(_HERE, "lib", "libbit
 
 CODEC_LZ4 = 1
 CODEC_DEFLATE = 2
+CODEC_ZSTD = 3
 SEGMENT_ERROR = 0xFFFFFFFF
 MAX_SEG_SIZE = 65536
 

@@ -24,6 +24,9 @@ __global__ void deflate_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint
 __global__ void inflate_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
                                uint32_t*);
+__global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
+                                       const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                       uint32_t*, uint32_t*);
 __global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t*);
 __global__ void pack_kernel(const uint8_t*, uint64_t, const uint32_t*, const uint64_t*, uint32_t,
                             uint8_t*);
@@ -163,6 +166,8 @@ uint64_t bitar_hip_slot_size(uint32_t codec, uint32_t seg) {
     bound = (uint64_t)seg + seg / 255u + 16u;           // LZ4_compressBound
   else if (codec == BITAR_HIP_CODEC_DEFLATE)
     bound = ((uint64_t)seg * 9 + 7) / 8 + 16u;          // fixed Huffman, 9 bits/literal
+  else if (codec == BITAR_HIP_CODEC_ZSTD)  // frame header + raw-literal blocks of <= 512 seqs
+    bound = (uint64_t)seg + 7u + 3u * ((uint64_t)seg / 2048u + 2u) + 8u;
   else
     return 0;
   return (bound + 255u) & ~(uint64_t)255u;
@@ -273,7 +278,8 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            const uint32_t* d_sizes, uint32_t nseg, uint32_t seg, void* d_out,
                            uint64_t capacity, uint32_t* d_produced) {
   if (int r = enter(ctx)) return r;
-  if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE)
+  if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE &&
+      codec != BITAR_HIP_CODEC_ZSTD)
     return fail(BITAR_HIP_NOT_IMPLEMENTED, "unknown codec");
   if (nseg == 0) return 0;  // reference device.cc:244-246
   if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
@@ -291,9 +297,12 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
   if (codec == BITAR_HIP_CODEC_LZ4)
     hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
                        stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
-  else
+  else if (codec == BITAR_HIP_CODEC_DEFLATE)
     hipLaunchKernelGGL(bitar_hip::inflate_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
                        stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
+  else
+    hipLaunchKernelGGL(bitar_hip::zstd_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs,
+                       slab, stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
   HIP_TRY(hipGetLastError(), "decompress launch");
   return 0;
 }

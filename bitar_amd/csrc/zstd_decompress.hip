@@ -1,0 +1,796 @@
+// zstd_decompress.hip -- Zstandard (RFC 8878) frame decode, one wavefront per segment
+// (gfx950).  Acceptance rules are those of the oracle's bo_zstd_decompress
+// (oracle/bitar_zstd.c): one frame per segment, no dictionary, raw / RLE / compressed
+// blocks, raw / RLE / Huffman literals (1 or 4 streams, FSE-compressed or direct weights,
+// treeless reuse), predefined / RLE / FSE / repeat sequence tables, repeat offsets, and the
+// XXH64 content checksum.
+//
+// Control is wave-uniform (scalar registers); the compressed stream is read through the
+// LDS window of stream_ring.hip.h and the output goes through its LDS history ring.  Tables
+// (FSE decode cells, the Huffman table) live in LDS and are built lane-parallel where the
+// construction allows it.  Huffman-coded literals are decoded into the tail of the
+// segment's output slot and copied from there by the sequence executor: output writes never
+// overtake the literal reads (op <= cap - remaining literals).
+#include "stream_ring.hip.h"
+
+namespace bitar_hip {
+
+namespace zsd {
+
+using namespace sr;
+
+constexpr uint32_t kHufMaxLog = 11;
+
+__constant__ uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,   7,   8,   9,    10,   11,
+                                     12, 13, 14, 15, 16, 18, 20,  22,  24,  28,   32,   40,
+                                     48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384,
+                                     32768, 65536};
+__constant__ uint8_t kLLBits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  0,  0,  1,  1,
+                                    1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ uint32_t kMLBase[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13,   14,   15,   16,
+                                     17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27,   28,   29,   30,
+                                     31, 32, 33, 34, 35, 37, 39, 41, 43, 47, 51,   59,   67,   83,
+                                     99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771,
+                                     65539};
+__constant__ uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1,
+                                    2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ int16_t kLLDefault[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                       2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+__constant__ int16_t kMLDefault[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                       1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                       1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+__constant__ int16_t kOFDefault[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
+                                       1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+
+struct Tabs {  // LDS, per wave
+  uint32_t fse[4][512];  // decode cells (LL, OF, ML, Huffman weights): sym | nbits << 8 | base << 16
+  uint16_t huf[1u << kHufMaxLog];  // sym | nbits << 8
+  int16_t norm[256];
+  uint8_t wts[256];
+};
+
+__device__ __forceinline__ uint32_t hb32(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
+
+// ---- scalar stream access ---------------------------------------------------------------
+// bytes [pos, pos + n) of the stream (n <= 4, all inside it), little-endian
+__device__ __forceinline__ uint32_t load_le(State& s, uint8_t* win, uint32_t pos, uint32_t n) {
+  const uint32_t w = win_at(s, win, pos, n);
+  lds_order();
+  const uint32_t lane = lane_id();
+  const uint32_t b = lane < n ? (uint32_t)win[w + lane] : 0u;
+  return readlane(b, 0) | (readlane(b, 1) << 8) | (readlane(b, 2) << 16) | (readlane(b, 3) << 24);
+}
+
+// forward bit reader (FSE table descriptions): bits past `len` read as zeros
+struct Fwd {
+  uint32_t start, len;
+  uint32_t bitpos;
+};
+__device__ __forceinline__ uint32_t fwd_peek(State& s, uint8_t* win, const Fwd& f, uint32_t n) {
+  const uint32_t byte = f.bitpos >> 3;
+  uint32_t avail = byte < f.len ? f.len - byte : 0u;
+  if (avail > 4) avail = 4;
+  const uint64_t w = avail ? (uint64_t)load_le(s, win, f.start + byte, avail) : 0ull;
+  return (uint32_t)(w >> (f.bitpos & 7u)) & ((1u << n) - 1);
+}
+
+// backward bit reader: bits [0, bitpos) of a stream remain; read(n) returns bits
+// [bitpos - n, bitpos) as a little-endian integer (zeros below bit 0); bitpos < 0 after a
+// read = the stream was overrun.  The container holds bits [8 lo, bitpos).
+struct Bwd {
+  uint32_t start;
+  int32_t bitpos;
+  uint64_t c;
+  int32_t cn;
+  uint32_t lo;
+};
+__device__ __forceinline__ bool bwd_init(State& s, uint8_t* win, Bwd& b, uint32_t start, uint32_t len) {
+  if (len == 0) return false;
+  const uint32_t last = load_le(s, win, start + len - 1, 1);
+  if (last == 0) return false;
+  const uint32_t h = hb32(last);
+  b.start = start;
+  b.bitpos = (int32_t)((len - 1) * 8 + h);
+  b.c = last & ((1u << h) - 1);
+  b.cn = (int32_t)h;
+  b.lo = len - 1;
+  return true;
+}
+__device__ __forceinline__ void bwd_fill(State& s, uint8_t* win, Bwd& b) {
+  if (b.cn <= 32 && b.lo >= 4) {
+    b.lo -= 4;
+    b.c = (b.c << 32) | load_le(s, win, b.start + b.lo, 4);
+    b.cn += 32;
+  }
+  while (b.cn <= 56 && b.lo > 0) {
+    b.lo -= 1;
+    b.c = (b.c << 8) | load_le(s, win, b.start + b.lo, 1);
+    b.cn += 8;
+  }
+}
+__device__ __forceinline__ uint32_t bwd_peek(State& s, uint8_t* win, Bwd& b, uint32_t n) {
+  if (b.cn < (int32_t)n) bwd_fill(s, win, b);
+  if (n == 0) return 0;
+  const uint64_t m = (1ull << n) - 1;
+  return b.cn >= (int32_t)n ? (uint32_t)((b.c >> (b.cn - (int32_t)n)) & m)
+                            : (uint32_t)((b.c << ((int32_t)n - b.cn)) & m);
+}
+__device__ __forceinline__ uint32_t bwd_read(State& s, uint8_t* win, Bwd& b, uint32_t n) {
+  const uint32_t v = bwd_peek(s, win, b, n);
+  b.cn -= (int32_t)n;
+  if (b.cn < 0) { b.cn = 0; b.c = 0; }
+  b.bitpos -= (int32_t)n;
+  return v;
+}
+__device__ __forceinline__ void bwd_skip(Bwd& b, uint32_t n) {
+  b.cn -= (int32_t)n;
+  if (b.cn < 0) { b.cn = 0; b.c = 0; }
+  b.bitpos -= (int32_t)n;
+}
+
+// ---- FSE ----------------------------------------------------------------------------------
+// FSE_readNCount from the stream at [start, start + len); returns bytes used, or -1
+__device__ int read_ncount(State& s, uint8_t* win, Tabs& t, uint32_t start, uint32_t len,
+                           uint32_t& max_sym, uint32_t& al, uint32_t max_al) {
+  Fwd f = {start, len, 0};
+  const uint32_t log = fwd_peek(s, win, f, 4) + 5;
+  if (log > max_al) return -1;
+  f.bitpos = 4;
+  int remaining = (1 << log) + 1;
+  int threshold = 1 << log;
+  uint32_t nbits = log + 1;
+  uint32_t sym = 0;
+  bool prev0 = false;
+  const uint32_t lane = lane_id();
+  while (remaining > 1 && sym <= max_sym) {
+    if (prev0) {
+      uint32_t n0 = sym;
+      while (fwd_peek(s, win, f, 16) == 0xFFFFu) { n0 += 24; f.bitpos += 16; }
+      while ((fwd_peek(s, win, f, 2) & 3u) == 3u) { n0 += 3; f.bitpos += 2; }
+      n0 += fwd_peek(s, win, f, 2) & 3u;
+      f.bitpos += 2;
+      if (n0 > max_sym) return -1;
+      lds_order();
+      for (uint32_t k = sym + lane; k < n0; k += kWave) t.norm[k] = 0;
+      lds_order();
+      sym = n0;
+    }
+    const int max = (2 * threshold - 1) - remaining;
+    int count;
+    const uint32_t v = fwd_peek(s, win, f, nbits);
+    if ((int)(v & (uint32_t)(threshold - 1)) < max) {
+      count = (int)(v & (uint32_t)(threshold - 1));
+      f.bitpos += nbits - 1;
+    } else {
+      count = (int)(v & (uint32_t)(2 * threshold - 1));
+      if (count >= threshold) count -= max;
+      f.bitpos += nbits;
+    }
+    count--;
+    remaining -= count < 0 ? -count : count;
+    lds_order();
+    if (lane == 0) t.norm[sym] = (int16_t)count;
+    lds_order();
+    sym++;
+    prev0 = count == 0;
+    while (remaining < threshold) { nbits--; threshold >>= 1; }
+  }
+  if (remaining != 1 || f.bitpos > len * 8) return -1;
+  max_sym = sym - 1;
+  al = log;
+  return (int)((f.bitpos + 7) >> 3);
+}
+
+// FSE_buildDTable from t.norm[0..max_sym] (max_sym <= 255: Huffman-weight tables may
+// declare symbols they never decode).  Per-symbol state counters live one per lane, in
+// four registers (symbol = 64 j + lane).
+__device__ __forceinline__ uint32_t pick4(const uint32_t (&v)[4], uint32_t j) {
+  return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
+}
+__device__ bool fse_build(Tabs& t, uint32_t* cells, uint32_t max_sym, uint32_t al) {
+  const uint32_t lane = lane_id();
+  const uint32_t size = 1u << al;
+  lds_order();
+  uint32_t nextv[4], normv[4];
+  uint32_t high = size - 1;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint32_t sm = 64 * j + lane;
+    const int nl = sm <= max_sym ? (int)t.norm[sm] : 0;
+    normv[j] = nl > 0 ? (uint32_t)nl : 0u;
+    nextv[j] = nl == -1 ? 1u : normv[j];
+    // symbols of "less than 1" probability take the top cells, in symbol order
+    for (uint64_t m = ballot(sm <= max_sym && nl == -1); m; m &= m - 1) {
+      const uint32_t sy = 64 * j + (uint32_t)__builtin_ctzll(m);
+      if (lane == 0) cells[high] = sy;
+      high--;
+    }
+  }
+  // spread (scalar: the step sequence skips the reserved top cells)
+  const uint32_t step = (size >> 1) + (size >> 3) + 3, mask = size - 1;
+  uint32_t pos = 0;
+  for (uint32_t sm = 0; sm <= max_sym; ++sm) {
+    const uint32_t cnt = readlane(pick4(normv, sm >> 6), sm & 63u);
+    for (uint32_t i = 0; i < cnt; ++i) {
+      if (lane == 0) cells[pos] = sm;
+      do { pos = (pos + step) & mask; } while (pos > high);
+    }
+  }
+  if (pos != 0) return false;
+  lds_order();
+  // states: cell u of symbol s gets next[s]++ in u order; lanes take 64 cells at a time and
+  // rank equal symbols with a ballot
+  for (uint32_t u0 = 0; u0 < size; u0 += kWave) {
+    const uint32_t u = u0 + lane;
+    const bool in = u < size;
+    const uint32_t sy = in ? (cells[u] & 0xFFu) : 0u;
+    uint64_t pend = ballot(in);
+    uint32_t ns = 0;
+    while (pend) {
+      const uint32_t l0 = (uint32_t)__builtin_ctzll(pend);
+      const uint32_t s0 = readlane(sy, l0);
+      const uint64_t mk = ballot(in && sy == s0) & pend;
+      const uint32_t j0 = s0 >> 6, l1 = s0 & 63u;
+      const uint32_t base = readlane(pick4(nextv, j0), l1);
+      if ((mk >> lane) & 1) ns = base + (uint32_t)__builtin_popcountll(mk & ((1ull << lane) - 1));
+      const uint32_t add = lane == l1 ? (uint32_t)__builtin_popcountll(mk) : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) nextv[j] += j == j0 ? add : 0u;
+      pend &= ~mk;
+    }
+    lds_order();
+    if (in) {
+      const uint32_t nb = al - hb32(ns);
+      cells[u] = sy | (nb << 8) | (((ns << nb) - size) << 16);
+    }
+    lds_order();
+  }
+  return true;
+}
+
+__device__ __forceinline__ void fse_rle(uint32_t* cells, uint32_t sym) {
+  lds_order();
+  if (lane_id() == 0) cells[0] = sym;  // nbits 0, base 0
+  lds_order();
+}
+
+__device__ __forceinline__ uint32_t cell(const uint32_t* cells, uint32_t st) {
+  lds_order();
+  return uniform(cells[st]);
+}
+
+// ---- Huffman -------------------------------------------------------------------------------
+// tree description at stream [start, start + len); returns bytes used or -1; sets log
+__device__ int huf_read(State& s, uint8_t* win, Tabs& t, uint32_t start, uint32_t len,
+                        uint32_t& log) {
+  const uint32_t lane = lane_id();
+  if (len < 1) return -1;
+  const uint32_t hb = load_le(s, win, start, 1);
+  uint32_t nw = 0;
+  int used;
+  if (hb < 128) {  // FSE-compressed weights in hb bytes
+    if (1 + hb > len) return -1;
+    uint32_t max_sym = 255, al;
+    const int n = read_ncount(s, win, t, start + 1, hb, max_sym, al, 6);
+    if (n < 0) return -1;
+    uint32_t* cells = t.fse[3];
+    if (!fse_build(t, cells, max_sym, al)) return -1;
+    Bwd b;
+    if (!bwd_init(s, win, b, start + 1 + (uint32_t)n, hb - (uint32_t)n)) return -1;
+    uint32_t s1 = bwd_read(s, win, b, al), s2 = bwd_read(s, win, b, al);
+    for (;;) {
+      if (nw > 254) return -1;
+      uint32_t c1 = cell(cells, s1);
+      if (lane == 0) t.wts[nw] = (uint8_t)c1;
+      nw++;
+      s1 = (c1 >> 16) + bwd_read(s, win, b, (c1 >> 8) & 0xFFu);
+      if (b.bitpos < 0) {
+        const uint32_t c2 = cell(cells, s2);
+        if (lane == 0) t.wts[nw] = (uint8_t)c2;
+        nw++;
+        break;
+      }
+      if (nw > 254) return -1;
+      const uint32_t c2 = cell(cells, s2);
+      if (lane == 0) t.wts[nw] = (uint8_t)c2;
+      nw++;
+      s2 = (c2 >> 16) + bwd_read(s, win, b, (c2 >> 8) & 0xFFu);
+      if (b.bitpos < 0) {
+        c1 = cell(cells, s1);
+        if (lane == 0) t.wts[nw] = (uint8_t)c1;
+        nw++;
+        break;
+      }
+    }
+    used = 1 + (int)hb;
+  } else {  // direct 4-bit weights
+    nw = hb - 127;
+    const uint32_t nb = (nw + 1) / 2;
+    if (1 + nb > len) return -1;
+    for (uint32_t k0 = 0; k0 < nw; k0 += kWave) {  // 64 weights = 32 bytes per step
+      const uint32_t k = k0 + lane;
+      const uint32_t w = win_at(s, win, start + 1 + k0 / 2, 32);
+      lds_order();
+      const uint32_t wk = k < nw ? (uint32_t)win[w + lane / 2] : 0u;
+      lds_order();
+      if (k < nw) t.wts[k] = (uint8_t)((k & 1) ? (wk & 15u) : (wk >> 4));
+      lds_order();
+    }
+    used = 1 + (int)nb;
+  }
+  lds_order();
+  // weights -> total, implied last weight, rank starts (lane-parallel over 4 x 64 symbols)
+  uint32_t total = 0;
+  bool bad = false;
+  for (uint32_t k0 = 0; k0 < nw; k0 += kWave) {
+    const uint32_t k = k0 + lane;
+    const uint32_t w = k < nw ? t.wts[k] : 0u;
+    bad |= ballot(w > 11) != 0;
+    uint32_t v = w ? (1u << (w - 1)) : 0u;
+    for (uint32_t d = 1; d < 64; d <<= 1) v += __shfl_xor((int)v, (int)d, 64);
+    total += readlane(v, 0);
+  }
+  if (bad || total == 0) return -1;
+  const uint32_t maxb = hb32(total) + 1;
+  if (maxb > kHufMaxLog) return -1;
+  const uint32_t rest = (1u << maxb) - total;
+  if (rest & (rest - 1)) return -1;
+  lds_order();
+  if (lane == 0) t.wts[nw] = (uint8_t)(hb32(rest) + 1);
+  lds_order();
+  nw++;
+  // rank starts: lane w (1..11) holds the first table index of weight w
+  uint32_t rankv = 0;  // lane w: count of symbols of weight w
+  for (uint32_t k0 = 0; k0 < nw; k0 += kWave) {
+    const uint32_t k = k0 + lane;
+    const uint32_t w = k < nw ? t.wts[k] : 0u;
+    for (uint32_t q = 1; q <= maxb; ++q) {
+      const uint32_t c = (uint32_t)__builtin_popcountll(ballot(k < nw && w == q));
+      rankv += lane == q ? c : 0u;
+    }
+  }
+  uint32_t startv = 0, nxt = 0;
+  for (uint32_t q = 1; q <= maxb; ++q) {
+    if (lane == q) startv = nxt;
+    nxt += readlane(rankv, q) << (q - 1);
+  }
+  if (nxt != (1u << maxb)) return -1;
+  // fill: symbol k of weight w takes 2^(w-1) entries from its rank slot, in symbol order
+  for (uint32_t k0 = 0; k0 < nw; k0 += kWave) {
+    const uint32_t k = k0 + lane;
+    const uint32_t w = k < nw ? t.wts[k] : 0u;
+    uint32_t my = 0;
+    for (uint32_t q = 1; q <= maxb; ++q) {
+      const uint64_t mk = ballot(k < nw && w == q);
+      const uint32_t st = readlane(startv, q);
+      if (w == q) my = st + ((uint32_t)__builtin_popcountll(mk & ((1ull << lane) - 1)) << (q - 1));
+      startv += lane == q ? ((uint32_t)__builtin_popcountll(mk) << (q - 1)) : 0u;
+    }
+    lds_order();
+    if (k < nw && w) {
+      const uint16_t e = (uint16_t)(k | ((maxb + 1 - w) << 8));
+      for (uint32_t j = 0; j < (1u << (w - 1)); ++j) t.huf[my + j] = e;
+    }
+    lds_order();
+  }
+  log = maxb;
+  return used;
+}
+
+// decode one Huffman stream of n symbols to out[0, n) (global); false if malformed
+__device__ bool huf_stream(State& s, uint8_t* win, Tabs& t, uint32_t log, uint32_t start,
+                           uint32_t len, GMEM uint8_t* out, uint32_t n) {
+  Bwd b;
+  if (!bwd_init(s, win, b, start, len)) return false;
+  const uint32_t lane = lane_id();
+  uint32_t v = 0, k = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t idx = bwd_peek(s, win, b, log);
+    lds_order();
+    const uint32_t e = uniform((uint32_t)t.huf[idx]);
+    bwd_skip(b, e >> 8);
+    if (lane == k) v = e & 0xFFu;
+    if (++k == kWave) {
+      out[i + 1 - kWave + lane] = (uint8_t)v;
+      k = 0;
+    }
+  }
+  if (k && lane < k) out[n - k + lane] = (uint8_t)v;
+  return b.bitpos == 0;
+}
+
+// ---- output helpers -------------------------------------------------------------------------
+__device__ __forceinline__ void out_fill(State& s, uint8_t* ring, uint32_t v, uint32_t n) {
+  const uintptr_t base = (uintptr_t)s.dst;
+  while (n) {
+    const uint32_t step = n < kWave ? n : kWave;
+    make_room(s, ring, step);
+    lds_order();
+    if (lane_id() < step) ring[(base + s.op + lane_id()) & kRingMask] = (uint8_t)v;
+    lds_order();
+    s.op += step;
+    n -= step;
+  }
+}
+// n bytes from global memory this wave wrote (fenced by the caller) into the output
+__device__ __forceinline__ void out_global(State& s, uint8_t* ring, const GMEM uint8_t* src, uint32_t n) {
+  const uintptr_t base = (uintptr_t)s.dst;
+  while (n) {
+    const uint32_t step = n < kWave ? n : kWave;
+    make_room(s, ring, step);
+    const uint32_t v = lane_id() < step ? (uint32_t)src[lane_id()] : 0u;
+    lds_order();
+    if (lane_id() < step) ring[(base + s.op + lane_id()) & kRingMask] = (uint8_t)v;
+    lds_order();
+    s.op += step;
+    src += step;
+    n -= step;
+  }
+}
+
+struct Frame {
+  uint32_t rep0, rep1, rep2;
+  uint32_t al[3];      // accuracy logs of the LL / OF / ML tables
+  bool have[3];
+  uint32_t huf_log;    // 0 = no Huffman table yet
+};
+
+// one compressed block at stream [p, p + len)
+__device__ bool block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr, uint32_t p,
+                      uint32_t len) {
+  const uint32_t lane = lane_id();
+  const uint32_t end = p + len;
+  // ---- literals section ----
+  const uint32_t b0 = load_le(s, win, p, 1);
+  const uint32_t lt = b0 & 3u, sf = (b0 >> 2) & 3u;
+  uint32_t regen, csz = 0, hsz, nstreams = 1;
+  if (lt < 2) {
+    if (sf == 0 || sf == 2) { regen = b0 >> 3; hsz = 1; }
+    else if (sf == 1) { if (len < 2) return false; regen = load_le(s, win, p, 2) >> 4; hsz = 2; }
+    else { if (len < 3) return false; regen = load_le(s, win, p, 3) >> 4; hsz = 3; }
+  } else {
+    if (sf <= 1) {
+      if (len < 3) return false;
+      const uint32_t c = load_le(s, win, p, 3);
+      regen = (c >> 4) & 0x3FFu; csz = (c >> 14) & 0x3FFu; hsz = 3; nstreams = sf == 0 ? 1 : 4;
+    } else if (sf == 2) {
+      if (len < 4) return false;
+      const uint32_t c = load_le(s, win, p, 4);
+      regen = (c >> 4) & 0x3FFFu; csz = (c >> 18) & 0x3FFFu; hsz = 4; nstreams = 4;
+    } else {
+      if (len < 5) return false;
+      const uint64_t c = (uint64_t)load_le(s, win, p, 4) | ((uint64_t)load_le(s, win, p + 4, 1) << 32);
+      regen = (uint32_t)(c >> 4) & 0x3FFFFu; csz = (uint32_t)(c >> 22) & 0x3FFFFu; hsz = 5; nstreams = 4;
+    }
+  }
+  if (regen > (128u << 10) || regen > s.cap - s.op) return false;
+  uint32_t q = p + hsz;
+  // where the literals come from: the stream (raw), one byte (RLE), or the slot tail
+  uint32_t lit_stream = 0, lit_byte = 0;
+  GMEM uint8_t* lit_tail = s.dst + (s.cap - regen);
+  if (lt == 0) {
+    if (q + regen > end) return false;
+    lit_stream = q;
+    q += regen;
+  } else if (lt == 1) {
+    if (q + 1 > end) return false;
+    lit_byte = load_le(s, win, q, 1);
+    q += 1;
+  } else {
+    if (q + csz > end) return false;
+    uint32_t cs = q, cl = csz;
+    if (lt == 2) {
+      uint32_t log;
+      const int n = huf_read(s, win, t, cs, cl, log);
+      if (n < 0) return false;
+      fr.huf_log = log;
+      cs += (uint32_t)n;
+      cl -= (uint32_t)n;
+    } else if (!fr.huf_log) {
+      return false;
+    }
+    if (nstreams == 1) {
+      if (!huf_stream(s, win, t, fr.huf_log, cs, cl, lit_tail, regen)) return false;
+    } else {
+      if (cl < 6) return false;
+      const uint32_t j = load_le(s, win, cs, 4);
+      const uint32_t s1 = j & 0xFFFFu, s2 = j >> 16, s3 = load_le(s, win, cs + 4, 2);
+      if (6ull + s1 + s2 + s3 > cl) return false;
+      const uint32_t s4 = cl - 6 - s1 - s2 - s3;
+      const uint32_t qq = (regen + 3) / 4;
+      if (3 * qq > regen) return false;
+      const uint32_t st = cs + 6;
+      if (!huf_stream(s, win, t, fr.huf_log, st, s1, lit_tail, qq)) return false;
+      if (!huf_stream(s, win, t, fr.huf_log, st + s1, s2, lit_tail + qq, qq)) return false;
+      if (!huf_stream(s, win, t, fr.huf_log, st + s1 + s2, s3, lit_tail + 2 * qq, qq)) return false;
+      if (!huf_stream(s, win, t, fr.huf_log, st + s1 + s2 + s3, s4, lit_tail + 3 * qq,
+                      regen - 3 * qq)) return false;
+    }
+    global_fence_wave();  // the executor reads back what the streams wrote
+    q += csz;
+  }
+  uint32_t lp = 0;  // literals consumed
+  auto copy_lits = [&](uint32_t n) __attribute__((always_inline)) {
+    if (lt == 0) {
+      s.ip = lit_stream + lp;
+      if (n >= kLongLit) literals_long(s, win, ring, n);
+      else if (n) literals_short(s, win, ring, n);
+    } else if (lt == 1) {
+      out_fill(s, ring, lit_byte, n);
+    } else {
+      out_global(s, ring, lit_tail + lp, n);
+    }
+    lp += n;
+  };
+  // ---- sequences section ----
+  if (q >= end) return false;
+  uint32_t nseq = load_le(s, win, q, 1);
+  if (nseq < 128) {
+    q += 1;
+  } else if (nseq < 255) {
+    if (q + 2 > end) return false;
+    nseq = ((nseq - 128) << 8) + load_le(s, win, q + 1, 1);
+    q += 2;
+  } else {
+    if (q + 3 > end) return false;
+    nseq = load_le(s, win, q + 1, 2) + 0x7F00u;
+    q += 3;
+  }
+  if (nseq) {
+    if (q >= end) return false;
+    const uint32_t modes = load_le(s, win, q, 1);
+    q += 1;
+    if (modes & 3u) return false;
+    // tables in order LL, OF, ML
+    for (uint32_t k = 0; k < 3; ++k) {
+      const uint32_t mode = (modes >> (6 - 2 * k)) & 3u;
+      const uint32_t maxs = k == 0 ? 35u : k == 1 ? 31u : 52u;
+      const uint32_t maxal = k == 1 ? 8u : 9u;
+      uint32_t* cells = t.fse[k];
+      if (mode == 0) {
+        const uint32_t dmax = k == 0 ? 35u : k == 1 ? 28u : 52u;
+        lds_order();
+        if (lane <= dmax)
+          t.norm[lane] = k == 0 ? kLLDefault[lane] : k == 1 ? kOFDefault[lane] : kMLDefault[lane];
+        lds_order();
+        const uint32_t dal = k == 1 ? 5u : 6u;
+        if (!fse_build(t, cells, dmax, dal)) return false;
+        fr.al[k] = dal;
+      } else if (mode == 1) {
+        if (q >= end) return false;
+        const uint32_t sy = load_le(s, win, q, 1);
+        if (sy > maxs) return false;
+        fse_rle(cells, sy);
+        fr.al[k] = 0;
+        q += 1;
+      } else if (mode == 2) {
+        uint32_t ms = maxs, al;
+        const int n = read_ncount(s, win, t, q, end - q, ms, al, maxal);
+        if (n < 0) return false;
+        if (!fse_build(t, cells, ms, al)) return false;
+        fr.al[k] = al;
+        q += (uint32_t)n;
+      } else if (!fr.have[k]) {
+        return false;
+      }
+      fr.have[k] = true;
+    }
+    Bwd b;
+    if (q >= end || !bwd_init(s, win, b, q, end - q)) return false;
+    uint32_t sll = bwd_read(s, win, b, fr.al[0]);
+    uint32_t sof = bwd_read(s, win, b, fr.al[1]);
+    uint32_t sml = bwd_read(s, win, b, fr.al[2]);
+    for (uint32_t k = 0; k < nseq; ++k) {
+      const uint32_t cll = cell(t.fse[0], sll), cof = cell(t.fse[1], sof), cml = cell(t.fse[2], sml);
+      const uint32_t llc = cll & 0xFFu, ofc = cof & 0xFFu, mlc = cml & 0xFFu;
+      if (llc > 35 || mlc > 52 || ofc > 31) return false;
+      const uint32_t ofv = (1u << ofc) + bwd_read(s, win, b, ofc);
+      const uint32_t ml = kMLBase[mlc] + bwd_read(s, win, b, kMLBits[mlc]);
+      const uint32_t ll = kLLBase[llc] + bwd_read(s, win, b, kLLBits[llc]);
+      if (k + 1 < nseq) {
+        sll = (cll >> 16) + bwd_read(s, win, b, (cll >> 8) & 0xFFu);
+        sml = (cml >> 16) + bwd_read(s, win, b, (cml >> 8) & 0xFFu);
+        sof = (cof >> 16) + bwd_read(s, win, b, (cof >> 8) & 0xFFu);
+      }
+      uint32_t off;
+      if (ofv > 3) {
+        off = ofv - 3;
+        fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+      } else {
+        const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
+        if (idx == 1) {
+          off = fr.rep0;
+        } else if (idx == 2) {
+          off = fr.rep1;
+          fr.rep1 = fr.rep0; fr.rep0 = off;
+        } else if (idx == 3) {
+          off = fr.rep2;
+          fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+        } else {
+          off = fr.rep0 - 1;
+          if (off == 0) return false;
+          fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+        }
+      }
+      // also keeps the output behind the unread Huffman literals in the slot tail
+      if (lp + ll > regen || (uint64_t)s.op + ml + (regen - lp) > s.cap) return false;
+      copy_lits(ll);
+      if (off == 0 || off > s.op) return false;
+      match_copy(s, ring, off, ml);
+    }
+    if (b.bitpos != 0) return false;
+  } else if (q != end) {
+    return false;
+  }
+  if ((uint64_t)s.op + (regen - lp) > s.cap) return false;
+  copy_lits(regen - lp);
+  return true;
+}
+
+// XXH64 of the first n output bytes (already flushed to HBM and fenced), low 32 bits
+__device__ uint32_t xxh64_low(const GMEM uint8_t* p, uint32_t n) {
+  constexpr uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull,
+                     P3 = 1609587929392839161ull, P4 = 9650029242287828579ull,
+                     P5 = 2870177450012600261ull;
+  auto rotl = [](uint64_t x, int r) { return (x << r) | (x >> (64 - r)); };
+  auto round = [&](uint64_t acc, uint64_t in) { acc += in * P2; acc = rotl(acc, 31); return acc * P1; };
+  const uint32_t lane = lane_id();
+  uint64_t h;
+  uint32_t i = 0;
+  if (n >= 32) {
+    uint64_t v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1;
+    const uint32_t nstripes = n / 32;
+    for (uint32_t s0 = 0; s0 < nstripes; s0 += 32) {  // 32 stripes = 1 KiB per step
+      const uint32_t off = s0 * 32 + 16 * lane;
+      uint64_t a = 0, c = 0;
+      if (off + 16 <= nstripes * 32) {
+        uint64_t lo = 0, hi = 0;
+        for (uint32_t b = 0; b < 8; ++b) lo |= (uint64_t)p[off + b] << (8 * b);
+        for (uint32_t b = 0; b < 8; ++b) hi |= (uint64_t)p[off + 8 + b] << (8 * b);
+        a = lo;
+        c = hi;
+      }
+      const uint32_t cnt = nstripes - s0 < 32 ? nstripes - s0 : 32;
+      for (uint32_t k = 0; k < cnt; ++k) {
+        const uint64_t x1 = ((uint64_t)readlane((uint32_t)(a >> 32), 2 * k) << 32) | readlane((uint32_t)a, 2 * k);
+        const uint64_t x2 = ((uint64_t)readlane((uint32_t)(c >> 32), 2 * k) << 32) | readlane((uint32_t)c, 2 * k);
+        const uint64_t x3 = ((uint64_t)readlane((uint32_t)(a >> 32), 2 * k + 1) << 32) | readlane((uint32_t)a, 2 * k + 1);
+        const uint64_t x4 = ((uint64_t)readlane((uint32_t)(c >> 32), 2 * k + 1) << 32) | readlane((uint32_t)c, 2 * k + 1);
+        v1 = round(v1, x1); v2 = round(v2, x2); v3 = round(v3, x3); v4 = round(v4, x4);
+      }
+    }
+    h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+    auto merge = [&](uint64_t acc, uint64_t v) { acc ^= round(0, v); return acc * P1 + P4; };
+    h = merge(h, v1); h = merge(h, v2); h = merge(h, v3); h = merge(h, v4);
+    i = nstripes * 32;
+  } else {
+    h = P5;
+  }
+  h += n;
+  // tail (< 32 bytes): lanes fetch, lane 0's scalar loop consumes
+  const uint32_t tb = i + lane < n ? (uint32_t)p[i + lane] : 0u;
+  uint32_t k = 0;
+  const uint32_t rem = n - i;
+  for (; k + 8 <= rem; k += 8) {
+    uint64_t x = 0;
+    for (uint32_t b = 0; b < 8; ++b) x |= (uint64_t)readlane(tb, k + b) << (8 * b);
+    h ^= round(0, x);
+    h = rotl(h, 27) * P1 + P4;
+  }
+  if (k + 4 <= rem) {
+    uint64_t x = 0;
+    for (uint32_t b = 0; b < 4; ++b) x |= (uint64_t)readlane(tb, k + b) << (8 * b);
+    h ^= x * P1;
+    h = rotl(h, 23) * P2 + P3;
+    k += 4;
+  }
+  for (; k < rem; ++k) {
+    h ^= (uint64_t)readlane(tb, k) * P5;
+    h = rotl(h, 11) * P1;
+  }
+  h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+  return (uint32_t)h;
+}
+
+}  // namespace zsd
+
+__global__ __launch_bounds__(64) void zstd_decompress_kernel(
+    const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
+    uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
+    uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err) {
+  using namespace zsd;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
+  __shared__ __attribute__((aligned(16))) Tabs t;
+  uint8_t* win = lds;
+  uint8_t* ring = lds + kWin;
+  const uint32_t i = blockIdx.x;
+  if (i >= nseg) return;
+  State s;
+  s.src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
+  s.csize = csizes[i];
+  s.dst = global_ptr(out + (uint64_t)i * seg);
+  s.cap = seg;
+  s.ip = 0;
+  s.op = 0;
+  s.flushed = 0;
+  s.fenced = 0;
+  s.wb = ~0ull;
+  s.wlen = 0;
+  bool ok = false;
+  do {
+    const uint32_t cs = s.csize;
+    if (cs < 6 || load_le(s, win, 0, 4) != 0xFD2FB528u) break;
+    uint32_t p = 4;
+    const uint32_t fhd = load_le(s, win, p++, 1);
+    const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1u, cks = (fhd >> 2) & 1u,
+                   did_flag = fhd & 3u;
+    if (fhd & 8u) break;
+    if (!single) {
+      if (p >= cs) break;
+      p++;
+    }
+    const uint32_t did_sz = did_flag == 3 ? 4u : did_flag;
+    if (p + did_sz > cs) break;
+    const uint32_t did = did_sz ? load_le(s, win, p, did_sz) : 0u;
+    p += did_sz;
+    if (did) break;
+    uint32_t fsz = fcs_flag == 0 ? (single ? 1u : 0u) : fcs_flag == 1 ? 2u : fcs_flag == 2 ? 4u : 8u;
+    if (p + fsz > cs) break;
+    uint64_t fcs = 0;
+    if (fsz == 8) fcs = (uint64_t)load_le(s, win, p, 4) | ((uint64_t)load_le(s, win, p + 4, 4) << 32);
+    else if (fsz) fcs = load_le(s, win, p, fsz);
+    if (fsz == 2) fcs += 256;
+    p += fsz;
+    if (fsz && fcs > s.cap) break;
+    Frame fr;
+    fr.rep0 = 1; fr.rep1 = 4; fr.rep2 = 8;
+    fr.have[0] = fr.have[1] = fr.have[2] = false;
+    fr.huf_log = 0;
+    bool bad = false, last = false;
+    while (!last) {
+      if (p + 3 > cs) { bad = true; break; }
+      const uint32_t bh = load_le(s, win, p, 3);
+      p += 3;
+      last = bh & 1u;
+      const uint32_t type = (bh >> 1) & 3u, bsz = bh >> 3;
+      if (type == 0) {
+        if (p + bsz > cs || (uint64_t)s.op + bsz > s.cap) { bad = true; break; }
+        s.ip = p;
+        if (bsz >= kLongLit) literals_long(s, win, ring, bsz);
+        else if (bsz) literals_short(s, win, ring, bsz);
+        p += bsz;
+      } else if (type == 1) {
+        if (p + 1 > cs || (uint64_t)s.op + bsz > s.cap) { bad = true; break; }
+        out_fill(s, ring, load_le(s, win, p, 1), bsz);
+        p += 1;
+      } else if (type == 2) {
+        if (bsz > (128u << 10) || p + bsz > cs) { bad = true; break; }
+        if (!block(s, win, ring, t, fr, p, bsz)) { bad = true; break; }
+        p += bsz;
+      } else {
+        bad = true;
+        break;
+      }
+    }
+    if (bad) break;
+    flush(s, ring, s.op, true);
+    if (cks) {
+      if (p + 4 > cs) break;
+      global_fence_wave();
+      if (xxh64_low(s.dst, s.op) != load_le(s, win, p, 4)) break;
+      p += 4;
+    }
+    if (p != cs) break;
+    if (fsz && fcs != s.op) break;
+    ok = true;
+  } while (false);
+  if (ok) {
+    if (lane_id() == 0) produced[i] = s.op;
+  } else if (lane_id() == 0) {
+    produced[i] = 0xFFFFFFFFu;
+    atomicOr(err, 1u);
+  }
+}
+
+}  // namespace bitar_hip

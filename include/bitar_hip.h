@@ -36,8 +36,13 @@ enum bitar_hip_status {
 
 /* Codec of one segment op.  DEFLATE = raw RFC 1951 stream per segment, the reference's
  * frame (reference src/config.cc:83-105, memory.cc:110).  LZ4 = raw LZ4 block per segment
- * (the north-star codec). */
-enum bitar_hip_codec { BITAR_HIP_CODEC_LZ4 = 1, BITAR_HIP_CODEC_DEFLATE = 2 };
+ * (the north-star codec).  ZSTD = one RFC 8878 Zstandard frame per segment (the DPDK
+ * RTE_COMP_ALGO_ZSTD path of reference src/config.cc:83-105 / BASELINE configs[5]). */
+enum bitar_hip_codec {
+  BITAR_HIP_CODEC_LZ4 = 1,
+  BITAR_HIP_CODEC_DEFLATE = 2,
+  BITAR_HIP_CODEC_ZSTD = 3
+};
 
 /* Per-segment marker written into sizes[] / produced[] when that segment's op failed
  * (malformed stream, or output larger than its slot: the reference's

@@ -29,8 +29,8 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(ORACLE_SO):
-            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        # make is a no-op when the library is current (rebuilds a stale one)
+        subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
         L = ctypes.CDLL(ORACLE_SO)
         u8p = ctypes.c_void_p
         L.bo_compressed_seg_size.restype = ctypes.c_uint32

@@ -1,0 +1,144 @@
+"""GPU parity tests for the Zstandard path (BASELINE configs[5]), through the C ABI.
+
+Pinning: the HIP frame decoder must reproduce every libzstd 1.4.9 golden vector (levels
+1/3/9/19, with and without content checksum / content size, small windows), decode frames
+libzstd produces at run time (the same library the golden vectors came from, when the box
+has it), decode the oracle's frames, and accept / reject exactly the streams the oracle
+(oracle/bitar_zstd.c) accepts / rejects -- including a few hundred seeded mutations.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import golden_lib
+import oracle_lib as O
+from test_gpu_lz4 import _decode_blobs, down, eng, up  # noqa: F401  (fixture reuse)
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _libzstd():
+    try:
+        L = ctypes.CDLL("/opt/conda/lib/libzstd.so.1.4.9")
+    except OSError:
+        pytest.skip("libzstd not present")
+    L.ZSTD_compress.restype = ctypes.c_size_t
+    L.ZSTD_compress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                ctypes.c_size_t, ctypes.c_int]
+    L.ZSTD_compressBound.restype = ctypes.c_size_t
+    L.ZSTD_compressBound.argtypes = [ctypes.c_size_t]
+    L.ZSTD_isError.restype = ctypes.c_uint
+    L.ZSTD_isError.argtypes = [ctypes.c_size_t]
+    return L
+
+
+def _check_batch(eng, blobs, plains, seg):
+    ok, out, prod = _decode_blobs(eng, O.CODEC_ZSTD, blobs, seg)
+    assert ok
+    for k, plain in enumerate(plains):
+        assert prod[k] == len(plain), (k, int(prod[k]), len(plain))
+        assert out[k * seg:k * seg + len(plain)].tobytes() == plain, k
+
+
+def test_zstd_decode_all_golden(eng):
+    vecs = [(e, blob, plain) for e, blob, plain in golden_lib.vectors("zstd")
+            if len(plain) <= 65536]
+    assert len(vecs) >= 200
+    seg = 65536
+    ok, out, prod = _decode_blobs(eng, O.CODEC_ZSTD, [b for _, b, _ in vecs], seg)
+    assert ok
+    for k, (e, blob, plain) in enumerate(vecs):
+        assert prod[k] == len(plain), (e["producer"], e["input"], int(prod[k]))
+        assert out[k * seg:k * seg + len(plain)].tobytes() == plain, (e["producer"], e["input"])
+
+
+@pytest.mark.parametrize("level", [1, 3, 6, 12, 19])
+def test_zstd_decode_libzstd_frames(eng, level):
+    Z = _libzstd()
+    blobs, plains = [], []
+    for kind in range(7):
+        for n in (0, 1, 100, 4096, 59460, 65536):
+            data = O.fill(kind, 1000 + level, n).tobytes()
+            cap = Z.ZSTD_compressBound(n)
+            buf = ctypes.create_string_buffer(cap)
+            r = Z.ZSTD_compress(buf, cap, data, n, level)
+            assert not Z.ZSTD_isError(r)
+            blobs.append(buf.raw[:r])
+            plains.append(data)
+    _check_batch(eng, blobs, plains, 65536)
+
+
+@pytest.mark.parametrize("seg", [65536, 59460, 4096, 13])
+def test_zstd_decode_oracle_frames(eng, seg):
+    import bitar_amd
+    n = 4 * seg + seg // 3 + 1 if seg > 100 else 700
+    for kind in range(7):
+        data = O.fill(kind, 31, n)
+        stride = bitar_amd.slot_size(bitar_amd.CODEC_ZSTD, seg)
+        r, slab, sizes = O.compress_segments(O.CODEC_ZSTD, data, seg, stride)
+        assert r == 0
+        blobs = [slab[i * stride:i * stride + sizes[i]].tobytes() for i in range(sizes.size)]
+        plains = [data[i * seg:(i + 1) * seg].tobytes() for i in range(sizes.size)]
+        _check_batch(eng, blobs, plains, seg)
+
+
+def _mutations(frame, rng, count):
+    out = []
+    for _ in range(count):
+        b = bytearray(frame)
+        kind = rng.integers(0, 3)
+        if kind == 0:  # bit flip
+            i = int(rng.integers(0, len(b)))
+            b[i] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 1:  # byte set
+            i = int(rng.integers(0, len(b)))
+            b[i] = int(rng.integers(0, 256))
+        else:  # truncation
+            b = b[:int(rng.integers(0, len(b)))]
+        out.append(bytes(b) if b else b"\x00")
+    return out
+
+
+def test_zstd_accepts_and_rejects_like_oracle(eng):
+    seg = 8192
+    vecs = [(blob, plain) for e, blob, plain in golden_lib.vectors("zstd")
+            if 200 <= len(plain) <= seg]
+    assert vecs
+    rng = np.random.default_rng(7)
+    cases = []
+    for blob, _ in vecs[:24]:
+        cases += _mutations(blob, rng, 12)
+    data = O.fill(O.KIND_MIXED, 3, 5000).tobytes()
+    r, frame = O.zstd_compress(data)
+    assert r == 0
+    cases += [frame[:3], frame[:-1], frame + b"\x00", b"\x28\xb5\x2f\xfe" + frame[4:],
+              frame[:4] + bytes([frame[4] | 8]) + frame[5:]]
+    ok, out, prod = _decode_blobs(eng, O.CODEC_ZSTD, cases, seg)
+    n_ok = 0
+    for k, c in enumerate(cases):
+        r, ref = O.zstd_decompress(c, seg)
+        if r == 0:
+            n_ok += 1
+            assert prod[k] == len(ref), (k, c[:16])
+            assert out[k * seg:k * seg + len(ref)].tobytes() == ref, k
+        else:
+            assert prod[k] == 0xFFFFFFFF, (k, r, int(prod[k]))
+    assert not ok  # at least the malformed tail cases fail
+    assert 0 < n_ok < len(cases)
+
+
+def test_zstd_checksum_and_capacity(eng):
+    vec = next((blob, plain) for e, blob, plain in golden_lib.vectors("zstd")
+               if "checksum" in e["producer"] and 100 < len(plain) <= 65536)
+    blob, plain = vec
+    bad = blob[:-1] + bytes([blob[-1] ^ 1])
+    ok, out, prod = _decode_blobs(eng, O.CODEC_ZSTD, [blob, bad], 65536)
+    assert prod[0] == len(plain) and out[:len(plain)].tobytes() == plain
+    assert prod[1] == 0xFFFFFFFF and not ok
+    # a frame larger than the segment is an error, not a truncation
+    seg = len(plain) - 1
+    ok, out, prod = _decode_blobs(eng, O.CODEC_ZSTD, [blob], seg)
+    assert prod[0] == 0xFFFFFFFF and not ok
