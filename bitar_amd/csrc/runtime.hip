@@ -24,6 +24,8 @@ __global__ void deflate_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint
 __global__ void inflate_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
                                uint32_t*);
+__global__ void zstd_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
+                                     uint8_t* const*, uint32_t*, uint32_t*);
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                        const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                        uint32_t*, uint32_t*);
@@ -166,8 +168,8 @@ uint64_t bitar_hip_slot_size(uint32_t codec, uint32_t seg) {
     bound = (uint64_t)seg + seg / 255u + 16u;           // LZ4_compressBound
   else if (codec == BITAR_HIP_CODEC_DEFLATE)
     bound = ((uint64_t)seg * 9 + 7) / 8 + 16u;          // fixed Huffman, 9 bits/literal
-  else if (codec == BITAR_HIP_CODEC_ZSTD)  // frame header + raw-literal blocks of <= 512 seqs
-    bound = (uint64_t)seg + 7u + 3u * ((uint64_t)seg / 2048u + 2u) + 8u;
+  else if (codec == BITAR_HIP_CODEC_ZSTD)  // oracle bo_zstd_bound: blocks of <= 256 sequences
+    bound = (uint64_t)seg + 7u + 3u * ((uint64_t)seg / 1024u + 2u) + 8u + 512u;
   else
     return 0;
   return (bound + 255u) & ~(uint64_t)255u;
@@ -212,7 +214,8 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
                          uint64_t n, uint32_t seg, void* d_slab, uint64_t slot_stride,
                          void* const* d_dsts, uint32_t* d_sizes) {
   if (int r = enter(ctx)) return r;
-  if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE)
+  if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE &&
+      codec != BITAR_HIP_CODEC_ZSTD)
     return fail(BITAR_HIP_NOT_IMPLEMENTED, "unknown codec");
   if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
   if (n == 0) return 0;  // empty input -> no segments (reference device.cc:161-164)
@@ -230,9 +233,12 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
   if (codec == BITAR_HIP_CODEC_LZ4)
     hipLaunchKernelGGL(bitar_hip::lz4_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
                        n, seg, slab, slot_stride, dsts, d_sizes, ctx->d_err);
-  else
+  else if (codec == BITAR_HIP_CODEC_DEFLATE)
     hipLaunchKernelGGL(bitar_hip::deflate_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
                        in, n, seg, slab, slot_stride, dsts, d_sizes, ctx->d_err);
+  else
+    hipLaunchKernelGGL(bitar_hip::zstd_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
+                       n, seg, slab, slot_stride, dsts, d_sizes, ctx->d_err);
   HIP_TRY(hipGetLastError(), "compress launch");
   return 0;
 }

@@ -604,7 +604,7 @@ done:
 /* ================================================================================ */
 /* encoder: the frame the HIP kernel emits                                            */
 /* ================================================================================ */
-#define ZS_MAX_SEQ 512u /* sequences per block (the kernel keeps a block's sequences in registers) */
+#define ZS_MAX_SEQ 256u /* sequences per block (the kernel keeps a block's sequences in 2 KiB of LDS) */
 
 typedef struct {
   uint16_t state[1u << 6];
@@ -793,11 +793,6 @@ static void zs_close_block(zs_enc* e, uint32_t last) {
 static void zs_emit(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t off, uint32_t mlen) {
   zs_enc* e = (zs_enc*)vctx;
   if (e->err) return;
-  if (mlen && e->nseq == ZS_MAX_SEQ) {
-    zs_close_block(e, 0);
-    zs_begin_block(e);
-    if (e->err) return;
-  }
   if (e->op + lit_len > e->cap) { e->err = 1; return; }
   memcpy(e->dst + e->op, e->src + lit_start, lit_len);
   e->op += lit_len;
@@ -809,14 +804,23 @@ static void zs_emit(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t o
     e->of[e->nseq] = off + 3;  /* Offset_Value: no repeat offsets */
     e->nseq++;
     e->in += mlen;
+    /* a block ends right after its ZS_MAX_SEQ-th match: the literals that follow belong to
+     * the next block, so the kernel writes every literal byte as soon as it is parsed */
+    if (e->nseq == ZS_MAX_SEQ) {
+      zs_close_block(e, 0);
+      zs_begin_block(e);
+    }
   }
 }
 
 uint32_t bo_zstd_bound(uint32_t n) {
   /* frame header 4+1+2, then per block of input: 3-byte header + at most the raw input
    * (a block never grows: it is stored raw instead) -- blocks split only at sequence
-   * boundaries, at most n/4/512+1 of them */
-  return n + 7 + 3 * (n / (4 * ZS_MAX_SEQ) + 2) + 8;
+   * boundaries, at most n/4/ZS_MAX_SEQ+1 of them.  The +512: a block is written compressed
+   * before it is judged, and its compressed form may exceed its raw size by < 2 B per
+   * sequence (<= 17 state + 16 literal-length + 12 offset bits vs a >= 4-byte match) plus
+   * its headers. */
+  return n + 7 + 3 * (n / (4 * ZS_MAX_SEQ) + 2) + 8 + 512;
 }
 
 int bo_zstd_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,

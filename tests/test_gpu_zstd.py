@@ -142,3 +142,73 @@ def test_zstd_checksum_and_capacity(eng):
     seg = len(plain) - 1
     ok, out, prod = _decode_blobs(eng, O.CODEC_ZSTD, [blob], seg)
     assert prod[0] == 0xFFFFFFFF and not ok
+
+
+# ---- the HIP Zstandard compressor (zstd_compress.hip) ------------------------------------
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("seg", [65536, 59460, 2048, 255, 13, 8])
+def test_zstd_compress_bit_exact_vs_oracle(eng, kind, seg):
+    """GPU frames equal the oracle's byte for byte and decode back (GPU and libzstd)."""
+    import bitar_amd
+    n = 5 * seg + seg // 3 + 1 if seg > 100 else 1000
+    data = O.fill(kind, 77, n)
+    slab, stride, sizes = eng.compress(bitar_amd.CODEC_ZSTD, up(data)[:n], seg)
+    eng.sync()
+    r, oslab, osizes = O.compress_segments(O.CODEC_ZSTD, data, seg, stride)
+    assert r == 0
+    gsizes = down(sizes).astype(np.uint32)
+    assert np.array_equal(gsizes, osizes)
+    gslab = down(slab)
+    for i in range(gsizes.size):
+        a = gslab[i * stride:i * stride + gsizes[i]]
+        b = oslab[i * stride:i * stride + osizes[i]]
+        assert np.array_equal(a, b), f"segment {i}"
+    out, prod = eng.decompress(bitar_amd.CODEC_ZSTD, slab, stride, sizes, seg)
+    eng.sync()
+    assert np.array_equal(down(out)[:n], data)
+    assert int(down(prod).astype(np.int64).sum()) == n
+
+
+def test_libzstd_decodes_gpu_frames(eng):
+    import bitar_amd
+    Z = _libzstd()
+    Z.ZSTD_decompress.restype = ctypes.c_size_t
+    Z.ZSTD_decompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                  ctypes.c_size_t]
+    seg = 65536
+    for kind in range(7):
+        n = 3 * seg + 999
+        data = O.fill(kind, 5, n)
+        slab, stride, sizes = eng.compress(bitar_amd.CODEC_ZSTD, up(data)[:n], seg)
+        eng.sync()
+        gs, g = down(sizes).astype(np.uint32), down(slab)
+        for i in range(gs.size):
+            frame = g[i * stride:i * stride + gs[i]].tobytes()
+            plain = data[i * seg:(i + 1) * seg].tobytes()
+            buf = ctypes.create_string_buffer(seg)
+            r = Z.ZSTD_decompress(buf, seg, frame, len(frame))
+            assert not Z.ZSTD_isError(r) and buf.raw[:r] == plain, (kind, i)
+
+
+@pytest.mark.parametrize("kind", [1, 2])
+def test_zstd_full_size_roundtrip_1gib(eng, kind):
+    """BASELINE configs[5] per GPU: 1 GiB, 64 KiB segments, round trip + oracle samples."""
+    import bitar_amd
+    n, seg = 1 << 30, 65536
+    data = eng.empty(n)
+    eng.fill(kind, 0, data)
+    slab, stride, sizes = eng.compress(bitar_amd.CODEC_ZSTD, data, seg)
+    eng.sync()
+    out, prod = eng.decompress(bitar_amd.CODEC_ZSTD, slab, stride, sizes, seg)
+    eng.sync()
+    assert torch.equal(out[:n], data)
+    assert int(prod.to(torch.int64).sum().item()) == n
+    gs = down(sizes).astype(np.uint32)
+    assert gs.sum() < n  # it compresses
+    for i in (0, 1, 4097, 16383):
+        plain = down(data[i * seg:(i + 1) * seg])
+        r, comp = O.zstd_compress(plain.tobytes())
+        assert r == 0 and len(comp) == gs[i]
+        assert down(slab[i * stride:i * stride + int(gs[i])]).tobytes() == comp, f"segment {i}"
+    del data, slab, out
+    torch.cuda.empty_cache()

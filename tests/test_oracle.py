@@ -212,3 +212,37 @@ def test_oracle_zstd_rejects_malformed():
             r, _ = O.zstd_decompress(blob[:-1] + bytes([blob[-1] ^ 1]), len(plain))
             assert r != 0
             break
+
+
+def _zstd_blocks(frame):
+    """(type, size, nseq) of every block of a single-segment frame the oracle wrote."""
+    fh = 6 if frame[4] == 0x20 else 7
+    p, out = fh, []
+    while True:
+        h = frame[p] | (frame[p + 1] << 8) | (frame[p + 2] << 16)
+        last, btype, bsize = h & 1, (h >> 1) & 3, h >> 3
+        nseq = None
+        if btype == 2:
+            lsz = (frame[p + 3] >> 4) | (frame[p + 4] << 4) | (frame[p + 5] << 12)
+            q = p + 6 + lsz
+            nseq = frame[q] if frame[q] < 128 else ((frame[q] - 128) << 8) + frame[q + 1]
+        out.append((btype, bsize, nseq))
+        p += 3 + bsize
+        if last:
+            break
+    assert p == len(frame)
+    return out
+
+
+@pytest.mark.parametrize("kind", [1, 2, 3, 4, 6])
+def test_oracle_zstd_block_split_rule(kind):
+    """Blocks close right after their 256th sequence; a block that does not shrink is raw."""
+    data = O.fill(kind, 11, 65536).tobytes()
+    r, frame = O.zstd_compress(data)
+    assert r == 0
+    blocks = _zstd_blocks(frame)
+    assert all(b[0] in (0, 2) for b in blocks)
+    assert all(b[2] is None or b[2] <= 256 for b in blocks)
+    assert all(b[2] == 256 for b in blocks[:-1] if b[0] == 2)
+    if kind in (1, 6):
+        assert len(blocks) > 1  # the split path is exercised
