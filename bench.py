@@ -7,6 +7,9 @@ configs[2]): every rank owns a 1 GiB HBM-resident buffer of the Silesia-style mi
 of the whole buffer into per-segment slots + (N > 1) the RCCL all-gather of the per-segment
 compressed sizes that builds the global frame index + LZ4 decompress of every slot back into
 a 1 GiB output.  value = bytes of uncompressed data round-tripped by all ranks / wall time.
+Beside it: "secondary" (BASELINE configs[1], random bytes, LZ4 decompress only, N = 1) and
+"zstd" (BASELINE configs[5], Zstd frames on Arrow record-batch bodies, same sharding and
+all-gather at every N).
 
 Prints ONE JSON line (rank 0).  Launch: python bench.py [--gpus N --steps K --warmup W];
 for N > 1 under torch.distributed.run (one process per GPU, RCCL).
@@ -32,11 +35,13 @@ def parse():
     p.add_argument("--bytes", type=int, default=1 << 30, help="bytes per rank")
     p.add_argument("--seg", type=int, default=65536)
     p.add_argument("--kind", type=int, default=1, help="0 random, 1 mixed, 2 arrow")
-    p.add_argument("--codec", default="lz4", choices=["lz4", "deflate"])
+    p.add_argument("--codec", default="lz4", choices=["lz4", "deflate", "zstd"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=256 << 20)
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the random-data decompress-only line (BASELINE configs[1])")
+    p.add_argument("--no-zstd", action="store_true",
+                   help="skip the Zstd round-trip line (BASELINE configs[5])")
     p.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
     return p.parse_args()
 
@@ -95,30 +100,26 @@ def cpu_baseline(args):
     }
 
 
-def main():
-    args = parse()
+KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
+           "deflate": ("deflate_compress_kernel", "inflate_kernel"),
+           "zstd": ("zstd_compress_kernel", "zstd_decompress_kernel")}
+CODEC_NAMES = {"lz4": "lz4-block", "deflate": "deflate-raw-fixed", "zstd": "zstd-frame"}
+
+
+def roundtrip(eng, ctx, codec_name, kind, n, seg, steps, warmup, seed):
+    """K timed steps of compress (+ RCCL size all-gather + frame index when world > 1) +
+    decompress of an n-byte HBM-resident buffer; returns the rank's timings and sizes."""
     import torch
     import torch.distributed as dist
     import bitar_amd
     from bitar_amd import dist as bd
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
-    eng = bitar_amd.Engine(dev)
-    codec = bitar_amd.CODEC_LZ4 if args.codec == "lz4" else bitar_amd.CODEC_DEFLATE
-    n, seg = args.bytes, args.seg
+    world = ctx["world"]
+    codec = {"lz4": bitar_amd.CODEC_LZ4, "deflate": bitar_amd.CODEC_DEFLATE,
+             "zstd": bitar_amd.CODEC_ZSTD}[codec_name]
     nseg = (n + seg - 1) // seg
     stride = bitar_amd.slot_size(codec, seg)
-
     data = eng.empty(n)
-    eng.fill(args.kind, rank, data)  # the rank's shard of the job (weak scaling)
+    eng.fill(kind, seed, data)  # the rank's shard of the job (weak scaling)
     slab = eng.empty(nseg * stride)
     sizes = eng.empty(nseg, dtype=torch.int32)
     out = eng.empty(nseg * seg)
@@ -126,7 +127,6 @@ def main():
     all_sizes = eng.empty(nseg * world, dtype=torch.int32) if world > 1 else None
     index = [None]
     stream = torch.cuda.current_stream()
-
     ev = []  # (compress start, compress end, decompress start, decompress end)
 
     def step(timed):
@@ -147,26 +147,26 @@ def main():
             e[3].record(stream)
             ev.append(e)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step(False)
     eng.sync()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    elapsed = time.perf_counter() - t0
     eng.sync()  # raises if any segment op failed
 
     # correctness of the timed output (byte equality of the round trip, demo_app.cc:534-543)
     ok = bool(torch.equal(out[:n], data)) and int(prod.to(torch.int64).sum().item()) == n
     csize = int(sizes.to(torch.int64).sum().item())
     if world > 1:
+        dev = torch.cuda.current_device()
         t = torch.tensor([elapsed, 0.0 if ok else 1.0, float(csize)], device=f"cuda:{dev}",
                          dtype=torch.float64)
         mx = t.clone()
@@ -178,32 +178,72 @@ def main():
         csize_total = int(sm[2].item())
         # the frame index every rank built from the all-gathered sizes spans the whole job
         ok = ok and int(index[0][-1].item()) == csize_total
-    else:
-        csize_total = csize
-
     t_comp = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev) / 1e3  # seconds
     t_dec = sum(e[2].elapsed_time(e[3]) for e in ev) / len(ev) / 1e3
+    del data, slab, out
+    torch.cuda.empty_cache()
+    return {"elapsed": elapsed, "ok": ok, "csize": csize, "t_comp": t_comp, "t_dec": t_dec,
+            "nseg": nseg}
+
+
+def kernel_lines(codec_name, r, n, traffic_json):
+    """roofline of the dominant kernel + per-kernel averages (HIP events on the launch stream)."""
+    U, C = float(n), float(r["csize"])
+    comp_bytes = U + C + 4.0 * r["nseg"]   # algorithmic bytes of one compress launch
+    dec_bytes = U + C                      # algorithmic bytes of one decompress launch
+    kc, kd = KERNELS[codec_name]
+    t_comp, t_dec = r["t_comp"], r["t_dec"]
+    dominant = (kc, comp_bytes, t_comp) if t_comp >= t_dec else (kd, dec_bytes, t_dec)
+    achieved = dominant[1] / dominant[2] / 1e9
+    traffic = None
+    try:
+        with open(traffic_json) as f:
+            traffic = json.load(f).get(dominant[0])
+    except (OSError, ValueError):
+        pass
+    roof = {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic, "algorithmic_bytes_per_launch": dominant[1],
+            "avg_launch_ms": round(dominant[2] * 1e3, 4)}
+    kernels = {kc: {"avg_ms": round(t_comp * 1e3, 4), "alg_GBs": round(comp_bytes / t_comp / 1e9, 2)},
+               kd: {"avg_ms": round(t_dec * 1e3, 4), "alg_GBs": round(dec_bytes / t_dec / 1e9, 2)}}
+    return roof, kernels
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import bitar_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+    eng = bitar_amd.Engine(dev)
+    ctx = {"world": world, "rank": rank}
+    n, seg = args.bytes, args.seg
+    r = roundtrip(eng, ctx, args.codec, args.kind, n, seg, args.steps, args.warmup, rank)
+    zs = None
+    if args.codec != "zstd" and not args.no_zstd:
+        # BASELINE configs[5]: Zstd level-1-class frames on Parquet-column-like buffers
+        # (kind 2, Arrow record-batch bodies), same sharding and all-gather, every rank
+        zs = roundtrip(eng, ctx, "zstd", 2, n, seg, args.steps, args.warmup, rank + 1000)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
 
     U = float(n)
-    C = float(csize)
-    value = world * U * args.steps / elapsed / GIB
-    comp_bytes = U + C + 4.0 * nseg        # algorithmic bytes of one compress launch
-    dec_bytes = U + C                      # algorithmic bytes of one decompress launch
-    kc, kd = (("lz4_compress_kernel", "lz4_decompress_kernel") if args.codec == "lz4"
-              else ("deflate_compress_kernel", "inflate_kernel"))
-    dominant = (kc, comp_bytes, t_comp) if t_comp >= t_dec else (kd, dec_bytes, t_dec)
-    achieved = dominant[1] / dominant[2] / 1e9
-    traffic = None
-    try:
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        traffic = tj.get(dominant[0])
-    except (OSError, ValueError):
-        pass
+    C = float(r["csize"])
+    value = world * U * args.steps / r["elapsed"] / GIB
+    roof, kernels = kernel_lines(args.codec, r, n, args.traffic_json)
+    std = args.kind == 1 and args.codec == "lz4"
     res = {
         "metric": "GiB/s compress+decompress on 1-GiB Arrow buffer, 1/2/4/8 GPUs; % HBM roofline",
         "value": round(value, 3),
@@ -211,7 +251,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -219,61 +259,80 @@ def main():
         "data": "synthetic (deterministic SplitMix64 generator, generated in HBM)",
         "config": {"workload": "LZ4 block compress + decompress round trip, 1 GiB per GPU, "
                                "64 KiB segments, Silesia-style mix (BASELINE configs[2])"
-                               if (args.kind == 1 and args.codec == "lz4")
-                               else f"{args.codec} round trip, kind {args.kind}, seg {seg}",
-                   "bytes_per_gpu": n, "segment_bytes": seg, "segments_per_gpu": nseg,
-                   "codec": "lz4-block" if args.codec == "lz4" else "deflate-raw-fixed",
+                               if std else f"{args.codec} round trip, kind {args.kind}, seg {seg}",
+                   "bytes_per_gpu": n, "segment_bytes": seg, "segments_per_gpu": r["nseg"],
+                   "codec": CODEC_NAMES[args.codec],
                    "input_kind": args.kind,
                    "parallelism": f"{world} independent shards (round-robin segments), "
                                   "RCCL all-gather of sizes" if world > 1 else "1 GPU"},
         "compression_ratio": round(U / C, 4),
-        "compress_gibs": round(U / t_comp / GIB, 3),
-        "decompress_gibs": round(U / t_dec / GIB, 3),
-        "roundtrip_ok": ok,
-        "roofline": {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "algorithmic_bytes_per_launch": dominant[1],
-                     "avg_launch_ms": round(dominant[2] * 1e3, 4)},
-        "kernels": {kc: {"avg_ms": round(t_comp * 1e3, 4),
-                         "alg_GBs": round(comp_bytes / t_comp / 1e9, 2)},
-                    kd: {"avg_ms": round(t_dec * 1e3, 4),
-                         "alg_GBs": round(dec_bytes / t_dec / 1e9, 2)}},
+        "compress_gibs": round(U / r["t_comp"] / GIB, 3),
+        "decompress_gibs": round(U / r["t_dec"] / GIB, 3),
+        "roundtrip_ok": r["ok"],
+        "roofline": roof,
+        "kernels": kernels,
     }
     if world == 1 and args.codec == "lz4" and not args.no_secondary:
         # BASELINE configs[1]: 1-GiB random-byte buffer, LZ4 decompress only (the HBM-bound
         # case of the same kernel), reported beside the headline round trip
-        eng.fill(0, 1, data)
-        eng.compress_into(codec, data, seg, slab, stride, sizes, n=n)
-        eng.sync()
-        c_rand = float(sizes.to(torch.int64).sum().item())
-        evs = []
-        for i in range(args.warmup + args.steps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            eng.decompress_slab_into(codec, slab, stride, sizes, nseg, seg, out, prod,
-                                     capacity=nseg * seg)
-            e1.record(stream)
-            if i >= args.warmup:
-                evs.append((e0, e1))
-        torch.cuda.synchronize()
-        eng.sync()
-        ok2 = bool(torch.equal(out[:n], data))
-        t2 = sum(a.elapsed_time(b) for a, b in evs) / len(evs) / 1e3
-        alg2 = (U + c_rand) / t2 / 1e9
-        res["secondary"] = {
-            "workload": "BASELINE configs[1]: 1 GiB random bytes, LZ4 block decompress only, "
-                        "64 KiB segments, HBM-resident",
-            "decompress_gibs": round(U / t2 / GIB, 3), "avg_launch_ms": round(t2 * 1e3, 4),
-            "roofline": {"bound": "hbm", "achieved": round(alg2, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(alg2 / HBM_PEAK_GBS, 4),
-                         "algorithmic_bytes_per_launch": U + c_rand},
-            "roundtrip_ok": ok2}
+        res["secondary"] = random_decompress(eng, n, seg, args)
+    if zs is not None:
+        zroof, zkern = kernel_lines("zstd", zs, n, args.traffic_json)
+        res["zstd"] = {
+            "workload": "BASELINE configs[5]: Zstd frame per 64 KiB segment (raw literals, "
+                        "predefined FSE sequences), compress + RCCL size all-gather + "
+                        "decompress, 1 GiB Arrow record-batch buffer per GPU",
+            "value": round(world * U * args.steps / zs["elapsed"] / GIB, 3), "unit": "GiB/s",
+            "ms_per_step": round(zs["elapsed"] / args.steps * 1e3, 4),
+            "compression_ratio": round(U / zs["csize"], 4),
+            "compress_gibs": round(U / zs["t_comp"] / GIB, 3),
+            "decompress_gibs": round(U / zs["t_dec"] / GIB, 3),
+            "roundtrip_ok": zs["ok"], "roofline": zroof, "kernels": zkern}
     if not args.no_cpu_baseline and world == 1 and args.codec == "lz4":
         res["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def random_decompress(eng, n, seg, args):
+    import torch
+    import bitar_amd
+    codec = bitar_amd.CODEC_LZ4
+    nseg = (n + seg - 1) // seg
+    stride = bitar_amd.slot_size(codec, seg)
+    data = eng.empty(n)
+    slab = eng.empty(nseg * stride)
+    sizes = eng.empty(nseg, dtype=torch.int32)
+    out = eng.empty(nseg * seg)
+    prod = eng.empty(nseg, dtype=torch.int32)
+    stream = torch.cuda.current_stream()
+    eng.fill(0, 1, data)
+    eng.compress_into(codec, data, seg, slab, stride, sizes, n=n)
+    eng.sync()
+    c_rand = float(sizes.to(torch.int64).sum().item())
+    evs = []
+    for i in range(args.warmup + args.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        eng.decompress_slab_into(codec, slab, stride, sizes, nseg, seg, out, prod,
+                                 capacity=nseg * seg)
+        e1.record(stream)
+        if i >= args.warmup:
+            evs.append((e0, e1))
+    torch.cuda.synchronize()
+    eng.sync()
+    ok2 = bool(torch.equal(out[:n], data))
+    t2 = sum(a.elapsed_time(b) for a, b in evs) / len(evs) / 1e3
+    alg2 = (float(n) + c_rand) / t2 / 1e9
+    return {
+        "workload": "BASELINE configs[1]: 1 GiB random bytes, LZ4 block decompress only, "
+                    "64 KiB segments, HBM-resident",
+        "decompress_gibs": round(n / t2 / GIB, 3), "avg_launch_ms": round(t2 * 1e3, 4),
+        "roofline": {"bound": "hbm", "achieved": round(alg2, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(alg2 / HBM_PEAK_GBS, 4),
+                     "algorithmic_bytes_per_launch": float(n) + c_rand},
+        "roundtrip_ok": ok2}
 
 
 if __name__ == "__main__":
