@@ -1,6 +1,6 @@
 // demo_app.cc -- the bitar demo/benchmark harness on MI355X (reference apps/demo_app.cc).
 //
-//   demo_app [--file|-f PATH] [--bytes|-b N] [--codec deflate|lz4] [--seg N] [--devices N]
+//   demo_app [--file|-f PATH] [--bytes|-b N] [--codec deflate|lz4|zstd] [--seg N] [--devices N]
 //            [--workers N]
 //
 // Reads raw bytes from PATH (mode 0 of the reference, demo_app.cc:113-130) or, without a
@@ -69,7 +69,9 @@ int main(int argc, char** argv) {
     data.resize(static_cast<size_t>(bytes));
     Fill(data);
   }
-  const auto codec = codec_name == "lz4" ? bitar::Codec::LZ4 : bitar::Codec::DEFLATE;
+  const auto codec = codec_name == "lz4"    ? bitar::Codec::LZ4
+                     : codec_name == "zstd" ? bitar::Codec::ZSTD
+                                            : bitar::Codec::DEFLATE;
   auto* driver = bitar::CompressDriver<bitar::Class_HIP_GFX950>::Instance();
   auto ids = driver->ListAvailableDeviceIds();
   if (!ids.ok()) { std::cerr << ids.status().ToString() << "\n"; return 1; }

@@ -39,8 +39,9 @@ using IsEnumConstant = std::enable_if_t<std::is_enum_v<EnumClass> &&
 using Class_HIP_GFX950 =
     std::integral_constant<internal::DriverClass, internal::DriverClass::HIP_GFX950>;
 
-/// The segment codec (the reference hard-codes RTE_COMP_ALGO_DEFLATE, config.cc:86-88).
-enum class Codec : std::uint8_t { DEFLATE = 1, LZ4 = 2 };
+/// The segment codec (the reference hard-codes RTE_COMP_ALGO_DEFLATE, config.cc:86-88;
+/// ZSTD is DPDK's RTE_COMP_ALGO_ZSTD-shaped option, BASELINE configs[5]).
+enum class Codec : std::uint8_t { DEFLATE = 1, LZ4 = 2, ZSTD = 3 };
 /// rte_comp_huffman
 enum class HuffmanEncoding : std::uint8_t { DEFAULT = 0, FIXED = 1, DYNAMIC = 2 };
 /// rte_comp_checksum_type

@@ -9,6 +9,7 @@ std::string_view ToString(Codec c) {
   switch (c) {
     case Codec::DEFLATE: return "DEFLATE";
     case Codec::LZ4: return "LZ4";
+    case Codec::ZSTD: return "ZSTD";
   }
   return "UNKNOWN";
 }

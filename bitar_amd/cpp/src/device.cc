@@ -180,7 +180,11 @@ bool OnDevice(std::uint64_t address, int device) {
 }
 
 std::uint32_t AbiCodec(Codec c) {
-  return c == Codec::LZ4 ? BITAR_HIP_CODEC_LZ4 : BITAR_HIP_CODEC_DEFLATE;
+  switch (c) {
+    case Codec::LZ4: return BITAR_HIP_CODEC_LZ4;
+    case Codec::ZSTD: return BITAR_HIP_CODEC_ZSTD;
+    default: return BITAR_HIP_CODEC_DEFLATE;
+  }
 }
 
 }  // namespace
@@ -421,7 +425,8 @@ arrow::Status CompressDevice<Class, Enable>::ValidateConfiguration() {
   }
   if (configuration_->burst_size() == 0)
     return arrow::Status::Invalid("Burst size must be greater than 0");
-  if (configuration_->codec() != Codec::DEFLATE && configuration_->codec() != Codec::LZ4)
+  if (configuration_->codec() != Codec::DEFLATE && configuration_->codec() != Codec::LZ4 &&
+      configuration_->codec() != Codec::ZSTD)
     return arrow::Status::NotImplemented("Compress device ", +device_id_,
                                          " does not support the codec");
   if (configuration_->max_sgl_segs() < 1) configuration_->set_max_sgl_segs(1);
@@ -432,7 +437,8 @@ arrow::Status CompressDevice<Class, Enable>::ValidateConfiguration() {
     return arrow::Status::Invalid("decompressed_seg_size is not in the range of [",
                                   internal::kMinSegSize, ", ", internal::kMaxSegSize32, "]");
   }
-  const std::uint8_t window = configuration_->codec() == Codec::LZ4 ? 16 : 15;
+  // window log: DEFLATE 2^15; LZ4 offsets and single-segment Zstd frames reach 2^16
+  const std::uint8_t window = configuration_->codec() == Codec::DEFLATE ? 15 : 16;
   if (configuration_->window_size() == 0) {
     configuration_->set_window_size(window);
   } else if (configuration_->window_size() != window) {

@@ -78,34 +78,70 @@ __device__ __forceinline__ uint32_t fwd_peek(State& s, uint8_t* win, const Fwd& 
 // backward bit reader: bits [0, bitpos) of a stream remain; read(n) returns bits
 // [bitpos - n, bitpos) as a little-endian integer (zeros below bit 0); bitpos < 0 after a
 // read = the stream was overrun.  The container holds bits [8 lo, bitpos).
+// The stream bytes come from two 256-B register chunks (lane l = one aligned dword), not from
+// the LDS window: the window keeps the raw literal section, which the sequence executor reads
+// at the other end of the block, staged.  c1 covers absolute [cb, cb + 256), c0 the 256 B
+// below it; when the reader moves wholly into c0 the pair slides down and c0 is reloaded,
+// so the next chunk's HBM latency overlaps ~60 sequences of decode.
 struct Bwd {
   uint32_t start;
   int32_t bitpos;
   uint64_t c;
   int32_t cn;
   uint32_t lo;
+  uint32_t c0, c1;  // register chunks (per lane: one dword)
+  uint64_t cb;      // absolute address of c1's first byte (4-aligned)
 };
+// aligned dword `lane` of the 256-B chunk at absolute address a (dwords holding no byte of
+// the stream read as zero and are never loaded)
+__device__ __forceinline__ uint32_t bwd_chunk(const State& s, uint64_t a) {
+  const uint64_t d = a + 4ull * lane_id();
+  const uint64_t lo = (uint64_t)(uintptr_t)s.src, hi = lo + s.csize;
+  uint32_t v = 0;
+  if (d < hi && d + 4 > lo) v = *reinterpret_cast<const GMEM uint32_t*>((uintptr_t)d);
+  return v;
+}
+// stream bytes [pos, pos + 4) (pos decreasing over the reader's life), little-endian
+__device__ __forceinline__ uint32_t bwd_dword(const State& s, Bwd& b, uint32_t pos) {
+  const uint64_t abs = (uint64_t)(uintptr_t)(s.src + pos);
+  while (abs + 4 <= b.cb) {  // wholly inside c0: slide down, prefetch the next chunk
+    b.c1 = b.c0;
+    b.cb -= 256;
+    b.c0 = bwd_chunk(s, b.cb - 256);
+  }
+  const uint32_t a = uniform((uint32_t)(abs - (b.cb - 256)));  // in [0, 508)
+  const uint32_t q = a >> 2, r = a & 3u, q1 = q + 1;
+  const uint32_t w0 = q < 64 ? readlane(b.c0, q) : readlane(b.c1, q - 64);
+  const uint32_t w1 = q1 < 64 ? readlane(b.c0, q1) : readlane(b.c1, (q1 - 64) & 63u);
+  return funnel(w0, w1, r);
+}
 __device__ __forceinline__ bool bwd_init(State& s, uint8_t* win, Bwd& b, uint32_t start, uint32_t len) {
   if (len == 0) return false;
   const uint32_t last = load_le(s, win, start + len - 1, 1);
   if (last == 0) return false;
   const uint32_t h = hb32(last);
+  start = uniform(start);
+  len = uniform(len);
   b.start = start;
   b.bitpos = (int32_t)((len - 1) * 8 + h);
   b.c = last & ((1u << h) - 1);
   b.cn = (int32_t)h;
   b.lo = len - 1;
+  const uint64_t top = uniform64(((uint64_t)(uintptr_t)(s.src + start + len) + 3) & ~3ull);
+  b.cb = top - 256;
+  b.c1 = bwd_chunk(s, b.cb);
+  b.c0 = bwd_chunk(s, b.cb - 256);
   return true;
 }
-__device__ __forceinline__ void bwd_fill(State& s, uint8_t* win, Bwd& b) {
+__device__ __forceinline__ void bwd_fill(State& s, uint8_t*, Bwd& b) {
   if (b.cn <= 32 && b.lo >= 4) {
     b.lo -= 4;
-    b.c = (b.c << 32) | load_le(s, win, b.start + b.lo, 4);
+    b.c = (b.c << 32) | uniform(bwd_dword(s, b, b.start + b.lo));
     b.cn += 32;
   }
   while (b.cn <= 56 && b.lo > 0) {
     b.lo -= 1;
-    b.c = (b.c << 8) | load_le(s, win, b.start + b.lo, 1);
+    b.c = (b.c << 8) | (uniform(bwd_dword(s, b, b.start + b.lo)) & 0xFFu);
     b.cn += 8;
   }
 }
@@ -131,7 +167,7 @@ __device__ __forceinline__ void bwd_skip(Bwd& b, uint32_t n) {
 
 // ---- FSE ----------------------------------------------------------------------------------
 // FSE_readNCount from the stream at [start, start + len); returns bytes used, or -1
-__device__ int read_ncount(State& s, uint8_t* win, Tabs& t, uint32_t start, uint32_t len,
+__device__ __forceinline__ int read_ncount(State& s, uint8_t* win, Tabs& t, uint32_t start, uint32_t len,
                            uint32_t& max_sym, uint32_t& al, uint32_t max_al) {
   Fwd f = {start, len, 0};
   const uint32_t log = fwd_peek(s, win, f, 4) + 5;
@@ -188,7 +224,7 @@ __device__ int read_ncount(State& s, uint8_t* win, Tabs& t, uint32_t start, uint
 __device__ __forceinline__ uint32_t pick4(const uint32_t (&v)[4], uint32_t j) {
   return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
 }
-__device__ bool fse_build(Tabs& t, uint32_t* cells, uint32_t max_sym, uint32_t al) {
+__device__ __forceinline__ bool fse_build(Tabs& t, uint32_t* cells, uint32_t max_sym, uint32_t al) {
   const uint32_t lane = lane_id();
   const uint32_t size = 1u << al;
   lds_order();
@@ -262,7 +298,7 @@ __device__ __forceinline__ uint32_t cell(const uint32_t* cells, uint32_t st) {
 
 // ---- Huffman -------------------------------------------------------------------------------
 // tree description at stream [start, start + len); returns bytes used or -1; sets log
-__device__ int huf_read(State& s, uint8_t* win, Tabs& t, uint32_t start, uint32_t len,
+__device__ __forceinline__ int huf_read(State& s, uint8_t* win, Tabs& t, uint32_t start, uint32_t len,
                         uint32_t& log) {
   const uint32_t lane = lane_id();
   if (len < 1) return -1;
@@ -379,7 +415,7 @@ __device__ int huf_read(State& s, uint8_t* win, Tabs& t, uint32_t start, uint32_
 }
 
 // decode one Huffman stream of n symbols to out[0, n) (global); false if malformed
-__device__ bool huf_stream(State& s, uint8_t* win, Tabs& t, uint32_t log, uint32_t start,
+__device__ __forceinline__ bool huf_stream(State& s, uint8_t* win, Tabs& t, uint32_t log, uint32_t start,
                            uint32_t len, GMEM uint8_t* out, uint32_t n) {
   Bwd b;
   if (!bwd_init(s, win, b, start, len)) return false;
@@ -433,13 +469,16 @@ struct Frame {
   uint32_t rep0, rep1, rep2;
   uint32_t al[3];      // accuracy logs of the LL / OF / ML tables
   bool have[3];
+  bool pre[3];         // table k holds the predefined distribution (built once per frame)
   uint32_t huf_log;    // 0 = no Huffman table yet
 };
 
 // one compressed block at stream [p, p + len)
-__device__ bool block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr, uint32_t p,
+__device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr, uint32_t p,
                       uint32_t len) {
   const uint32_t lane = lane_id();
+  p = uniform(p);
+  len = uniform(len);
   const uint32_t end = p + len;
   // ---- literals section ----
   const uint32_t b0 = load_le(s, win, p, 1);
@@ -542,32 +581,38 @@ __device__ bool block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr,
     const uint32_t modes = load_le(s, win, q, 1);
     q += 1;
     if (modes & 3u) return false;
-    // tables in order LL, OF, ML
+    // tables in order LL, OF, ML (unrolled: fr.al / fr.have stay in registers)
+#pragma unroll
     for (uint32_t k = 0; k < 3; ++k) {
       const uint32_t mode = (modes >> (6 - 2 * k)) & 3u;
       const uint32_t maxs = k == 0 ? 35u : k == 1 ? 31u : 52u;
       const uint32_t maxal = k == 1 ? 8u : 9u;
       uint32_t* cells = t.fse[k];
       if (mode == 0) {
-        const uint32_t dmax = k == 0 ? 35u : k == 1 ? 28u : 52u;
-        lds_order();
-        if (lane <= dmax)
-          t.norm[lane] = k == 0 ? kLLDefault[lane] : k == 1 ? kOFDefault[lane] : kMLDefault[lane];
-        lds_order();
         const uint32_t dal = k == 1 ? 5u : 6u;
-        if (!fse_build(t, cells, dmax, dal)) return false;
+        if (!fr.pre[k]) {
+          const uint32_t dmax = k == 0 ? 35u : k == 1 ? 28u : 52u;
+          lds_order();
+          if (lane <= dmax)
+            t.norm[lane] = k == 0 ? kLLDefault[lane] : k == 1 ? kOFDefault[lane] : kMLDefault[lane];
+          lds_order();
+          if (!fse_build(t, cells, dmax, dal)) return false;
+          fr.pre[k] = true;
+        }
         fr.al[k] = dal;
       } else if (mode == 1) {
         if (q >= end) return false;
         const uint32_t sy = load_le(s, win, q, 1);
         if (sy > maxs) return false;
         fse_rle(cells, sy);
+        fr.pre[k] = false;
         fr.al[k] = 0;
         q += 1;
       } else if (mode == 2) {
         uint32_t ms = maxs, al;
         const int n = read_ncount(s, win, t, q, end - q, ms, al, maxal);
         if (n < 0) return false;
+        fr.pre[k] = false;
         if (!fse_build(t, cells, ms, al)) return false;
         fr.al[k] = al;
         q += (uint32_t)n;
@@ -578,6 +623,10 @@ __device__ bool block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr,
     }
     Bwd b;
     if (q >= end || !bwd_init(s, win, b, q, end - q)) return false;
+    // baseline | extra-bit count << 24 of every LL / ML code, one code per lane: the loop
+    // reads them with v_readlane instead of a dependent constant-memory load per sequence
+    const uint32_t llt = lane < 36 ? kLLBase[lane] | ((uint32_t)kLLBits[lane] << 24) : 0u;
+    const uint32_t mlt = lane < 53 ? kMLBase[lane] | ((uint32_t)kMLBits[lane] << 24) : 0u;
     uint32_t sll = bwd_read(s, win, b, fr.al[0]);
     uint32_t sof = bwd_read(s, win, b, fr.al[1]);
     uint32_t sml = bwd_read(s, win, b, fr.al[2]);
@@ -585,13 +634,14 @@ __device__ bool block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr,
       const uint32_t cll = cell(t.fse[0], sll), cof = cell(t.fse[1], sof), cml = cell(t.fse[2], sml);
       const uint32_t llc = cll & 0xFFu, ofc = cof & 0xFFu, mlc = cml & 0xFFu;
       if (llc > 35 || mlc > 52 || ofc > 31) return false;
-      const uint32_t ofv = (1u << ofc) + bwd_read(s, win, b, ofc);
-      const uint32_t ml = kMLBase[mlc] + bwd_read(s, win, b, kMLBits[mlc]);
-      const uint32_t ll = kLLBase[llc] + bwd_read(s, win, b, kLLBits[llc]);
+      const uint32_t ofv = uniform((1u << ofc) + bwd_read(s, win, b, ofc));
+      const uint32_t mle = readlane(mlt, mlc), lle = readlane(llt, llc);
+      const uint32_t ml = uniform((mle & 0xFFFFFFu) + bwd_read(s, win, b, mle >> 24));
+      const uint32_t ll = uniform((lle & 0xFFFFFFu) + bwd_read(s, win, b, lle >> 24));
       if (k + 1 < nseq) {
-        sll = (cll >> 16) + bwd_read(s, win, b, (cll >> 8) & 0xFFu);
-        sml = (cml >> 16) + bwd_read(s, win, b, (cml >> 8) & 0xFFu);
-        sof = (cof >> 16) + bwd_read(s, win, b, (cof >> 8) & 0xFFu);
+        sll = uniform((cll >> 16) + bwd_read(s, win, b, (cll >> 8) & 0xFFu));
+        sml = uniform((cml >> 16) + bwd_read(s, win, b, (cml >> 8) & 0xFFu));
+        sof = uniform((cof >> 16) + bwd_read(s, win, b, (cof >> 8) & 0xFFu));
       }
       uint32_t off;
       if (ofv > 3) {
@@ -615,9 +665,36 @@ __device__ bool block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr,
       }
       // also keeps the output behind the unread Huffman literals in the slot tail
       if (lp + ll > regen || (uint64_t)s.op + ml + (regen - lp) > s.cap) return false;
-      copy_lits(ll);
-      if (off == 0 || off > s.op) return false;
-      match_copy(s, ring, off, ml);
+      if (off == 0 || off > s.op + ll) return false;
+      if (lt == 0 && ll + ml <= kWave && off <= kNearOff) {
+        // one step for the whole sequence: every output lane gathers its byte from the
+        // window (a literal, or a match byte that copies a literal of this step) or from the
+        // ring (history), with one LDS read and one LDS write
+        make_room(s, ring, ll + ml);
+        const uint32_t w = win_at(s, win, lit_stream + lp, ll);
+        const uint32_t m = lane - ll;  // match lanes: index in the match
+        uint32_t rel = m;
+        if (off < ml) {  // m mod off, exact for m, off < 64
+          const float qf = floorf(((float)m + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+          rel = m - (uint32_t)qf * off;
+        }
+        const uint32_t from = s.op + ll + rel - off;  // output position a match byte copies
+        const uintptr_t base = (uintptr_t)s.dst;
+        const uint32_t a = lane < ll ? w + lane
+                           : from >= s.op ? w + (from - s.op)
+                                          : kWin + (uint32_t)((base + from) & kRingMask);
+        const bool act = lane < ll + ml;
+        lds_order();
+        const uint32_t v = act ? (uint32_t)win[a] : 0u;  // win and ring are one LDS array
+        lds_order();
+        if (act) ring[(base + s.op + lane) & kRingMask] = (uint8_t)v;
+        lds_order();
+        s.op += ll + ml;
+        lp += ll;
+      } else {
+        copy_lits(ll);
+        match_copy(s, ring, off, ml);
+      }
     }
     if (b.bitpos != 0) return false;
   } else if (q != end) {
@@ -629,7 +706,7 @@ __device__ bool block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr,
 }
 
 // XXH64 of the first n output bytes (already flushed to HBM and fenced), low 32 bits
-__device__ uint32_t xxh64_low(const GMEM uint8_t* p, uint32_t n) {
+__device__ __forceinline__ uint32_t xxh64_low(const GMEM uint8_t* p, uint32_t n) {
   constexpr uint64_t P1 = 11400714785074694791ull, P2 = 14029467366897019727ull,
                      P3 = 1609587929392839161ull, P4 = 9650029242287828579ull,
                      P5 = 2870177450012600261ull;
@@ -746,6 +823,7 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     Frame fr;
     fr.rep0 = 1; fr.rep1 = 4; fr.rep2 = 8;
     fr.have[0] = fr.have[1] = fr.have[2] = false;
+    fr.pre[0] = fr.pre[1] = fr.pre[2] = false;
     fr.huf_log = 0;
     bool bad = false, last = false;
     while (!last) {

@@ -19,8 +19,9 @@ def main():
     import torch
     import bitar_amd
     eng = bitar_amd.Engine(0)
-    codec = bitar_amd.CODEC_LZ4 if a.codec == "lz4" else bitar_amd.CODEC_DEFLATE
-    seg = 65536 if a.codec == "lz4" else 59460
+    codec = {"lz4": bitar_amd.CODEC_LZ4, "deflate": bitar_amd.CODEC_DEFLATE,
+             "zstd": bitar_amd.CODEC_ZSTD}[a.codec]
+    seg = 59460 if a.codec == "deflate" else 65536
     n = a.bytes
     nseg = (n + seg - 1) // seg
     stride = bitar_amd.slot_size(codec, seg)

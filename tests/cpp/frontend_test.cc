@@ -108,7 +108,7 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
   CHECK(data.size() > 100000);
   auto host_in = std::make_shared<arrow::Buffer>(data.data(), static_cast<int64_t>(data.size()));
 
-  for (auto codec : {bitar::Codec::DEFLATE, bitar::Codec::LZ4}) {
+  for (auto codec : {bitar::Codec::DEFLATE, bitar::Codec::LZ4, bitar::Codec::ZSTD}) {
     const std::uint32_t seg = codec == bitar::Codec::DEFLATE ? 59460 : 65536;
     auto& dev = (*devs)[0];
     // not initialized yet -> Invalid (EntryGuard, device.cc:446-451)
@@ -135,7 +135,10 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
     const auto nseg = (data.size() + seg - 1) / seg;
     CHECK(comp->size() == nseg);
     for (const auto& b : *comp) CHECK(!b->is_cpu());
-    WriteSegments(outdir + (codec == bitar::Codec::DEFLATE ? "/deflate.segs" : "/lz4.segs"), *comp);
+    WriteSegments(outdir + (codec == bitar::Codec::DEFLATE ? "/deflate.segs"
+                            : codec == bitar::Codec::LZ4   ? "/lz4.segs"
+                                                           : "/zstd.segs"),
+                  *comp);
 
     auto out = arrow::AllocateResizableBuffer(static_cast<int64_t>(nseg * seg));
     CHECK_OK(out.status());
@@ -172,7 +175,7 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
       bv.emplace_back(std::make_unique<arrow::Buffer>(bogus->data(), 4));
       auto o = arrow::AllocateResizableBuffer(seg);
       std::unique_ptr<arrow::ResizableBuffer> ob = std::move(*o);
-      if (codec == bitar::Codec::DEFLATE) CHECK(d->Decompress(0, bv, ob).IsIOError());
+      if (codec != bitar::Codec::LZ4) CHECK(d->Decompress(0, bv, ob).IsIOError());
     }
 
     // async on both queue pairs (CompressAsync / WaitLcore, util.h:216-236)

@@ -4,7 +4,7 @@ memory-pool / async API of the reference, over libbitar_hip.so.
 CPU: the library and test binary build against Arrow 25 and the configuration rules hold.
 GPU: Compress / Decompress / Recycle / async through a real device; every compressed
 segment it returns must decode with the third-party decoder (zlib for DEFLATE, the pinned
-oracle for LZ4) to the matching input slice.
+oracle for LZ4 and Zstd) to the matching input slice.
 """
 import os
 import struct
@@ -63,4 +63,9 @@ def test_frontend_on_gpu(tmp_path):
     assert len(segs) == (len(data) + seg - 1) // seg
     for i, s in enumerate(segs):
         rc, plain = O.lz4_decompress(s, seg)
+        assert rc == 0 and plain == data[i * seg:(i + 1) * seg]
+    segs = _segments(tmp_path / "zstd.segs")
+    assert len(segs) == (len(data) + seg - 1) // seg
+    for i, s in enumerate(segs):
+        rc, plain = O.zstd_decompress(s, seg)
         assert rc == 0 and plain == data[i * seg:(i + 1) * seg]
