@@ -5,7 +5,9 @@
 // grid or a size it does not assume (one wave per segment, seg <= 65536).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -28,7 +30,10 @@ __global__ void zstd_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t
                                      uint8_t* const*, uint32_t*, uint32_t*);
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                        const uint32_t*, uint32_t, uint32_t, uint8_t*,
-                                       uint32_t*, uint32_t*);
+                                       uint32_t*, uint32_t*, uint32_t);
+template <uint32_t L>
+__global__ void zstd_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
+                                  const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
 __global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t*);
 __global__ void pack_kernel(const uint8_t*, uint64_t, const uint32_t*, const uint64_t*, uint32_t,
                             uint8_t*);
@@ -279,6 +284,22 @@ int bitar_hip_pointer_info(const void* ptr, int* kind, int* device) {
   return 0;
 }
 
+// segments per wave of zstd_lanes_kernel: BITAR_HIP_ZSTD_LANES = 64 / 32 / 16 / 8, 0 = off
+// (tests switch it with bitar_hip_debug_set_zstd_lanes to cover both decoders)
+static uint32_t lanes_from(long x) {
+  return x <= 0 ? 0u : x >= 64 ? 64u : x >= 32 ? 32u : x >= 16 ? 16u : 8u;
+}
+static std::atomic<uint32_t> g_zstd_lanes{[] {
+  const char* e = std::getenv("BITAR_HIP_ZSTD_LANES");
+  return lanes_from(e ? std::strtol(e, nullptr, 10) : 16);
+}()};
+static uint32_t zstd_lanes() { return g_zstd_lanes.load(std::memory_order_relaxed); }
+extern "C" int bitar_hip_debug_set_zstd_lanes(int lanes) {
+  const uint32_t old = zstd_lanes();
+  g_zstd_lanes.store(lanes_from(lanes));
+  return (int)old;
+}
+
 static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            const void* const* d_srcs, const void* d_slab, uint64_t stride,
                            const uint32_t* d_sizes, uint32_t nseg, uint32_t seg, void* d_out,
@@ -306,9 +327,29 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
   else if (codec == BITAR_HIP_CODEC_DEFLATE)
     hipLaunchKernelGGL(bitar_hip::inflate_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
                        stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
-  else
+  else {
+    // lane-per-segment decoder first; the wave-per-segment decoder then takes the segments it
+    // deferred (zstd_lanes.hip)
+    const uint32_t L = zstd_lanes();
+    if (L) {
+      const dim3 g((nseg + L - 1) / L);
+      if (L == 64)
+        hipLaunchKernelGGL(bitar_hip::zstd_lanes_kernel<64>, g, dim3(64), 0, s, srcs, slab,
+                           stride, d_sizes, nseg, seg, out, d_produced);
+      else if (L == 32)
+        hipLaunchKernelGGL(bitar_hip::zstd_lanes_kernel<32>, g, dim3(64), 0, s, srcs, slab,
+                           stride, d_sizes, nseg, seg, out, d_produced);
+      else if (L == 16)
+        hipLaunchKernelGGL(bitar_hip::zstd_lanes_kernel<16>, g, dim3(64), 0, s, srcs, slab,
+                           stride, d_sizes, nseg, seg, out, d_produced);
+      else
+        hipLaunchKernelGGL(bitar_hip::zstd_lanes_kernel<8>, g, dim3(64), 0, s, srcs, slab,
+                           stride, d_sizes, nseg, seg, out, d_produced);
+    }
     hipLaunchKernelGGL(bitar_hip::zstd_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs,
-                       slab, stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
+                       slab, stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err,
+                       L ? 1u : 0u);
+  }
   HIP_TRY(hipGetLastError(), "decompress launch");
   return 0;
 }

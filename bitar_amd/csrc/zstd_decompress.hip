@@ -13,11 +13,28 @@
 // overtake the literal reads (op <= cap - remaining literals).
 #include "stream_ring.hip.h"
 
+#include <type_traits>
+
 namespace bitar_hip {
 
 namespace zsd {
 
 using namespace sr;
+
+// ZPROF builds (scripts/build_variant.sh NAME -DZPROF) accumulate s_memtime cycles per phase
+// in LDS and add them to g_zprof at wave end (bitar_hip_debug_zstd_prof reads them).
+#ifdef ZPROF
+__device__ unsigned long long g_zprof[16];
+__shared__ unsigned long long zp_lds[16];
+#define ZP_T() ((uint64_t)__builtin_amdgcn_s_memtime())
+#define ZP_BEGIN(v) const uint64_t v = ZP_T()
+#define ZP_ADD(i, x) do { if (lane_id() == 0) zp_lds[i] += (x); } while (0)
+#define ZP_END(i, v) ZP_ADD(i, ZP_T() - (v))
+#else
+#define ZP_BEGIN(v)
+#define ZP_ADD(i, x)
+#define ZP_END(i, v)
+#endif
 
 constexpr uint32_t kHufMaxLog = 11;
 
@@ -465,6 +482,107 @@ __device__ __forceinline__ void out_global(State& s, uint8_t* ring, const GMEM u
   }
 }
 
+// Fast backward bit reader (sequence sections): C = the 8 stream bytes at [ptr, ptr + 8),
+// little-endian, with bytes below the section start zeroed; `used` bits are consumed from
+// its top.  reload() moves ptr down by the whole bytes consumed (libzstd's
+// BIT_reloadDStream), so after a reload at least 57 bits are readable.  The bytes come from
+// two register chunks of 256 B (lane l = one aligned dword) overlapping by 128 B: c1 covers
+// [cb, cb + 256), c0 [cb - 128, cb + 128), prefetched one slide ahead.
+struct FastBits {
+  uint64_t C;
+  uint32_t used;
+  int32_t ptr, cb;  // stream positions (relative to s.src; may go below 0 on overrun)
+  uint32_t c0, c1;
+  // aligned dword `lane` of the 256 B at stream position `at` (4-aligned in absolute terms);
+  // dwords holding no byte of the segment read as zero and are never loaded
+  __device__ __forceinline__ static uint32_t chunk(const State& s, int32_t at) {
+    const uint64_t lo = (uint64_t)(uintptr_t)s.src, hi = lo + s.csize;
+    const uint64_t d = lo + (uint64_t)(int64_t)at + 4ull * lane_id();
+    uint32_t v = 0;
+    if (d < hi && d + 4 > lo) v = *reinterpret_cast<const GMEM uint32_t*>((uintptr_t)d);
+    return v;
+  }
+  __device__ __forceinline__ void load(const State& s, uint32_t q) {
+    while (ptr < cb) {
+      c1 = c0;
+      cb -= 128;
+      c0 = chunk(s, cb - 128);
+    }
+    const uint32_t o = (uint32_t)(ptr - cb), qd = o >> 2, r = (o & 3u) * 8;
+    const uint32_t w0 = readlane(c1, qd), w1 = readlane(c1, qd + 1), w2 = readlane(c1, qd + 2);
+    const uint32_t lo = (uint32_t)((((uint64_t)w1 << 32) | w0) >> r);
+    const uint32_t hi = (uint32_t)((((uint64_t)w2 << 32) | w1) >> r);
+    C = ((uint64_t)hi << 32) | lo;
+    if (ptr < (int32_t)q) {
+      const uint32_t k = (uint32_t)((int32_t)q - ptr);
+      C = k >= 8 ? 0ull : C & (~0ull << (8 * k));
+    }
+  }
+  // section [q, end): false if empty or its last byte holds no end marker
+  __device__ __forceinline__ bool init(State& s, uint32_t q, uint32_t end) {
+    // the marker byte, read through the chunk path below (ptr = end - 8)
+    ptr = (int32_t)end - 8;
+    const int32_t mis = (int32_t)(((uintptr_t)s.src + (uint32_t)ptr) & 3u);
+    cb = ptr - mis - 128;
+    c1 = chunk(s, cb);
+    c0 = chunk(s, cb - 128);
+    load(s, q);
+    const uint32_t last = (uint32_t)(C >> 56);
+    if (last == 0) return false;
+    used = 8 - hb32(last);
+    return true;
+  }
+  __device__ __forceinline__ void reload(const State& s, uint32_t q) {
+    ptr -= (int32_t)(used >> 3);
+    used &= 7u;
+    load(s, q);
+  }
+  __device__ __forceinline__ uint32_t read(uint32_t n) {
+    const uint32_t sh = (64 - used - n) & 63u;  // n == used == 0: any shift, masked to 0
+    const uint32_t v = (uint32_t)(C >> sh) & ((1u << n) - 1u);
+    used += n;
+    return v;
+  }
+  __device__ __forceinline__ int32_t remaining(uint32_t q) const {
+    return 8 * (ptr - (int32_t)q) + 64 - (int32_t)used;
+  }
+};
+
+// Produce a pending chunk of co <= 64 output bytes.  Lane j (< co) is byte j of the chunk:
+// rec = first lane of its sequence | literal count << 8 | chunk literal index << 16, roff =
+// the sequence's offset; literal bytes are in LDS at w0 + chunk literal index.  Sources:
+// a literal, the ring (history before the chunk), or another lane of the chunk (a match
+// reaching into it), resolved by pointer doubling; then one LDS gather + one ring store.
+// Lanes >= co write ring slots ahead of the output, which are kRing - 64 bytes old,
+// already flushed, and rewritten before they are read.
+__device__ __forceinline__ void exec_chunk(State& s, uint8_t* win, uint8_t* ring, uint32_t co,
+                                           uint32_t rec, uint32_t roff, uint32_t w0) {
+  const uint32_t lane = lane_id();
+  make_room(s, ring, co);
+  const uint32_t base = (uint32_t)(uintptr_t)s.dst;
+  const uint32_t o = rec & 0xFFu, ll = (rec >> 8) & 0xFFu, lq = rec >> 16;
+  const uint32_t r = lane - o;
+  const bool is_lit = r < ll;
+  const uint32_t m = (r - ll) & 63u;
+  const uint32_t off = roff;
+  const float qf = floorf(((float)m + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+  const uint32_t mm = off <= m ? m - (uint32_t)qf * off : m;  // m mod off (exact below 64)
+  const int32_t srel = (int32_t)(o + ll + mm) - (int32_t)off;  // vs the chunk start
+  const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
+  uint32_t st = lane >= co ? kWin : is_lit ? w0 + lq + r
+                : srel >= 0 ? ((uint32_t)srel | 0x80000000u) : hist;
+  while (ballot((st & 0x80000000u) != 0u)) {  // alias chains strictly descend
+    const uint32_t other = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((st & 63u) << 2), (int)st);
+    st = (st & 0x80000000u) ? other : st;
+  }
+  uint8_t* lds = win;  // win and ring are one LDS array
+  lds_order();
+  const uint8_t v = lds[st];
+  ring[(base + s.op + lane) & kRingMask] = v;
+  lds_order();
+  s.op += co;
+}
+
 struct Frame {
   uint32_t rep0, rep1, rep2;
   uint32_t al[3];      // accuracy logs of the LL / OF / ML tables
@@ -480,6 +598,7 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
   p = uniform(p);
   len = uniform(len);
   const uint32_t end = p + len;
+  ZP_BEGIN(th);
   // ---- literals section ----
   const uint32_t b0 = load_le(s, win, p, 1);
   const uint32_t lt = b0 & 3u, sf = (b0 >> 2) & 3u;
@@ -576,8 +695,10 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
     nseq = load_le(s, win, q + 1, 2) + 0x7F00u;
     q += 3;
   }
+  ZP_END(2, th);
   if (nseq) {
     if (q >= end) return false;
+    ZP_BEGIN(tm);
     const uint32_t modes = load_le(s, win, q, 1);
     q += 1;
     if (modes & 3u) return false;
@@ -621,82 +742,189 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
       }
       fr.have[k] = true;
     }
-    Bwd b;
-    if (q >= end || !bwd_init(s, win, b, q, end - q)) return false;
+    if (q >= end) return false;
+    ZP_END(3, tm);
+    // FSE tables of <= 64 cells (every predefined one) move into registers: lane u holds cell
+    // u and a state lookup is one v_readlane instead of an LDS round trip
+    const bool rt = fr.al[0] <= 6 && fr.al[1] <= 6 && fr.al[2] <= 6;
+    lds_order();
+    const uint32_t tll = t.fse[0][lane], tof = t.fse[1][lane], tml = t.fse[2][lane];
     // baseline | extra-bit count << 24 of every LL / ML code, one code per lane: the loop
     // reads them with v_readlane instead of a dependent constant-memory load per sequence
     const uint32_t llt = lane < 36 ? kLLBase[lane] | ((uint32_t)kLLBits[lane] << 24) : 0u;
     const uint32_t mlt = lane < 53 ? kMLBase[lane] | ((uint32_t)kMLBits[lane] << 24) : 0u;
-    uint32_t sll = bwd_read(s, win, b, fr.al[0]);
-    uint32_t sof = bwd_read(s, win, b, fr.al[1]);
-    uint32_t sml = bwd_read(s, win, b, fr.al[2]);
-    for (uint32_t k = 0; k < nseq; ++k) {
-      const uint32_t cll = cell(t.fse[0], sll), cof = cell(t.fse[1], sof), cml = cell(t.fse[2], sml);
-      const uint32_t llc = cll & 0xFFu, ofc = cof & 0xFFu, mlc = cml & 0xFFu;
-      if (llc > 35 || mlc > 52 || ofc > 31) return false;
-      const uint32_t ofv = uniform((1u << ofc) + bwd_read(s, win, b, ofc));
-      const uint32_t mle = readlane(mlt, mlc), lle = readlane(llt, llc);
-      const uint32_t ml = uniform((mle & 0xFFFFFFu) + bwd_read(s, win, b, mle >> 24));
-      const uint32_t ll = uniform((lle & 0xFFFFFFu) + bwd_read(s, win, b, lle >> 24));
-      if (k + 1 < nseq) {
-        sll = uniform((cll >> 16) + bwd_read(s, win, b, (cll >> 8) & 0xFFu));
-        sml = uniform((cml >> 16) + bwd_read(s, win, b, (cml >> 8) & 0xFFu));
-        sof = uniform((cof >> 16) + bwd_read(s, win, b, (cof >> 8) & 0xFFu));
+    // Pending output chunk: short sequences (<= 64 output bytes, history in the ring) are
+    // packed into the next 64 output bytes; lane j of the chunk keeps the sequence it falls
+    // in (rec = first lane | literal count << 8 | chunk literal index << 16, roff = offset).
+    // A full chunk is produced with one gather + one ring store (exec_chunk).
+    uint32_t rec = 0, roff = 1, co = 0, lq = 0;
+    auto exec = [&]() __attribute__((always_inline)) {
+      if (!co) return;
+      uint32_t w0;
+      const uint32_t lp0 = lp - lq;
+      if (lt == 0) {
+        w0 = win_at(s, win, lit_stream + lp0, lq ? lq : 1u);
+      } else {  // RLE byte or Huffman-decoded literals (slot tail): stage them in the window
+        uint32_t v = lit_byte;
+        if (lt != 1 && lane < lq) v = lit_tail[lp0 + lane];
+        lds_order();
+        win[lane] = (uint8_t)v;
+        lds_order();
+        s.wb = ~0ull;  // the window no longer mirrors the stream
+        w0 = 0;
       }
-      uint32_t off;
-      if (ofv > 3) {
-        off = ofv - 3;
-        fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
-      } else {
-        const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
-        if (idx == 1) {
-          off = fr.rep0;
-        } else if (idx == 2) {
-          off = fr.rep1;
-          fr.rep1 = fr.rep0; fr.rep0 = off;
-        } else if (idx == 3) {
-          off = fr.rep2;
+      ZP_BEGIN(tx);
+      exec_chunk(s, win, ring, co, rec, roff, w0);
+      ZP_END(5, tx);
+      ZP_ADD(10, 1);
+      co = 0;
+      lq = 0;
+    };
+    // general sequence loop: any table size (cells in LDS), the bit-exact Bwd reader
+    auto run = [&]() __attribute__((always_inline)) -> bool {
+      Bwd b;
+      if (q >= end || !bwd_init(s, win, b, q, end - q)) return false;
+      uint32_t sll = bwd_read(s, win, b, fr.al[0]);
+      uint32_t sof = bwd_read(s, win, b, fr.al[1]);
+      uint32_t sml = bwd_read(s, win, b, fr.al[2]);
+      for (uint32_t k = 0; k < nseq; ++k) {
+        const uint32_t cll = cell(t.fse[0], sll), cof = cell(t.fse[1], sof), cml = cell(t.fse[2], sml);
+        const uint32_t llc = cll & 0xFFu, ofc = cof & 0xFFu, mlc = cml & 0xFFu;
+        if (llc > 35 || mlc > 52 || ofc > 31) return false;
+        const uint32_t ofv = uniform((1u << ofc) + bwd_read(s, win, b, ofc));
+        const uint32_t mle = readlane(mlt, mlc), lle = readlane(llt, llc);
+        const uint32_t ml = uniform((mle & 0xFFFFFFu) + bwd_read(s, win, b, mle >> 24));
+        const uint32_t ll = uniform((lle & 0xFFFFFFu) + bwd_read(s, win, b, lle >> 24));
+        if (k + 1 < nseq) {
+          sll = uniform((cll >> 16) + bwd_read(s, win, b, (cll >> 8) & 0xFFu));
+          sml = uniform((cml >> 16) + bwd_read(s, win, b, (cml >> 8) & 0xFFu));
+          sof = uniform((cof >> 16) + bwd_read(s, win, b, (cof >> 8) & 0xFFu));
+        }
+        uint32_t off;
+        if (ofv > 3) {
+          off = ofv - 3;
           fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
         } else {
-          off = fr.rep0 - 1;
-          if (off == 0) return false;
+          const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
+          if (idx == 1) {
+            off = fr.rep0;
+          } else if (idx == 2) {
+            off = fr.rep1;
+            fr.rep1 = fr.rep0; fr.rep0 = off;
+          } else if (idx == 3) {
+            off = fr.rep2;
+            fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+          } else {
+            off = fr.rep0 - 1;
+            if (off == 0) return false;
+            fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+          }
+        }
+        const uint32_t opv = s.op + co;  // output position including the pending chunk
+        // also keeps the output behind the unread Huffman literals in the slot tail
+        if (lp + ll > regen || (uint64_t)opv + ml + (regen - lp) > s.cap) return false;
+        if (off == 0 || off > opv + ll) return false;
+        const uint32_t ol = ll + ml;
+        if (ol <= kWave && off <= kNearOff) {
+          if (co + ol > kWave) exec();
+          if (lane - co < ol) {
+            rec = co | (ll << 8) | (lq << 16);
+            roff = off;
+          }
+          co += ol;
+          lq += ll;
+          lp += ll;
+        } else {
+          exec();
+          copy_lits(ll);
+          match_copy(s, ring, off, ml);
+        }
+      }
+      exec();
+      return b.bitpos == 0;
+    };
+    // fast sequence loop for tables of <= 64 cells (every predefined one): the tables live in
+    // registers, lane u = cell u packed as baseline (17 bits) | extra-bit count << 17 |
+    // state bits << 22 | next-state base << 25 (offset table: the code in place of the
+    // baseline), so one v_readlane per table and sequence fetches everything; the bit reader
+    // is an 8-byte container reloaded from two overlapping 256-B register chunks (FastBits)
+    auto fast = [&]() __attribute__((always_inline)) -> bool {
+      uint32_t info[3];
+#pragma unroll
+      for (uint32_t k = 0; k < 3; ++k) {
+        const uint32_t c = k == 0 ? tll : k == 1 ? tof : tml;
+        const uint32_t sym = c & 0xFFu;
+        const uint32_t code = k == 1 ? (sym & 31u) | ((sym & 31u) << 17)
+                                     : (uint32_t)__builtin_amdgcn_ds_bpermute((int)(sym << 2), (int)(k == 0 ? llt : mlt));
+        const uint32_t bv = k == 1 ? code : (code & 0x1FFFFu) | ((code >> 24) << 17);
+        info[k] = bv | (((c >> 8) & 7u) << 22) | (((c >> 16) & 63u) << 25);
+      }
+      FastBits fb;
+      if (!fb.init(s, q, end)) return false;
+      uint32_t sll = fb.read(fr.al[0]), sof = fb.read(fr.al[1]), sml = fb.read(fr.al[2]);
+      for (uint32_t k = 0; k < nseq; ++k) {
+        fb.reload(s, q);
+        const uint32_t il = readlane(info[0], sll), io = readlane(info[1], sof),
+                       im = readlane(info[2], sml);
+        const uint32_t ofc = (io >> 17) & 31u;
+        const uint32_t ofv = (1u << ofc) + fb.read(ofc);
+        const uint32_t ml = (im & 0x1FFFFu) + fb.read((im >> 17) & 31u);
+        if (fb.used > 31) fb.reload(s, q);
+        const uint32_t ll = (il & 0x1FFFFu) + fb.read((il >> 17) & 31u);
+        if (k + 1 < nseq) {
+          sll = (il >> 25) + fb.read((il >> 22) & 7u);
+          sml = (im >> 25) + fb.read((im >> 22) & 7u);
+          sof = (io >> 25) + fb.read((io >> 22) & 7u);
+        }
+        uint32_t off;
+        if (ofv > 3) {
+          off = ofv - 3;
           fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+        } else {
+          const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
+          if (idx == 1) {
+            off = fr.rep0;
+          } else if (idx == 2) {
+            off = fr.rep1;
+            fr.rep1 = fr.rep0; fr.rep0 = off;
+          } else if (idx == 3) {
+            off = fr.rep2;
+            fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+          } else {
+            off = fr.rep0 - 1;
+            if (off == 0) return false;
+            fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+          }
+        }
+        const uint32_t opv = s.op + co;
+        if (lp + ll > regen || (uint64_t)opv + ml + (regen - lp) > s.cap) return false;
+        if (off == 0 || off > opv + ll) return false;
+        const uint32_t ol = ll + ml;
+        if (ol <= kWave && off <= kNearOff) {
+          if (co + ol > kWave) exec();
+          if (lane - co < ol) {
+            rec = co | (ll << 8) | (lq << 16);
+            roff = off;
+          }
+          co += ol;
+          lq += ll;
+          lp += ll;
+        } else {
+          exec();
+          ZP_BEGIN(tg);
+          copy_lits(ll);
+          match_copy(s, ring, off, ml);
+          ZP_END(6, tg);
+          ZP_ADD(12, 1);
         }
       }
-      // also keeps the output behind the unread Huffman literals in the slot tail
-      if (lp + ll > regen || (uint64_t)s.op + ml + (regen - lp) > s.cap) return false;
-      if (off == 0 || off > s.op + ll) return false;
-      if (lt == 0 && ll + ml <= kWave && off <= kNearOff) {
-        // one step for the whole sequence: every output lane gathers its byte from the
-        // window (a literal, or a match byte that copies a literal of this step) or from the
-        // ring (history), with one LDS read and one LDS write
-        make_room(s, ring, ll + ml);
-        const uint32_t w = win_at(s, win, lit_stream + lp, ll);
-        const uint32_t m = lane - ll;  // match lanes: index in the match
-        uint32_t rel = m;
-        if (off < ml) {  // m mod off, exact for m, off < 64
-          const float qf = floorf(((float)m + 0.5f) * __builtin_amdgcn_rcpf((float)off));
-          rel = m - (uint32_t)qf * off;
-        }
-        const uint32_t from = s.op + ll + rel - off;  // output position a match byte copies
-        const uintptr_t base = (uintptr_t)s.dst;
-        const uint32_t a = lane < ll ? w + lane
-                           : from >= s.op ? w + (from - s.op)
-                                          : kWin + (uint32_t)((base + from) & kRingMask);
-        const bool act = lane < ll + ml;
-        lds_order();
-        const uint32_t v = act ? (uint32_t)win[a] : 0u;  // win and ring are one LDS array
-        lds_order();
-        if (act) ring[(base + s.op + lane) & kRingMask] = (uint8_t)v;
-        lds_order();
-        s.op += ll + ml;
-        lp += ll;
-      } else {
-        copy_lits(ll);
-        match_copy(s, ring, off, ml);
-      }
-    }
-    if (b.bitpos != 0) return false;
+      exec();
+      return fb.remaining(q) == 0;
+    };
+    ZP_BEGIN(tq);
+    ZP_ADD(11, nseq);
+    if (!(rt ? fast() : run())) return false;
+    ZP_END(4, tq);
   } else if (q != end) {
     return false;
   }
@@ -775,7 +1003,8 @@ __device__ __forceinline__ uint32_t xxh64_low(const GMEM uint8_t* p, uint32_t n)
 __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
-    uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err) {
+    uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
+    uint32_t defer_only) {
   using namespace zsd;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
   __shared__ __attribute__((aligned(16))) Tabs t;
@@ -783,6 +1012,8 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
   uint8_t* ring = lds + kWin;
   const uint32_t i = blockIdx.x;
   if (i >= nseg) return;
+  // after zstd_lanes_kernel: only the segments it deferred (zstd_lanes.hip)
+  if (defer_only && produced[i] != 0xFFFFFFFEu) return;
   State s;
   s.src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
   s.csize = csizes[i];
@@ -794,6 +1025,10 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
   s.fenced = 0;
   s.wb = ~0ull;
   s.wlen = 0;
+#ifdef ZPROF
+  if (lane_id() < 16) zp_lds[lane_id()] = 0;
+  const uint64_t t_all = ZP_T();
+#endif
   bool ok = false;
   do {
     const uint32_t cs = s.csize;
@@ -835,8 +1070,11 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
       if (type == 0) {
         if (p + bsz > cs || (uint64_t)s.op + bsz > s.cap) { bad = true; break; }
         s.ip = p;
+        ZP_BEGIN(tr);
         if (bsz >= kLongLit) literals_long(s, win, ring, bsz);
         else if (bsz) literals_short(s, win, ring, bsz);
+        ZP_END(7, tr);
+        ZP_ADD(14, 1);
         p += bsz;
       } else if (type == 1) {
         if (p + 1 > cs || (uint64_t)s.op + bsz > s.cap) { bad = true; break; }
@@ -844,7 +1082,10 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
         p += 1;
       } else if (type == 2) {
         if (bsz > (128u << 10) || p + bsz > cs) { bad = true; break; }
+        ZP_BEGIN(tb);
         if (!block(s, win, ring, t, fr, p, bsz)) { bad = true; break; }
+        ZP_END(1, tb);
+        ZP_ADD(13, 1);
         p += bsz;
       } else {
         bad = true;
@@ -863,6 +1104,11 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     if (fsz && fcs != s.op) break;
     ok = true;
   } while (false);
+#ifdef ZPROF
+  ZP_ADD(0, ZP_T() - t_all);
+  lds_order();
+  if (lane_id() < 16) atomicAdd(&g_zprof[lane_id()], zp_lds[lane_id()]);
+#endif
   if (ok) {
     if (lane_id() == 0) produced[i] = s.op;
   } else if (lane_id() == 0) {
@@ -872,3 +1118,14 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
 }
 
 }  // namespace bitar_hip
+
+#ifdef ZPROF
+extern "C" int bitar_hip_debug_zstd_prof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bitar_hip::zsd::g_zprof), 16 * 8) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(bitar_hip::zsd::g_zprof), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

@@ -1,0 +1,443 @@
+// zstd_lanes.hip -- Zstandard frame decode with ONE LANE PER SEGMENT (gfx950).
+//
+// Why a second decoder: a Zstd sequence section is one backward FSE bitstream whose states
+// chain from sequence to sequence, so inside a segment the decode is serial.  The
+// wave-per-segment kernel (zstd_decompress.hip) runs that chain on the scalar unit, which
+// a CU shares among all its waves -- ~100 scalar instructions per sequence saturate it.
+// Here every lane of a wave owns its own segment and runs the chain on the vector ALU:
+// 64 sequence chains advance per vector instruction, and the FSE tables (the predefined
+// distributions, built at compile time) are one LDS array shared by the lanes.
+//
+// Scope (the frames zstd_compress_kernel writes, and many libzstd level-1 frames): raw and
+// RLE blocks, compressed blocks with raw or RLE literals and predefined (or repeated
+// predefined) sequence tables, repeat offsets, single-segment frames with or without the
+// content size.  A segment that needs anything else -- Huffman literals, FSE-described or
+// RLE sequence tables, a dictionary id, a content checksum -- or that fails ANY of the
+// wave kernel's checks is marked kDefer (produced[i]) and left to zstd_decompress_kernel,
+// which the runtime launches next in defer-only mode; so acceptance, rejection and error
+// reporting are exactly the wave kernel's (= the oracle's, oracle/bitar_zstd.c).
+//
+// Memory: each lane reads its compressed segment and writes its output with 8-byte
+// (unaligned) global accesses; a match reads its history back from the lane's own output
+// (same-thread read-after-write through L2).  The 8-byte forms never write past the frame's
+// content size (or the capacity when the frame does not state it).  Raw and RLE blocks,
+// where lanes would copy up to 64 KiB each, are instead copied by the whole wave, one
+// lane's block after another, with coalesced 16-B accesses.
+#include "wave.hip.h"
+
+namespace bitar_hip {
+
+namespace zsl {
+
+constexpr uint32_t kDefer = 0xFFFFFFFEu;
+
+// ---- predefined distributions (RFC 8878 3.1.1.3.2.2) -> decode tables at compile time ----
+constexpr uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,   7,   8,   9,    10,   11,
+                                  12, 13, 14, 15, 16, 18, 20,  22,  24,  28,   32,   40,
+                                  48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384,
+                                  32768, 65536};
+constexpr uint8_t kLLBits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  0,  0,  1,  1,
+                                 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+constexpr uint32_t kMLBase[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13,   14,   15,   16,
+                                  17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27,   28,   29,   30,
+                                  31, 32, 33, 34, 35, 37, 39, 41, 43, 47, 51,   59,   67,   83,
+                                  99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771,
+                                  65539};
+constexpr uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1,
+                                 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+constexpr int16_t kLLNorm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+constexpr int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+constexpr int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+
+// One decode cell: baseline (17 bits) | extra-bit count << 17 | state bits << 22 |
+// next-state base << 25.  The offset table keeps the offset code in the extra-bit field
+// (Offset_Value = 2^code + code extra bits) and no baseline.
+struct DTab {
+  uint32_t c[64];
+};
+
+constexpr uint32_t hbc(uint32_t v) {
+  uint32_t r = 0;
+  while (v >>= 1) ++r;
+  return r;
+}
+
+// FSE_buildDTable (RFC 8878 4.1.1) for a predefined distribution; kind 0 LL, 1 OF, 2 ML
+constexpr DTab build_dtab(const int16_t* norm, uint32_t max_sym, uint32_t al, int kind) {
+  DTab d{};
+  const uint32_t size = 1u << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+  uint32_t high = size - 1;
+  uint32_t sym_at[64] = {};
+  uint32_t next[64] = {};
+  for (uint32_t s = 0; s <= max_sym; ++s) {
+    if (norm[s] == -1) {
+      sym_at[high--] = s;
+      next[s] = 1;
+    } else {
+      next[s] = (uint32_t)norm[s];
+    }
+  }
+  uint32_t pos = 0;
+  for (uint32_t s = 0; s <= max_sym; ++s)
+    for (int i = 0; i < norm[s]; ++i) {
+      sym_at[pos] = s;
+      do {
+        pos = (pos + step) & mask;
+      } while (pos > high);
+    }
+  for (uint32_t u = 0; u < size; ++u) {
+    const uint32_t s = sym_at[u];
+    const uint32_t ns = next[s]++;
+    const uint32_t nb = al - hbc(ns);
+    const uint32_t base = (ns << nb) - size;
+    uint32_t v = 0;
+    if (kind == 0) v = kLLBase[s] | ((uint32_t)kLLBits[s] << 17);
+    else if (kind == 1) v = s << 17;
+    else v = kMLBase[s] | ((uint32_t)kMLBits[s] << 17);
+    d.c[u] = v | (nb << 22) | (base << 25);
+  }
+  return d;
+}
+
+constexpr DTab kLLTab = build_dtab(kLLNorm, 35, 6, 0);
+constexpr DTab kOFTab = build_dtab(kOFNorm, 28, 5, 1);
+constexpr DTab kMLTab = build_dtab(kMLNorm, 52, 6, 2);
+__constant__ DTab kTabs[3] = {kLLTab, kOFTab, kMLTab};
+
+// ---- per-lane global access -------------------------------------------------------------
+__device__ __forceinline__ uint64_t ld8(const GMEM uint8_t* p) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
+  return v;
+}
+__device__ __forceinline__ void st8(GMEM uint8_t* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
+// little-endian value of the n <= 4 bytes at p (byte loads: never reads past p + n)
+__device__ __forceinline__ uint32_t ldn(const GMEM uint8_t* p, uint32_t n) {
+  uint32_t v = 0;
+  for (uint32_t k = 0; k < n; ++k) v |= (uint32_t)p[k] << (8 * k);
+  return v;
+}
+
+// Per-lane backward bit reader over the section [q, end) of the segment: C = the 8 stream
+// bytes at [ptr, ptr + 8), bytes below q zeroed; `used` bits consumed from its top.
+struct Bits {
+  uint64_t C;
+  uint32_t used;
+  int32_t ptr;
+  __device__ __forceinline__ void load(const GMEM uint8_t* src, uint32_t q) {
+    if (ptr + 8 <= (int32_t)q) {
+      C = 0;  // wholly below the section (an overrun; the final bit count rejects it)
+    } else {
+      C = ld8(src + ptr);  // ptr >= q - 7 >= 5: inside the frame
+      if (ptr < (int32_t)q) C &= ~0ull << (8 * (uint32_t)((int32_t)q - ptr));
+    }
+  }
+  __device__ __forceinline__ void reload(const GMEM uint8_t* src, uint32_t q) {
+    ptr -= (int32_t)(used >> 3);
+    used &= 7u;
+    load(src, q);
+  }
+  __device__ __forceinline__ uint32_t read(uint32_t n) {
+    const uint32_t sh = (64 - used - n) & 63u;
+    const uint32_t v = (uint32_t)(C >> sh) & ((1u << n) - 1u);
+    used += n;
+    return v;
+  }
+  __device__ __forceinline__ int32_t remaining(uint32_t q) const {
+    return 8 * (ptr - (int32_t)q) + 64 - (int32_t)used;
+  }
+};
+
+// n literal bytes s -> d (no overlap).  Wildcopy when both sides have 16 bytes of room.
+__device__ __forceinline__ void copy_lits(GMEM uint8_t* d, const GMEM uint8_t* s, uint32_t n,
+                                         bool room) {
+  if (n <= 16 && room) {
+    st8(d, ld8(s));
+    if (n > 8) st8(d + 8, ld8(s + 8));
+    return;
+  }
+  uint32_t j = 0;
+  for (; j + 8 <= n; j += 8) st8(d + j, ld8(s + j));
+  for (; j < n; ++j) d[j] = s[j];
+}
+
+// n bytes of a match at distance off (1 <= off <= d - segment start): d[j] = d[j - off]
+__device__ __forceinline__ void copy_match(GMEM uint8_t* d, uint32_t off, uint32_t n,
+                                           bool room) {
+  const GMEM uint8_t* s = d - off;
+  if (room) {  // d + n + 8 <= end of the segment
+    if (off >= 8) {
+      for (uint32_t j = 0; j < n; j += 8) st8(d + j, ld8(s + j));
+    } else {
+      // the first `off` bytes repeat: build an 8-byte word of the pattern, store it every
+      // `step` bytes (the largest multiple of off <= 8)
+      uint64_t rep = ld8(s) & (~0ull >> (64 - 8 * off));
+      for (uint32_t len = off; len < 8; len *= 2) rep |= rep << (8 * len);
+      const uint32_t step = 8 - (8 % off);
+      for (uint32_t j = 0; j < n; j += step) st8(d + j, rep);
+    }
+    return;
+  }
+  for (uint32_t j = 0; j < n; ++j) d[j] = s[j];
+}
+
+// One compressed block at stream [p, p + len) of lane's segment.  False = defer.
+__device__ __forceinline__ bool block(const GMEM uint8_t* src, uint32_t cs, GMEM uint8_t* dst,
+                                      uint32_t cap, uint32_t capw, uint32_t& op, uint32_t p, uint32_t len,
+                                      uint32_t (&rep)[3], bool& pre, const uint32_t* tab) {
+  const uint32_t end = p + len;
+  const uint32_t b0 = src[p];
+  const uint32_t lt = b0 & 3u, sf = (b0 >> 2) & 3u;
+  if (lt >= 2) return false;  // Huffman literals: the wave kernel
+  uint32_t regen, hsz;
+  if (sf == 0 || sf == 2) { regen = b0 >> 3; hsz = 1; }
+  else if (sf == 1) { if (len < 2) return false; regen = ldn(src + p, 2) >> 4; hsz = 2; }
+  else { if (len < 3) return false; regen = ldn(src + p, 3) >> 4; hsz = 3; }
+  if (regen > (128u << 10) || regen > cap - op) return false;
+  uint32_t q = p + hsz;
+  uint32_t lit = 0, litb = 0;
+  if (lt == 0) {
+    if (q + regen > end) return false;
+    lit = q;
+    q += regen;
+  } else {
+    if (q + 1 > end) return false;
+    litb = src[q];
+    q += 1;
+  }
+  if (q >= end) return false;
+  uint32_t nseq = src[q];
+  if (nseq < 128) {
+    q += 1;
+  } else if (nseq < 255) {
+    if (q + 2 > end) return false;
+    nseq = ((nseq - 128) << 8) + src[q + 1];
+    q += 2;
+  } else {
+    if (q + 3 > end) return false;
+    nseq = ldn(src + q + 1, 2) + 0x7F00u;
+    q += 3;
+  }
+  uint32_t lp = 0;
+  auto lits = [&](uint32_t n) __attribute__((always_inline)) {
+    if (lt == 0) {
+      copy_lits(dst + op, src + lit + lp, n, op + 16 <= capw && lit + lp + 16 <= cs);
+    } else {
+      const uint64_t w = 0x0101010101010101ull * litb;
+      if (op + n + 8 <= capw) {
+        for (uint32_t j = 0; j < n; j += 8) st8(dst + op + j, w);
+      } else {
+        for (uint32_t j = 0; j < n; ++j) dst[op + j] = (uint8_t)litb;
+      }
+    }
+  };
+  if (nseq) {
+    if (q >= end) return false;
+    const uint32_t modes = src[q];
+    q += 1;
+    if (modes & 3u) return false;
+    // predefined (0) or repeated predefined (3) for all three tables
+    for (uint32_t k = 0; k < 3; ++k) {
+      const uint32_t m = (modes >> (6 - 2 * k)) & 3u;
+      if (m == 1 || m == 2 || (m == 3 && !pre)) return false;
+    }
+    pre = true;
+    if (q >= end) return false;
+    Bits b;
+    b.ptr = (int32_t)end - 8;
+    b.load(src, q);
+    const uint32_t last = (uint32_t)(b.C >> 56);
+    if (last == 0) return false;
+    b.used = 8 - (31u - (uint32_t)__builtin_clz(last));
+    uint32_t sll = b.read(6), sof = b.read(5), sml = b.read(6);
+    for (uint32_t k = 0; k < nseq; ++k) {
+      b.reload(src, q);
+      const uint32_t il = tab[sll], io = tab[64 + sof], im = tab[128 + sml];
+      const uint32_t ofc = (io >> 17) & 31u;
+      const uint32_t ofv = (1u << ofc) + b.read(ofc);
+      const uint32_t ml = (im & 0x1FFFFu) + b.read((im >> 17) & 31u);
+      if (b.used > 31) b.reload(src, q);
+      const uint32_t ll = (il & 0x1FFFFu) + b.read((il >> 17) & 31u);
+      if (k + 1 < nseq) {
+        sll = (il >> 25) + b.read((il >> 22) & 7u);
+        sml = (im >> 25) + b.read((im >> 22) & 7u);
+        sof = (io >> 25) + b.read((io >> 22) & 7u);
+      }
+      uint32_t off;
+      if (ofv > 3) {
+        off = ofv - 3;
+        rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = off;
+      } else {
+        const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
+        if (idx == 1) {
+          off = rep[0];
+        } else if (idx == 2) {
+          off = rep[1];
+          rep[1] = rep[0]; rep[0] = off;
+        } else if (idx == 3) {
+          off = rep[2];
+          rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = off;
+        } else {
+          off = rep[0] - 1;
+          if (off == 0) return false;
+          rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = off;
+        }
+      }
+      if (lp + ll > regen || (uint64_t)op + ml + (regen - lp) > cap) return false;
+      if (off == 0 || off > op + ll) return false;
+      lits(ll);
+      op += ll;
+      lp += ll;
+      copy_match(dst + op, off, ml, op + ml + 8 <= capw);
+      op += ml;
+    }
+    if (b.remaining(q) != 0) return false;
+  } else if (q != end) {
+    return false;
+  }
+  if ((uint64_t)op + (regen - lp) > cap) return false;
+  lits(regen - lp);
+  op += regen - lp;
+  return true;
+}
+
+}  // namespace zsl
+
+// L segments per wave (lane l < L owns segment blockIdx.x * L + l); the launch has 64 lanes
+// per workgroup so the raw/RLE block copies can use the whole wave.
+template <uint32_t L>
+__global__ __launch_bounds__(64) void zstd_lanes_kernel(
+    const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
+    uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
+    uint8_t* __restrict__ out, uint32_t* __restrict__ produced) {
+  using namespace zsl;
+  __shared__ uint32_t tab[3 * 64];
+  const uint32_t lane = lane_id();
+  tab[lane] = kTabs[0].c[lane];
+  tab[64 + lane] = kTabs[1].c[lane];
+  tab[128 + lane] = kTabs[2].c[lane];
+  lds_order();
+  const uint32_t i = blockIdx.x * L + lane;
+  bool active = lane < L && i < nseg;
+  const GMEM uint8_t* src = nullptr;
+  GMEM uint8_t* dst = nullptr;
+  uint32_t cs = 0, op = 0, p = 0, fcs = 0, fsz = 0;
+  const uint32_t cap = seg;
+  if (active) {
+    src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
+    cs = csizes[i];
+    dst = global_ptr(out + (uint64_t)i * seg);
+    // frame header
+    bool ok = cs >= 6 && ldn(src, 4) == 0xFD2FB528u;
+    uint32_t fhd = 0;
+    if (ok) {
+      fhd = src[4];
+      p = 5;
+      // reserved bit, content checksum and dictionary ids go to the wave kernel
+      ok = (fhd & (8u | 4u | 3u)) == 0;
+    }
+    if (ok) {
+      const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1u;
+      if (!single) {
+        if (p >= cs) ok = false;
+        p++;
+      }
+      fsz = fcs_flag == 0 ? (single ? 1u : 0u) : fcs_flag == 1 ? 2u : fcs_flag == 2 ? 4u : 8u;
+      if (ok && (p + fsz > cs || fsz == 8)) ok = false;
+      if (ok) {
+        fcs = fsz ? ldn(src + p, fsz) : 0u;
+        if (fsz == 2) fcs += 256;
+        p += fsz;
+        if (fsz && fcs > cap) ok = false;
+      }
+    }
+    if (!ok) {
+      produced[i] = kDefer;
+      active = false;
+    }
+  }
+  uint32_t rep[3] = {1, 4, 8};
+  bool pre = false;
+  // block loop: lanes walk their own blocks; all lanes meet at every block header, where
+  // raw / RLE blocks are copied by the whole wave
+  while (ballot(active)) {
+    uint32_t type = 3, bsz = 0;
+    bool last = false;
+    if (active) {
+      if (p + 3 > cs) {
+        active = false;
+        produced[i] = kDefer;
+      } else {
+        const uint32_t bh = ldn(src + p, 3);
+        p += 3;
+        last = bh & 1u;
+        type = (bh >> 1) & 3u;
+        bsz = bh >> 3;
+        bool ok = type != 3;
+        if (type == 0) ok = p + bsz <= cs && (uint64_t)op + bsz <= cap;
+        else if (type == 1) ok = p + 1 <= cs && (uint64_t)op + bsz <= cap;
+        else if (type == 2) ok = bsz <= (128u << 10) && p + bsz <= cs;
+        if (!ok) {
+          active = false;
+          produced[i] = kDefer;
+        }
+      }
+    }
+    // raw and RLE blocks: the whole wave copies / fills, one lane's block at a time
+    for (uint64_t m = ballot(active && type < 2); m; m &= m - 1) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(m);
+      const uint64_t d = uniform64(readlane((uint32_t)(uintptr_t)dst, l) |
+                                   ((uint64_t)readlane((uint32_t)((uintptr_t)dst >> 32), l) << 32));
+      const uint64_t s = uniform64(readlane((uint32_t)(uintptr_t)src, l) |
+                                   ((uint64_t)readlane((uint32_t)((uintptr_t)src >> 32), l) << 32));
+      const uint32_t lop = readlane(op, l), lp = readlane(p, l), n = readlane(bsz, l);
+      GMEM uint8_t* dd = (GMEM uint8_t*)(uintptr_t)d + lop;
+      const GMEM uint8_t* ss = (const GMEM uint8_t*)(uintptr_t)s + lp;
+      if (readlane(type, l) == 0) {
+        wave_copy_global(dd, ss, n);
+      } else {
+        const uint32_t v = readlane(active ? (uint32_t)src[p] : 0u, l);
+        for (uint32_t k = lane; k < n; k += kWave) dd[k] = (uint8_t)v;
+      }
+      global_fence_wave();  // lane l reads this output back as match history
+    }
+    if (active) {
+      if (type == 0) {
+        op += bsz;
+        p += bsz;
+      } else if (type == 1) {
+        op += bsz;
+        p += 1;
+      } else if (!block(src, cs, dst, cap, fsz ? fcs : cap, op, p, bsz, rep, pre, tab)) {
+        active = false;
+        produced[i] = kDefer;
+      } else {
+        p += bsz;
+      }
+      if (active && last) {
+        active = false;
+        produced[i] = (p == cs && (!fsz || fcs == op)) ? op : kDefer;
+      }
+    }
+  }
+}
+
+template __global__ void zstd_lanes_kernel<64>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                               const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                               uint32_t*);
+template __global__ void zstd_lanes_kernel<32>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                               const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                               uint32_t*);
+template __global__ void zstd_lanes_kernel<8>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                              const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                              uint32_t*);
+template __global__ void zstd_lanes_kernel<16>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                               const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                               uint32_t*);
+
+}  // namespace bitar_hip

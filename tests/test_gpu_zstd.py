@@ -20,6 +20,18 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
+@pytest.fixture(autouse=True, params=[16, 64, 0], ids=["lanes16", "lanes64", "wave"])
+def zstd_decoder(request):
+    """Every test runs with the lane-per-segment decoder in front (zstd_lanes.hip, 16 or 64
+    segments per wave; it defers what it does not take to the wave kernel) and with the
+    wave-per-segment decoder alone."""
+    import bitar_amd
+    L = bitar_amd.lib()
+    old = L.bitar_hip_debug_set_zstd_lanes(request.param)
+    yield request.param
+    L.bitar_hip_debug_set_zstd_lanes(old)
+
+
 def _libzstd():
     try:
         L = ctypes.CDLL("/opt/conda/lib/libzstd.so.1.4.9")
