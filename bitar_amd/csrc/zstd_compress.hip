@@ -123,10 +123,7 @@ __constant__ Codes kCodes = build_codes();
 
 __device__ __forceinline__ uint32_t hb32(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 
-// v with lane l replaced by the wave-uniform s
-__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t s, uint32_t l) {
-  return lane_id() == l ? s : v;
-}
+
 
 using cmp::InRing;
 using cmp::Window;
@@ -139,6 +136,8 @@ using cmp::kObufMask;
 // match (the window is split at that lane).
 struct ZstdOut : cmp::ByteOut {
   uint2* seqs;              // LDS, kMaxSeq records {ll | offset_value << 16, match length}
+  uint32_t* ew;             // LDS, 4 x 64: per-chain symbol transforms / state bits
+  const uint8_t* tabs;      // LDS, the OF / ML / LL next-state tables at 0 / 64 / 128
   const GMEM uint8_t* src;  // the segment's input (raw blocks are copied from it)
   uint32_t blk;             // output offset of the open block's header
   uint32_t in0;             // input position the open block starts at
@@ -275,17 +274,25 @@ struct ZstdOut : cmp::ByteOut {
     op = p0 + (bits >> 3);
   }
 
-  // The sequences bitstream of the open block (nseq >= 1), oracle zs_close_block.  A scalar
-  // walk over the sequences, highest first, runs the three FSE state chains with the state
-  // tables held in VGPRs (lane s = state s, read with v_readlane); every lane then assembles
-  // its sequence's field (state bits + extra bits, <= 61 bits), placed by a prefix sum.
+  // The sequences bitstream of the open block (nseq >= 1), oracle zs_close_block.  Per 64
+  // sequences (highest first): every lane computes its sequence's codes and symbol
+  // transforms and stores them chain-major in LDS (ew[4 k + c]: c = 0 OF, 1 ML, 2 LL,
+  // deltaNbBits | deltaFindState << 24); then lanes 0..2 walk the three FSE state chains on
+  // the vector ALU, one chain per lane, sequence 63 down to 0, each step one LDS read of the
+  // transform and one of the chain's state table (tabs), writing the state bits back over
+  // the transform; finally every lane assembles its sequence's field (state bits + extra
+  // bits, <= 61 bits), placed by a prefix sum.  The walk costs a few scalar instructions per
+  // sequence: the scalar unit stays with the parse, which every wave of the CU shares.
   __device__ __forceinline__ void encode_sequences() {
     const uint32_t lane = lane_id();
-    const uint32_t tLL = kCtLL.state[lane], tML = kCtML.state[lane], tOF = kCtOF.state[lane & 31u];
     const uint32_t p0 = op;
     uint32_t bits = 0, zeroed = p0;
-    uint32_t sLL = 0, sML = 0, sOF = 0;
+    uint32_t st = 0;  // lane c < 3: the state of chain c
     const uint32_t top = nseq - 1;
+    // chain of this lane: its table base in tabs (lanes >= 3 walk a dummy chain whose
+    // reads stay inside the tables and whose writes go to ew[4 k + 3])
+    const uint32_t cl = lane < 3 ? lane : 3u;
+    const uint32_t tb = cl == 0 ? 0u : cl == 1 ? 64u : cl == 2 ? 128u : 192u;
     for (int32_t c = (int32_t)(top >> 6); c >= 0; --c) {
       const uint32_t j = (uint32_t)c * kWave + lane;
       const bool act = j < nseq;
@@ -296,49 +303,45 @@ struct ZstdOut : cmp::ByteOut {
       const uint32_t mlc = mlb < 128 ? kCodes.ml[mlb] : hb32(mlb) + 36u;
       const uint32_t ofc = hb32(of);
       const uint2 eLL = kCtLL.sym[llc], eML = kCtML.sym[mlc], eOF = kCtOF.sym[ofc];
-      // each sequence's state bits (OF, ML, LL, LSB first) | their count << 24, to its lane
-      uint32_t stb = 0;
+      auto pack = [](uint2 e) { return e.x | (e.y << 24); };  // d < 2^19, f in [-64, 64)
+      ew[4 * lane + 0] = pack(eOF);
+      ew[4 * lane + 1] = pack(eML);
+      ew[4 * lane + 2] = pack(eLL);
+      ew[4 * lane + 3] = 0u;
+      lds_order();
       int32_t k = 63;
       if (c == (int32_t)(top >> 6)) {  // the last sequence initialises the three states
         k = (int32_t)(top & 63u);
-        const uint32_t kk = (uint32_t)k;
-        auto init = [&](uint32_t e_x, uint32_t e_y, uint32_t t) __attribute__((always_inline)) {
-          const uint32_t d = readlane(e_x, kk);
-          const int32_t f = (int32_t)(int16_t)(readlane(e_y, kk) & 0xFFFFu);
-          const uint32_t nbo = (d + (1u << 15)) >> 16;
-          const uint32_t val = (nbo << 16) - d;
-          return readlane(t, (uint32_t)((int32_t)(val >> nbo) + f));
-        };
-        sLL = init(eLL.x, eLL.y, tLL);
-        sML = init(eML.x, eML.y, tML);
-        sOF = init(eOF.x, eOF.y, tOF);
+        const uint32_t e = ew[4 * (uint32_t)k + cl];
+        const uint32_t d = e & 0xFFFFFFu;
+        const int32_t f = (int32_t)e >> 24;
+        const uint32_t nbo = (d + (1u << 15)) >> 16;
+        const uint32_t val = (nbo << 16) - d;
+        st = tabs[(tb + (uint32_t)((int32_t)(val >> nbo) + f)) & 255u];
+        lds_order();
+        ew[4 * (uint32_t)k + cl] = 0u;  // no state bits
         --k;
       }
       for (; k >= 0; --k) {
-        const uint32_t kk = (uint32_t)k;
-        auto enc = [&](uint32_t& s, uint32_t e_x, uint32_t e_y, uint32_t t, uint32_t& nb)
-            __attribute__((always_inline)) {
-          const uint32_t d = readlane(e_x, kk);
-          const int32_t f = (int32_t)(int16_t)(readlane(e_y, kk) & 0xFFFFu);
-          nb = (s + d) >> 16;
-          const uint32_t out = s & ((1u << nb) - 1u);
-          s = readlane(t, (uint32_t)((int32_t)(s >> nb) + f));
-          return out;
-        };
-        uint32_t nof, nml, nll;
-        const uint32_t oof = enc(sOF, eOF.x, eOF.y, tOF, nof);
-        const uint32_t oml = enc(sML, eML.x, eML.y, tML, nml);
-        const uint32_t oll = enc(sLL, eLL.x, eLL.y, tLL, nll);
-        const uint32_t cat = oof | (oml << nof) | (oll << (nof + nml));
-        stb = writelane(stb, cat | ((nof + nml + nll) << 24), kk);
+        lds_order();
+        const uint32_t e = ew[4 * (uint32_t)k + cl];
+        const uint32_t nb = (st + (e & 0xFFFFFFu)) >> 16;
+        const uint32_t out = st & ((1u << nb) - 1u);
+        st = tabs[(tb + (uint32_t)((int32_t)(st >> nb) + ((int32_t)e >> 24))) & 255u];
+        ew[4 * (uint32_t)k + cl] = out | (nb << 24);
       }
+      lds_order();
+      const uint32_t w0 = ew[4 * lane + 0], w1 = ew[4 * lane + 1], w2 = ew[4 * lane + 2];
+      const uint32_t nof = w0 >> 24, nml = w1 >> 24, nll = w2 >> 24;
+      const uint32_t stb = ((w0 & 0xFFFFFFu) | ((w1 & 0xFFFFFFu) << nof) |
+                            ((w2 & 0xFFFFFFu) << (nof + nml))) & 0xFFFFFFu;
       // each lane's field: state bits, then literal-length, match-length and offset extras
-      const uint32_t stn = stb >> 24;
+      const uint32_t stn = nof + nml + nll;
       const uint32_t llb = eLL.y >> 16, mlbits = eML.y >> 16;
       const uint64_t llx = ll & ((1u << llb) - 1u);
       const uint64_t mlx = mlb & ((1u << mlbits) - 1u);
       const uint64_t ofx = of & ((1u << ofc) - 1u);
-      uint64_t v = (uint64_t)(stb & 0xFFFFFFu) | (llx << stn) | (mlx << (stn + llb)) |
+      uint64_t v = (uint64_t)stb | (llx << stn) | (mlx << (stn + llb)) |
                    (ofx << (stn + llb + mlbits));
       uint32_t nb = stn + llb + mlbits + ofc;
       if (!act) {
@@ -349,6 +352,7 @@ struct ZstdOut : cmp::ByteOut {
       if (overflow) return;
     }
     // final states (ML, OF, LL: the decoder reads LL first) and the end mark
+    const uint32_t sOF = readlane(st, 0), sML = readlane(st, 1), sLL = readlane(st, 2);
     const uint32_t fin = (sML & 63u) | ((sOF & 31u) << 6) | ((sLL & 63u) << 11) | (1u << 17);
     put_bits(lane == 0 ? fin : 0u, lane == 0 ? 18u : 0u, p0, bits, zeroed);
     op = p0 + ((bits + 7) >> 3);
@@ -405,6 +409,8 @@ __global__ __launch_bounds__(64) void zstd_compress_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];  // + trash bytes
   __shared__ __attribute__((aligned(16))) uint2 seqs[zse::kMaxSeq];
+  __shared__ __attribute__((aligned(16))) uint32_t ew[4 * kWave];
+  __shared__ __attribute__((aligned(16))) uint8_t tabs[256];
   const uint32_t i_seg = blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
@@ -418,6 +424,12 @@ __global__ __launch_bounds__(64) void zstd_compress_kernel(
   o.flushed = 0;
   o.overflow = false;
   o.seqs = seqs;
+  o.ew = ew;
+  o.tabs = tabs;
+  tabs[lane] = (uint8_t)zse::kCtOF.state[lane & 31u];
+  tabs[64 + lane] = (uint8_t)zse::kCtML.state[lane];
+  tabs[128 + lane] = (uint8_t)zse::kCtLL.state[lane];
+  tabs[192 + lane] = 0;
   o.src = global_ptr(input + seg_off);
   // frame header: magic, Single_Segment with the content size (1 byte below 256, else 2)
   const uint32_t fh = n < 256 ? 6u : 7u;
