@@ -26,9 +26,12 @@ def per_kernel(path):
     with open(path) as f:
         for r in csv.DictReader(f):
             name = r["Kernel_Name"].split("(")[0]
+            if name.startswith("void "):  # templated kernels: "void ns::k<16u>"
+                name = name[5:]
             if not name.startswith("bitar_hip::"):
                 continue
-            agg.setdefault(name.split("::")[-1], []).append(float(r["Counter_Value"]))
+            key = name.split("::")[-1].split("<")[0]
+            agg.setdefault(key, []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
