@@ -85,7 +85,7 @@ ABI_SYMBOLS = ("bitar_hip_abi_version", "bitar_hip_last_error", "bitar_hip_devic
                "bitar_hip_host_alloc", "bitar_hip_host_free", "bitar_hip_memcpy",
                "bitar_hip_compress", "bitar_hip_compress_scattered", "bitar_hip_pointer_info",
                "bitar_hip_decompress", "bitar_hip_decompress_slab",
-               "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_fill")
+               "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_pack_lz4f", "bitar_hip_fill")
 
 
 def check(rc):

@@ -1,6 +1,7 @@
 // bitar/bitar.h -- umbrella header of the MI355X bitar front-end.
 #pragma once
 
+#include "bitar/arrow_codec.h"
 #include "bitar/config.h"
 #include "bitar/device.h"
 #include "bitar/driver.h"

@@ -1,0 +1,379 @@
+// arrow_codec.cc -- arrow::util::Codec adapters (ZSTD, LZ4_FRAME) over the C ABI.
+// See include/bitar/arrow_codec.h for the stream layouts.  Every payload byte is compressed
+// and decompressed on the device; the host only walks frame / block headers (sizes) and
+// writes the 7-byte LZ4 frame header and EndMark.
+#include "bitar/arrow_codec.h"
+
+#include <arrow/status.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "bitar_hip.h"
+#include "hip_ctx.h"
+
+namespace bitar {
+
+namespace {
+
+constexpr uint32_t kSeg = 65536;  // segment = Zstd frame content = LZ4 frame block
+constexpr uint32_t kZstdMagic = 0xFD2FB528u, kLz4fMagic = 0x184D2204u;
+
+uint32_t Rd32(const uint8_t* p) {
+  return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+}
+
+// XXH32 (the LZ4 frame descriptor's header checksum is its second byte; header bytes only)
+uint32_t Xxh32(const uint8_t* p, size_t n, uint32_t seed) {
+  constexpr uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
+                     P5 = 374761393u;
+  auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
+  size_t i = 0;
+  uint32_t h;
+  if (n >= 16) {
+    uint32_t v[4] = {seed + P1 + P2, seed + P2, seed, seed - P1};
+    for (; i + 16 <= n; i += 16)
+      for (int k = 0; k < 4; ++k) v[k] = rotl(v[k] + Rd32(p + i + 4 * k) * P2, 13) * P1;
+    h = rotl(v[0], 1) + rotl(v[1], 7) + rotl(v[2], 12) + rotl(v[3], 18);
+  } else {
+    h = seed + P5;
+  }
+  h += static_cast<uint32_t>(n);
+  for (; i + 4 <= n; i += 4) h = rotl(h + Rd32(p + i) * P3, 17) * P4;
+  for (; i < n; ++i) h = rotl(h + p[i] * P5, 11) * P1;
+  h ^= h >> 15;
+  h *= P2;
+  h ^= h >> 13;
+  h *= P3;
+  h ^= h >> 16;
+  return h;
+}
+
+// one segment of a compressed stream: csize bytes at offset; raw = stored (LZ4 frame);
+// content = its decompressed size when the header states it (Zstd), else 0
+struct Piece {
+  uint64_t offset;
+  uint32_t csize;
+  uint32_t content;
+  bool raw;
+};
+
+class HipCodec : public arrow::util::Codec {
+ public:
+  HipCodec(arrow::Compression::type type, int device, bitar_hip_ctx* ctx)
+      : type_(type), device_(device), ctx_(ctx) {}
+  ~HipCodec() override {
+    for (void* p : {d_in_, d_slab_, d_sizes_, d_off_, d_frame_, d_out_, d_srcs_, d_aux_})
+      if (p) bitar_hip_free(ctx_, p);
+    bitar_hip_close(ctx_);
+  }
+
+  int minimum_compression_level() const override { return 1; }
+  int maximum_compression_level() const override { return 1; }
+  int default_compression_level() const override { return 1; }
+  int compression_level() const override { return 1; }
+  arrow::Compression::type compression_type() const override { return type_; }
+
+  int64_t MaxCompressedLen(int64_t input_len, const uint8_t*) override {
+    const uint64_t nseg = (static_cast<uint64_t>(input_len) + kSeg - 1) / kSeg;
+    if (type_ == arrow::Compression::ZSTD)
+      return static_cast<int64_t>(9 + nseg * bitar_hip_slot_size(BITAR_HIP_CODEC_ZSTD, kSeg));
+    return static_cast<int64_t>(7 + nseg * (4 + kSeg) + 4);
+  }
+
+  arrow::Result<std::shared_ptr<arrow::util::Compressor>> MakeCompressor() override {
+    return arrow::Status::NotImplemented("streaming compression on the HIP codec");
+  }
+  arrow::Result<std::shared_ptr<arrow::util::Decompressor>> MakeDecompressor() override {
+    return arrow::Status::NotImplemented("streaming decompression on the HIP codec");
+  }
+
+  arrow::Result<int64_t> Compress(int64_t input_len, const uint8_t* input,
+                                  int64_t output_buffer_len, uint8_t* output) override;
+  arrow::Result<int64_t> Decompress(int64_t input_len, const uint8_t* input,
+                                    int64_t output_buffer_len, uint8_t* output) override;
+
+ private:
+  // grow-only HBM scratch
+  arrow::Status Reserve(void*& p, uint64_t& cap, uint64_t bytes) {
+    if (bytes <= cap) return arrow::Status::OK();
+    if (p) bitar_hip_free(ctx_, p);
+    p = nullptr;
+    cap = 0;
+    BITAR_ABI(bitar_hip_alloc(ctx_, bytes, &p), "bitar_hip_alloc");
+    cap = bytes;
+    return arrow::Status::OK();
+  }
+  bool OnDevice(const void* p) const {
+    int kind = 0, dev = -1;
+    return bitar_hip_pointer_info(p, &kind, &dev) == 0 && kind == 2 && dev == device_;
+  }
+  arrow::Status Copy(void* dst, const void* src, uint64_t n) {
+    if (n) BITAR_ABI(bitar_hip_memcpy(ctx_, dst, src, n, nullptr), "bitar_hip_memcpy");
+    return arrow::Status::OK();
+  }
+  arrow::Status Sync() {
+    BITAR_ABI(bitar_hip_sync(ctx_, nullptr), "segment codec");
+    return arrow::Status::OK();
+  }
+  arrow::Result<std::vector<Piece>> WalkZstd(const uint8_t* p, uint64_t n) const;
+  arrow::Result<std::vector<Piece>> WalkLz4f(const uint8_t* p, uint64_t n) const;
+
+  arrow::Compression::type type_;
+  int device_;
+  bitar_hip_ctx* ctx_;
+  std::mutex mu_;  // one stream per codec; Arrow may share a codec between threads
+  void *d_in_ = nullptr, *d_slab_ = nullptr, *d_sizes_ = nullptr, *d_off_ = nullptr,
+       *d_frame_ = nullptr, *d_out_ = nullptr, *d_srcs_ = nullptr, *d_aux_ = nullptr;
+  uint64_t c_in_ = 0, c_slab_ = 0, c_sizes_ = 0, c_off_ = 0, c_frame_ = 0, c_out_ = 0,
+           c_srcs_ = 0, c_aux_ = 0;
+};
+
+arrow::Result<int64_t> HipCodec::Compress(int64_t input_len, const uint8_t* input,
+                                          int64_t output_buffer_len, uint8_t* output) {
+  const std::lock_guard<std::mutex> lock(mu_);
+  if (input_len < 0) return arrow::Status::Invalid("negative input length");
+  if (output_buffer_len < MaxCompressedLen(input_len, input))
+    return arrow::Status::Invalid("output buffer smaller than MaxCompressedLen");
+  const uint64_t n = static_cast<uint64_t>(input_len);
+  const uint64_t nseg = (n + kSeg - 1) / kSeg;
+  const bool zstd = type_ == arrow::Compression::ZSTD;
+  const bool out_dev = OnDevice(output);
+  // LZ4 frame header: magic, FLG (version 01, independent blocks), BD (64 KiB blocks), HC
+  uint8_t hdr[7] = {0x04, 0x22, 0x4D, 0x18, 0x60, 0x40, 0};
+  hdr[6] = static_cast<uint8_t>((Xxh32(hdr + 4, 2, 0) >> 8) & 0xFF);
+  const uint64_t head = zstd ? 0 : sizeof hdr;
+  if (n == 0) {
+    // an empty stream: one empty frame (Zstd: single segment, content size 0, one empty
+    // last raw block), or the LZ4 frame header + EndMark
+    static const uint8_t kEmptyZstd[9] = {0x28, 0xB5, 0x2F, 0xFD, 0x20, 0x00, 0x01, 0x00, 0x00};
+    uint8_t lz4[11];
+    std::memcpy(lz4, hdr, 7);
+    std::memset(lz4 + 7, 0, 4);
+    const uint8_t* src = zstd ? kEmptyZstd : lz4;
+    const uint64_t len = zstd ? sizeof kEmptyZstd : sizeof lz4;
+    if (out_dev) ARROW_RETURN_NOT_OK(Copy(output, src, len));
+    else std::memcpy(output, src, len);
+    return static_cast<int64_t>(len);
+  }
+  const uint32_t codec = zstd ? BITAR_HIP_CODEC_ZSTD : BITAR_HIP_CODEC_LZ4;
+  const uint64_t stride = bitar_hip_slot_size(codec, kSeg);
+  const void* d_in = input;
+  if (!OnDevice(input)) {
+    ARROW_RETURN_NOT_OK(Reserve(d_in_, c_in_, n));
+    ARROW_RETURN_NOT_OK(Copy(d_in_, input, n));
+    d_in = d_in_;
+  }
+  ARROW_RETURN_NOT_OK(Reserve(d_slab_, c_slab_, nseg * stride));
+  ARROW_RETURN_NOT_OK(Reserve(d_sizes_, c_sizes_, nseg * 4));
+  ARROW_RETURN_NOT_OK(Reserve(d_aux_, c_aux_, nseg * 4));
+  ARROW_RETURN_NOT_OK(Reserve(d_off_, c_off_, (nseg + 1) * 8));
+  ARROW_RETURN_NOT_OK(Reserve(d_frame_, c_frame_, head + nseg * (stride > kSeg + 4 ? stride : kSeg + 4) + 4));
+  auto* sizes = static_cast<uint32_t*>(d_sizes_);
+  auto* offs = static_cast<uint64_t*>(d_off_);
+  auto* frame = static_cast<uint8_t*>(d_frame_);
+  BITAR_ABI(bitar_hip_compress(ctx_, nullptr, codec, d_in, n, kSeg, d_slab_, stride, sizes),
+            "bitar_hip_compress");
+  if (zstd) {
+    BITAR_ABI(bitar_hip_pack(ctx_, nullptr, d_slab_, stride, sizes, static_cast<uint32_t>(nseg),
+                             offs, frame),
+              "bitar_hip_pack");
+  } else {
+    BITAR_ABI(bitar_hip_pack_lz4f(ctx_, nullptr, d_in, n, kSeg, d_slab_, stride, sizes,
+                                  static_cast<uint32_t*>(d_aux_), offs, frame + head),
+              "bitar_hip_pack_lz4f");
+  }
+  ARROW_RETURN_NOT_OK(Sync());
+  uint64_t body = 0;
+  ARROW_RETURN_NOT_OK(Copy(&body, offs + nseg, sizeof body));
+  ARROW_RETURN_NOT_OK(Sync());
+  const uint64_t total = head + body + (zstd ? 0 : 4);
+  if (total > static_cast<uint64_t>(output_buffer_len))
+    return arrow::Status::CapacityError("compressed stream exceeds the output buffer");
+  if (out_dev) {
+    if (!zstd) ARROW_RETURN_NOT_OK(Copy(output, hdr, head));
+    ARROW_RETURN_NOT_OK(Copy(output + head, frame + head, body));
+    if (!zstd) {
+      static const uint8_t kEnd[4] = {0, 0, 0, 0};
+      ARROW_RETURN_NOT_OK(Copy(output + head + body, kEnd, 4));
+    }
+  } else {
+    if (!zstd) std::memcpy(output, hdr, head);
+    ARROW_RETURN_NOT_OK(Copy(output + head, frame + head, body));
+    if (!zstd) std::memset(output + head + body, 0, 4);
+  }
+  ARROW_RETURN_NOT_OK(Sync());
+  return static_cast<int64_t>(total);
+}
+
+// Zstandard frames: each must state its content size (== kSeg except the last, <= kSeg)
+arrow::Result<std::vector<Piece>> HipCodec::WalkZstd(const uint8_t* p, uint64_t n) const {
+  std::vector<Piece> v;
+  uint64_t pos = 0;
+  while (pos < n) {
+    const uint64_t start = pos;
+    if (n - pos < 6 || Rd32(p + pos) != kZstdMagic)
+      return arrow::Status::NotImplemented("not a Zstandard frame at offset ", pos);
+    pos += 4;
+    const uint32_t fhd = p[pos++];
+    const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1u, did_flag = fhd & 3u;
+    if (fhd & 8u) return arrow::Status::Invalid("Zstandard frame with reserved bit set");
+    if (did_flag) return arrow::Status::NotImplemented("Zstandard dictionaries");
+    if (!single) pos += 1;
+    const uint32_t fsz = fcs_flag == 0 ? (single ? 1u : 0u) : fcs_flag == 1 ? 2u
+                         : fcs_flag == 2 ? 4u : 8u;
+    if (fsz == 0) return arrow::Status::NotImplemented("Zstandard frame without content size");
+    if (pos + fsz > n) return arrow::Status::Invalid("truncated Zstandard frame header");
+    uint64_t fcs = 0;
+    for (uint32_t k = 0; k < fsz; ++k) fcs |= uint64_t(p[pos + k]) << (8 * k);
+    if (fsz == 2) fcs += 256;
+    pos += fsz;
+    for (bool last = false; !last;) {
+      if (pos + 3 > n) return arrow::Status::Invalid("truncated Zstandard block header");
+      const uint32_t bh = uint32_t(p[pos]) | uint32_t(p[pos + 1]) << 8 | uint32_t(p[pos + 2]) << 16;
+      last = bh & 1u;
+      const uint32_t type = (bh >> 1) & 3u, bsz = bh >> 3;
+      if (type == 3) return arrow::Status::Invalid("reserved Zstandard block type");
+      pos += 3 + (type == 1 ? 1u : bsz);
+    }
+    if ((fhd >> 2) & 1u) pos += 4;  // content checksum (verified on the device)
+    if (pos > n) return arrow::Status::Invalid("truncated Zstandard frame");
+    if (fcs > kSeg) return arrow::Status::NotImplemented("Zstandard frame larger than 64 KiB");
+    v.push_back({start, static_cast<uint32_t>(pos - start), static_cast<uint32_t>(fcs), false});
+  }
+  for (size_t i = 0; i + 1 < v.size(); ++i)
+    if (v[i].content != kSeg)
+      return arrow::Status::NotImplemented("Zstandard frames of other than 64 KiB content");
+  return v;
+}
+
+// LZ4 frames: version 01, independent blocks of <= 64 KiB, no block / content checksums
+arrow::Result<std::vector<Piece>> HipCodec::WalkLz4f(const uint8_t* p, uint64_t n) const {
+  std::vector<Piece> v;
+  uint64_t pos = 0;
+  while (pos < n) {
+    if (n - pos < 7 || Rd32(p + pos) != kLz4fMagic)
+      return arrow::Status::NotImplemented("not an LZ4 frame at offset ", pos);
+    const uint32_t flg = p[pos + 4], bd = p[pos + 5];
+    if ((flg >> 6) != 1) return arrow::Status::Invalid("LZ4 frame version");
+    if (!((flg >> 5) & 1)) return arrow::Status::NotImplemented("LZ4 frame with linked blocks");
+    if ((flg >> 4) & 1) return arrow::Status::NotImplemented("LZ4 block checksums");
+    if ((flg >> 2) & 1) return arrow::Status::NotImplemented("LZ4 content checksum");
+    if (flg & 1) return arrow::Status::NotImplemented("LZ4 dictionary id");
+    if (((bd >> 4) & 7) != 4) return arrow::Status::NotImplemented("LZ4 blocks larger than 64 KiB");
+    const uint64_t dlen = 2 + (((flg >> 3) & 1) ? 8 : 0);
+    if (pos + 4 + dlen + 1 > n) return arrow::Status::Invalid("truncated LZ4 frame header");
+    if (((Xxh32(p + pos + 4, dlen, 0) >> 8) & 0xFF) != p[pos + 4 + dlen])
+      return arrow::Status::Invalid("LZ4 frame header checksum");
+    pos += 4 + dlen + 1;
+    for (;;) {
+      if (pos + 4 > n) return arrow::Status::Invalid("truncated LZ4 frame");
+      const uint32_t bs = Rd32(p + pos);
+      pos += 4;
+      if (bs == 0) break;  // EndMark
+      const uint32_t len = bs & 0x7FFFFFFFu;
+      if (len > kSeg || pos + len > n) return arrow::Status::Invalid("bad LZ4 block size");
+      v.push_back({pos, len, 0, (bs >> 31) != 0});
+      pos += len;
+    }
+  }
+  return v;
+}
+
+arrow::Result<int64_t> HipCodec::Decompress(int64_t input_len, const uint8_t* input,
+                                            int64_t output_buffer_len, uint8_t* output) {
+  const std::lock_guard<std::mutex> lock(mu_);
+  if (input_len < 0 || output_buffer_len < 0) return arrow::Status::Invalid("negative length");
+  const uint64_t n = static_cast<uint64_t>(input_len);
+  const bool zstd = type_ == arrow::Compression::ZSTD;
+  const bool in_dev = OnDevice(input), out_dev = OnDevice(output);
+  // the header walk needs the bytes on the host
+  std::vector<uint8_t> host;
+  const uint8_t* hp = input;
+  if (in_dev) {
+    host.resize(n);
+    ARROW_RETURN_NOT_OK(Copy(host.data(), input, n));
+    ARROW_RETURN_NOT_OK(Sync());
+    hp = host.data();
+  }
+  std::vector<Piece> pieces;
+  if (zstd) {
+    ARROW_ASSIGN_OR_RAISE(pieces, WalkZstd(hp, n));
+  } else {
+    ARROW_ASSIGN_OR_RAISE(pieces, WalkLz4f(hp, n));
+  }
+  const uint64_t nseg = pieces.size();
+  if (nseg == 0) return 0;
+  if (nseg > 0x7FFFFFFFull) return arrow::Status::Invalid("too many segments");
+  const uint8_t* d_in = input;
+  if (!in_dev) {
+    ARROW_RETURN_NOT_OK(Reserve(d_in_, c_in_, n + 16));
+    ARROW_RETURN_NOT_OK(Copy(d_in_, input, n));
+    d_in = static_cast<const uint8_t*>(d_in_);
+  }
+  // a stored LZ4 block decodes as an empty one (a lone 0x00 token) and is copied after
+  ARROW_RETURN_NOT_OK(Reserve(d_aux_, c_aux_, std::max<uint64_t>(nseg * 4, 16)));
+  static const uint8_t kEmptyBlock[16] = {0};
+  ARROW_RETURN_NOT_OK(Copy(d_aux_, kEmptyBlock, 16));
+  const uint8_t* empty = static_cast<const uint8_t*>(d_aux_);
+  std::vector<const uint8_t*> srcs(nseg);
+  std::vector<uint32_t> csz(nseg);
+  for (uint64_t i = 0; i < nseg; ++i) {
+    const bool raw = pieces[i].raw;
+    srcs[i] = raw ? empty : d_in + pieces[i].offset;
+    csz[i] = raw ? 1u : pieces[i].csize;
+  }
+  ARROW_RETURN_NOT_OK(Reserve(d_srcs_, c_srcs_, nseg * sizeof(void*)));
+  ARROW_RETURN_NOT_OK(Reserve(d_sizes_, c_sizes_, nseg * 4));
+  ARROW_RETURN_NOT_OK(Reserve(d_off_, c_off_, nseg * 4));  // produced sizes
+  ARROW_RETURN_NOT_OK(Reserve(d_out_, c_out_, nseg * kSeg));
+  ARROW_RETURN_NOT_OK(Copy(d_srcs_, srcs.data(), nseg * sizeof(void*)));
+  ARROW_RETURN_NOT_OK(Copy(d_sizes_, csz.data(), nseg * 4));
+  auto* dout = static_cast<uint8_t*>(d_out_);
+  BITAR_ABI(bitar_hip_decompress(ctx_, nullptr, zstd ? BITAR_HIP_CODEC_ZSTD : BITAR_HIP_CODEC_LZ4,
+                                 reinterpret_cast<const void* const*>(d_srcs_),
+                                 static_cast<const uint32_t*>(d_sizes_),
+                                 static_cast<uint32_t>(nseg), kSeg, dout, nseg * kSeg,
+                                 static_cast<uint32_t*>(d_off_)),
+            "bitar_hip_decompress");
+  for (uint64_t i = 0; i < nseg; ++i)
+    if (pieces[i].raw)
+      ARROW_RETURN_NOT_OK(Copy(dout + i * kSeg, d_in + pieces[i].offset, pieces[i].csize));
+  ARROW_RETURN_NOT_OK(Sync());
+  std::vector<uint32_t> prod(nseg);
+  ARROW_RETURN_NOT_OK(Copy(prod.data(), d_off_, nseg * 4));
+  ARROW_RETURN_NOT_OK(Sync());
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < nseg; ++i) {
+    const uint32_t got = pieces[i].raw ? pieces[i].csize : prod[i];
+    if (zstd && got != pieces[i].content)
+      return arrow::Status::IOError("Zstandard frame ", i, " decoded to a wrong size");
+    if (i + 1 < nseg && got != kSeg)
+      return arrow::Status::NotImplemented("LZ4 frame blocks of other than 64 KiB");
+    total += got;
+  }
+  if (total > static_cast<uint64_t>(output_buffer_len))
+    return arrow::Status::Invalid("decompressed size ", total, " exceeds the output buffer (",
+                                  output_buffer_len, ")");
+  ARROW_RETURN_NOT_OK(Copy(output, dout, total));
+  ARROW_RETURN_NOT_OK(Sync());
+  (void)out_dev;  // bitar_hip_memcpy handles host and device destinations alike
+  return static_cast<int64_t>(total);
+}
+
+}  // namespace
+
+arrow::Result<std::unique_ptr<arrow::util::Codec>> MakeArrowCodec(arrow::Compression::type type,
+                                                                  int device) {
+  if (type != arrow::Compression::ZSTD && type != arrow::Compression::LZ4_FRAME)
+    return arrow::Status::NotImplemented("HIP codec for ",
+                                         arrow::util::Codec::GetCodecAsString(type));
+  bitar_hip_config cfg{1, 0};
+  bitar_hip_ctx* ctx = nullptr;
+  BITAR_ABI(bitar_hip_open(device, &cfg, &ctx), "bitar_hip_open");
+  return std::unique_ptr<arrow::util::Codec>(new HipCodec(type, device, ctx));
+}
+
+}  // namespace bitar

@@ -38,6 +38,9 @@ __global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t*);
 __global__ void pack_kernel(const uint8_t*, uint64_t, const uint32_t*, const uint64_t*, uint32_t,
                             uint8_t*);
 __global__ void fill_kernel(int, uint64_t, uint8_t*, uint64_t);
+__global__ void lz4f_sizes_kernel(const uint32_t*, uint32_t, uint64_t, uint32_t, uint32_t*);
+__global__ void lz4f_pack_kernel(const uint8_t*, uint64_t, uint32_t, const uint8_t*, uint64_t,
+                                 const uint32_t*, const uint64_t*, uint32_t, uint8_t*);
 }  // namespace bitar_hip
 
 struct bitar_hip_ctx {
@@ -401,6 +404,36 @@ int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_
                        static_cast<const uint8_t*>(d_slab), slot_stride, d_sizes, d_offsets,
                        nseg, static_cast<uint8_t*>(d_frame));
     HIP_TRY(hipGetLastError(), "pack launch");
+  }
+  return 0;
+}
+
+int bitar_hip_pack_lz4f(bitar_hip_ctx* ctx, void* stream, const void* d_in, uint64_t n,
+                        uint32_t seg, const void* d_slab, uint64_t slot_stride,
+                        const uint32_t* d_sizes, uint32_t* d_framed, uint64_t* d_offsets,
+                        void* d_frame) {
+  if (int r = enter(ctx)) return r;
+  if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
+  const uint64_t nseg64 = (n + seg - 1) / seg;
+  if (nseg64 > 0x7FFFFFFFull) return fail(BITAR_HIP_INVALID, "too many segments");
+  const uint32_t nseg = (uint32_t)nseg64;
+  if (!d_sizes || !d_framed || !d_offsets) return fail(BITAR_HIP_INVALID, "null buffer");
+  hipStream_t s = pick_stream(ctx, stream);
+  if (nseg) {
+    hipLaunchKernelGGL(bitar_hip::lz4f_sizes_kernel, dim3((nseg + 255) / 256), dim3(256), 0, s,
+                       d_sizes, nseg, n, seg, d_framed);
+    HIP_TRY(hipGetLastError(), "lz4f sizes launch");
+  }
+  hipLaunchKernelGGL(bitar_hip::scan_sizes_kernel, dim3(1), dim3(1024), 0, s, d_framed, nseg,
+                     d_offsets);
+  HIP_TRY(hipGetLastError(), "scan launch");
+  if (d_frame && nseg) {
+    if (!d_slab || !d_in) return fail(BITAR_HIP_INVALID, "null input or slab");
+    hipLaunchKernelGGL(bitar_hip::lz4f_pack_kernel, dim3(nseg), dim3(64), 0, s,
+                       static_cast<const uint8_t*>(d_in), n, seg,
+                       static_cast<const uint8_t*>(d_slab), slot_stride, d_sizes, d_offsets,
+                       nseg, static_cast<uint8_t*>(d_frame));
+    HIP_TRY(hipGetLastError(), "lz4f pack launch");
   }
   return 0;
 }

@@ -56,6 +56,38 @@ __global__ __launch_bounds__(64) void pack_kernel(const uint8_t* __restrict__ sl
   wave_copy_global(global_ptr(frame + offsets[i]), global_ptr(slab + (uint64_t)i * stride), sizes[i]);
 }
 
+// LZ4 frame data blocks (lz4 frame format, independent blocks): framed size of block i =
+// 4-byte size field + the compressed block, or the raw slice when it did not shrink (a
+// compressed block may not exceed the frame's maximum block size).
+__global__ __launch_bounds__(256) void lz4f_sizes_kernel(const uint32_t* __restrict__ sizes,
+                                                         uint32_t nseg, uint64_t n, uint32_t seg,
+                                                         uint32_t* __restrict__ framed) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nseg) return;
+  const uint64_t off = (uint64_t)i * seg;
+  const uint32_t len = (uint32_t)(n - off < seg ? n - off : seg);
+  framed[i] = 4 + (sizes[i] < len ? sizes[i] : len);
+}
+
+// block i at frame + offsets[i]: LE32 size (| 1 << 31 when stored raw) + its bytes
+__global__ __launch_bounds__(64) void lz4f_pack_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                       uint32_t seg, const uint8_t* __restrict__ slab,
+                                                       uint64_t stride,
+                                                       const uint32_t* __restrict__ sizes,
+                                                       const uint64_t* __restrict__ offsets,
+                                                       uint32_t nseg, uint8_t* __restrict__ frame) {
+  const uint32_t i = blockIdx.x;
+  if (i >= nseg) return;
+  const uint64_t off = (uint64_t)i * seg;
+  const uint32_t len = (uint32_t)(n - off < seg ? n - off : seg);
+  const bool raw = sizes[i] >= len;
+  const uint32_t body = raw ? len : sizes[i];
+  const uint32_t field = raw ? (len | 0x80000000u) : body;
+  GMEM uint8_t* d = global_ptr(frame + offsets[i]);
+  if (lane_id() < 4) d[lane_id()] = (uint8_t)(field >> (8 * lane_id()));
+  wave_copy_global(d + 4, raw ? global_ptr(in + off) : global_ptr(slab + (uint64_t)i * stride), body);
+}
+
 // ---- synthetic input: a device restatement-free generator; tests check it against the
 // oracle's bo_fill byte for byte.  One thread per 64-byte line.
 __device__ __forceinline__ uint64_t sm64(uint64_t seed, uint64_t k) {

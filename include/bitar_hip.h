@@ -143,6 +143,18 @@ int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream);
 int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_t slot_stride,
                    const uint32_t* d_sizes, uint32_t nseg, uint64_t* d_offsets, void* d_frame);
 
+/* The data blocks of an LZ4 frame (LZ4 frame format, block independence) from LZ4 segments
+ * of n input bytes (d_in, segment size seg <= 65536, so the frame's maximum block size is
+ * 64 KiB): block i = LE32 size + the compressed block, or LE32(len | 1<<31) + the raw input
+ * slice when the block did not shrink.  d_framed (nseg uint32) receives the framed sizes,
+ * d_offsets (nseg+1 uint64) their exclusive prefix sum; d_frame may be NULL to size only.
+ * The frame header and EndMark are the caller's.  Used by the Arrow util::Codec adapter
+ * (arrow::Compression::LZ4_FRAME, the Arrow IPC body codec). */
+int bitar_hip_pack_lz4f(bitar_hip_ctx* ctx, void* stream, const void* d_in, uint64_t n,
+                        uint32_t seg, const void* d_slab, uint64_t slot_stride,
+                        const uint32_t* d_sizes, uint32_t* d_framed, uint64_t* d_offsets,
+                        void* d_frame);
+
 /* Deterministic synthetic input (SplitMix64-based; kinds as in the oracle's bo_fill:
  * 0 random, 1 Silesia-style mix, 2 Arrow record-batch body, 3 constant, 4 periodic,
  * 5 int64 small-range only, 6 log text only). */

@@ -4,8 +4,12 @@
 // (Compress/Decompress/Recycle/async through real devices; compressed segments are written
 // to <outdir> so the Python side can check them with zlib / liblz4).  Mirrors the reference's
 // only behavioural checks (apps/demo_app.cc:288-290, 500-501, 534-543, 671-686).
+#include <arrow/api.h>
 #include <arrow/buffer.h>
+#include <arrow/io/memory.h>
+#include <arrow/ipc/api.h>
 #include <arrow/memory_pool.h>
+#include <arrow/util/compression.h>
 
 #include <cstdio>
 #include <cstring>
@@ -223,6 +227,110 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
   CHECK_OK(d0->Decompress(0, bitar::BufferVector{}, none));
 }
 
+// The Arrow util::Codec adapters (bitar/arrow_codec.h): round trips,
+// the stock Arrow codecs decode what they write, and an Arrow IPC stream written with GPU
+// body compression reads back with the stock reader.  Writes <outdir>/arrow_{zstd,lz4f}.bin
+// and <outdir>/ipc_{zstd,lz4f}.arrows for the Python side (pyarrow) to check.
+std::shared_ptr<arrow::RecordBatch> IpcBatch() {
+  // deterministic: int64 i * 7 % 1000, utf8 "row" + (i % 977), for i < 200000
+  arrow::Int64Builder ib;
+  arrow::StringBuilder sb;
+  for (int64_t i = 0; i < 200000; ++i) {
+    (void)ib.Append(i * 7 % 1000);
+    (void)sb.Append("row" + std::to_string(i % 977));
+  }
+  std::shared_ptr<arrow::Array> a, b;
+  (void)ib.Finish(&a);
+  (void)sb.Finish(&b);
+  auto schema = arrow::schema({arrow::field("v", arrow::int64()), arrow::field("s", arrow::utf8())});
+  return arrow::RecordBatch::Make(schema, a->length(), {a, b});
+}
+
+void ArrowCodecTests(const std::string& input_path, const std::string& outdir) {
+  std::ifstream f(input_path, std::ios::binary);
+  std::vector<uint8_t> data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  CHECK(!bitar::MakeArrowCodec(arrow::Compression::SNAPPY).ok());
+  for (auto type : {arrow::Compression::ZSTD, arrow::Compression::LZ4_FRAME}) {
+    const std::string tag = type == arrow::Compression::ZSTD ? "zstd" : "lz4f";
+    auto codec = bitar::MakeArrowCodec(type, 0);
+    CHECK_OK(codec.status());
+    if (!codec.ok()) continue;
+    auto& c = *codec;
+    CHECK(c->compression_type() == type);
+    for (size_t n : {data.size(), size_t(0), size_t(1), size_t(65536), size_t(65537)}) {
+      if (n > data.size()) continue;
+      const int64_t max = c->MaxCompressedLen(static_cast<int64_t>(n), data.data());
+      std::vector<uint8_t> comp(static_cast<size_t>(max));
+      auto clen = c->Compress(static_cast<int64_t>(n), data.data(), max, comp.data());
+      CHECK_OK(clen.status());
+      if (!clen.ok()) continue;
+      std::vector<uint8_t> back(n + 1);
+      auto dlen = c->Decompress(*clen, comp.data(), static_cast<int64_t>(n), back.data());
+      CHECK_OK(dlen.status());
+      CHECK(dlen.ok() && *dlen == static_cast<int64_t>(n) &&
+            std::memcmp(back.data(), data.data(), n) == 0);
+      // the stock Arrow codec decodes the GPU stream
+      auto stock = arrow::util::Codec::Create(type);
+      CHECK_OK(stock.status());
+      if (stock.ok()) {
+        std::vector<uint8_t> sb(n + 1);
+        auto r = (*stock)->Decompress(*clen, comp.data(), static_cast<int64_t>(n), sb.data());
+        CHECK_OK(r.status());
+        CHECK(r.ok() && *r == static_cast<int64_t>(n) && std::memcmp(sb.data(), data.data(), n) == 0);
+      }
+      if (n == data.size()) {
+        std::ofstream o(outdir + "/arrow_" + tag + ".bin", std::ios::binary);
+        o.write(reinterpret_cast<const char*>(comp.data()), *clen);
+      }
+    }
+    // a stream the stock codec wrote: decoded on the GPU when it has our shape, else
+    // NotImplemented (never a wrong result)
+    {
+      auto stock = arrow::util::Codec::Create(type);
+      if (stock.ok()) {
+        const size_t n = std::min<size_t>(data.size(), 60000);
+        const int64_t max = (*stock)->MaxCompressedLen(static_cast<int64_t>(n), data.data());
+        std::vector<uint8_t> comp(static_cast<size_t>(max));
+        auto clen = (*stock)->Compress(static_cast<int64_t>(n), data.data(), max, comp.data());
+        CHECK_OK(clen.status());
+        std::vector<uint8_t> back(n);
+        auto r = c->Decompress(*clen, comp.data(), static_cast<int64_t>(n), back.data());
+        if (type == arrow::Compression::ZSTD) {
+          CHECK_OK(r.status());
+          CHECK(r.ok() && *r == static_cast<int64_t>(n) && std::memcmp(back.data(), data.data(), n) == 0);
+        } else {
+          CHECK((r.ok() && *r == static_cast<int64_t>(n) &&
+                 std::memcmp(back.data(), data.data(), n) == 0) ||
+                r.status().IsNotImplemented());
+        }
+      }
+    }
+    // Arrow IPC with GPU body compression, read back by the stock reader
+    auto batch = IpcBatch();
+    auto opts = arrow::ipc::IpcWriteOptions::Defaults();
+    opts.codec = std::shared_ptr<arrow::util::Codec>(std::move(c));
+    auto sink = arrow::io::BufferOutputStream::Create();
+    CHECK_OK(sink.status());
+    auto writer = arrow::ipc::MakeStreamWriter(*sink, batch->schema(), opts);
+    CHECK_OK(writer.status());
+    if (!writer.ok()) continue;
+    CHECK_OK((*writer)->WriteRecordBatch(*batch));
+    CHECK_OK((*writer)->Close());
+    auto buf = (*sink)->Finish();
+    CHECK_OK(buf.status());
+    auto reader = arrow::ipc::RecordBatchStreamReader::Open(
+        std::make_shared<arrow::io::BufferReader>(*buf));
+    CHECK_OK(reader.status());
+    if (reader.ok()) {
+      std::shared_ptr<arrow::RecordBatch> got;
+      CHECK_OK((*reader)->ReadNext(&got));
+      CHECK(got && got->Equals(*batch));
+    }
+    std::ofstream o(outdir + "/ipc_" + tag + ".arrows", std::ios::binary);
+    o.write(reinterpret_cast<const char*>((*buf)->data()), (*buf)->size());
+  }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -232,10 +340,12 @@ int main(int argc, char** argv) {
     // no GPU in the build container: discovery must fail cleanly, not crash
     auto ids = bitar::CompressDriver<bitar::Class_HIP_GFX950>::Instance()->ListAvailableDeviceIds();
     if (!ids.ok()) CHECK(ids.status().IsInvalid());
+  } else if (argc >= 4 && mode == "arrow") {
+    ArrowCodecTests(argv[2], argv[3]);
   } else if (argc >= 4) {
     GpuTests(argv[2], argv[3]);
   } else {
-    std::cerr << "usage: frontend_test cpu | gpu <input> <outdir>\n";
+    std::cerr << "usage: frontend_test cpu | gpu <input> <outdir> | arrow <input> <outdir>\n";
     return 2;
   }
   std::cout << (g_failures ? "FAILED " : "PASSED ") << g_failures << " failures\n";
