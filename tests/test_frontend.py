@@ -95,3 +95,42 @@ def test_arrow_codec_adapter_on_gpu(tmp_path):
         n = 200000
         assert table.column("v").to_pylist() == [i * 7 % 1000 for i in range(n)], tag
         assert table.column("s").to_pylist() == [f"row{i % 977}" for i in range(n)], tag
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt,ipc", [("parquet", "none"), ("feather", "zstd"), ("raw", "none")])
+def test_demo_app_modes(tmp_path, fmt, ipc):
+    """demo_app (reference apps/demo_app.cc): mode 1 reads a Parquet / Feather table and
+    serializes it to an Arrow IPC stream (optionally GPU-compressed bodies), mode 0 reads raw
+    bytes; then EvaluateSync and EvaluateAsync (2 devices' worth of queue pairs on one GPU)
+    must report byte-identical round trips."""
+    pa = pytest.importorskip("pyarrow")
+    n = 300000
+    table = pa.table({"v": pa.array([i * 7 % 1000 for i in range(n)], pa.int64()),
+                      "s": pa.array([f"row{i % 977}" for i in range(n)])})
+    if fmt == "parquet":
+        import pyarrow.parquet as pq
+        path = tmp_path / "t.parquet"
+        pq.write_table(table, path)
+        args = ["--mode", "1"]
+    elif fmt == "feather":
+        import pyarrow.feather as pf
+        path = tmp_path / "t.feather"
+        pf.write_feather(table, path)
+        args = ["--mode", "1"]
+    else:
+        path = tmp_path / "t.bin"
+        path.write_bytes(O.fill(O.KIND_ARROW, 3, 3 << 20).tobytes())
+        args = ["--mode", "0", "--bytes", str(2 << 20)]
+    demo = os.path.join(CPP, "build", "demo_app")
+    if not os.path.exists(demo):
+        _build()
+    r = subprocess.run([demo, "--file", str(path), *args, "--codec", "lz4", "--seg", "65536",
+                        "--workers", "3", "--ipc-codec", ipc],
+                       capture_output=True, text=True, timeout=600)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out
+    assert "The decompressed data is equivalent to the input buffer" in out, out
+    assert "parts is equivalent to the input buffer" in out, out
+    if fmt != "raw":
+        assert "Deserialize Table" in out, out
