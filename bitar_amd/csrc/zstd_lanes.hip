@@ -129,13 +129,15 @@ struct Bits {
   uint64_t C;
   uint32_t used;
   int32_t ptr;
+  // branch-free: the load address is clamped into [q - 8, ...) (inside the frame, q >= 12);
+  // bytes below q are masked off, all of them when ptr + 8 <= q (an overrun, rejected by
+  // the final bit count)
   __device__ __forceinline__ void load(const GMEM uint8_t* src, uint32_t q) {
-    if (ptr + 8 <= (int32_t)q) {
-      C = 0;  // wholly below the section (an overrun; the final bit count rejects it)
-    } else {
-      C = ld8(src + ptr);  // ptr >= q - 7 >= 5: inside the frame
-      if (ptr < (int32_t)q) C &= ~0ull << (8 * (uint32_t)((int32_t)q - ptr));
-    }
+    const int32_t lo = (int32_t)q - 8;
+    const int32_t at = ptr < lo ? lo : ptr;
+    const uint64_t v = ld8(src + at);
+    const int32_t below = (int32_t)q - ptr;  // bytes of [ptr, ptr + 8) below q
+    C = below <= 0 ? v : below >= 8 ? 0ull : v & (~0ull << (8 * (uint32_t)below));
   }
   __device__ __forceinline__ void reload(const GMEM uint8_t* src, uint32_t q) {
     ptr -= (int32_t)(used >> 3);
@@ -269,27 +271,16 @@ __device__ __forceinline__ bool block(const GMEM uint8_t* src, uint32_t cs, GMEM
         sof = (io >> 25) + b.read((io >> 22) & 7u);
       }
       uint32_t off;
-      if (ofv > 3) {
-        off = ofv - 3;
-        rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = off;
-      } else {
-        const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
-        if (idx == 1) {
-          off = rep[0];
-        } else if (idx == 2) {
-          off = rep[1];
-          rep[1] = rep[0]; rep[0] = off;
-        } else if (idx == 3) {
-          off = rep[2];
-          rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = off;
-        } else {
-          off = rep[0] - 1;
-          if (off == 0) return false;
-          rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = off;
-        }
-      }
+      // repeat offsets in select form (no exec-mask branches; the three stay in VGPRs)
+      const uint32_t c0 = rep[0], c1 = rep[1], c2 = rep[2];
+      const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
+      off = ofv > 3 ? ofv - 3 : idx == 1 ? c0 : idx == 2 ? c1 : idx == 3 ? c2 : c0 - 1;
+      const bool shift2 = ofv > 3 || idx >= 3, shift1 = ofv > 3 || idx >= 2;
+      rep[2] = shift2 ? c1 : c2;
+      rep[1] = shift1 ? c0 : c1;
+      rep[0] = off;
       if (lp + ll > regen || (uint64_t)op + ml + (regen - lp) > cap) return false;
-      if (off == 0 || off > op + ll) return false;
+      if (off == 0 || off > op + ll) return false;  // also the rep0 - 1 == 0 case
       lits(ll);
       op += ll;
       lp += ll;
