@@ -172,8 +172,27 @@ __device__ __forceinline__ void copy_lits(GMEM uint8_t* d, const GMEM uint8_t* s
 __device__ __forceinline__ void copy_match(GMEM uint8_t* d, uint32_t off, uint32_t n,
                                            bool room) {
   const GMEM uint8_t* s = d - off;
-  if (room) {  // d + n + 8 <= end of the segment
-    if (off >= 8) {
+  if (room) {  // d + n + 32 <= end of the segment
+    if (off >= 16 && n <= 16) {  // the common short match: two loads, then two stores
+      const uint64_t a = ld8(s), b = ld8(s + 8);
+      st8(d, a);
+      st8(d + 8, b);
+    } else if (off >= 32) {  // 32-byte steps: four loads in flight, then four stores
+      for (uint32_t j = 0; j < n; j += 32) {
+        const uint64_t a = ld8(s + j), b = ld8(s + j + 8), c = ld8(s + j + 16),
+                       e = ld8(s + j + 24);
+        st8(d + j, a);
+        st8(d + j + 8, b);
+        st8(d + j + 16, c);
+        st8(d + j + 24, e);
+      }
+    } else if (off >= 16) {  // 16-byte steps
+      for (uint32_t j = 0; j < n; j += 16) {
+        const uint64_t a = ld8(s + j), b = ld8(s + j + 8);
+        st8(d + j, a);
+        st8(d + j + 8, b);
+      }
+    } else if (off >= 8) {
       for (uint32_t j = 0; j < n; j += 8) st8(d + j, ld8(s + j));
     } else {
       // the first `off` bytes repeat: build an 8-byte word of the pattern, store it every
@@ -227,6 +246,7 @@ __device__ __forceinline__ bool block(const GMEM uint8_t* src, uint32_t cs, GMEM
   }
   uint32_t lp = 0;
   auto lits = [&](uint32_t n) __attribute__((always_inline)) {
+    if (n == 0) return;
     if (lt == 0) {
       copy_lits(dst + op, src + lit + lp, n, op + 16 <= capw && lit + lp + 16 <= cs);
     } else {
@@ -284,7 +304,7 @@ __device__ __forceinline__ bool block(const GMEM uint8_t* src, uint32_t cs, GMEM
       lits(ll);
       op += ll;
       lp += ll;
-      copy_match(dst + op, off, ml, op + ml + 8 <= capw);
+      copy_match(dst + op, off, ml, op + ml + 32 <= capw);
       op += ml;
     }
     if (b.remaining(q) != 0) return false;
