@@ -158,12 +158,20 @@ struct Bits {
 // n literal bytes s -> d (no overlap).  Wildcopy when both sides have 16 bytes of room.
 __device__ __forceinline__ void copy_lits(GMEM uint8_t* d, const GMEM uint8_t* s, uint32_t n,
                                          bool room) {
-  if (n <= 16 && room) {
-    st8(d, ld8(s));
-    if (n > 8) st8(d + 8, ld8(s + 8));
+  if (n <= 16 && room) {  // both loads in flight, then the stores
+    const uint64_t a = ld8(s), b = ld8(s + 8);
+    st8(d, a);
+    if (n > 8) st8(d + 8, b);
     return;
   }
   uint32_t j = 0;
+  for (; j + 32 <= n; j += 32) {
+    const uint64_t a = ld8(s + j), b = ld8(s + j + 8), c = ld8(s + j + 16), e = ld8(s + j + 24);
+    st8(d + j, a);
+    st8(d + j + 8, b);
+    st8(d + j + 16, c);
+    st8(d + j + 24, e);
+  }
   for (; j + 8 <= n; j += 8) st8(d + j, ld8(s + j));
   for (; j < n; ++j) d[j] = s[j];
 }
