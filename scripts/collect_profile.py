@@ -8,7 +8,8 @@ usage: python scripts/collect_profile.py TAG ROUND_DIR
 
 Traffic per launch (MI355X_MICROARCH.md "HBM"): FETCH_SIZE and WRITE_SIZE are in KiB; on
 gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane streaming reads, which is how
-every bulk read of these kernels is issued, so it is doubled; WRITE_SIZE is exact for
+every bulk read of the wave-per-segment kernels is issued, so it is doubled (not for the
+lane-per-segment zstd_lanes_kernel, whose reads are 8 B per lane); WRITE_SIZE is exact for
 16-B-per-lane stores.  Each counter comes from its own --pmc pass; the value is averaged
 over the kernel's launches in that pass.
 """
@@ -19,6 +20,9 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the x2 correction is for 16-B-per-lane streaming reads; zstd_lanes_kernel reads 8 B per
+# lane (one lane per segment), so its FETCH_SIZE is taken as reported
+FETCH_FACTOR = {"zstd_lanes_kernel": 1.0}
 
 
 def per_kernel(path):
@@ -48,9 +52,10 @@ def main():
     traffic, lines = {}, []
     for k in sorted(set(fetch) | set(write)):
         f_kib, w_kib = fetch.get(k, 0.0), write.get(k, 0.0)
-        b = (2.0 * f_kib + w_kib) * 1024.0
+        x = FETCH_FACTOR.get(k, 2.0)
+        b = (x * f_kib + w_kib) * 1024.0
         traffic[k] = round(b)
-        lines.append(f"{k:28s} FETCH_SIZE {f_kib:14.1f} KiB (x2 = {2 * f_kib * 1024:.4g} B)  "
+        lines.append(f"{k:28s} FETCH_SIZE {f_kib:14.1f} KiB (x{x:g} = {x * f_kib * 1024:.4g} B)  "
                      f"WRITE_SIZE {w_kib:14.1f} KiB  -> {b:.4g} B per launch")
     with open(os.path.join(rdir, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
