@@ -25,7 +25,10 @@ __global__ void deflate_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint
                                         uint8_t* const*, uint32_t*, uint32_t*);
 __global__ void inflate_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
-                               uint32_t*);
+                               uint32_t*, uint32_t);
+template <uint32_t L>
+__global__ void inflate_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
+                                     const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
 __global__ void zstd_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
                                      uint8_t* const*, uint32_t*, uint32_t*);
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
@@ -303,6 +306,19 @@ extern "C" int bitar_hip_debug_set_zstd_lanes(int lanes) {
   return (int)old;
 }
 
+// segments per wave of inflate_lanes_kernel: BITAR_HIP_INFLATE_LANES = 32 / 16, 0 = off
+static std::atomic<uint32_t> g_inflate_lanes{[] {
+  const char* e = std::getenv("BITAR_HIP_INFLATE_LANES");
+  const long x = e ? std::strtol(e, nullptr, 10) : 16;
+  return x <= 0 ? 0u : x >= 32 ? 32u : 16u;
+}()};
+static uint32_t inflate_lanes() { return g_inflate_lanes.load(std::memory_order_relaxed); }
+extern "C" int bitar_hip_debug_set_inflate_lanes(int lanes) {
+  const uint32_t old = inflate_lanes();
+  g_inflate_lanes.store(lanes <= 0 ? 0u : lanes >= 32 ? 32u : 16u);
+  return (int)old;
+}
+
 static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            const void* const* d_srcs, const void* d_slab, uint64_t stride,
                            const uint32_t* d_sizes, uint32_t nseg, uint32_t seg, void* d_out,
@@ -327,9 +343,22 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
   if (codec == BITAR_HIP_CODEC_LZ4)
     hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
                        stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
-  else if (codec == BITAR_HIP_CODEC_DEFLATE)
+  else if (codec == BITAR_HIP_CODEC_DEFLATE) {
+    // lane-per-segment decoder for stored / fixed-Huffman streams first; the wave decoder
+    // then takes the segments it deferred (inflate_lanes.hip)
+    const uint32_t L = inflate_lanes();
+    if (L) {
+      const dim3 g((nseg + L - 1) / L);
+      if (L == 32)
+        hipLaunchKernelGGL(bitar_hip::inflate_lanes_kernel<32>, g, dim3(64), 0, s, srcs, slab,
+                           stride, d_sizes, nseg, seg, out, d_produced);
+      else
+        hipLaunchKernelGGL(bitar_hip::inflate_lanes_kernel<16>, g, dim3(64), 0, s, srcs, slab,
+                           stride, d_sizes, nseg, seg, out, d_produced);
+    }
     hipLaunchKernelGGL(bitar_hip::inflate_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
-                       stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
+                       stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err, L ? 1u : 0u);
+  }
   else {
     // lane-per-segment decoder first; the wave-per-segment decoder then takes the segments it
     // deferred (zstd_lanes.hip)

@@ -19,6 +19,18 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
+@pytest.fixture(autouse=True, params=[16, 32, 0], ids=["lanes16", "lanes32", "wave"])
+def inflate_decoder(request):
+    """Every test runs with the lane-per-segment inflater in front (inflate_lanes.hip; it
+    defers dynamic-Huffman and failing streams to the wave kernel) and with the
+    wave-per-segment inflater alone."""
+    import bitar_amd
+    L = bitar_amd.lib()
+    old = L.bitar_hip_debug_set_inflate_lanes(request.param)
+    yield request.param
+    L.bitar_hip_debug_set_inflate_lanes(old)
+
+
 def test_inflate_all_golden(eng):
     vecs = [(e, blob, plain) for e, blob, plain in golden_lib.vectors("deflate")
             if len(plain) <= 65536]  # one segment each (larger inputs: oracle tests)
