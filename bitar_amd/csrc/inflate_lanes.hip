@@ -193,10 +193,10 @@ __global__ __launch_bounds__(64) void inflate_lanes_kernel(
         if (kind == 0) {
           if (op >= cap) break;
           dst[op++] = (uint8_t)e;
-          // up to three more literals on the same refill (>= 56 - 9 bits are left, each
-          // literal takes <= 9); anything else is decoded at the loop head
+          // up to five more literals on the same refill (>= 56 bits after it, each literal
+          // takes <= 9); anything else is decoded at the loop head
 #pragma unroll
-          for (uint32_t r = 0; r < 3; ++r) {
+          for (uint32_t r = 0; r < 5; ++r) {
             const uint32_t e2 = tlit[b.peek(9)];
             if ((e2 >> 30) != 0 || op >= cap) break;
             b.skip((e2 >> 24) & 15u);
@@ -219,6 +219,14 @@ __global__ __launch_bounds__(64) void inflate_lanes_kernel(
         if (dist > op || op + len > cap) break;
         copy_match(dst + op, dist, len, op + len + 32 <= cap);
         op += len;
+        // the match took <= 32 of the >= 56 bits: up to two literals more before the refill
+#pragma unroll
+        for (uint32_t r = 0; r < 2; ++r) {
+          const uint32_t e2 = tlit[b.peek(9)];
+          if ((e2 >> 30) != 0 || op >= cap) break;
+          b.skip((e2 >> 24) & 15u);
+          dst[op++] = (uint8_t)e2;
+        }
       }
       if (!eob) {
         active = false;
