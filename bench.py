@@ -7,9 +7,9 @@ configs[2]): every rank owns a 1 GiB HBM-resident buffer of the Silesia-style mi
 of the whole buffer into per-segment slots + (N > 1) the RCCL all-gather of the per-segment
 compressed sizes that builds the global frame index + LZ4 decompress of every slot back into
 a 1 GiB output.  value = bytes of uncompressed data round-tripped by all ranks / wall time.
-Beside it: "secondary" (BASELINE configs[1], random bytes, LZ4 decompress only, N = 1) and
+Beside it: "secondary" (BASELINE configs[1], random bytes, LZ4 decompress only, N = 1),
 "zstd" (BASELINE configs[5], Zstd frames on Arrow record-batch bodies, same sharding and
-all-gather at every N).
+all-gather at every N) and "deflate" (the reference's own codec at its 59460-B segments).
 
 Prints ONE JSON line (rank 0).  Launch: python bench.py [--gpus N --steps K --warmup W];
 for N > 1 under torch.distributed.run (one process per GPU, RCCL).
@@ -42,6 +42,8 @@ def parse():
                    help="skip the random-data decompress-only line (BASELINE configs[1])")
     p.add_argument("--no-zstd", action="store_true",
                    help="skip the Zstd round-trip line (BASELINE configs[5])")
+    p.add_argument("--no-deflate", action="store_true",
+                   help="skip the DEFLATE line (the reference's own codec, 59460-B segments)")
     p.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
     return p.parse_args()
 
@@ -101,7 +103,9 @@ def cpu_baseline(args):
 
 
 KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
-           "deflate": ("deflate_compress_kernel", "inflate_kernel"),
+           # decompress = inflate_lanes_kernel (lane per segment) + inflate_kernel in
+           # defer-only mode; timed together
+           "deflate": ("deflate_compress_kernel", "inflate_lanes_kernel"),
            # decompress = zstd_lanes_kernel (lane per segment) + zstd_decompress_kernel in
            # defer-only mode (an early exit per segment for our frames); timed together
            "zstd": ("zstd_compress_kernel", "zstd_lanes_kernel")}
@@ -236,6 +240,12 @@ def main():
         # BASELINE configs[5]: Zstd level-1-class frames on Parquet-column-like buffers
         # (kind 2, Arrow record-batch bodies), same sharding and all-gather, every rank
         zs = roundtrip(eng, ctx, "zstd", 2, n, seg, args.steps, args.warmup, rank + 1000)
+    df = None
+    if args.codec != "deflate" and not args.no_deflate:
+        # the reference's own segment codec (RTE_COMP_ALGO_DEFLATE, config.cc:83-105) at its
+        # default segment size (59460 B, app_common.h:39), same input as the headline
+        df = roundtrip(eng, ctx, "deflate", args.kind, n, 59460, args.steps, args.warmup,
+                       rank + 2000)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -290,6 +300,17 @@ def main():
             "compress_gibs": round(U / zs["t_comp"] / GIB, 3),
             "decompress_gibs": round(U / zs["t_dec"] / GIB, 3),
             "roundtrip_ok": zs["ok"], "roofline": zroof, "kernels": zkern}
+    if df is not None:
+        droof, dkern = kernel_lines("deflate", df, n, args.traffic_json)
+        res["deflate"] = {
+            "workload": "the reference's codec: raw DEFLATE (fixed-Huffman blocks) per 59460-B "
+                        "segment, compress + decompress, same input and sharding as the headline",
+            "value": round(world * U * args.steps / df["elapsed"] / GIB, 3), "unit": "GiB/s",
+            "ms_per_step": round(df["elapsed"] / args.steps * 1e3, 4),
+            "compression_ratio": round(U / df["csize"], 4),
+            "compress_gibs": round(U / df["t_comp"] / GIB, 3),
+            "decompress_gibs": round(U / df["t_dec"] / GIB, 3),
+            "roundtrip_ok": df["ok"], "roofline": droof, "kernels": dkern}
     if not args.no_cpu_baseline and world == 1 and args.codec == "lz4":
         res["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(res), flush=True)
