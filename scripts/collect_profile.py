@@ -9,7 +9,7 @@ usage: python scripts/collect_profile.py TAG ROUND_DIR
 Traffic per launch (MI355X_MICROARCH.md "HBM"): FETCH_SIZE and WRITE_SIZE are in KiB; on
 gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane streaming reads, which is how
 every bulk read of the wave-per-segment kernels is issued, so it is doubled (not for the
-lane-per-segment zstd_lanes_kernel, whose reads are 8 B per lane); WRITE_SIZE is exact for
+lane-per-segment zstd_lanes_kernel and inflate_lanes_kernel, whose reads are 8 B per lane); WRITE_SIZE is exact for
 16-B-per-lane stores.  Each counter comes from its own --pmc pass; the value is averaged
 over the kernel's launches in that pass.
 """
@@ -20,9 +20,10 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# the x2 correction is for 16-B-per-lane streaming reads; zstd_lanes_kernel reads 8 B per
-# lane (one lane per segment), so its FETCH_SIZE is taken as reported
-FETCH_FACTOR = {"zstd_lanes_kernel": 1.0}
+# the x2 correction is for 16-B-per-lane streaming reads; the lane-per-segment decoders
+# (zstd_lanes_kernel, inflate_lanes_kernel) read 8 B per lane, so their FETCH_SIZE is taken
+# as reported
+FETCH_FACTOR = {"zstd_lanes_kernel": 1.0, "inflate_lanes_kernel": 1.0}
 
 
 def per_kernel(path):
