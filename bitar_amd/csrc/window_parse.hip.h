@@ -11,7 +11,7 @@
 // blocks would make the compiler wait for every load in flight.
 //
 // Per fixed window of 64 positions (one per lane):
-//   1. hash the 4 bytes at every position (from the ring), look up a 2048-entry LDS table of
+//   1. hash the 4 bytes at every position (from the ring), look up a 1024-entry LDS table of
 //      u16 positions, then insert every position (the largest position wins a slot);
 //   2. lanes with a candidate verify + measure the match on 16 bytes from the ring, and
 //      lanes still matching extend in parallel up to 32 bytes;
@@ -31,7 +31,7 @@ namespace cmp {
 // Build-time knobs for tuning experiments (scripts/build_variant.sh); the defaults are the
 // shipped configuration and the one the oracle restates.
 #ifndef BITAR_CMP_HASH_LOG
-#define BITAR_CMP_HASH_LOG 11
+#define BITAR_CMP_HASH_LOG 10
 #endif
 #ifndef BITAR_CMP_OBUF
 #define BITAR_CMP_OBUF 1024

@@ -78,16 +78,17 @@ int bo_lz4_decompress_block(const uint8_t* src, uint32_t csize, uint8_t* dst, ui
  * Restated exactly as the HIP kernels run it (DESIGN.md "Window-scan parse"):
  *   positions 0..n-12 (legal match starts) are visited in FIXED windows of 64, one per
  *   wavefront lane: window w covers [64w, 64w+64);
- *   every window position looks up hash(read32(p)) in a 2048-entry table holding the most
+ *   every window position looks up hash(read32(p)) in a 1024-entry table holding the most
  *   recent position inserted by an EARLIER window, then all window positions are inserted
  *   (the largest position wins a shared slot) -- the table never depends on the parse;
  *   greedily, from the current position, the first window position whose candidate c
  *   satisfies c < p, p - c <= max_dist and read32(c) == read32(p) starts a match,
  *   extended forward while bytes agree, never past n-5 nor max_mlen; the search resumes
  *   at the match end (possibly several windows later).                                  */
-/* 2048 entries: the kernel keeps the table in 4 KiB of LDS so 12 waves fit a CU (vs 8 with
- * 4096 entries); measured ~1% ratio cost on the synthetic corpora, 18% faster compress. */
-#define BO_HASH_LOG 11
+/* 1024 entries: the kernel keeps the table in 2 KiB of LDS so 14 waves fit a CU (12 with
+ * 2048 entries, 8 with 4096); measured on kind 1 / 2 / 5 / 6 input: ratio -1.8 / -1.3 /
+ * -4.6 / -2.8 % against 2048 entries, LZ4 compress 12 % faster. */
+#define BO_HASH_LOG 10
 #define BO_WIN 64
 #define BO_MINMATCH 4
 #define BO_LASTLITERALS 5
