@@ -3,10 +3,10 @@
 // per segment (gfx950).  Restated exactly by the oracle's bo_window_parse
 // (oracle/bitar_oracle.c); every compressor must match the oracle's output byte for byte.
 //
-// Input staging.  The segment streams through an 8 KiB LDS input ring in 1 KiB rows (one
+// Input staging.  The segment streams through a 4 KiB LDS input ring in 1 KiB rows (one
 // aligned 16-B block per lane): each row is loaded into registers a whole row of windows
 // before it is written into the ring, and the ring runs 576..1536 B ahead of the scan.
-// Every byte a position, a candidate (matches are capped at 6656 B back) or a literal needs
+// Every byte a position, a candidate (matches are capped at 2560 B back) or a literal needs
 // is then an LDS read.  One register block in a fixed register: a rotation between
 // blocks would make the compiler wait for every load in flight.
 //
@@ -43,11 +43,16 @@ constexpr uint32_t kHashLog = BITAR_CMP_HASH_LOG;
 constexpr uint32_t kMinMatch = 4;
 constexpr uint32_t kLastLiterals = 5;
 constexpr uint32_t kMfLimit = 12;
-// Match distance cap (both codecs): at window x the input ring holds positions
-// [F - 8192, F) with F <= x + 1536, so every candidate (>= x - 6656) is in LDS; it is also
-// inside the LZ4 decoder's 8 KiB history ring (reach 8048), so our streams decode from LDS.
-constexpr uint32_t kMaxDist = 6656;
-constexpr uint32_t kIn = 8192, kInMask = kIn - 1;  // LDS input ring
+// Match distance cap (all codecs): at window x the input ring holds positions
+// [F - kIn, F) with F <= x + 1536, so every candidate (>= x - (kIn - 1536)) is in LDS; it
+// is also inside the LZ4 decoder's 8 KiB history ring (reach 8048), so our streams decode
+// from LDS.  4 KiB ring + 1024-entry table = 7.3 KiB of LDS per wave, 22 waves per CU
+// (the VGPR limit is 24); an 8 KiB ring (cap 6656) measured 12-18 % slower for ~1 % ratio.
+#ifndef BITAR_CMP_RING
+#define BITAR_CMP_RING 4096
+#endif
+constexpr uint32_t kIn = BITAR_CMP_RING, kInMask = kIn - 1;  // LDS input ring
+constexpr uint32_t kMaxDist = kIn - 1536;
 constexpr uint32_t kInPad = 64;  // mirror of ring[0, 64) after its end: probes never wrap
 constexpr uint32_t kRow = 1024;                   // prefetch row: one 16-B block per lane
 constexpr uint32_t kPreExt = 32;                  // parallel per-lane match extension limit

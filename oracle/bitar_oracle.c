@@ -179,13 +179,13 @@ static void lz4_emit(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t 
   if (ml >= 15) lz4_put_len(c, ml - 15);
 }
 
-/* Match distance cap of the bitar parse (both codecs): 6656 B.  The compressor streams its
- * input through an 8 KiB LDS ring that runs up to 1.5 KiB ahead of the scan, so every
+/* Match distance cap of the bitar parse (all codecs): 2560 B.  The compressor streams its
+ * input through a 4 KiB LDS ring that runs up to 1.5 KiB ahead of the scan, so every
  * candidate of a window is in LDS; the LZ4 decoder's 8 KiB history ring reaches 8048 B back,
  * so every match of our own streams decodes from LDS.  Standard LZ4 allows 65535 and
- * DEFLATE 32768; the cap costs ~1-2% ratio on the synthetic corpora (DESIGN.md
- * "Window-scan parse"). */
-#define BO_MAX_DIST 6656u
+ * DEFLATE 32768; against a 6656-B cap (8 KiB ring) it costs 0.7-1.4 % ratio on the
+ * synthetic corpora for 12-18 % faster compression (DESIGN.md "Window-scan parse"). */
+#define BO_MAX_DIST 2560u
 _Static_assert(BO_MAX_DIST == BO_MAX_DIST_ALL, "one distance cap for all codecs");
 
 int bo_lz4_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,

@@ -91,7 +91,7 @@ typedef void (*bo_emit_fn)(void* ctx, uint32_t lit_start, uint32_t lit_len, uint
                            uint32_t mlen);
 void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t max_mlen,
                      bo_emit_fn emit, void* ctx);
-#define BO_MAX_DIST_ALL 6656u
+#define BO_MAX_DIST_ALL 2560u
 
 /* ---- segment-level restatement of CompressDevice ------------------------------- */
 /* Compress (device.cc:156-238): cut `in` into ceil(n/seg) segments in order, compress each
