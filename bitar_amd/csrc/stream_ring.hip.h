@@ -16,9 +16,15 @@ namespace bitar_hip {
 
 namespace sr {
 
-constexpr uint32_t kRing = 8192;
+#ifndef BITAR_DEC_RING
+#define BITAR_DEC_RING 4096
+#endif
+#ifndef BITAR_DEC_WIN
+#define BITAR_DEC_WIN 1024
+#endif
+constexpr uint32_t kRing = BITAR_DEC_RING;
 constexpr uint32_t kRingMask = kRing - 1;
-constexpr uint32_t kWin = 2048;        // 2 dwordx4 per lane
+constexpr uint32_t kWin = BITAR_DEC_WIN;  // dwordx4 per lane per refill step
 constexpr uint32_t kLongLit = 1024;    // literal runs at least this long go HBM -> HBM
 constexpr uint32_t kFlushAt = kRing / 2;
 constexpr uint32_t kNearOff = kRing - 2 * kWave - 16;  // ring holds the source
