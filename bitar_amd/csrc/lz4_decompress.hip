@@ -28,6 +28,8 @@ using namespace sr;
 // stream bytes the batch path may touch past ip: 64 candidate tokens, each with up to two
 // length bytes and <= 60 literals, plus its offset
 constexpr uint32_t kBatchIn = 132;
+// output bytes one batch may produce (one per lane)
+constexpr uint32_t kBatchOut = kWave;
 
 // 256 stream bytes held in ONE register, dword-packed: lane l holds bytes vb+4l .. vb+4l+3
 // (vb 4-byte aligned in absolute address terms).  The parse reads tokens, extensions and
@@ -85,6 +87,43 @@ __device__ __forceinline__ bool ext_len(State& s, uint8_t* win, SVec& sv, uint32
   return read_ext(s, win, len);
 }
 
+
+// The batch's token walk: from lane 0, follow the chain of candidate tokens while each
+// sequence is eligible and fits in lim output bytes; sequence records (pr of the token
+// lane) are dropped into the lane of the sequence's first output byte.  Returns the output
+// byte count; k = the first unconsumed token lane.  Written out because the scalar chain is
+// the batch's bound (the SQ issues one SALU per SIMD every 4 cycles): 8 SALU + 3 VALU per
+// sequence, output position kept in m0 (the v_writelane lane select).
+__device__ __forceinline__ uint32_t walk_tokens(uint32_t pw, uint32_t pr, uint32_t lim,
+                                                uint32_t& k, uint32_t& vrec) {
+  uint32_t out, e, r, ol, n, m0_saved;
+  // m0 is reserved to the compiler: saved and restored around the loop
+  __asm__ volatile(
+      "s_mov_b32 %[m0s], m0\n"
+      "s_mov_b32 %[k], 0\n"
+      "s_mov_b32 m0, 0\n"
+      "L_walk_%=:\n"
+      "v_readlane_b32 %[e], %[pw], %[k]\n"
+      "v_readlane_b32 %[r], %[pr], %[k]\n"
+      "s_lshr_b32 %[ol], %[e], 7\n"
+      "s_add_u32 %[n], m0, %[ol]\n"
+      "s_cmp_gt_u32 %[n], %[lim]\n"
+      "s_cbranch_scc1 L_done_%=\n"
+      "v_writelane_b32 %[vr], %[r], m0\n"
+      "s_mov_b32 m0, %[n]\n"
+      "s_and_b32 %[k], %[e], 0x7f\n"
+      "s_cmp_lt_u32 %[k], 64\n"
+      "s_cbranch_scc1 L_walk_%=\n"
+      "L_done_%=:\n"
+      "s_mov_b32 %[out], m0\n"
+      "s_mov_b32 m0, %[m0s]\n"
+      : [k] "=&s"(k), [out] "=&s"(out), [e] "=&s"(e), [r] "=&s"(r), [ol] "=&s"(ol),
+        [n] "=&s"(n), [m0s] "=&s"(m0_saved), [vr] "+v"(vrec)
+      : [pw] "v"(pw), [pr] "v"(pr), [lim] "s"(lim)
+      : "scc");
+  return out;
+}
+
 }  // namespace lz4d
 
 __global__ __launch_bounds__(64) void lz4_decompress_kernel(
@@ -118,19 +157,24 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   const uint32_t base = (uint32_t)(uintptr_t)s.dst;  // ring index = absolute address & mask
   const uint32_t src_lo = (uint32_t)(uintptr_t)s.src;
   while (ok) {
-    // ---- batch fast path: up to 64 output bytes of short sequences per step -------------
+    // ---- batch fast path: up to kBatchOut output bytes of short sequences per step ------
     // 1. every lane l decodes "a token at stream position ip+l" from the LDS window
     //    (token, literal count, match length, offset): a speculative parse of 64 candidates;
     // 2. a scalar walk follows the real token chain from ip (one v_readlane per sequence)
-    //    while the sequences are short (no length extension), not last, and fit in 64 bytes;
-    // 3. each output lane t finds its sequence (recorded during the walk), and its source:
-    //    a literal byte in the window, a history byte in the ring, or -- for a match reaching
-    //    into this batch -- another lane, resolved by pointer doubling over lanes;
-    // 4. ONE ds_read gathers all 64 bytes, ONE ds_write stores them into the ring.
-    // Lanes past the batch write too: their ring slots are >= kRing - 64 behind the output,
-    // older than any near source and already flushed, and are rewritten before use.
+    //    while the sequences are short (no length extension), not last, and fit the batch;
+    //    it drops each sequence's record into the lane of its first output byte
+    //    (v_writelane), and a DPP prefix max hands every output byte its sequence's record
+    //    (the output start sits in the top bits, so the latest start wins);
+    // 3. each output byte (lane t holds bytes t, t+64, ...) finds its source: a literal byte
+    //    in the window, a history byte in the ring, or -- for a match reaching into this
+    //    batch -- another byte of the batch, resolved by pointer doubling;
+    // 4. one ds_read per 64 bytes gathers the batch, one ds_write stores it into the ring.
+    // Bytes past the batch are written too: their ring slots are >= kRing - kBatchOut
+    // behind the output, older than any near source and already flushed, and are rewritten
+    // before use.
     for (;;) {
-      if (s.ip + kBatchIn > s.csize || s.op + 64 - s.flushed > kFlushAt) break;
+      if (s.ip + kBatchIn > s.csize) break;
+      if (s.op + kBatchOut - s.flushed > kFlushAt) flush(s, ring, s.op, false);
       uint32_t wrel = src_lo + s.ip - (uint32_t)s.wb;  // window index of ip (mod 2^32)
       if (wrel > kWin - kBatchIn) {
         win_at(s, win, s.ip, kBatchIn);
@@ -150,57 +194,53 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t coff = cb0 | (cb1 << 8);
       const uint32_t cml = 4 + (mx ? 15u + b2 : cm4);
       const uint32_t colen = cL + cml;
-      // eligible: at most one length byte each (< 255), <= 31 literals, fits a batch, real
-      // offset, near, and (conservatively, as if this token opened the batch) not before the
-      // segment start
+      // eligible: at most one length byte each (< 255), <= 31 literals, <= 64 output bytes,
+      // real offset, near, and (conservatively, as if this token opened the batch) not
+      // before the segment start
       const bool csimple = (!lx || b1 < 255u) && (!mx || b2 < 255u) && cL <= 31u &&
                            colen <= 64u && coff != 0 && coff <= kNearOff && coff <= s.op + cL;
-      // the walk's record, one dword: next token lane (7 bits, capped at 64) | olen (7 bits:
-      // output length, 127 when not eligible -- the walk's one compare then stops) |
-      // literal count (5 bits) | offset (13 bits; eligible offsets are <= 8048)
+      // walk record: next token lane (7 bits, <= 99; the walk stops at a lane >= 64, which
+      // was not parsed, after consuming the sequence) | output length (255: not eligible,
+      // the walk's one compare then stops).  Sequence record: offset (12 bits; eligible
+      // offsets are <= kNearOff, and never 0) | literal count (5 bits) | token lane (6 bits)
+      // -- the output start goes into bits 24..29 after the walk.
       const uint32_t nxt = lane + 3 + (lx ? 1u : 0u) + (mx ? 1u : 0u) + cL;
-      const uint32_t pack = (nxt < 64u ? nxt : 64u) | ((csimple ? colen : 127u) << 7) |
-                            ((cL & 31u) << 14) | (coff << 19);
-      // (2) scalar walk over the real tokens (capacity: checked once for the whole batch);
-      // every output lane keeps the record and token lane of the sequence it falls in
+      const uint32_t pw = nxt | ((csimple ? colen : 255u) << 7);
+      const uint32_t pr = (coff & 4095u) | ((cL & 31u) << 12) | (lane << 17);
+      // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
       const uint32_t room = s.cap - s.op;
-      const uint32_t lim = room < 64 ? room : 64;
-      uint32_t k = 0, out = 0;
-      uint32_t sel = 0, seqlane = 0, ostart = 0;
-      for (;;) {
-        const uint32_t e = readlane(pack, k);
-        const uint32_t ol = (e >> 7) & 127u;
-        if (out + ol > lim) break;
-        if (lane - out < ol) { sel = e; seqlane = k; ostart = out; }
-        out += ol;
-        k = e & 127u;
-        if (k >= 64) break;
-      }
+      const uint32_t lim = room < kBatchOut ? room : kBatchOut;
+      uint32_t k, vrec = 0;
+      const uint32_t out = walk_tokens(pw, pr, lim, k, vrec);
       if (out == 0) break;
-      // (3) sources: window literal / ring history / alias of an earlier lane of the batch
-      // (branch-free: every lane computes both forms)
-      const uint32_t t = lane;
-      const uint32_t jL = (sel >> 14) & 31u;
-      const uint32_t joff = sel >> 19;
-      const uint32_t r = t - ostart;
+      // every output byte takes the record of the latest sequence starting at or before it
+      const uint32_t key = wave_incl_max(vrec ? vrec | (lane << 24) : 0u);
+      // (3) sources: window literal / ring history / alias of an earlier byte of the batch
+      // (branch-free: every lane computes both forms).  bit31: alias (low 6 bits: the
+      // source lane); else an LDS byte address.
+      const uint32_t ostart = key >> 24;
+      const uint32_t seqlane = (key >> 17) & 63u;
+      const uint32_t jL = (key >> 12) & 31u;
+      const uint32_t joff = key & 4095u;
+      const uint32_t r = lane - ostart;
       const bool is_lit = r < jL;
       const uint32_t m = r - jL;
-      const float qf = floorf(((float)(m & 63u) + 0.5f) * __builtin_amdgcn_rcpf((float)(joff > 1u ? joff : 1u)));
+      const float qf = floorf(((float)(m & 63u) + 0.5f) *
+                              __builtin_amdgcn_rcpf((float)(joff > 1u ? joff : 1u)));
       const uint32_t mm = joff <= m ? (m & 63u) - (uint32_t)qf * joff : m;
       const int32_t srel = (int32_t)(ostart + jL + mm) - (int32_t)joff;  // vs op
       const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
       const uint32_t lit_addr = wrel + seqlane + 1 + (jL >= 15u ? 1u : 0u) + r;
-      // bit31: alias (low bits: the source lane); else an LDS byte address
       uint32_t st = is_lit ? lit_addr : srel >= 0 ? ((uint32_t)srel | 0x80000000u) : hist;
       // pointer doubling until no lane of the batch aliases another (chains strictly descend)
-      while (ballot((st & 0x80000000u) != 0u && t < out)) {
+      while (ballot((st & 0x80000000u) != 0u && lane < out)) {
         const uint32_t other = bpermute_lane(st, st & 63u);
         st = (st & 0x80000000u) ? other : st;
       }
       // (4) one gather, one store
       lds_order();
-      const uint8_t b = lds[st & 0x3FFFu];
-      ring[(base + s.op + t) & kRingMask] = b;
+      const uint8_t g = lds[st & 0x3FFFu];
+      ring[(base + s.op + lane) & kRingMask] = g;
       lds_order();
       s.ip += k;
       s.op += out;

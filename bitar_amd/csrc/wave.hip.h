@@ -28,6 +28,13 @@ __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
+// v with lane l replaced by the (wave-uniform) x
+__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x, uint32_t l) {
+  uint32_t r;
+  // two SGPR operands break the constant-bus limit: the lane select goes through m0
+  __asm__("v_writelane_b32 %0, %1, m0" : "=v"(r) : "s"(x), "{m0}"(l), "0"(v));
+  return r;
+}
 // Pointers into global memory (HBM) are typed GMEM (address space 1).  A generic pointer
 // (loaded from a slot table, or rebuilt from an integer) makes the compiler emit FLAT
 // accesses: those count against both vmcnt and lgkmcnt, and every later LDS access must
@@ -151,5 +158,34 @@ __device__ __forceinline__ void wave_copy_global(GMEM uint8_t* d, const GMEM uin
   const uint32_t tail = (uint32_t)(len - done);
   if (lane < tail) d[done + lane] = s[done + lane];
 }
+
+// inclusive prefix sum over the wave's 64 lanes (DPP row shifts + row broadcasts)
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return (uint32_t)x;
+}
+
+// inclusive prefix max (unsigned) over the wave's 64 lanes
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  uint32_t x = v;
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+  return x;
+}
+// lane l gets lane l-1's value, lane 0 gets 0 (DPP wave_shr:1)
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+
 
 }  // namespace bitar_hip

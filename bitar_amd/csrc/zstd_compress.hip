@@ -220,8 +220,8 @@ struct ZstdOut : cmp::ByteOut {
     const uint32_t q = W.x + lane;
     const bool cl = (W.chain >> lane) & 1;
     // match ends increase along the chain: "end of the previous match" is a prefix max
-    const uint32_t end_incl = cmp::wave_incl_max(cl ? q + W.mlen : 0u);
-    const uint32_t end_excl = cmp::wave_shr1(end_incl);
+    const uint32_t end_incl = wave_incl_max(cl ? q + W.mlen : 0u);
+    const uint32_t end_excl = wave_shr1(end_incl);
     const uint32_t lit_start = max(anchor, cl ? end_excl : end_incl);
     const uint32_t ll = q - lit_start;  // chain lanes: their literal length
     const bool lit = !cl && q >= W.pos_in && q >= end_incl && q < n;
@@ -249,7 +249,7 @@ struct ZstdOut : cmp::ByteOut {
   __device__ __forceinline__ void put_bits(uint64_t v, uint32_t nb, uint32_t p0, uint32_t& bits,
                                            uint32_t& zeroed) {
     const uint32_t lane = lane_id();
-    const uint32_t incl = cmp::wave_incl_sum(nb);
+    const uint32_t incl = wave_incl_sum(nb);
     const uint32_t total = readlane(incl, 63);
     op = p0 + (bits >> 3);
     if (!room((total >> 3) + 16)) return;
