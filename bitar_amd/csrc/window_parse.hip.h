@@ -199,6 +199,39 @@ struct ByteOut {
   }
 };
 
+// The greedy chain's common step, written out (the parse is bound by scalar issue: the SQ
+// issues one SALU per SIMD every 4 cycles): from the non-empty lane set m, take the first
+// lane l; if l is in extm (its match may extend past kPreExt) return l with m unchanged;
+// else add it to chain, set e = l + len[l], keep only lanes of m at or past e, and go on.
+// Returns kWave (m = 0) when the chain leaves the window.  9 SALU + 1 VALU per match.
+__device__ __forceinline__ uint32_t chain_fast(uint64_t& m, uint64_t extm, uint32_t len,
+                                               uint64_t& chain, uint32_t& e) {
+  uint32_t l, ml;
+  uint64_t t;
+  __asm__ volatile(
+      "L_ch_%=:\n"
+      "s_ff1_i32_b64 %[l], %[m]\n"
+      "s_bitcmp1_b64 %[x], %[l]\n"
+      "s_cbranch_scc1 L_out_%=\n"
+      "v_readlane_b32 %[ml], %[len], %[l]\n"
+      "s_bitset1_b64 %[ch], %[l]\n"
+      "s_add_u32 %[e], %[l], %[ml]\n"
+      "s_cmp_gt_u32 %[e], 63\n"
+      "s_cbranch_scc1 L_end_%=\n"
+      "s_lshl_b64 %[t], -1, %[e]\n"
+      "s_and_b64 %[m], %[m], %[t]\n"
+      "s_cbranch_scc1 L_ch_%=\n"
+      "L_end_%=:\n"
+      "s_mov_b64 %[m], 0\n"
+      "s_mov_b32 %[l], 64\n"
+      "L_out_%=:\n"
+      : [l] "=&s"(l), [ml] "=&s"(ml), [t] "=&s"(t), [m] "+s"(m), [ch] "+s"(chain),
+        [e] "+s"(e)
+      : [x] "s"(extm), [len] "v"(len)
+      : "scc");
+  return l;
+}
+
 // The window-scan parse over one segment; hands each window to E::window and the tail to
 // E::sequence.
 template <class E>
@@ -281,9 +314,11 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
       uint64_t m = valid;
       uint32_t e = 0;
       while (m) {  // the greedy chain: the next match is the first valid lane past the end
-        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        // matches that need no extension: the hand-scheduled scalar loop
+        const uint32_t l = chain_fast(m, extm, len, chain, e);
+        if (l >= kWave) break;
         uint32_t mlen = readlane(len, l);
-        if ((extm >> l) & 1) {
+        {  // lane l's match reached kPreExt bytes: extend it cooperatively
           const uint32_t i = x + l;
           uint32_t li = match_limit - i;
           if (li > max_mlen) li = max_mlen;
