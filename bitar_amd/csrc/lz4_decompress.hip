@@ -194,19 +194,18 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t coff = cb0 | (cb1 << 8);
       const uint32_t cml = 4 + (mx ? 15u + b2 : cm4);
       const uint32_t colen = cL + cml;
-      // eligible: at most one length byte each (< 255), <= 31 literals, <= 64 output bytes,
+      // eligible: at most one length byte each (< 255), <= 64 output bytes (so <= 60 literals),
       // real offset, near, and (conservatively, as if this token opened the batch) not
       // before the segment start
-      const bool csimple = (!lx || b1 < 255u) && (!mx || b2 < 255u) && cL <= 31u &&
-                           colen <= 64u && coff != 0 && coff <= kNearOff && coff <= s.op + cL;
+      const bool csimple = (!lx || b1 < 255u) && (!mx || b2 < 255u) && colen <= 64u && coff != 0 && coff <= kNearOff && coff <= s.op + cL;
       // walk record: next token lane (7 bits, <= 99; the walk stops at a lane >= 64, which
       // was not parsed, after consuming the sequence) | output length (255: not eligible,
       // the walk's one compare then stops).  Sequence record: offset (12 bits; eligible
-      // offsets are <= kNearOff, and never 0) | literal count (5 bits) | token lane (6 bits)
+      // offsets are <= kNearOff, and never 0) | literal count (6 bits) | token lane (6 bits)
       // -- the output start goes into bits 24..29 after the walk.
       const uint32_t nxt = lane + 3 + (lx ? 1u : 0u) + (mx ? 1u : 0u) + cL;
       const uint32_t pw = nxt | ((csimple ? colen : 255u) << 7);
-      const uint32_t pr = (coff & 4095u) | ((cL & 31u) << 12) | (lane << 17);
+      const uint32_t pr = (coff & 4095u) | ((cL & 63u) << 12) | (lane << 18);
       // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
       const uint32_t room = s.cap - s.op;
       const uint32_t lim = room < kBatchOut ? room : kBatchOut;
@@ -219,8 +218,8 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       // (branch-free: every lane computes both forms).  bit31: alias (low 6 bits: the
       // source lane); else an LDS byte address.
       const uint32_t ostart = key >> 24;
-      const uint32_t seqlane = (key >> 17) & 63u;
-      const uint32_t jL = (key >> 12) & 31u;
+      const uint32_t seqlane = (key >> 18) & 63u;
+      const uint32_t jL = (key >> 12) & 63u;
       const uint32_t joff = key & 4095u;
       const uint32_t r = lane - ostart;
       const bool is_lit = r < jL;
