@@ -224,9 +224,14 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t r = lane - ostart;
       const bool is_lit = r < jL;
       const uint32_t m = r - jL;
-      const float qf = floorf(((float)(m & 63u) + 0.5f) *
-                              __builtin_amdgcn_rcpf((float)(joff > 1u ? joff : 1u)));
-      const uint32_t mm = joff <= m ? (m & 63u) - (uint32_t)qf * joff : m;
+      // overlapping copy (offset <= match position): fold the source into the first period
+      // (m mod off, exact in fp32 for m, off < 64); skipped when no byte of the batch needs it
+      uint32_t mm = m;
+      if (ballot(!is_lit && joff <= m && lane < out)) {
+        const float qf = floorf(((float)(m & 63u) + 0.5f) *
+                                __builtin_amdgcn_rcpf((float)(joff > 1u ? joff : 1u)));
+        mm = joff <= m ? (m & 63u) - (uint32_t)qf * joff : m;
+      }
       const int32_t srel = (int32_t)(ostart + jL + mm) - (int32_t)joff;  // vs op
       const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
       const uint32_t lit_addr = wrel + seqlane + 1 + (jL >= 15u ? 1u : 0u) + r;
