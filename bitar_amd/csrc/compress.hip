@@ -86,12 +86,12 @@ struct Lz4Out : ByteOut {
     const uint32_t lit_start = max(anchor, cl ? end_excl : end_incl);
     const uint32_t lit_len = q - lit_start;  // chain lanes: their literal run
     const uint32_t ml = W.mlen - kMinMatch;
-    const bool bad = cl && (lit_len >= 270 || ml >= 270);
     const uint32_t nlx = lit_len >= 15 ? 1u : 0u, nmx = ml >= 15 ? 1u : 0u;
     const uint32_t e = cl ? 1 + nlx + lit_len + 2 + nmx : 0u;
     const uint32_t incl = wave_incl_sum(e);
     const uint32_t total = readlane(incl, 63);
-    if (ballot(bad) || anchor < I.lo || (uint64_t)op + total > cap) {
+    if (((ballot(lit_len >= 270) | ballot(ml >= 270)) & W.chain) || anchor < I.lo ||
+        (uint64_t)op + total > cap) {
       // general path, one sequence at a time
       uint64_t m = W.chain;
       uint32_t a = anchor;

@@ -237,7 +237,8 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t lit_addr = wrel + seqlane + 1 + (jL >= 15u ? 1u : 0u) + r;
       uint32_t st = is_lit ? lit_addr : srel >= 0 ? ((uint32_t)srel | 0x80000000u) : hist;
       // pointer doubling until no lane of the batch aliases another (chains strictly descend)
-      while (ballot((st & 0x80000000u) != 0u && lane < out)) {
+      const uint64_t live = out >= 64 ? ~0ull : (1ull << out) - 1;  // lanes of the batch
+      while (ballot((int32_t)st < 0) & live) {
         const uint32_t other = bpermute_lane(st, st & 63u);
         st = (st & 0x80000000u) ? other : st;
       }

@@ -24,7 +24,9 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
   return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+// (ballot of a single compare is one v_cmp into an SGPR pair; ballot of a compound
+// condition costs a v_cndmask + v_cmp more -- AND single-compare ballots instead)
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }

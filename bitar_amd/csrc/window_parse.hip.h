@@ -298,7 +298,8 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
       // lanes still matching after 16 bytes extend in parallel, up to kPreExt
       for (uint32_t k = 16; k < kPreExt; k += 16) {
         const bool go = pre && len == k && lim > k;
-        if (!ballot(go)) break;
+        // (len == k >= 16 implies pre: two single-compare ballots, see wave.hip.h)
+        if (!(ballot(len == k) & ballot(lim > k))) break;
         const uint32_t l2 = k + common16(I.bytes16(p + k), I.bytes16(cand + k));
         len = go ? (l2 < lim ? l2 : lim) : len;
       }
@@ -306,9 +307,9 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
       // reached kPreExt bytes and may go on (cooperative extension during the walk)
       const uint32_t pos_in = pos;
       const uint32_t start = pos > x ? pos - x : 0u;
-      const bool okl = pre && len >= kMinMatch && lane >= start;
-      const uint64_t valid = ballot(okl);
-      const uint64_t extm = ballot(okl && len == kPreExt && lim > kPreExt);
+      // (len >= kMinMatch implies pre; ballots of single compares, see wave.hip.h)
+      const uint64_t valid = ballot(len >= kMinMatch) & (start < kWave ? ~0ull << start : 0ull);
+      const uint64_t extm = valid & ballot(len == kPreExt) & ballot(lim > kPreExt);
       uint64_t chain = 0;
       uint32_t mlen_v = len;
       uint64_t m = valid;
