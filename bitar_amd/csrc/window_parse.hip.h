@@ -79,14 +79,21 @@ __device__ __forceinline__ uint4 ld16u(const GMEM uint8_t* p, const GMEM uint8_t
 
 // number of equal leading bytes of two 16-byte little-endian values (branch-free: all four
 // dwords are compared, so the compiler cannot defer the loads behind data-dependent branches)
+// v_ffbl_b32: index of the lowest set bit, ~0u for 0
+__device__ __forceinline__ uint32_t ffbl(uint32_t d) {
+  uint32_t r;
+  __asm__("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(d));
+  return r;
+}
 __device__ __forceinline__ uint32_t common16(uint4 a, uint4 b) {
   const uint32_t d0 = a.x ^ b.x, d1 = a.y ^ b.y, d2 = a.z ^ b.z, d3 = a.w ^ b.w;
-  uint32_t r = 128;
-  r = d3 ? 96 + __builtin_ctz(d3) : r;
-  r = d2 ? 64 + __builtin_ctz(d2) : r;
-  r = d1 ? 32 + __builtin_ctz(d1) : r;
-  r = d0 ? __builtin_ctz(d0) : r;
-  return r >> 3;
+  // first differing bit = min over dwords of (32 k + ffbl), ~0u (saturating add) for equal
+  // dwords: 4 xor, 4 ffbl, 3 add, 2 min3, 1 shift
+  const uint32_t c0 = ffbl(d0);
+  const uint32_t c1 = __builtin_elementwise_add_sat(ffbl(d1), 32u);
+  const uint32_t c2 = __builtin_elementwise_add_sat(ffbl(d2), 64u);
+  const uint32_t c3 = __builtin_elementwise_add_sat(ffbl(d3), 96u);
+  return min(min(min(c0, c1), min(c2, c3)), 128u) >> 3;
 }
 
 // number of equal leading bytes of two little-endian values
@@ -386,12 +393,14 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
       // (the empty asm pins the read-back's use, and so its wait, here)
       uint32_t bk = back;
       __asm__ volatile("" : "+v"(bk));
-      bool redo = act && bk < p;
-      while (ballot(redo)) {
-        lds_order();
-        if (redo) table[h] = (uint16_t)p;
-        lds_order();
-        redo = redo && table[h] < p;
+      if (ballot(bk < p) & ballot(act)) {  // rare: only on same-slot collisions
+        bool redo = act && bk < p;
+        while (ballot(redo)) {
+          lds_order();
+          if (redo) table[h] = (uint16_t)p;
+          lds_order();
+          redo = redo && table[h] < p;
+        }
       }
     };
     // Row k+1 goes into the ring at x = 1024 k + 512 (the ring then runs 576..1536 B ahead
