@@ -1,18 +1,32 @@
 #!/usr/bin/env python3
 """bench.py -- the driver-facing benchmark of the MI355X segment codec engine.
 
-Workload (BASELINE.json metric "GiB/s compress+decompress on 1-GiB Arrow buffer";
-configs[2]): every rank owns a 1 GiB HBM-resident buffer of the Silesia-style mix
-(kind 1), cut into 64 KiB segments (16384 per GiB).  One step = LZ4 compress
-of the whole buffer into per-segment slots + (N > 1) the RCCL all-gather of the per-segment
-compressed sizes that builds the global frame index + LZ4 decompress of every slot back into
-a 1 GiB output.  value = bytes of uncompressed data round-tripped by all ranks / wall time.
-Beside it: "secondary" (BASELINE configs[1], random bytes, LZ4 decompress only, N = 1),
-"zstd" (BASELINE configs[5], Zstd frames on Arrow record-batch bodies, same sharding and
-all-gather at every N) and "deflate" (the reference's own codec at its 59460-B segments).
+Headline (BASELINE.json metric "GiB/s compress+decompress on 1-GiB Arrow buffer";
+configs[2]): a job of N GiB of the Silesia-style mix (kind 1) cut into 64 KiB
+segments, dealt to the N ranks in round-robin batches of 256 segments (bitar_amd.dist,
+apps/demo_app.cc:249-256), so every GPU holds 1 GiB in HBM (weak scaling).  One step = LZ4
+compress of the rank's segments into per-segment slots + the RCCL all-gather of the
+per-segment compressed sizes and the global frame index + LZ4 decompress of every slot.
+value = uncompressed bytes round-tripped by all ranks / wall time (max over ranks).
 
-Prints ONE JSON line (rank 0).  Launch: python bench.py [--gpus N --steps K --warmup W];
-for N > 1 under torch.distributed.run (one process per GPU, RCCL).
+Beside it, on the same JSON line:
+  recordbatch   BASELINE configs[3]: an 8 GiB Arrow record-batch job (64 KiB chunks), the
+                same round-robin batches, K queue-pair streams per GPU running concurrently
+                (CompressAsync / DecompressAsync, util.h:216-236), RCCL size all-gather;
+                total work fixed (strong scaling), at every N.
+  secondary     BASELINE configs[1]: 1 GiB random bytes, LZ4 decompress only (N = 1).
+  zstd          BASELINE configs[4]: Zstd frames on Arrow record-batch bodies (weak).
+  deflate       the reference's own codec (raw DEFLATE, 59460-B segments; weak).
+  stock_decode  GPU decode of streams the STOCK libraries wrote on the host (liblz4 default,
+                zlib level 1 raw DEFLATE = the reference's codec, libzstd level 1), N = 1.
+  stock_ratio   the stock libraries' ratio on the headline input, beside ours.
+  cpu_baseline  stock liblz4 / zlib-1 on this host's cores, 1 core and all cores, plus
+                BASELINE configs[0] (1 MiB Arrow IPC of a Parquet-like table, 1 core).
+
+Launch: python bench.py [--gpus N --steps K --warmup W].  With --gpus N > 1 and no launcher
+around it, the process starts N rank processes itself (bitar_amd.launch; the parent never
+touches the GPU); under torch.distributed.run the ranks come from the environment.  Rank 0
+prints ONE JSON line.
 """
 import argparse
 import json
@@ -32,74 +46,27 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--bytes", type=int, default=1 << 30, help="bytes per rank")
+    p.add_argument("--bytes", type=int, default=1 << 30, help="headline bytes per rank")
     p.add_argument("--seg", type=int, default=65536)
     p.add_argument("--kind", type=int, default=1, help="0 random, 1 mixed, 2 arrow")
     p.add_argument("--codec", default="lz4", choices=["lz4", "deflate", "zstd"])
+    p.add_argument("--streams", type=int, default=4,
+                   help="queue-pair streams per GPU in the configs[3] record-batch leg")
+    p.add_argument("--record-bytes", type=int, default=8 << 30,
+                   help="total job bytes of the configs[3] record-batch leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=256 << 20)
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the random-data decompress-only line (BASELINE configs[1])")
-    p.add_argument("--no-zstd", action="store_true",
-                   help="skip the Zstd round-trip line (BASELINE configs[5])")
-    p.add_argument("--no-deflate", action="store_true",
-                   help="skip the DEFLATE line (the reference's own codec, 59460-B segments)")
+    p.add_argument("--no-zstd", action="store_true")
+    p.add_argument("--no-deflate", action="store_true")
+    p.add_argument("--no-recordbatch", action="store_true")
+    p.add_argument("--no-stock", action="store_true",
+                   help="skip the stock-stream GPU decode legs")
+    p.add_argument("--only", default=None,
+                   help="comma list of legs to run besides the headline (profiling runs)")
     p.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
     return p.parse_args()
-
-
-def cpu_baseline(args):
-    """The oracle's C LZ4 codec (a port: bitar has no software LZ4 path)
-    timed on this host's cores over a bounded sample of the same workload."""
-    import ctypes
-    import numpy as np
-    sys.path.insert(0, os.path.join(HERE, "tests"))
-    import oracle_lib as O  # cpu_baseline leg only: the oracle is the CPU reference here
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    n = args.cpu_sample
-    seg = args.seg
-    data = O.fill(args.kind, 0, n)
-    stride = O.lz4_bound(seg) + 64
-    nseg = (n + seg - 1) // seg
-    L = O.lib()
-    slab = np.zeros(nseg * stride, np.uint8)
-    sizes = np.zeros(nseg, np.uint32)
-    out = np.zeros(nseg * seg, np.uint8)
-    prod = np.zeros(nseg, np.uint32)
-    nout = ctypes.c_uint32(0)
-    total = ctypes.c_uint64(0)
-
-    def comp():
-        r = L.bo_compress(O.CODEC_LZ4, O._ptr(data), n, seg, O._ptr(slab), stride, O._ptr(sizes),
-                          ctypes.byref(nout), threads)
-        assert r == 0
-
-    ptrs = None
-
-    def decomp():
-        r = L.bo_decompress(O.CODEC_LZ4, O._ptr(ptrs), O._ptr(sizes), nseg, seg, O._ptr(out),
-                            nseg * seg, ctypes.byref(total), O._ptr(prod), threads)
-        assert r == 0
-
-    comp()
-    ptrs = np.array([slab.ctypes.data + i * stride for i in range(nseg)], dtype=np.uint64)
-    decomp()
-    assert np.array_equal(out[:n], data)
-    best_c = best_d = 1e30
-    for _ in range(3):  # best of kNumTests = 3 (reference apps/demo_app.h:45)
-        t0 = time.perf_counter(); comp(); t1 = time.perf_counter(); decomp()
-        t2 = time.perf_counter()
-        best_c, best_d = min(best_c, t1 - t0), min(best_d, t2 - t1)
-    return {
-        "value": round(n / GIB / (best_c + best_d), 4),
-        "unit": "GiB/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{n >> 20} MiB of the same kind-{args.kind} input, {seg}-B segments, "
-                  f"oracle C LZ4 (window-scan parse) compress+decompress, best of 3",
-        "compress_gibs": round(n / GIB / best_c, 4),
-        "decompress_gibs": round(n / GIB / best_d, 4),
-    }
 
 
 KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
@@ -107,96 +74,99 @@ KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
            # defer-only mode; timed together
            "deflate": ("deflate_compress_kernel", "inflate_lanes_kernel"),
            # decompress = zstd_lanes_kernel (lane per segment) + zstd_decompress_kernel in
-           # defer-only mode (an early exit per segment for our frames); timed together
+           # defer-only mode; timed together
            "zstd": ("zstd_compress_kernel", "zstd_lanes_kernel")}
 CODEC_NAMES = {"lz4": "lz4-block", "deflate": "deflate-raw-fixed", "zstd": "zstd-frame"}
 
 
-def roundtrip(eng, ctx, codec_name, kind, n, seg, steps, warmup, seed):
-    """K timed steps of compress (+ RCCL size all-gather + frame index when world > 1) +
-    decompress of an n-byte HBM-resident buffer; returns the rank's timings and sizes."""
+def codec_id(name):
+    import bitar_amd
+    return {"lz4": bitar_amd.CODEC_LZ4, "deflate": bitar_amd.CODEC_DEFLATE,
+            "zstd": bitar_amd.CODEC_ZSTD}[name]
+
+
+def reduce_max_sum(vals_max, vals_sum, world):
+    """MAX over ranks of vals_max, SUM over ranks of vals_sum (float64 lists)."""
+    if world == 1:
+        return list(vals_max), list(vals_sum)
     import torch
     import torch.distributed as dist
-    import bitar_amd
-    from bitar_amd import dist as bd
-    world = ctx["world"]
-    codec = {"lz4": bitar_amd.CODEC_LZ4, "deflate": bitar_amd.CODEC_DEFLATE,
-             "zstd": bitar_amd.CODEC_ZSTD}[codec_name]
-    nseg = (n + seg - 1) // seg
-    stride = bitar_amd.slot_size(codec, seg)
-    data = eng.empty(n)
-    eng.fill(kind, seed, data)  # the rank's shard of the job (weak scaling)
-    slab = eng.empty(nseg * stride)
-    sizes = eng.empty(nseg, dtype=torch.int32)
-    out = eng.empty(nseg * seg)
-    prod = eng.empty(nseg, dtype=torch.int32)
-    all_sizes = eng.empty(nseg * world, dtype=torch.int32) if world > 1 else None
-    index = [None]
-    stream = torch.cuda.current_stream()
-    ev = []  # (compress start, compress end, decompress start, decompress end)
+    dev = torch.cuda.current_device()
+    a = torch.tensor(list(vals_max), dtype=torch.float64, device=f"cuda:{dev}")
+    b = torch.tensor(list(vals_sum), dtype=torch.float64, device=f"cuda:{dev}")
+    dist.all_reduce(a, op=dist.ReduceOp.MAX)
+    dist.all_reduce(b, op=dist.ReduceOp.SUM)
+    return a.tolist(), b.tolist()
+
+
+def run_job(eng, codec_name, kind, job_bytes, seg, nstreams, steps, warmup, world, rank,
+            seed=0):
+    """K timed steps of a sharded job (bitar_amd.job.ShardedJob): compress on every part's
+    stream, RCCL size all-gather + global frame index, decompress.  Returns the timings
+    (max over ranks), the byte-equality verdict (all ranks) and the job's sizes."""
+    import torch
+    import torch.distributed as dist
+    from bitar_amd.job import ShardedJob
+    job = ShardedJob(eng, codec_id(codec_name), job_bytes, seg, world, rank, nstreams)
+    job.generate(kind, seed)
+    dev = eng.device
+    ev = []  # per step: {part stream: (c0, c1)}, {part stream: (d0, d1)}
 
     def step(timed):
         if timed:
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-            e[0].record(stream)
-        eng.compress_into(codec, data, seg, slab, stride, sizes, n=n)
-        if timed:
-            e[1].record(stream)
-        if world > 1:  # global frame index: per-segment sizes of every rank (SURVEY.md §8e)
-            dist.all_gather_into_tensor(all_sizes, sizes)
-            index[0] = bd.frame_index(all_sizes)  # rank-major = global segment order
-        if timed:
-            e[2].record(stream)
-        eng.decompress_slab_into(codec, slab, stride, sizes, nseg, seg, out, prod,
-                                 capacity=nseg * seg)
-        if timed:
-            e[3].record(stream)
-            ev.append(e)
+            ce = {p.stream: (torch.cuda.Event(enable_timing=True),
+                             torch.cuda.Event(enable_timing=True)) for p in job.layout.parts}
+            de = {p.stream: (torch.cuda.Event(enable_timing=True),
+                             torch.cuda.Event(enable_timing=True)) for p in job.layout.parts}
+            ev.append((ce, de))
+        else:
+            ce = de = None
+        job.compress(ce)
+        job.gather_index()
+        job.decompress(de)
 
     for _ in range(warmup):
         step(False)
-    eng.sync()
+    job.sync()
+    torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         step(True)
-    torch.cuda.synchronize()
+    torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    eng.sync()  # raises if any segment op failed
-
-    # correctness of the timed output (byte equality of the round trip, demo_app.cc:534-543)
-    ok = bool(torch.equal(out[:n], data)) and int(prod.to(torch.int64).sum().item()) == n
-    csize = int(sizes.to(torch.int64).sum().item())
-    if world > 1:
-        dev = torch.cuda.current_device()
-        t = torch.tensor([elapsed, 0.0 if ok else 1.0, float(csize)], device=f"cuda:{dev}",
-                         dtype=torch.float64)
-        mx = t.clone()
-        dist.all_reduce(mx[:2], op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm[2:], op=dist.ReduceOp.SUM)
-        elapsed = float(mx[0].item())
-        ok = mx[1].item() == 0.0
-        csize_total = int(sm[2].item())
-        # the frame index every rank built from the all-gathered sizes spans the whole job
-        ok = ok and int(index[0][-1].item()) == csize_total
-    t_comp = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev) / 1e3  # seconds
-    t_dec = sum(e[2].elapsed_time(e[3]) for e in ev) / len(ev) / 1e3
-    del data, slab, out
-    torch.cuda.empty_cache()
-    return {"elapsed": elapsed, "ok": ok, "csize": csize, "t_comp": t_comp, "t_dec": t_dec,
-            "nseg": nseg}
+    job.sync()  # raises if any segment op failed
+    ok = job.verify()
+    csize = job.local_compressed_bytes()
+    ok = ok and int(job.index[-1].item()) >= csize  # the global index spans the job
+    # per-launch durations (each event pair brackets exactly one kernel launch)
+    comp_ms = [c0.elapsed_time(c1) for ce, _ in ev for c0, c1 in ce.values()]
+    dec_ms = [d0.elapsed_time(d1) for _, de in ev for d0, d1 in de.values()]
+    local = {"nbytes": job.layout.local_bytes, "nseg": job.layout.local_nseg,
+             "parts": len(job.layout.parts)}
+    total_c = int(job.index[-1].item())
+    job.free()
+    (elapsed, bad), (csum,) = reduce_max_sum([elapsed, 0.0 if ok else 1.0], [float(csize)], world)
+    return {"elapsed": elapsed, "ok": bad == 0.0, "csize_local": csize, "csize_total": total_c,
+            "t_comp": sum(comp_ms) / len(comp_ms) / 1e3, "t_dec": sum(dec_ms) / len(dec_ms) / 1e3,
+            "local": local, "job_bytes": job_bytes}
 
 
-def kernel_lines(codec_name, r, n, traffic_json):
-    """roofline of the dominant kernel + per-kernel averages (HIP events on the launch stream)."""
-    U, C = float(n), float(r["csize"])
-    comp_bytes = U + C + 4.0 * r["nseg"]   # algorithmic bytes of one compress launch
-    dec_bytes = U + C                      # algorithmic bytes of one decompress launch
+def kernel_lines(codec_name, r, traffic_json):
+    """roofline of the dominant kernel + per-kernel averages.  Durations are HIP events
+    bracketing each launch on its own stream; algorithmic bytes per launch =
+    U + C (+ 4 B per segment for compress) of the part that launch covered."""
+    parts = r["local"]["parts"]
+    U = float(r["local"]["nbytes"]) / parts
+    C = float(r["csize_local"]) / parts
+    nseg = float(r["local"]["nseg"]) / parts
+    comp_bytes = U + C + 4.0 * nseg
+    dec_bytes = U + C
     kc, kd = KERNELS[codec_name]
     t_comp, t_dec = r["t_comp"], r["t_dec"]
     dominant = (kc, comp_bytes, t_comp) if t_comp >= t_dec else (kd, dec_bytes, t_dec)
@@ -216,109 +186,20 @@ def kernel_lines(codec_name, r, n, traffic_json):
     return roof, kernels
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-    import bitar_amd
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
-    eng = bitar_amd.Engine(dev)
-    ctx = {"world": world, "rank": rank}
-    n, seg = args.bytes, args.seg
-    r = roundtrip(eng, ctx, args.codec, args.kind, n, seg, args.steps, args.warmup, rank)
-    zs = None
-    if args.codec != "zstd" and not args.no_zstd:
-        # BASELINE configs[5]: Zstd level-1-class frames on Parquet-column-like buffers
-        # (kind 2, Arrow record-batch bodies), same sharding and all-gather, every rank
-        zs = roundtrip(eng, ctx, "zstd", 2, n, seg, args.steps, args.warmup, rank + 1000)
-    df = None
-    if args.codec != "deflate" and not args.no_deflate:
-        # the reference's own segment codec (RTE_COMP_ALGO_DEFLATE, config.cc:83-105) at its
-        # default segment size (59460 B, app_common.h:39), same input as the headline
-        df = roundtrip(eng, ctx, "deflate", args.kind, n, 59460, args.steps, args.warmup,
-                       rank + 2000)
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
-
-    U = float(n)
-    C = float(r["csize"])
-    value = world * U * args.steps / r["elapsed"] / GIB
-    roof, kernels = kernel_lines(args.codec, r, n, args.traffic_json)
-    std = args.kind == 1 and args.codec == "lz4"
-    res = {
-        "metric": "GiB/s compress+decompress on 1-GiB Arrow buffer, 1/2/4/8 GPUs; % HBM roofline",
-        "value": round(value, 3),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (deterministic SplitMix64 generator, generated in HBM)",
-        "config": {"workload": "LZ4 block compress + decompress round trip, 1 GiB per GPU, "
-                               "64 KiB segments, Silesia-style mix (BASELINE configs[2])"
-                               if std else f"{args.codec} round trip, kind {args.kind}, seg {seg}",
-                   "bytes_per_gpu": n, "segment_bytes": seg, "segments_per_gpu": r["nseg"],
-                   "codec": CODEC_NAMES[args.codec],
-                   "input_kind": args.kind,
-                   "parallelism": f"{world} independent shards (round-robin segments), "
-                                  "RCCL all-gather of sizes" if world > 1 else "1 GPU"},
-        "compression_ratio": round(U / C, 4),
-        "compress_gibs": round(U / r["t_comp"] / GIB, 3),
-        "decompress_gibs": round(U / r["t_dec"] / GIB, 3),
-        "roundtrip_ok": r["ok"],
-        "roofline": roof,
-        "kernels": kernels,
-    }
-    if world == 1 and args.codec == "lz4" and not args.no_secondary:
-        # BASELINE configs[1]: 1-GiB random-byte buffer, LZ4 decompress only (the HBM-bound
-        # case of the same kernel), reported beside the headline round trip
-        res["secondary"] = random_decompress(eng, n, seg, args)
-    if zs is not None:
-        zroof, zkern = kernel_lines("zstd", zs, n, args.traffic_json)
-        res["zstd"] = {
-            "workload": "BASELINE configs[5]: Zstd frame per 64 KiB segment (raw literals, "
-                        "predefined FSE sequences), compress + RCCL size all-gather + "
-                        "decompress, 1 GiB Arrow record-batch buffer per GPU",
-            "value": round(world * U * args.steps / zs["elapsed"] / GIB, 3), "unit": "GiB/s",
-            "ms_per_step": round(zs["elapsed"] / args.steps * 1e3, 4),
-            "compression_ratio": round(U / zs["csize"], 4),
-            "compress_gibs": round(U / zs["t_comp"] / GIB, 3),
-            "decompress_gibs": round(U / zs["t_dec"] / GIB, 3),
-            "roundtrip_ok": zs["ok"], "roofline": zroof, "kernels": zkern}
-    if df is not None:
-        droof, dkern = kernel_lines("deflate", df, n, args.traffic_json)
-        res["deflate"] = {
-            "workload": "the reference's codec: raw DEFLATE (fixed-Huffman blocks) per 59460-B "
-                        "segment, compress + decompress, same input and sharding as the headline",
-            "value": round(world * U * args.steps / df["elapsed"] / GIB, 3), "unit": "GiB/s",
-            "ms_per_step": round(df["elapsed"] / args.steps * 1e3, 4),
-            "compression_ratio": round(U / df["csize"], 4),
-            "compress_gibs": round(U / df["t_comp"] / GIB, 3),
-            "decompress_gibs": round(U / df["t_dec"] / GIB, 3),
-            "roundtrip_ok": df["ok"], "roofline": droof, "kernels": dkern}
-    if not args.no_cpu_baseline and world == 1 and args.codec == "lz4":
-        res["cpu_baseline"] = cpu_baseline(args)
-    print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+def leg_summary(name, r, world, steps, traffic_json, workload):
+    roof, kern = kernel_lines(name, r, traffic_json)
+    U = float(r["job_bytes"])
+    return {"workload": workload,
+            "value": round(U * steps / r["elapsed"] / GIB, 3), "unit": "GiB/s",
+            "ms_per_step": round(r["elapsed"] / steps * 1e3, 4),
+            "compression_ratio": round(U / r["csize_total"], 4) if r["csize_total"] else None,
+            "compress_gibs_per_launch": round(r["local"]["nbytes"] / r["local"]["parts"] / r["t_comp"] / GIB, 3),
+            "decompress_gibs_per_launch": round(r["local"]["nbytes"] / r["local"]["parts"] / r["t_dec"] / GIB, 3),
+            "roundtrip_ok": r["ok"], "roofline": roof, "kernels": kern}
 
 
 def random_decompress(eng, n, seg, args):
+    """BASELINE configs[1]: 1 GiB random bytes, LZ4 decompress only."""
     import torch
     import bitar_amd
     codec = bitar_amd.CODEC_LZ4
@@ -348,14 +229,306 @@ def random_decompress(eng, n, seg, args):
     ok2 = bool(torch.equal(out[:n], data))
     t2 = sum(a.elapsed_time(b) for a, b in evs) / len(evs) / 1e3
     alg2 = (float(n) + c_rand) / t2 / 1e9
+    del data, slab, out
+    torch.cuda.empty_cache()
     return {
         "workload": "BASELINE configs[1]: 1 GiB random bytes, LZ4 block decompress only, "
                     "64 KiB segments, HBM-resident",
         "decompress_gibs": round(n / t2 / GIB, 3), "avg_launch_ms": round(t2 * 1e3, 4),
-        "roofline": {"bound": "hbm", "achieved": round(alg2, 2), "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "lz4_decompress_kernel",
+                     "achieved": round(alg2, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg2 / HBM_PEAK_GBS, 4),
                      "algorithmic_bytes_per_launch": float(n) + c_rand},
         "roundtrip_ok": ok2}
+
+
+def host_threads():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        return os.cpu_count() or 1
+
+
+def stock_decode(eng, args):
+    """GPU decode of streams the stock libraries produced on the host from the same input
+    (compressed and uploaded outside the timed region; the decode is timed with HIP events
+    and checked byte for byte).  Also yields the stock ratios of the headline input."""
+    import numpy as np
+    import torch
+    import bitar_amd
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import stock_lib as S  # stock third-party codecs (baseline infrastructure)
+    n = args.bytes
+    th = max(1, min(64, host_threads()))
+    legs = (("lz4", S.LZ4, 1, 65536, args.kind, "liblz4 1.9.3 LZ4_compress_default"),
+            ("deflate", S.DEFLATE, 1, 59460, args.kind,
+             "zlib 1.2.11 raw DEFLATE level 1 (dynamic Huffman), the reference's codec "
+             "(config.cc:83-105) at its 59460-B segments (app_common.h:39)"),
+            ("zstd", S.ZSTD, 1, 65536, 2, "libzstd level 1 (Huffman literals, FSE tables)"))
+    res, ratios = {}, {}
+    for name, sc, level, seg, kind, desc in legs:
+        data = eng.empty(n)
+        eng.fill(kind, 0, data)
+        host = data.cpu().numpy()
+        slab_h, stride, sizes_h = S.compress(sc, host, seg, level, th)
+        nseg = sizes_h.size
+        C = float(sizes_h.astype(np.int64).sum())
+        ratios[name] = round(n / C, 4)
+        slab = torch.from_numpy(slab_h).to(f"cuda:{eng.device}")
+        sizes = torch.from_numpy(sizes_h.view(np.int32)).to(f"cuda:{eng.device}")
+        del slab_h, host
+        out = eng.empty(nseg * seg)
+        prod = eng.empty(nseg, dtype=torch.int32)
+        stream = torch.cuda.current_stream()
+        codec = codec_id(name)
+        evs = []
+        for i in range(args.warmup + args.steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            eng.decompress_slab_into(codec, slab, stride, sizes, nseg, seg, out, prod,
+                                     capacity=nseg * seg)
+            e1.record(stream)
+            if i >= args.warmup:
+                evs.append((e0, e1))
+        torch.cuda.synchronize()
+        eng.sync()
+        ok = bool(torch.equal(out[:n], data)) and int(prod.to(torch.int64).sum().item()) == n
+        t = sum(a.elapsed_time(b) for a, b in evs) / len(evs) / 1e3
+        alg = (n + C) / t / 1e9
+        res[name] = {"stream": desc, "input_kind": kind, "segment_bytes": seg,
+                     "stock_ratio": ratios[name], "decompress_gibs": round(n / t / GIB, 3),
+                     "avg_launch_ms": round(t * 1e3, 4),
+                     "roofline": {"bound": "hbm", "achieved": round(alg, 2),
+                                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(alg / HBM_PEAK_GBS, 4),
+                                  "algorithmic_bytes_per_launch": n + C},
+                     "roundtrip_ok": ok}
+        del data, slab, sizes, out, prod
+        torch.cuda.empty_cache()
+    return res, ratios
+
+
+def ipc_sample(nbytes):
+    """BASELINE configs[0]'s input: the first nbytes of an Arrow IPC stream of a synthetic
+    Parquet-like table (seed 42: int64 uniform [0,1000), float64 N(0,1), dictionary
+    strings), as demo_app's ReadTableBytes serializes a table (demo_app.cc:195-204)."""
+    import numpy as np
+    try:
+        import pyarrow as pa
+    except ImportError:  # pragma: no cover - pyarrow is in this image
+        return None
+    rng = np.random.default_rng(42)
+    rows = max(1, nbytes // 12)
+    words = np.array([f"value_{i:04d}" for i in range(500)])
+    t = pa.table({"i": pa.array(rng.integers(0, 1000, rows, dtype=np.int64)),
+                  "f": pa.array(rng.standard_normal(rows)),
+                  "s": pa.DictionaryArray.from_arrays(
+                      pa.array(rng.integers(0, 500, rows).astype(np.int32)),
+                      pa.array(words))})
+    sink = pa.BufferOutputStream()
+    with pa.ipc.new_stream(sink, t.schema) as w:
+        w.write_table(t)
+    buf = np.frombuffer(sink.getvalue(), np.uint8)
+    return buf[:nbytes].copy()
+
+
+def cpu_baseline(args):
+    """The stock libraries on this host's cores over a bounded sample of the same workload:
+    liblz4 (north-star codec, 64 KiB segments) and zlib level-1 raw DEFLATE (the reference's
+    codec at 59460-B segments), 1 core and every core of this process's CPU set, best of
+    kNumTests = 3 (apps/demo_app.h:45); plus BASELINE configs[0] on 1 core."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import oracle_lib as O  # the generator of the same input (baseline leg only)
+    import stock_lib as S
+    nall = host_threads()
+    n = args.cpu_sample
+    data = O.fill(args.kind, 0, n)
+
+    def timed(sc, seg, level, sample, threads, reps=3):
+        d = data[:sample]
+        slab, stride, sizes = S.compress(sc, d, seg, level, threads)  # warm-up (+ pages)
+        out = S.decompress(sc, slab, stride, sizes, sample, seg, threads)
+        assert np.array_equal(out, d)
+        bc = bd = 1e30
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            S.compress(sc, d, seg, level, threads, stride=stride)
+            t1 = time.perf_counter()
+            S.decompress(sc, slab, stride, sizes, sample, seg, threads, out=out)
+            t2 = time.perf_counter()
+            bc, bd = min(bc, t1 - t0), min(bd, t2 - t1)
+        return {"roundtrip_gibs": round(sample / GIB / (bc + bd), 4),
+                "compress_gibs": round(sample / GIB / bc, 4),
+                "decompress_gibs": round(sample / GIB / bd, 4),
+                "ratio": round(sample / float(sizes.astype(np.int64).sum()), 4),
+                "sample_bytes": sample, "threads": threads}
+
+    lz4_all = timed(S.LZ4, 65536, 1, n, nall)
+    lz4_one = timed(S.LZ4, 65536, 1, min(n, 64 << 20), 1)
+    # zlib-1 compresses ~0.1 GiB/s per core: smaller samples keep this leg ~10 s
+    z_all = timed(S.DEFLATE, 59460, 1, min(n, max(16 << 20, nall * (8 << 20))), nall)
+    z_one = timed(S.DEFLATE, 59460, 1, 16 << 20, 1)
+    cfg0 = None
+    ipc = ipc_sample(1 << 20)
+    if ipc is not None:
+        c0 = {}
+        for name, sc, seg in (("deflate_raw_l1_59460", S.DEFLATE, 59460),
+                              ("lz4_64k", S.LZ4, 65536)):
+            slab, stride, sizes = S.compress(sc, ipc, seg, 1, 1)
+            out = S.decompress(sc, slab, stride, sizes, ipc.size, seg, 1)
+            assert np.array_equal(out, ipc)
+            reps = 20
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                S.compress(sc, ipc, seg, 1, 1, stride=stride)
+            t1 = time.perf_counter()
+            for _ in range(reps):
+                S.decompress(sc, slab, stride, sizes, ipc.size, seg, 1, out=out)
+            t2 = time.perf_counter()
+            tc, td = (t1 - t0) / reps, (t2 - t1) / reps
+            c0[name] = {"compress_gibs": round(ipc.size / GIB / tc, 4),
+                        "decompress_gibs": round(ipc.size / GIB / td, 4),
+                        "roundtrip_gibs": round(ipc.size / GIB / (tc + td), 4),
+                        "ratio": round(ipc.size / float(sizes.astype(np.int64).sum()), 4),
+                        "segments": int(sizes.size)}
+        cfg0 = {"workload": "BASELINE configs[0]: 1 MiB Arrow IPC stream of a Parquet-like "
+                            "table (seed 42), 1 host core", **c0}
+    return {
+        "value": lz4_all["roundtrip_gibs"],
+        "unit": "GiB/s",
+        "cores": nall,
+        "kind": "port",
+        "sample": f"{n >> 20} MiB of the same kind-{args.kind} input, 65536-B segments, stock "
+                  f"liblz4 1.9.3 (LZ4_compress_default + LZ4_decompress_safe) on {nall} "
+                  f"threads (one per core of this process's CPU set; os.cpu_count() = "
+                  f"{os.cpu_count()}), best of 3 -- the reference has no software LZ4 path, "
+                  f"so the stock library stands in for it",
+        "lz4": {"all_cores": lz4_all, "one_core": lz4_one},
+        "deflate_zlib1": {"all_cores": z_all, "one_core": z_one,
+                          "note": "the reference's codec in software: zlib 1.2.11 raw DEFLATE "
+                                  "level 1, 59460-B segments"},
+        "configs0": cfg0,
+        "os_cpu_count": os.cpu_count(),
+    }
+
+
+def want(args, leg):
+    if args.only is None:
+        return True
+    return leg in args.only.split(",")
+
+
+def main():
+    args = parse()
+    from bitar_amd import launch
+    if args.gpus > 1 and not launch.is_rank_process():
+        # one process per GPU, started from this parent (which never touches the GPU)
+        sys.exit(launch.spawn(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    import torch
+    import torch.distributed as dist
+    import bitar_amd
+
+    world, rank, local = launch.rank_env()
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+    eng = bitar_amd.Engine(dev, num_streams=max(1, args.streams))
+    n, seg = args.bytes, args.seg
+    r = run_job(eng, args.codec, args.kind, world * n, seg, 1, args.steps, args.warmup, world,
+                rank)
+    rb = zs = df = None
+    if not args.no_recordbatch and want(args, "recordbatch"):
+        rb = run_job(eng, "lz4", 2, args.record_bytes, 65536, max(1, args.streams),
+                     args.steps, args.warmup, world, rank, seed=3)
+    if args.codec != "zstd" and not args.no_zstd and want(args, "zstd"):
+        zs = run_job(eng, "zstd", 2, world * n, seg, 1, args.steps, args.warmup, world, rank,
+                     seed=1000)
+    if args.codec != "deflate" and not args.no_deflate and want(args, "deflate"):
+        df = run_job(eng, "deflate", args.kind, world * n, 59460, 1, args.steps, args.warmup,
+                     world, rank, seed=2000)
+    sec = stock = None
+    if world == 1 and args.codec == "lz4":
+        if not args.no_secondary and want(args, "secondary"):
+            sec = random_decompress(eng, n, seg, args)
+        if not args.no_stock and want(args, "stock"):
+            stock = stock_decode(eng, args)
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    U = float(world * n)
+    value = U * args.steps / r["elapsed"] / GIB
+    roof, kernels = kernel_lines(args.codec, r, args.traffic_json)
+    std = args.kind == 1 and args.codec == "lz4"
+    res = {
+        "metric": "GiB/s compress+decompress on 1-GiB Arrow buffer, 1/2/4/8 GPUs; % HBM roofline",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (deterministic SplitMix64 generator, generated in HBM)",
+        "config": {"workload": "LZ4 block compress + decompress round trip, 1 GiB per GPU, "
+                               "64 KiB segments, Silesia-style mix (BASELINE configs[2])"
+                               if std else f"{args.codec} round trip, kind {args.kind}, seg {seg}",
+                   "bytes_per_gpu": n, "segment_bytes": seg,
+                   "segments_per_gpu": r["local"]["nseg"],
+                   "codec": CODEC_NAMES[args.codec],
+                   "input_kind": args.kind,
+                   "parallelism": (f"{world} ranks, round-robin batches of 256 segments, "
+                                   "RCCL all-gather of sizes") if world > 1 else "1 GPU"},
+        "compression_ratio": round(U / r["csize_total"], 4),
+        "compress_gibs": round(r["local"]["nbytes"] / r["t_comp"] / GIB, 3),
+        "decompress_gibs": round(r["local"]["nbytes"] / r["t_dec"] / GIB, 3),
+        "roundtrip_ok": r["ok"],
+        "roofline": roof,
+        "kernels": kernels,
+    }
+    if stock is not None:
+        res["stock_ratio"] = {
+            "ours_lz4": res["compression_ratio"] if std else None,
+            "liblz4_default": stock[1]["lz4"],
+            "zlib1_raw_deflate_59460": stock[1]["deflate"],
+            "libzstd1_on_arrow_kind2": stock[1]["zstd"]}
+    if rb is not None:
+        s = leg_summary("lz4", rb, world, args.steps, args.traffic_json,
+                        f"BASELINE configs[3]: {args.record_bytes >> 30} GiB Arrow record-batch "
+                        f"job, 64 KiB chunks, round-robin batches of 256 chunks over {world} "
+                        f"GPU(s), {args.streams} concurrent queue-pair streams per GPU, LZ4 "
+                        f"compress + RCCL size all-gather + decompress (total work fixed)")
+        s["scaling"] = "strong"
+        s["streams_per_gpu"] = args.streams
+        res["recordbatch"] = s
+    if sec is not None:
+        res["secondary"] = sec
+    if zs is not None:
+        res["zstd"] = leg_summary(
+            "zstd", zs, world, args.steps, args.traffic_json,
+            "BASELINE configs[4] codec: Zstd frame per 64 KiB segment (raw literals, "
+            "predefined FSE sequences), compress + decompress, 1 GiB Arrow record-batch "
+            "buffer per GPU" + (", RCCL size all-gather" if world > 1 else ""))
+    if df is not None:
+        res["deflate"] = leg_summary(
+            "deflate", df, world, args.steps, args.traffic_json,
+            "the reference's codec: raw DEFLATE (fixed-Huffman blocks) per 59460-B segment, "
+            "compress + decompress, same input and sharding as the headline")
+    if stock is not None:
+        res["stock_decode"] = stock[0]
+    if not args.no_cpu_baseline and world == 1 and args.codec == "lz4" and args.only is None:
+        res["cpu_baseline"] = cpu_baseline(args)
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -69,6 +69,7 @@ def lib():
         "bitar_hip_sync": (i32, [vp, vp]),
         "bitar_hip_pack": (i32, [vp, vp, vp, u64, vp, u32, vp, vp]),
         "bitar_hip_fill": (i32, [vp, vp, i32, u64, vp, u64]),
+        "bitar_hip_fill_at": (i32, [vp, vp, i32, u64, u64, vp, u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -85,7 +86,8 @@ ABI_SYMBOLS = ("bitar_hip_abi_version", "bitar_hip_last_error", "bitar_hip_devic
                "bitar_hip_host_alloc", "bitar_hip_host_free", "bitar_hip_memcpy",
                "bitar_hip_compress", "bitar_hip_compress_scattered", "bitar_hip_pointer_info",
                "bitar_hip_decompress", "bitar_hip_decompress_slab",
-               "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_pack_lz4f", "bitar_hip_fill")
+               "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_pack_lz4f", "bitar_hip_fill",
+               "bitar_hip_fill_at")
 
 
 def check(rc):
@@ -184,9 +186,11 @@ class Engine:
         check(lib().bitar_hip_pack(self.ctx, self._stream(stream), _ptr(slab), stride,
                                    _ptr(sizes), nseg, _ptr(offsets), _ptr(frame)))
 
-    def fill(self, kind, seed, out, n=None, stream=None):
+    def fill(self, kind, seed, out, n=None, stream=None, offset=0):
+        """bytes [offset, offset + n) of the synthetic stream `kind` into `out`."""
         n = out.numel() if n is None else n
-        check(lib().bitar_hip_fill(self.ctx, self._stream(stream), kind, seed, _ptr(out), n))
+        check(lib().bitar_hip_fill_at(self.ctx, self._stream(stream), kind, seed, offset,
+                                      _ptr(out), n))
 
     def sync(self, stream=None):
         s = self._stream(stream) if stream is not False else None

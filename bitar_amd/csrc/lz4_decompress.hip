@@ -30,6 +30,14 @@ using namespace sr;
 constexpr uint32_t kBatchIn = 132;
 // output bytes one batch may produce (one per lane)
 constexpr uint32_t kBatchOut = kWave;
+// Largest next-token lane of an ELIGIBLE token (colen <= 64, minmatch 4): lane 63 + token +
+// 2 offset bytes + a literal-length byte + max(60 literals with no match-length byte,
+// 45 literals + a match-length byte, since an extended match is >= 19 bytes).  The walk
+// record keeps it in 7 bits; widening eligibility must keep this <= 127.
+constexpr uint32_t kMaxEligibleNext =
+    (kWave - 1) + 3 + 1 + ((kBatchOut - 4) > (kBatchOut - 19) + 1 ? (kBatchOut - 4)
+                                                                    : (kBatchOut - 19) + 1);
+static_assert(kMaxEligibleNext <= 127, "next-token lane overflows the walk record's 7 bits");
 
 // 256 stream bytes held in ONE register, dword-packed: lane l holds bytes vb+4l .. vb+4l+3
 // (vb 4-byte aligned in absolute address terms).  The parse reads tokens, extensions and
@@ -198,9 +206,11 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       // real offset, near, and (conservatively, as if this token opened the batch) not
       // before the segment start
       const bool csimple = (!lx || b1 < 255u) && (!mx || b2 < 255u) && colen <= 64u && coff != 0 && coff <= kNearOff && coff <= s.op + cL;
-      // walk record: next token lane (7 bits, <= 99; the walk stops at a lane >= 64, which
-      // was not parsed, after consuming the sequence) | output length (255: not eligible,
-      // the walk's one compare then stops).  Sequence record: offset (12 bits; eligible
+      // walk record: next token lane (7 bits, <= 127 for an eligible token, see
+      // kMaxEligibleNext; the walk stops at a lane >= 64, which was not parsed, after
+      // consuming the sequence) | output length (255: not eligible, the walk's one compare
+      // then stops; an ineligible token's wider nxt only ORs into those already-set bits).
+      // Sequence record: offset (12 bits; eligible
       // offsets are <= kNearOff, and never 0) | literal count (6 bits) | token lane (6 bits)
       // -- the output start goes into bits 24..29 after the walk.
       const uint32_t nxt = lane + 3 + (lx ? 1u : 0u) + (mx ? 1u : 0u) + cL;

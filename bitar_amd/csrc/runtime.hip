@@ -37,19 +37,28 @@ __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, ui
 template <uint32_t L>
 __global__ void zstd_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                   const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
-__global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t*);
+__global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t, uint64_t*, uint32_t*);
 __global__ void pack_kernel(const uint8_t*, uint64_t, const uint32_t*, const uint64_t*, uint32_t,
                             uint8_t*);
-__global__ void fill_kernel(int, uint64_t, uint8_t*, uint64_t);
+__global__ void fill_kernel(int, uint64_t, uint64_t, uint8_t*, uint64_t);
 __global__ void lz4f_sizes_kernel(const uint32_t*, uint32_t, uint64_t, uint32_t, uint32_t*);
 __global__ void lz4f_pack_kernel(const uint8_t*, uint64_t, uint32_t, const uint8_t*, uint64_t,
                                  const uint32_t*, const uint64_t*, uint32_t, uint8_t*);
 }  // namespace bitar_hip
 
+// Error words: one sticky uint32 per stream (bit0 decode error, bit1 slot overflow, bit2 a
+// failed segment handed to pack).  Word 0 serves the NULL stream, word q+1 queue pair q, and
+// further words are handed out on first use to foreign streams (e.g. torch's current
+// stream), so a failure on one queue pair is never reported by -- or cleared by -- another
+// (the reference reports errors per queue pair: device.cc:84-110, 512-520).
+constexpr uint32_t kErrWords = 1024;
+
 struct bitar_hip_ctx {
   int device = -1;
   std::vector<hipStream_t> streams;
-  uint32_t* d_err = nullptr;  // sticky error word (bit0 decode error, bit1 slot overflow)
+  uint32_t* d_err = nullptr;  // kErrWords words
+  std::mutex mu;              // guards `words`
+  std::vector<std::pair<hipStream_t, uint32_t>> words;  // stream -> error word index
 };
 
 namespace {
@@ -85,6 +94,32 @@ hipStream_t pick_stream(bitar_hip_ctx*, void* stream) {
 }
 
 constexpr uint32_t kMaxSeg = BITAR_HIP_MAX_SEG_SIZE;
+
+// index of the error word of `stream`; words run out only after 1000+ distinct foreign
+// streams, after which they share the NULL stream's word (still correct, merely coarser)
+uint32_t word_index(bitar_hip_ctx* ctx, hipStream_t stream) {
+  if (!stream) return 0;
+  for (uint32_t q = 0; q < ctx->streams.size(); ++q)
+    if (ctx->streams[q] == stream) return q + 1;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  for (auto& w : ctx->words)
+    if (w.first == stream) return w.second;
+  const uint32_t next = (uint32_t)(ctx->streams.size() + 1 + ctx->words.size());
+  if (next >= kErrWords) return 0;
+  ctx->words.emplace_back(stream, next);
+  return next;
+}
+
+uint32_t* err_word(bitar_hip_ctx* ctx, hipStream_t stream) {
+  return ctx->d_err + word_index(ctx, stream);
+}
+
+int sync_error(uint32_t err) {
+  if (!err) return 0;
+  if (err & 2u) return fail(BITAR_HIP_IO_ERROR, "Compress data output is larger than allocated buffer");
+  if (err & 4u) return fail(BITAR_HIP_IO_ERROR, "pack: a segment's size exceeds its slot (failed op)");
+  return fail(BITAR_HIP_IO_ERROR, "Some operations have failed");
+}
 
 }  // namespace
 
@@ -137,8 +172,8 @@ int bitar_hip_open(int device, const bitar_hip_config* cfg, bitar_hip_ctx** out)
     }
     ctx->streams.push_back(s);
   }
-  hipError_t e = hipMalloc(&ctx->d_err, 256);
-  if (e == hipSuccess) e = hipMemset(ctx->d_err, 0, 256);
+  hipError_t e = hipMalloc(&ctx->d_err, kErrWords * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(ctx->d_err, 0, kErrWords * sizeof(uint32_t));
   if (e != hipSuccess) {
     bitar_hip_close(ctx);
     return hip_fail(e, "error word");
@@ -243,13 +278,13 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
   auto* dsts = reinterpret_cast<uint8_t* const*>(d_dsts);
   if (codec == BITAR_HIP_CODEC_LZ4)
     hipLaunchKernelGGL(bitar_hip::lz4_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
-                       n, seg, slab, slot_stride, dsts, d_sizes, ctx->d_err);
+                       n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
   else if (codec == BITAR_HIP_CODEC_DEFLATE)
     hipLaunchKernelGGL(bitar_hip::deflate_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
-                       in, n, seg, slab, slot_stride, dsts, d_sizes, ctx->d_err);
+                       in, n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
   else
     hipLaunchKernelGGL(bitar_hip::zstd_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
-                       n, seg, slab, slot_stride, dsts, d_sizes, ctx->d_err);
+                       n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
   HIP_TRY(hipGetLastError(), "compress launch");
   return 0;
 }
@@ -342,7 +377,7 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
   auto* out = static_cast<uint8_t*>(d_out);
   if (codec == BITAR_HIP_CODEC_LZ4)
     hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
-                       stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err);
+                       stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s));
   else if (codec == BITAR_HIP_CODEC_DEFLATE) {
     // lane-per-segment decoder for stored / fixed-Huffman streams first; the wave decoder
     // then takes the segments it deferred (inflate_lanes.hip)
@@ -357,7 +392,7 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            stride, d_sizes, nseg, seg, out, d_produced);
     }
     hipLaunchKernelGGL(bitar_hip::inflate_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
-                       stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err, L ? 1u : 0u);
+                       stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s), L ? 1u : 0u);
   }
   else {
     // lane-per-segment decoder first; the wave-per-segment decoder then takes the segments it
@@ -379,7 +414,7 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            stride, d_sizes, nseg, seg, out, d_produced);
     }
     hipLaunchKernelGGL(bitar_hip::zstd_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs,
-                       slab, stride, d_sizes, nseg, seg, out, d_produced, ctx->d_err,
+                       slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
                        L ? 1u : 0u);
   }
   HIP_TRY(hipGetLastError(), "decompress launch");
@@ -405,30 +440,42 @@ int bitar_hip_decompress_slab(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
 
 int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream) {
   if (int r = enter(ctx)) return r;
-  HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)), "hipStreamSynchronize");
-  if (!stream)
-    for (auto s : ctx->streams) HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
-  uint32_t err = 0;
-  HIP_TRY(hipMemcpy(&err, ctx->d_err, sizeof(err), hipMemcpyDeviceToHost), "read error word");
-  if (err) {
-    HIP_TRY(hipMemset(ctx->d_err, 0, sizeof(err)), "clear error word");
-    if (err & 2u)
-      return fail(BITAR_HIP_IO_ERROR, "Compress data output is larger than allocated buffer");
-    return fail(BITAR_HIP_IO_ERROR, "Some operations have failed");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (s) {
+    // this stream's word only: read and clear it in stream order, so work queued on other
+    // streams (other queue pairs) can neither be reported here nor lose its error
+    uint32_t* w = err_word(ctx, s);
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, w, sizeof(err), hipMemcpyDeviceToHost, s), "read error word");
+    HIP_TRY(hipMemsetAsync(w, 0, sizeof(err), s), "clear error word");
+    HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+    return sync_error(err);
   }
-  return 0;
+  // NULL: all work on the device (default, queue-pair and foreign streams); every word
+  HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  std::vector<uint32_t> words(kErrWords);
+  HIP_TRY(hipMemcpy(words.data(), ctx->d_err, kErrWords * sizeof(uint32_t),
+                    hipMemcpyDeviceToHost), "read error words");
+  uint32_t err = 0;
+  for (uint32_t x : words) err |= x;
+  if (err) HIP_TRY(hipMemset(ctx->d_err, 0, kErrWords * sizeof(uint32_t)), "clear error words");
+  return sync_error(err);
 }
 
 int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_t slot_stride,
                    const uint32_t* d_sizes, uint32_t nseg, uint64_t* d_offsets, void* d_frame) {
   if (int r = enter(ctx)) return r;
   if (!d_sizes || !d_offsets) return fail(BITAR_HIP_INVALID, "null buffer");
+  if (d_frame && nseg && (!d_slab || slot_stride == 0))
+    return fail(BITAR_HIP_INVALID, "null slab or zero slot stride");
   hipStream_t s = pick_stream(ctx, stream);
+  // sizes above the slot stride (a failed op's SEGMENT_ERROR) pack as 0 bytes and flag the
+  // stream's error word, so the next sync reports IOError instead of copying out of bounds
+  const uint64_t limit = slot_stride ? slot_stride : (uint64_t)BITAR_HIP_SEGMENT_ERROR - 1;
   hipLaunchKernelGGL(bitar_hip::scan_sizes_kernel, dim3(1), dim3(1024), 0, s, d_sizes, nseg,
-                     d_offsets);
+                     limit, d_offsets, err_word(ctx, s));
   HIP_TRY(hipGetLastError(), "scan launch");
   if (d_frame && nseg) {
-    if (!d_slab) return fail(BITAR_HIP_INVALID, "null slab");
     hipLaunchKernelGGL(bitar_hip::pack_kernel, dim3(nseg), dim3(64), 0, s,
                        static_cast<const uint8_t*>(d_slab), slot_stride, d_sizes, d_offsets,
                        nseg, static_cast<uint8_t*>(d_frame));
@@ -454,7 +501,7 @@ int bitar_hip_pack_lz4f(bitar_hip_ctx* ctx, void* stream, const void* d_in, uint
     HIP_TRY(hipGetLastError(), "lz4f sizes launch");
   }
   hipLaunchKernelGGL(bitar_hip::scan_sizes_kernel, dim3(1), dim3(1024), 0, s, d_framed, nseg,
-                     d_offsets);
+                     (uint64_t)BITAR_HIP_SEGMENT_ERROR - 1, d_offsets, err_word(ctx, s));
   HIP_TRY(hipGetLastError(), "scan launch");
   if (d_frame && nseg) {
     if (!d_slab || !d_in) return fail(BITAR_HIP_INVALID, "null input or slab");
@@ -467,18 +514,25 @@ int bitar_hip_pack_lz4f(bitar_hip_ctx* ctx, void* stream, const void* d_in, uint
   return 0;
 }
 
-int bitar_hip_fill(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed, void* d_out,
-                   uint64_t n) {
+int bitar_hip_fill_at(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed,
+                      uint64_t offset, void* d_out, uint64_t n) {
   if (int r = enter(ctx)) return r;
+  if (offset & 63u) return fail(BITAR_HIP_INVALID, "fill offset must be a multiple of 64");
   if (!n) return 0;
   if (!d_out) return fail(BITAR_HIP_INVALID, "null buffer");
   const uint64_t lines = (n + 63) / 64;
   uint64_t blocks = (lines + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(bitar_hip::fill_kernel, dim3((uint32_t)blocks), dim3(256), 0,
-                     pick_stream(ctx, stream), kind, seed, static_cast<uint8_t*>(d_out), n);
+                     pick_stream(ctx, stream), kind, seed, offset,
+                     static_cast<uint8_t*>(d_out), n);
   HIP_TRY(hipGetLastError(), "fill launch");
   return 0;
+}
+
+int bitar_hip_fill(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed, void* d_out,
+                   uint64_t n) {
+  return bitar_hip_fill_at(ctx, stream, kind, seed, 0, d_out, n);
 }
 
 }  // extern "C"

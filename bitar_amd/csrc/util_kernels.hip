@@ -3,12 +3,25 @@
 
 namespace bitar_hip {
 
+// A size larger than `limit` (the slot stride; BITAR_HIP_SEGMENT_ERROR of a failed op in
+// particular) counts as 0 bytes and raises bit 2 of the stream's error word: pack must
+// never copy past a slot.
+__device__ __forceinline__ uint32_t clamp_size(uint32_t v, uint64_t limit,
+                                               uint32_t* __restrict__ err) {
+  if ((uint64_t)v > limit) {
+    atomicOr(err, 4u);
+    return 0u;
+  }
+  return v;
+}
+
 // Exclusive prefix sum of nseg sizes -> offsets[0..nseg], one 1024-thread workgroup.
 // nseg is at most a few hundred thousand (8 GiB / 64 KiB = 131072): a single block walks
 // the array in 1024-element tiles with a carried base.
 __global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint32_t* __restrict__ sizes,
-                                                          uint32_t nseg,
-                                                          uint64_t* __restrict__ offsets) {
+                                                          uint32_t nseg, uint64_t limit,
+                                                          uint64_t* __restrict__ offsets,
+                                                          uint32_t* __restrict__ err) {
   __shared__ uint64_t part[1024 / kWave];
   __shared__ uint64_t carry;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -16,7 +29,7 @@ __global__ __launch_bounds__(1024) void scan_sizes_kernel(const uint32_t* __rest
   __syncthreads();
   for (uint32_t base = 0; base < nseg; base += 1024) {
     const uint32_t idx = base + t;
-    uint64_t v = idx < nseg ? (uint64_t)sizes[idx] : 0ull;
+    uint64_t v = idx < nseg ? (uint64_t)clamp_size(sizes[idx], limit, err) : 0ull;
     uint64_t incl = v;  // inclusive wave scan (Hillis-Steele over 64 lanes)
 #pragma unroll
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -53,7 +66,9 @@ __global__ __launch_bounds__(64) void pack_kernel(const uint8_t* __restrict__ sl
                                                   uint32_t nseg, uint8_t* __restrict__ frame) {
   const uint32_t i = blockIdx.x;
   if (i >= nseg) return;
-  wave_copy_global(global_ptr(frame + offsets[i]), global_ptr(slab + (uint64_t)i * stride), sizes[i]);
+  // the same clamp as the scan (which already flagged it): a failed slot packs 0 bytes
+  const uint32_t len = (uint64_t)sizes[i] > stride ? 0u : sizes[i];
+  wave_copy_global(global_ptr(frame + offsets[i]), global_ptr(slab + (uint64_t)i * stride), len);
 }
 
 // LZ4 frame data blocks (lz4 frame format, independent blocks): framed size of block i =
@@ -66,7 +81,7 @@ __global__ __launch_bounds__(256) void lz4f_sizes_kernel(const uint32_t* __restr
   if (i >= nseg) return;
   const uint64_t off = (uint64_t)i * seg;
   const uint32_t len = (uint32_t)(n - off < seg ? n - off : seg);
-  framed[i] = 4 + (sizes[i] < len ? sizes[i] : len);
+  framed[i] = 4 + (sizes[i] < len ? sizes[i] : len);  // a failed op (SEGMENT_ERROR) ships raw
 }
 
 // block i at frame + offsets[i]: LE32 size (| 1 << 31 when stored raw) + its bytes
@@ -128,11 +143,15 @@ __device__ void log_line(uint64_t seed, uint64_t j, uint8_t* l) {
   l[63] = '\n';
 }
 
-__global__ __launch_bounds__(256) void fill_kernel(int kind, uint64_t seed, uint8_t* __restrict__ out,
-                                                   uint64_t n) {
+// Bytes [off, off + n) of the stream (off a multiple of 64): out[b] = stream[off + b].  A
+// rank generates only the batches of a job it was dealt (bitar_amd/job.py).
+__global__ __launch_bounds__(256) void fill_kernel(int kind, uint64_t seed, uint64_t off,
+                                                   uint8_t* __restrict__ out, uint64_t n) {
   const uint64_t nlines = (n + 63) / 64;
-  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < nlines;
-       j += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t line0 = off / 64;
+  for (uint64_t jl = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; jl < nlines;
+       jl += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t j = line0 + jl;  // line of the whole stream (the generator's index)
     __attribute__((aligned(16))) uint8_t line[64];
     uint64_t w[8];
     const uint64_t k0 = j * 8;
@@ -190,7 +209,7 @@ __global__ __launch_bounds__(256) void fill_kernel(int kind, uint64_t seed, uint
       for (int i = 0; i < 8; ++i)
         for (int b = 0; b < 8; ++b) line[i * 8 + b] = (uint8_t)(w[i] >> (8 * b));
     }
-    const uint64_t base = j * 64;
+    const uint64_t base = jl * 64;  // output position
     if (base + 64 <= n) {
       uint4* d = reinterpret_cast<uint4*>(out + base);
       const uint4* s = reinterpret_cast<const uint4*>(line);

@@ -131,15 +131,20 @@ int bitar_hip_decompress_slab(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                               const uint32_t* d_sizes, uint32_t nseg, uint32_t seg,
                               void* d_out, uint64_t capacity, uint32_t* d_produced);
 
-/* Wait for `stream` (NULL = the default stream and every queue-pair stream).  Returns BITAR_HIP_IO_ERROR if
- * any segment op launched on this context failed since the last sync (the sticky
- * device-side error word), which it then clears.  Replaces the completion polling of
- * DequeueBurst + GetErrorCount (reference src/device.cc:84-110, 490-535). */
+/* Wait for `stream` and return BITAR_HIP_IO_ERROR if a segment op launched on THAT stream
+ * failed since its last sync (each stream has its own sticky device-side error word, read
+ * and cleared in stream order, so concurrent queue pairs never see each other's failures).
+ * NULL waits for the whole device and reports/clears every stream's word.  Replaces the
+ * completion polling of DequeueBurst + GetErrorCount (reference src/device.cc:84-110,
+ * 490-535). */
 int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream);
 
 /* Exclusive prefix sum of d_sizes (nseg entries) into d_offsets (nseg+1 entries), then
  * gather each slot into one contiguous frame at d_frame (d_frame may be NULL to compute
- * offsets only).  Builds the packed frame / global frame index. */
+ * offsets only).  Builds the packed frame / global frame index.  A size
+ * above slot_stride (BITAR_HIP_SEGMENT_ERROR of a failed op) packs as 0 bytes and makes the
+ * next bitar_hip_sync of `stream` return BITAR_HIP_IO_ERROR; slot_stride may be 0 only when
+ * d_frame is NULL. */
 int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_t slot_stride,
                    const uint32_t* d_sizes, uint32_t nseg, uint64_t* d_offsets, void* d_frame);
 
@@ -160,6 +165,11 @@ int bitar_hip_pack_lz4f(bitar_hip_ctx* ctx, void* stream, const void* d_in, uint
  * 5 int64 small-range only, 6 log text only). */
 int bitar_hip_fill(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed, void* d_out,
                    uint64_t n);
+
+/* Bytes [offset, offset + n) of the same deterministic stream (offset a multiple of 64), so
+ * a rank can generate just the batches of a job it was dealt. */
+int bitar_hip_fill_at(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed,
+                      uint64_t offset, void* d_out, uint64_t n);
 
 /* Where `ptr` lives: *kind = 0 pageable host, 1 pinned host, 2 device memory (then *device
  * is its ordinal).  Replaces rte_mem_virt2iova() residency assumptions (memory.cc:388). */

@@ -211,6 +211,37 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
     CHECK(aout->size() == static_cast<int64_t>(data.size()) &&
           std::memcmp(aout->data(), data.data(), data.size()) == 0);
 
+    // concurrent failure on one queue pair: qp 1 decodes a malformed segment while qp 0
+    // decodes a valid frame; only qp 1 may report IOError (per-queue-pair status,
+    // reference device.cc:84-110, 512-520).  Repeated so the two calls overlap.
+    {
+      static const uint8_t kBad[3] = {0, 0, 0};  // LZ4: offset 0; DEFLATE/Zstd: truncated
+      bitar::BufferVector bad;
+      bad.emplace_back(std::make_unique<arrow::Buffer>(kBad, 3));
+      for (int rep = 0; rep < 8; ++rep) {
+        arrow::Status st[2];
+        auto scb = [&](std::uint8_t, std::uint16_t qp, const arrow::Status& s) {
+          st[qp] = s;
+          return bitar::kAsyncReturnOK;
+        };
+        auto g0 = arrow::AllocateResizableBuffer(static_cast<int64_t>(nseg * seg));
+        auto g1 = arrow::AllocateResizableBuffer(static_cast<int64_t>(seg));
+        std::unique_ptr<arrow::ResizableBuffer> good_out = std::move(*g0);
+        std::unique_ptr<arrow::ResizableBuffer> bad_out = std::move(*g1);
+        using SParam = bitar::DecompressParam<bitar::Class_HIP_GFX950, decltype(scb)>;
+        auto q1 = std::make_unique<SParam>(d, 1, bad, bad_out, scb);
+        auto q0 = std::make_unique<SParam>(d, 0, async_out[0], good_out, scb);
+        CHECK(bitar::DecompressAsync(q1) == 0);
+        CHECK(bitar::DecompressAsync(q0) == 0);
+        CHECK(bitar::WaitLcore(d->LcoreOf(1)) == bitar::kAsyncReturnOK);
+        CHECK(bitar::WaitLcore(d->LcoreOf(0)) == bitar::kAsyncReturnOK);
+        CHECK(st[0].ok());
+        CHECK(st[1].IsIOError());
+        CHECK(good_out->size() == static_cast<int64_t>(data.size()) &&
+              std::memcmp(good_out->data(), data.data(), data.size()) == 0);
+      }
+    }
+
     // Recycle returns every slot exactly once (demo_app.cc:288-290)
     CHECK(d->Recycle(*comp) == comp->size());
     CHECK(d->Recycle(*comp) == 0);

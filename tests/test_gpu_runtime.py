@@ -1,0 +1,202 @@
+"""GPU tests of the runtime around the kernels, through the C ABI: per-stream error words
+(a failure on one queue pair is reported by that queue pair only, reference
+device.cc:84-110, 512-520), bitar_hip_pack's handling of failed segments, and seeded
+mutations of LZ4 streams long enough to reach the decoder's batch fast path (accept / reject
+and output exactly as the oracle's bo_lz4_decompress_block)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from test_gpu_lz4 import _decode_blobs, down, eng, up  # noqa: F401  (fixture reuse)
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _slab(blobs, stride):
+    slab = np.zeros(len(blobs) * stride, np.uint8)
+    for i, b in enumerate(blobs):
+        slab[i * stride:i * stride + len(b)] = np.frombuffer(b, np.uint8)
+    return up(slab), torch.tensor([len(b) for b in blobs], dtype=torch.int32).cuda()
+
+
+def test_error_word_is_per_stream():
+    """qp 1 decodes a malformed segment, qp 0 a valid one, concurrently: sync(qp0) is OK,
+    sync(qp1) is IOError, and qp1's error survives qp0's sync (it is not cleared by it)."""
+    import bitar_amd
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    e = bitar_amd.Engine(0, num_streams=2)
+    try:
+        s0, s1 = e.queue_pair_stream(0), e.queue_pair_stream(1)
+        seg = 65536
+        data = O.fill(O.KIND_MIXED, 9, 8 * seg)
+        r, comp = O.lz4_compress(data[:seg].tobytes())
+        assert r == 0
+        good = [comp] * 8
+        bad = [bytes([0, 0, 0])]  # token 0, offset 0: invalid
+        for rep in range(4):
+            gs, gz = _slab(good, 65536 + 512)
+            bs, bz = _slab(bad, 512)
+            torch.cuda.synchronize()
+            go, gp = e.empty(8 * seg), e.empty(8, dtype=torch.int32)
+            bo, bp = e.empty(seg), e.empty(1, dtype=torch.int32)
+            e.decompress_slab_into(O.CODEC_LZ4, bs, 512, bz, 1, seg, bo, bp, stream=s1)
+            e.decompress_slab_into(O.CODEC_LZ4, gs, 65536 + 512, gz, 8, seg, go, gp, stream=s0)
+            e.sync(s0)  # must not see qp 1's failure, nor clear it
+            with pytest.raises(bitar_amd.BitarError) as ex:
+                e.sync(s1)
+            assert ex.value.code == -5
+            e.sync(s1)  # cleared by its own sync
+            assert np.array_equal(down(gp).astype(np.uint32), [seg] * 8)
+            assert down(bp).astype(np.uint32)[0] == 0xFFFFFFFF
+            assert np.array_equal(down(go)[:seg], data[:seg])
+        # a failure on a foreign stream (torch's) is reported by sync(NULL) too
+        bs, bz = _slab(bad, 512)
+        bo, bp = e.empty(seg), e.empty(1, dtype=torch.int32)
+        e.decompress_slab_into(O.CODEC_LZ4, bs, 512, bz, 1, seg, bo, bp)
+        with pytest.raises(bitar_amd.BitarError):
+            e.sync(False)
+        e.sync(False)
+    finally:
+        e.close()
+
+
+def test_pack_skips_failed_segments(eng):
+    """A SEGMENT_ERROR (or any size above the slot stride) packs as 0 bytes and makes the
+    next sync return IOError instead of copying out of bounds."""
+    import bitar_amd
+    stride = 256
+    nseg = 4
+    slab = up(np.arange(nseg * stride, dtype=np.uint32).astype(np.uint8))
+    sizes = torch.tensor([10, -1, 20, stride + 1], dtype=torch.int32).cuda()
+    offsets = eng.empty(nseg + 1, dtype=torch.int64)
+    frame = eng.empty(64)
+    eng.pack(slab, stride, sizes, nseg, offsets, frame)
+    with pytest.raises(bitar_amd.BitarError) as ex:
+        eng.sync()
+    assert ex.value.code == -5
+    assert down(offsets).tolist() == [0, 10, 10, 30, 30]
+    s = down(slab)
+    f = down(frame)
+    assert np.array_equal(f[:10], s[:10])
+    assert np.array_equal(f[10:30], s[2 * stride:2 * stride + 20])
+    eng.sync()
+    # offsets only (no frame): same clamp
+    sizes2 = torch.tensor([5, -1], dtype=torch.int32).cuda()
+    off2 = eng.empty(3, dtype=torch.int64)
+    eng.pack(None, 0, sizes2, 2, off2)
+    with pytest.raises(bitar_amd.BitarError):
+        eng.sync()
+    assert down(off2).tolist() == [0, 5, 5]
+
+
+def test_pack_rejects_null_slab(eng):
+    import bitar_amd
+    sizes = torch.tensor([5], dtype=torch.int32).cuda()
+    off = eng.empty(2, dtype=torch.int64)
+    with pytest.raises(bitar_amd.BitarError) as ex:
+        eng.pack(None, 256, sizes, 1, off, eng.empty(16))
+    assert ex.value.code == -4
+
+
+def _lz4_sequences(comp):
+    """(token position, offset position or None) of every sequence of an LZ4 block."""
+    seqs, ip, n = [], 0, len(comp)
+    while ip < n:
+        tok = comp[ip]
+        t0 = ip
+        ip += 1
+        lit = tok >> 4
+        if lit == 15:
+            while True:
+                b = comp[ip]
+                ip += 1
+                lit += b
+                if b != 255:
+                    break
+        ip += lit
+        if ip >= n:
+            seqs.append((t0, None))
+            break
+        seqs.append((t0, ip))
+        ip += 2
+        if tok & 15 == 15:
+            while comp[ip] == 255:
+                ip += 1
+            ip += 1
+    return seqs
+
+
+def _lz4_cases(rng):
+    """Valid streams of >= 200 bytes (ours and liblz4's, which has far offsets), their
+    seeded byte mutations, and targeted bad offsets / lengths in the first and in middle
+    sequences of a batch."""
+    bases = []
+    for kind, seed, n in ((1, 1, 3000), (2, 2, 6000), (5, 3, 4000), (6, 4, 8000), (4, 5, 2500)):
+        plain = O.fill(kind, seed, n).tobytes()
+        r, c = O.lz4_compress(plain)
+        assert r == 0 and len(c) >= 200
+        bases.append(c)
+    try:
+        L = ctypes.CDLL("liblz4.so.1")
+        L.LZ4_compress_default.restype = ctypes.c_int
+        for kind, seed, n in ((1, 6, 30000), (6, 7, 20000), (2, 8, 40000)):
+            plain = O.fill(kind, seed, n).tobytes()
+            buf = ctypes.create_string_buffer(n + n // 255 + 16)
+            r = L.LZ4_compress_default(plain, buf, n, len(buf))
+            assert r > 0
+            bases.append(buf.raw[:r])
+    except OSError:
+        pass
+    cases = []
+    for c in bases:
+        cases.append(c)
+        for _ in range(24):
+            b = bytearray(c)
+            k = int(rng.integers(0, 3))
+            i = int(rng.integers(0, len(b)))
+            if k == 0:
+                b[i] ^= 1 << int(rng.integers(0, 8))
+            elif k == 1:
+                b[i] = int(rng.integers(0, 256))
+            else:
+                b = b[:max(1, i)]
+            cases.append(bytes(b))
+        seqs = [s for s in _lz4_sequences(c) if s[1] is not None]
+        picks = [0, 1, 2, len(seqs) // 3, len(seqs) // 2, len(seqs) - 1]
+        for j in sorted(set(p for p in picks if 0 <= p < len(seqs))):
+            t, o = seqs[j]
+            for off in (0, 0xFFFF, 1, 4097):  # zero, too far, overlap, beyond the ring
+                b = bytearray(c)
+                b[o], b[o + 1] = off & 255, off >> 8
+                cases.append(bytes(b))
+            b = bytearray(c)
+            b[t] = (b[t] & 0xF0) | 15  # match length extension where there was none
+            cases.append(bytes(b))
+            b = bytearray(c)
+            b[t] = 0xF0 | (b[t] & 15)  # literal length extension where there was none
+            cases.append(bytes(b))
+    return cases
+
+
+def test_lz4_mutations_match_oracle(eng):
+    rng = np.random.default_rng(11)
+    cases = _lz4_cases(rng)
+    seg = 65536
+    for lo in range(0, len(cases), 128):
+        chunk = cases[lo:lo + 128]
+        ok, out, prod = _decode_blobs(eng, O.CODEC_LZ4, chunk, seg)
+        n_bad = 0
+        for k, c in enumerate(chunk):
+            r, ref = O.lz4_decompress(c, seg)
+            if r == 0:
+                assert prod[k] == len(ref), (lo + k, len(c))
+                assert out[k * seg:k * seg + len(ref)].tobytes() == ref, lo + k
+            else:
+                n_bad += 1
+                assert prod[k] == 0xFFFFFFFF, (lo + k, r, int(prod[k]))
+        assert ok == (n_bad == 0)
