@@ -49,7 +49,7 @@ def parse():
     p.add_argument("--bytes", type=int, default=1 << 30, help="headline bytes per rank")
     p.add_argument("--seg", type=int, default=65536)
     p.add_argument("--kind", type=int, default=1, help="0 random, 1 mixed, 2 arrow")
-    p.add_argument("--codec", default="lz4", choices=["lz4", "deflate", "zstd"])
+    p.add_argument("--codec", default="lz4", choices=["lz4", "deflate", "zstd", "deflate_dyn"])
     p.add_argument("--streams", type=int, default=4,
                    help="queue-pair streams per GPU in the configs[3] record-batch leg")
     p.add_argument("--record-bytes", type=int, default=8 << 30,
@@ -75,14 +75,19 @@ KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
            "deflate": ("deflate_compress_kernel", "inflate_lanes_kernel"),
            # decompress = zstd_lanes_kernel (lane per segment) + zstd_decompress_kernel in
            # defer-only mode; timed together
-           "zstd": ("zstd_compress_kernel", "zstd_lanes_kernel")}
-CODEC_NAMES = {"lz4": "lz4-block", "deflate": "deflate-raw-fixed", "zstd": "zstd-frame"}
+           "zstd": ("zstd_compress_kernel", "zstd_lanes_kernel"),
+           # compress = deflate_dyn_parse_kernel + deflate_dyn_emit_kernel (one event pair
+           # brackets both); decompress = inflate_lanes_kernel deferring every dynamic block
+           # to inflate_kernel
+           "deflate_dyn": ("deflate_dyn_parse_kernel+deflate_dyn_emit_kernel", "inflate_kernel")}
+CODEC_NAMES = {"lz4": "lz4-block", "deflate": "deflate-raw-fixed", "zstd": "zstd-frame",
+               "deflate_dyn": "deflate-raw-dynamic"}
 
 
 def codec_id(name):
     import bitar_amd
     return {"lz4": bitar_amd.CODEC_LZ4, "deflate": bitar_amd.CODEC_DEFLATE,
-            "zstd": bitar_amd.CODEC_ZSTD}[name]
+            "zstd": bitar_amd.CODEC_ZSTD, "deflate_dyn": bitar_amd.CODEC_DEFLATE_DYNAMIC}[name]
 
 
 def reduce_max_sum(vals_max, vals_sum, world):
@@ -450,6 +455,11 @@ def main():
     if args.codec != "deflate" and not args.no_deflate and want(args, "deflate"):
         df = run_job(eng, "deflate", args.kind, world * n, 59460, 1, args.steps, args.warmup,
                      world, rank, seed=2000)
+    dd = None
+    if args.codec != "deflate_dyn" and not args.no_deflate and want(args, "deflate_dyn"):
+        # the reference's default frame: dynamic Huffman (config.h:151)
+        dd = run_job(eng, "deflate_dyn", args.kind, world * n, 59460, 1, args.steps,
+                     args.warmup, world, rank, seed=2000)
     sec = stock = None
     if world == 1 and args.codec == "lz4":
         if not args.no_secondary and want(args, "secondary"):
@@ -522,6 +532,12 @@ def main():
             "deflate", df, world, args.steps, args.traffic_json,
             "the reference's codec: raw DEFLATE (fixed-Huffman blocks) per 59460-B segment, "
             "compress + decompress, same input and sharding as the headline")
+    if dd is not None:
+        res["deflate_dynamic"] = leg_summary(
+            "deflate_dyn", dd, world, args.steps, args.traffic_json,
+            "the reference's DEFAULT frame: raw DEFLATE with dynamic Huffman codes "
+            "(HuffmanEncoding::DYNAMIC, config.h:151) per 59460-B segment, compress + "
+            "decompress, same input and sharding as the headline")
     if stock is not None:
         res["stock_decode"] = stock[0]
     if not args.no_cpu_baseline and world == 1 and args.codec == "lz4" and args.only is None:

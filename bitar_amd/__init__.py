@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("BITAR_HIP_LIB") or os.path.join(_HERE, "lib", "libbit
 CODEC_LZ4 = 1
 CODEC_DEFLATE = 2
 CODEC_ZSTD = 3
+CODEC_DEFLATE_DYNAMIC = 4  # HuffmanEncoding::DYNAMIC (decoded as CODEC_DEFLATE)
 SEGMENT_ERROR = 0xFFFFFFFF
 MAX_SEG_SIZE = 65536
 

@@ -129,7 +129,7 @@ class Configuration {
   std::uint32_t decompressed_seg_size_ = internal::kDefaultSegSize;
   std::uint32_t compressed_seg_size_{};
   std::uint8_t window_size_ = 0U;
-  HuffmanEncoding huffman_enc_ = HuffmanEncoding::DEFAULT;
+  HuffmanEncoding huffman_enc_ = HuffmanEncoding::DYNAMIC;  // reference config.h:151
   std::uint16_t max_preallocate_memzones_ = 1024;
   Codec codec_ = Codec::DEFLATE;
 };

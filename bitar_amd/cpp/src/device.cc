@@ -179,11 +179,16 @@ bool OnDevice(std::uint64_t address, int device) {
   return kind == 2 && dev == device;
 }
 
-std::uint32_t AbiCodec(Codec c) {
-  switch (c) {
+// DEFLATE + FIXED -> fixed-Huffman blocks; DEFLATE + DYNAMIC (the reference default,
+// config.h:151) or DEFAULT (the PMD's choice) -> dynamic Huffman
+template <typename Cfg>
+std::uint32_t AbiCodec(const Cfg& c) {
+  switch (c.codec()) {
     case Codec::LZ4: return BITAR_HIP_CODEC_LZ4;
     case Codec::ZSTD: return BITAR_HIP_CODEC_ZSTD;
-    default: return BITAR_HIP_CODEC_DEFLATE;
+    default:
+      return c.huffman_enc() == HuffmanEncoding::FIXED ? BITAR_HIP_CODEC_DEFLATE
+                                                      : BITAR_HIP_CODEC_DEFLATE_DYNAMIC;
   }
 }
 
@@ -208,7 +213,7 @@ arrow::Status CompressDevice<Class, Enable>::PreAllocateMemory() {
   bitar_hip_config cfg{num_qps(), 0};
   BITAR_ABI(bitar_hip_open(device_id_, &cfg, &ctx_), "Device configuration failed");
   set_state(internal::DeviceState::kConfigured);
-  const auto codec = internal::AbiCodec(configuration_->codec());
+  const auto codec = internal::AbiCodec(*configuration_);
   const std::uint32_t seg = configuration_->decompressed_seg_size();
   slot_size_ = std::max<std::uint64_t>(bitar_hip_slot_size(codec, seg),
                                        (configuration_->compressed_seg_size() + 255u) & ~255u);
@@ -270,7 +275,7 @@ arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
   const std::uint32_t seg = configuration_->decompressed_seg_size();
   const auto n = static_cast<std::uint64_t>(decompressed_buffer->size());
   const auto nseg = static_cast<std::uint32_t>((n + seg - 1) / seg);
-  const auto codec = internal::AbiCodec(configuration_->codec());
+  const auto codec = internal::AbiCodec(*configuration_);
 
   // input: read HBM in place, else stage it (the reference attaches it zero-copy, 380-399)
   const void* d_in = reinterpret_cast<const void*>(decompressed_buffer->address());
@@ -332,7 +337,7 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
   } guard{this, queue_pair_id};
 
   const auto nseg = static_cast<std::uint32_t>(compressed_buffers.size());
-  const auto codec = internal::AbiCodec(configuration_->codec());
+  const auto codec = internal::AbiCodec(*configuration_);
   ARROW_RETURN_NOT_OK(m->Tables(nseg));
 
   // sources: HBM buffers in place; host buffers staged behind the output area
@@ -416,7 +421,7 @@ CompressDevice<Class, Enable>::CompressDevice(std::uint8_t device_id,
 template <typename Class, typename Enable>
 arrow::Status CompressDevice<Class, Enable>::ValidateConfiguration() {
   // device capabilities: <= 64 queue pairs, no chained segments, window 2^15 (DEFLATE) or
-  // 2^16 (LZ4), fixed Huffman (reference device.cc:352-415)
+  // 2^16 (LZ4), fixed or dynamic Huffman (reference device.cc:352-415, 566-574)
   constexpr std::uint16_t kMaxQueuePairs = 64;
   if (num_qps() == 0 || num_qps() > kMaxQueuePairs) {
     return arrow::Status::Invalid("The requested number of queue pairs (", num_qps(),
@@ -444,10 +449,6 @@ arrow::Status CompressDevice<Class, Enable>::ValidateConfiguration() {
   } else if (configuration_->window_size() != window) {
     return arrow::Status::Invalid("window_size is not in the range of [", +window, ", ",
                                   +window, "]");
-  }
-  if (configuration_->codec() == Codec::DEFLATE &&
-      configuration_->huffman_enc() == HuffmanEncoding::DYNAMIC) {
-    return arrow::Status::Invalid("Compress device does not supported dynamic Huffman");
   }
   if (configuration_->max_preallocate_memzones() < internal::kMinPreallocateSlots) {
     return arrow::Status::Invalid("max_preallocate_memzones (",

@@ -1,0 +1,570 @@
+// deflate_dyn.hip -- raw DEFLATE with DYNAMIC Huffman codes per segment (gfx950): the
+// reference's default frame (RTE_COMP_HUFFMAN_DYNAMIC, reference src/include/config.h:151;
+// accepted by the BlueField device, src/device.cc:566-574).  Restated exactly by the oracle's
+// bo_deflate_dynamic_block (oracle/bitar_deflate_dyn.c); the GPU output must match it byte for
+// byte.
+//
+// Two launches, one wavefront per segment each, through a scratch area of
+// kPlanBytes + slot_stride bytes per segment:
+//   deflate_dyn_parse_kernel  the window-scan parse of window_parse.hip.h with a "record"
+//                             emitter: per window of 64 positions, the 8-byte chain mask of
+//                             selected matches + one u32 (length | distance << 16) per match,
+//                             staged in LDS and flushed with 16-B stores; literal/length and
+//                             distance histograms counted with LDS atomics.
+//   deflate_dyn_emit_kernel   builds the codes from the histograms (length-limited Huffman,
+//                             code-length RLE, code-length code), sizes the dynamic / fixed /
+//                             stored alternatives and writes the smallest: per window every
+//                             lane places its literal code or whole match symbol (up to 45 bits)
+//                             by a prefix sum of bit lengths into an LDS bit ring, from the
+//                             records and the input bytes.
+// The parse (the expensive part, ~250 instructions per window) runs once; the emit pass is
+// a streaming read of records + input and write of the stream.
+#include "window_parse.hip.h"
+
+namespace bitar_hip {
+
+namespace dyn {
+
+using namespace cmp;
+
+constexpr uint32_t kPlanBytes = 2048;  // per segment: histograms + record count
+constexpr uint32_t kNLit = 286, kNDist = 30, kNCl = 19;
+constexpr uint32_t kPlanRecBytes = kNLit + kNDist;  // word index of the record byte count
+
+__device__ __forceinline__ uint32_t len_sym(uint32_t mlen, uint32_t& nx, uint32_t& xv) {
+  // RFC 1951 3.2.5, branch-free (mlen in [3, 258])
+  const uint32_t v = mlen - 3;
+  const uint32_t lev = 29u - __builtin_clz(v | 8u);  // floor(log2 v) - 2 for v >= 8
+  nx = mlen == 258 || v < 8 ? 0u : lev;
+  xv = v & ((1u << nx) - 1);
+  return mlen == 258 ? 28u : v < 8 ? v : 4 * lev + 4 + ((v >> lev) & 3u);
+}
+__device__ __forceinline__ uint32_t dist_sym(uint32_t off, uint32_t& nx, uint32_t& xv) {
+  const uint32_t d = off - 1;
+  const uint32_t dev = 30u - __builtin_clz(d | 4u);  // floor(log2 d) - 1 for d >= 4
+  nx = d < 4 ? 0u : dev;
+  xv = d & ((1u << nx) - 1);
+  return d < 4 ? d : 2 * dev + 2 + ((d >> dev) & 1u);
+}
+__device__ __forceinline__ uint32_t len_extra_bits(uint32_t ls) {  // kLenExtra[ls]
+  return ls < 8 || ls == 28 ? 0u : (ls - 4) >> 2;
+}
+__device__ __forceinline__ uint32_t dist_extra_bits(uint32_t ds) {  // kDistExtra[ds]
+  return ds < 4 ? 0u : (ds - 2) >> 1;
+}
+// transmission order of the code-length code's lengths (RFC 1951 3.2.7)
+__constant__ uint8_t kClo[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+__device__ __forceinline__ uint32_t fixed_len(uint32_t s) {
+  return s < 144 ? 8u : s < 256 ? 9u : s < 280 ? 7u : 8u;
+}
+
+// ---- pass 1: records + histograms ---------------------------------------------------------
+struct RecOut : ByteOut {
+  uint32_t* lh;  // LDS literal/length histogram (286)
+  uint32_t* dh;  // LDS distance histogram (30)
+
+  __device__ __forceinline__ void window(const GMEM uint8_t*, const InRing&, const Window& W,
+                                         uint32_t, uint32_t n) {
+    const uint32_t lane = lane_id();
+    const uint32_t q = W.x + lane;
+    const bool cl = (W.chain >> lane) & 1;
+    const uint32_t pend = wave_incl_max(cl ? q + W.mlen : 0u);
+    const bool covered = q < W.pos_in || (!cl && q < pend);
+    const bool lit = !cl && !covered && q < n;
+    uint32_t nx, xv;
+    const uint32_t ls = len_sym(cl ? W.mlen : 3u, nx, xv);
+    const uint32_t ds = dist_sym(cl ? W.off : 1u, nx, xv);
+    lds_order();
+    if (lit) atomicAdd(&lh[W.byte], 1u);
+    if (cl) {
+      atomicAdd(&lh[257 + ls], 1u);
+      atomicAdd(&dh[ds], 1u);
+    }
+    lds_order();
+    if (overflow) return;
+    const uint32_t nm = (uint32_t)__builtin_popcountll(W.chain);
+    const uint32_t total = 8 + 4 * nm;
+    if (!room(total)) return;
+    const uint32_t rank = (uint32_t)__builtin_popcountll(W.chain & ((1ull << lane) - 1));
+    uint32_t* r32 = reinterpret_cast<uint32_t*>(ring);
+    lds_order();
+    if (lane < 2) r32[at(op + 4 * lane) >> 2] = lane ? (uint32_t)(W.chain >> 32) : (uint32_t)W.chain;
+    if (cl) r32[at(op + 8 + 4 * rank) >> 2] = W.mlen | (W.off << 16);
+    lds_order();
+    op += total;
+  }
+  // the tail literals [s, s + n)
+  __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I, uint32_t s,
+                                           uint32_t n, uint32_t, uint32_t) {
+    const uint32_t lane = lane_id();
+    const bool ring_ok = s >= I.lo;
+    for (uint32_t k = 0; k < n; k += kWave) {
+      const uint32_t step = n - k < kWave ? n - k : kWave;
+      const uint32_t q = s + k + (lane < step ? lane : 0);
+      lds_order();
+      const uint32_t b = ring_ok ? I.byte(q) : (uint32_t)in[q];
+      if (lane < step) atomicAdd(&lh[b], 1u);
+      lds_order();
+    }
+  }
+  __device__ __forceinline__ uint32_t pending_from(uint32_t, uint32_t emitted) const { return emitted; }
+};
+
+// ---- code construction (restated by oracle/bitar_deflate_dyn.c) --------------------------
+struct TreeLds {
+  uint32_t fw[kNLit];      // frequencies (padded)
+  uint32_t w[2 * kNLit];   // node weights
+  uint16_t parent[2 * kNLit];
+  uint16_t order[2 * kNLit];
+  uint16_t leaf[kNLit];
+  uint8_t nlen[2 * kNLit];
+  uint16_t blc[16];        // bl_count / next_code
+};
+
+// Length-limited Huffman code lengths of nsym symbols (bo_huff_lengths).
+__device__ void huff_lengths(const uint32_t* freq, uint32_t nsym, uint32_t maxlen, uint8_t* lens,
+                             TreeLds& T) {
+  const uint32_t lane = lane_id();
+  uint32_t m = 0;
+  lds_order();
+  for (uint32_t s0 = 0; s0 < nsym; s0 += kWave) {
+    const uint32_t s = s0 + lane;
+    const uint32_t f = s < nsym ? freq[s] : 0u;
+    if (s < nsym) {
+      T.fw[s] = f;
+      lens[s] = 0;
+    }
+    m += (uint32_t)__builtin_popcountll(ballot(f != 0));
+  }
+  lds_order();
+  if (m < 2 && lane == 0) {
+    for (uint32_t s = 0; s < nsym && m < 2; ++s)
+      if (!T.fw[s]) { T.fw[s] = 1; ++m; }
+  }
+  lds_order();
+  m = m < 2 ? 2u : m;
+  // leaves in (frequency, symbol) order: rank of every used symbol
+  for (uint32_t s0 = 0; s0 < nsym; s0 += kWave) {
+    const uint32_t s = s0 + lane;
+    const uint32_t fs = s < nsym ? T.fw[s] : 0u;
+    uint32_t r = 0;
+    for (uint32_t t = 0; t < nsym; ++t) {
+      const uint32_t ft = T.fw[t];
+      r += (ft != 0u && (ft < fs || (ft == fs && t < s))) ? 1u : 0u;
+    }
+    lds_order();
+    if (fs) T.leaf[r] = (uint16_t)s;
+    lds_order();
+  }
+  if (lane == 0) {
+    for (uint32_t k = 0; k < m; ++k) T.w[k] = T.fw[T.leaf[k]];
+    uint32_t i = 0, j = m, next = m, no = 0;
+    for (uint32_t step = 0; step + 1 < m; ++step) {
+      uint32_t ab[2];
+      for (int t = 0; t < 2; ++t) {
+        const bool take_leaf = i < m && (j >= next || T.w[i] <= T.w[j]);
+        ab[t] = take_leaf ? i++ : j++;
+        T.order[no++] = (uint16_t)ab[t];
+      }
+      T.w[next] = T.w[ab[0]] + T.w[ab[1]];
+      T.parent[ab[0]] = (uint16_t)next;
+      T.parent[ab[1]] = (uint16_t)next;
+      ++next;
+    }
+    const uint32_t root = 2 * m - 2;
+    T.order[no++] = (uint16_t)root;
+    for (uint32_t b = 0; b < 16; ++b) T.blc[b] = 0;
+    int overflow = 0;
+    T.nlen[root] = 0;
+    for (int k = (int)no - 2; k >= 0; --k) {
+      const uint32_t nd = T.order[k];
+      uint32_t bits = T.nlen[T.parent[nd]] + 1u;
+      if (bits > maxlen) { bits = maxlen; ++overflow; }
+      T.nlen[nd] = (uint8_t)bits;
+      if (nd < m) T.blc[bits]++;
+    }
+    if (overflow) {
+      do {
+        uint32_t bits = maxlen - 1;
+        while (T.blc[bits] == 0) --bits;
+        T.blc[bits]--;
+        T.blc[bits + 1] += 2;
+        T.blc[maxlen]--;
+        overflow -= 2;
+      } while (overflow > 0);
+      uint32_t h = 0;
+      for (uint32_t bits = maxlen; bits != 0; --bits) {
+        uint32_t n = T.blc[bits];
+        while (n != 0) {
+          const uint32_t nd = T.order[h++];
+          if (nd >= m) continue;
+          T.nlen[nd] = (uint8_t)bits;
+          --n;
+        }
+      }
+    }
+    for (uint32_t k = 0; k < m; ++k) lens[T.leaf[k]] = T.nlen[k];
+  }
+  lds_order();
+}
+
+// canonical codes (RFC 1951 3.2.2), bit-reversed: tab[s] = code | len << 16
+__device__ void canon_codes(const uint8_t* lens, uint32_t n, uint32_t* tab, TreeLds& T) {
+  const uint32_t lane = lane_id();
+  if (lane == 0) {
+    uint32_t bl[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) bl[b] = 0;
+    for (uint32_t s = 0; s < n; ++s) {
+      const uint32_t l = lens[s];
+#pragma unroll
+      for (int b = 1; b < 16; ++b) bl[b] += l == (uint32_t)b ? 1u : 0u;
+    }
+    uint32_t code = 0;
+#pragma unroll
+    for (int b = 1; b < 16; ++b) {
+      code = (code + (b > 1 ? bl[b - 1] : 0u)) << 1;
+      T.blc[b] = (uint16_t)code;
+    }
+    for (uint32_t s = 0; s < n; ++s) {
+      const uint32_t l = lens[s];
+      uint32_t c = 0;
+      if (l) {
+        c = T.blc[l];
+        T.blc[l] = (uint16_t)(c + 1);
+      }
+      tab[s] = (l ? __builtin_bitreverse32(c) >> (32 - l) : 0u) | (l << 16);
+    }
+  }
+  lds_order();
+}
+
+// zlib send_tree: RLE of lens[0..n) into (symbol | extra << 8); returns the count
+__device__ uint32_t rle_lens(const uint8_t* lens, uint32_t n, uint16_t* out) {
+  uint32_t k = 0;
+  int prevlen = -1, count = 0, max_count = 7, min_count = 4;
+  int nextlen = lens[0];
+  if (nextlen == 0) { max_count = 138; min_count = 3; }
+  for (uint32_t i = 0; i < n; ++i) {
+    const int curlen = nextlen;
+    nextlen = i + 1 < n ? (int)lens[i + 1] : 0xFFFF;
+    if (++count < max_count && curlen == nextlen) continue;
+    if (count < min_count) {
+      do { out[k++] = (uint16_t)curlen; } while (--count != 0);
+    } else if (curlen != 0) {
+      if (curlen != prevlen) { out[k++] = (uint16_t)curlen; --count; }
+      out[k++] = (uint16_t)(16 | ((count - 3) << 8));
+    } else if (count <= 10) {
+      out[k++] = (uint16_t)(17 | ((count - 3) << 8));
+    } else {
+      out[k++] = (uint16_t)(18 | ((count - 11) << 8));
+    }
+    count = 0;
+    prevlen = curlen;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+    else { max_count = 7; min_count = 4; }
+  }
+  return k;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return readlane(wave_incl_sum(v), 63); }
+
+// ---- pass 2 output: LDS bit ring of 64-bit lane contributions -----------------------------
+constexpr uint32_t kStageWords = 512, kStageMask = kStageWords - 1;
+
+struct BitOut {
+  uint32_t* stage;     // LDS, zero outside the pending range
+  GMEM uint32_t* dst;  // slot (16-B aligned)
+  uint64_t cap;        // bytes
+  uint64_t bits;
+  uint32_t wflushed;
+  bool overflow;
+
+  __device__ __forceinline__ void flush_words(uint32_t upto) {
+    const uint32_t lane = lane_id();
+    lds_order();
+    for (uint32_t w = wflushed + lane; w < upto; w += kWave) {
+      dst[w] = stage[w & kStageMask];
+      stage[w & kStageMask] = 0;
+    }
+    lds_order();
+    wflushed = upto;
+  }
+  // append each lane's (val, nb) in lane order, nb <= 64
+  __device__ __forceinline__ void put(uint64_t val, uint32_t nb) {
+    if (overflow) return;
+    const uint32_t incl = wave_incl_sum(nb);
+    const uint32_t total = readlane(incl, 63);
+    if ((bits + total + 7) / 8 > cap) { overflow = true; return; }
+    const uint64_t bp = bits + incl - nb;
+    const uint32_t w = (uint32_t)(bp >> 5), sh = (uint32_t)(bp & 31);
+    const uint64_t lo = val << sh;
+    const uint32_t w2 = sh && sh + nb > 64 ? (uint32_t)(val >> (64 - sh)) : 0u;
+    lds_order();
+    atomicOr(&stage[w & kStageMask], (uint32_t)lo);
+    atomicOr(&stage[(w + 1) & kStageMask], (uint32_t)(lo >> 32));
+    atomicOr(&stage[(w + 2) & kStageMask], w2);
+    lds_order();
+    bits += total;
+    const uint32_t full = (uint32_t)(bits >> 5);
+    if (full - wflushed >= kStageWords - 128) flush_words(full);  // a put adds <= 91 words
+  }
+};
+
+}  // namespace dyn
+
+__global__ __launch_bounds__(64) void deflate_dyn_parse_kernel(
+    const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
+    uint8_t* __restrict__ scratch, uint64_t scr_stride, uint32_t* __restrict__ err) {
+  using namespace dyn;
+  __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
+  __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
+  __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
+  __shared__ uint32_t hist[kNLit + kNDist];
+  const uint32_t i_seg = blockIdx.x;
+  const uint64_t seg_off = (uint64_t)i_seg * seg;
+  if (seg_off >= n_total) return;
+  const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
+  for (uint32_t k = lane_id(); k < kNLit + kNDist; k += kWave) hist[k] = 0;
+  GMEM uint8_t* scr = global_ptr(scratch + (uint64_t)i_seg * scr_stride);
+  RecOut o;
+  o.ring = obuf;
+  o.dst = scr + kPlanBytes;
+  o.cap = scr_stride - kPlanBytes;
+  o.op = 0;
+  o.flushed = 0;
+  o.overflow = false;
+  o.lh = hist;
+  o.dh = hist + kNLit;
+  parse(global_ptr(input + seg_off), n, global_ptr(input + n_total), table, inring, kMaxDist,
+        258u, o);
+  o.flush(o.op, true);
+  lds_order();
+  GMEM uint32_t* plan = reinterpret_cast<GMEM uint32_t*>(scr);
+  for (uint32_t k = lane_id(); k < kNLit + kNDist; k += kWave) plan[k] = hist[k];
+  if (lane_id() == 0) plan[kPlanRecBytes] = o.overflow ? 0xFFFFFFFFu : o.op;
+  if (o.overflow && lane_id() == 0) atomicOr(err, 2u);
+}
+
+__global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
+    const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
+    const uint8_t* __restrict__ scratch, uint64_t scr_stride, uint8_t* __restrict__ slab,
+    uint64_t slot_stride, uint8_t* const* __restrict__ dsts, uint32_t* __restrict__ sizes,
+    uint32_t* __restrict__ err) {
+  using namespace dyn;
+  __shared__ uint32_t hist[kNLit + kNDist];
+  __shared__ uint32_t ltab[288];
+  __shared__ uint32_t dtab[kNDist];
+  __shared__ uint32_t ctab[kNCl];
+  __shared__ uint8_t lens[kNLit + kNDist + kNCl + 1];
+  __shared__ uint16_t cls[kNLit + kNDist + 4];
+  __shared__ uint32_t clf[kNCl];
+  // the tree scratch and the output bit ring share LDS: codes are built before any output
+  __shared__ __attribute__((aligned(16))) uint8_t pool[sizeof(TreeLds) > kStageWords * 4
+                                                           ? sizeof(TreeLds) : kStageWords * 4];
+  TreeLds& T = *reinterpret_cast<TreeLds*>(pool);
+  const uint32_t lane = lane_id();
+  const uint32_t i_seg = blockIdx.x;
+  const uint64_t seg_off = (uint64_t)i_seg * seg;
+  if (seg_off >= n_total) return;
+  const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
+  const GMEM uint8_t* in = global_ptr(input + seg_off);
+  const GMEM uint8_t* scr = global_ptr(scratch + (uint64_t)i_seg * scr_stride);
+  const GMEM uint32_t* plan = reinterpret_cast<const GMEM uint32_t*>(scr);
+  GMEM uint8_t* dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
+  if (plan[kPlanRecBytes] == 0xFFFFFFFFu) {  // pass 1 overflowed its record area
+    if (lane == 0) sizes[i_seg] = 0xFFFFFFFFu;
+    return;
+  }
+  for (uint32_t k = lane; k < kNLit + kNDist; k += kWave) hist[k] = plan[k];
+  lds_order();
+  if (lane == 0) hist[256] = 1;  // end of block
+  lds_order();
+  uint8_t* ll = lens;
+  uint8_t* dl = lens + kNLit;
+  uint8_t* cll = lens + kNLit + kNDist;
+  huff_lengths(hist, kNLit, 15, ll, T);
+  huff_lengths(hist + kNLit, kNDist, 15, dl, T);
+  // HLIT / HDIST: trailing zero lengths trimmed
+  uint32_t hlit = 257, hdist = 1;
+  for (uint32_t s = lane; s < kNLit; s += kWave)
+    if (ll[s]) hlit = max(hlit, s + 1);
+  for (uint32_t s = lane; s < kNDist; s += kWave)
+    if (dl[s]) hdist = max(hdist, s + 1);
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    hlit = max(hlit, (uint32_t)__shfl_xor((int)hlit, (int)d, 64));
+    hdist = max(hdist, (uint32_t)__shfl_xor((int)hdist, (int)d, 64));
+  }
+  uint32_t ncl = 0;
+  if (lane == 0) {
+    ncl = rle_lens(ll, hlit, cls);
+    ncl += rle_lens(dl, hdist, cls + ncl);
+  }
+  ncl = readlane(ncl, 0);
+  lds_order();
+  if (lane < kNCl) clf[lane] = 0;
+  lds_order();
+  for (uint32_t k = lane; k < ncl; k += kWave) atomicAdd(&clf[cls[k] & 31u], 1u);
+  lds_order();
+  huff_lengths(clf, kNCl, 7, cll, T);
+  // the code-length code's lengths in transmission order, trailing zeros trimmed
+  uint32_t hclen = 4;
+  if (lane < kNCl && cll[kClo[lane]]) hclen = lane + 1;
+  for (uint32_t d = 1; d < 64; d <<= 1) hclen = max(hclen, (uint32_t)__shfl_xor((int)hclen, (int)d, 64));
+  // sizes of the three alternatives (bits; stored in bytes)
+  uint32_t dyn_p = 0, fix_p = 0;
+  for (uint32_t s = lane; s < kNLit; s += kWave) {
+    const uint32_t f = hist[s];
+    const uint32_t x = s > 256 ? len_extra_bits(s - 257) : 0u;
+    dyn_p += f * (ll[s] + x);
+    fix_p += f * (fixed_len(s) + x);
+  }
+  if (lane < kNDist) {
+    const uint32_t f = hist[kNLit + lane];
+    dyn_p += f * (dl[lane] + dist_extra_bits(lane));
+    fix_p += f * (5u + dist_extra_bits(lane));
+  }
+  if (lane < kNCl) {
+    const uint32_t f = clf[lane];
+    dyn_p += f * (cll[lane] + (lane == 16 ? 2u : lane == 17 ? 3u : lane == 18 ? 7u : 0u));
+  }
+  const uint64_t dyn_bits = 3 + 14 + 3 * (uint64_t)hclen + wave_sum(dyn_p);
+  const uint64_t fix_bits = 3 + (uint64_t)wave_sum(fix_p);
+  const uint64_t nblk = (n + 65534u) / 65535u;
+  const uint64_t stored = nblk * 5 + n;
+  uint32_t mode = dyn_bits < fix_bits ? 2u : 1u;
+  const uint64_t best = ((mode == 2 ? dyn_bits : fix_bits) + 7) / 8;
+  if (stored < best) mode = 0;
+
+  if (mode == 0) {  // stored blocks of <= 65535 bytes
+    if (stored > slot_stride) {
+      if (lane == 0) { sizes[i_seg] = 0xFFFFFFFFu; atomicOr(err, 2u); }
+      return;
+    }
+    uint32_t p = 0, o = 0;
+    for (uint64_t b = 0; b < nblk; ++b) {
+      const uint32_t len = n - p < 65535u ? n - p : 65535u;
+      const uint32_t hdr[5] = {(uint32_t)(b + 1 == nblk), len & 0xFFu, len >> 8,
+                               ~len & 0xFFu, (~len >> 8) & 0xFFu};
+      if (lane < 5) dst[o + lane] = (uint8_t)(lane == 0 ? hdr[0] : lane == 1 ? hdr[1] : lane == 2 ? hdr[2] : lane == 3 ? hdr[3] : hdr[4]);
+      wave_copy_global(dst + o + 5, in + p, len);
+      o += 5 + len;
+      p += len;
+    }
+    if (lane == 0) sizes[i_seg] = o;
+    return;
+  }
+  // codes
+  if (mode == 2) {
+    canon_codes(ll, kNLit, ltab, T);
+    canon_codes(dl, kNDist, dtab, T);
+    canon_codes(cll, kNCl, ctab, T);
+  } else {
+    uint8_t* fl = reinterpret_cast<uint8_t*>(T.w);  // 288 fixed lengths
+    for (uint32_t s = lane; s < 288; s += kWave) fl[s] = (uint8_t)fixed_len(s);
+    if (lane < kNDist) lens[kNLit + lane] = 5;
+    lds_order();
+    canon_codes(fl, 288, ltab, T);
+    canon_codes(dl, kNDist, dtab, T);  // dl = 5 everywhere now
+  }
+  // the bit ring (over the tree scratch): zero, then the block header
+  uint32_t* stage = reinterpret_cast<uint32_t*>(pool);
+  lds_order();
+  for (uint32_t k = lane; k < kStageWords; k += kWave) stage[k] = 0;
+  lds_order();
+  BitOut o;
+  o.stage = stage;
+  o.dst = reinterpret_cast<GMEM uint32_t*>(dst);
+  o.cap = slot_stride;
+  o.bits = 0;
+  o.wflushed = 0;
+  o.overflow = false;
+  uint32_t hbits = 0;
+  if (lane == 0) {
+    uint64_t bp = 0;
+    auto putb = [&](uint32_t v, uint32_t nb) {
+      const uint32_t w = (uint32_t)(bp >> 5), sh = (uint32_t)(bp & 31);
+      stage[w] |= v << sh;
+      if (sh + nb > 32) stage[w + 1] |= v >> (32 - sh);
+      bp += nb;
+    };
+    putb(1u | (mode << 1), 3);  // BFINAL = 1, BTYPE = 01 fixed / 10 dynamic
+    if (mode == 2) {
+      putb(hlit - 257, 5);
+      putb(hdist - 1, 5);
+      putb(hclen - 4, 4);
+      for (uint32_t k = 0; k < hclen; ++k) putb(cll[kClo[k]], 3);
+      for (uint32_t k = 0; k < ncl; ++k) {
+        const uint32_t c = cls[k], s = c & 31u, x = c >> 8;
+        const uint32_t t = ctab[s];
+        putb(t & 0xFFFFu, t >> 16);
+        if (s == 16) putb(x, 2);
+        else if (s == 17) putb(x, 3);
+        else if (s == 18) putb(x, 7);
+      }
+    }
+    hbits = (uint32_t)bp;
+  }
+  lds_order();
+  o.bits = readlane(hbits, 0);  // < kStageWords * 32 - 128 * 32: no flush needed yet
+
+  // symbols, window by window from the records
+  const GMEM uint32_t* rec = reinterpret_cast<const GMEM uint32_t*>(scr + kPlanBytes);
+  uint32_t pos = 0, emitted = 0, rp = 0;
+  if (n >= kMfLimit + 1) {
+    const uint32_t last_start = n - kMfLimit;
+    for (uint32_t x = 0; x <= last_start; x += kWave) {
+      const uint64_t chain = (uint64_t)rec[rp] | ((uint64_t)rec[rp + 1] << 32);
+      const uint32_t q = x + lane;
+      const bool cl = (chain >> lane) & 1;
+      const uint32_t rank = (uint32_t)__builtin_popcountll(chain & ((1ull << lane) - 1));
+      const uint32_t r = cl ? rec[rp + 2 + rank] : 0x00010003u;
+      const uint32_t byte = q < n ? (uint32_t)in[q] : 0u;
+      const uint32_t mlen = r & 0xFFFFu, off = r >> 16;
+      const uint32_t pend = wave_incl_max(cl ? q + mlen : 0u);
+      const bool covered = q < pos || (!cl && q < pend);
+      const bool lit = !cl && !covered && q < n;
+      uint32_t lnx, lxv, dnx, dxv;
+      const uint32_t ls = len_sym(mlen, lnx, lxv);
+      const uint32_t ds = dist_sym(off, dnx, dxv);
+      lds_order();
+      const uint32_t lt = ltab[cl ? 257 + ls : byte];
+      const uint32_t dt = dtab[ds];
+      const uint32_t ln = lt >> 16, dn = dt >> 16;
+      const uint64_t mv = (uint64_t)(lt & 0xFFFFu) | ((uint64_t)lxv << ln) |
+                          ((uint64_t)(dt & 0xFFFFu) << (ln + lnx)) |
+                          ((uint64_t)dxv << (ln + lnx + dn));
+      const uint32_t mb = ln + lnx + dn + dnx;
+      o.put(cl ? mv : lit ? (uint64_t)(lt & 0xFFFFu) : 0ull, cl ? mb : lit ? ln : 0u);
+      if (chain) {
+        const uint32_t hl = highbit(chain);
+        pos = x + hl + readlane(mlen, hl);
+      }
+      emitted = pos > x + kWave ? pos : x + kWave;
+      rp += 2 + (uint32_t)__builtin_popcountll(chain);
+    }
+  }
+  // tail literals
+  for (uint32_t k = emitted; k < n; k += kWave) {
+    const uint32_t q = k + lane;
+    const bool act = q < n;
+    const uint32_t b = act ? (uint32_t)in[q] : 0u;
+    lds_order();
+    const uint32_t lt = ltab[b];
+    o.put(act ? (uint64_t)(lt & 0xFFFFu) : 0ull, act ? (lt >> 16) : 0u);
+  }
+  {
+    lds_order();
+    const uint32_t eob = ltab[256];
+    o.put(lane == 0 ? (uint64_t)(eob & 0xFFFFu) : 0ull, lane == 0 ? (eob >> 16) : 0u);
+  }
+  o.flush_words((uint32_t)((o.bits + 31) >> 5));
+  if (lane == 0) {
+    sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : (uint32_t)((o.bits + 7) >> 3);
+    if (o.overflow) atomicOr(err, 2u);
+  }
+}
+
+}  // namespace bitar_hip

@@ -37,6 +37,11 @@ __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, ui
 template <uint32_t L>
 __global__ void zstd_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                   const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
+__global__ void deflate_dyn_parse_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
+                                         uint32_t*);
+__global__ void deflate_dyn_emit_kernel(const uint8_t*, uint64_t, uint32_t, const uint8_t*,
+                                        uint64_t, uint8_t*, uint64_t, uint8_t* const*, uint32_t*,
+                                        uint32_t*);
 __global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t, uint64_t*, uint32_t*);
 __global__ void pack_kernel(const uint8_t*, uint64_t, const uint32_t*, const uint64_t*, uint32_t,
                             uint8_t*);
@@ -172,6 +177,16 @@ int bitar_hip_open(int device, const bitar_hip_config* cfg, bitar_hip_ctx** out)
     }
     ctx->streams.push_back(s);
   }
+  // stream-ordered scratch (dynamic-Huffman DEFLATE) comes from the device's default pool;
+  // keep its memory cached between calls instead of returning it at every sync
+  {
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+      uint64_t keep = ~0ull;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    (void)hipGetLastError();
+  }
   hipError_t e = hipMalloc(&ctx->d_err, kErrWords * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(ctx->d_err, 0, kErrWords * sizeof(uint32_t));
   if (e != hipSuccess) {
@@ -212,7 +227,7 @@ uint64_t bitar_hip_slot_size(uint32_t codec, uint32_t seg) {
   uint64_t bound;
   if (codec == BITAR_HIP_CODEC_LZ4)
     bound = (uint64_t)seg + seg / 255u + 16u;           // LZ4_compressBound
-  else if (codec == BITAR_HIP_CODEC_DEFLATE)
+  else if (codec == BITAR_HIP_CODEC_DEFLATE || codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC)
     bound = ((uint64_t)seg * 9 + 7) / 8 + 16u;          // fixed Huffman, 9 bits/literal
   else if (codec == BITAR_HIP_CODEC_ZSTD)  // oracle bo_zstd_bound: blocks of <= 256 sequences
     bound = (uint64_t)seg + 7u + 3u * ((uint64_t)seg / 1024u + 2u) + 8u + 512u;
@@ -261,7 +276,7 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
                          void* const* d_dsts, uint32_t* d_sizes) {
   if (int r = enter(ctx)) return r;
   if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE &&
-      codec != BITAR_HIP_CODEC_ZSTD)
+      codec != BITAR_HIP_CODEC_ZSTD && codec != BITAR_HIP_CODEC_DEFLATE_DYNAMIC)
     return fail(BITAR_HIP_NOT_IMPLEMENTED, "unknown codec");
   if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
   if (n == 0) return 0;  // empty input -> no segments (reference device.cc:161-164)
@@ -282,6 +297,21 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
   else if (codec == BITAR_HIP_CODEC_DEFLATE)
     hipLaunchKernelGGL(bitar_hip::deflate_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
                        in, n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
+  else if (codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC) {
+    // pass 1 (parse -> records + histograms) and pass 2 (codes + emit) through a
+    // stream-ordered scratch of 2 KiB plan + one slot per segment (deflate_dyn.hip)
+    const uint64_t scr_stride = bitar_hip_slot_size(BITAR_HIP_CODEC_DEFLATE, seg) + 2048u;
+    void* scratch = nullptr;
+    HIP_TRY(hipMallocAsync(&scratch, nseg * scr_stride, s), "scratch allocation");
+    hipLaunchKernelGGL(bitar_hip::deflate_dyn_parse_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
+                       in, n, seg, static_cast<uint8_t*>(scratch), scr_stride, err_word(ctx, s));
+    hipLaunchKernelGGL(bitar_hip::deflate_dyn_emit_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
+                       in, n, seg, static_cast<const uint8_t*>(scratch), scr_stride, slab,
+                       slot_stride, dsts, d_sizes, err_word(ctx, s));
+    const hipError_t le = hipGetLastError();
+    HIP_TRY(hipFreeAsync(scratch, s), "scratch release");
+    HIP_TRY(le, "compress launch");
+  }
   else
     hipLaunchKernelGGL(bitar_hip::zstd_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
                        n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
@@ -359,6 +389,7 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            const uint32_t* d_sizes, uint32_t nseg, uint32_t seg, void* d_out,
                            uint64_t capacity, uint32_t* d_produced) {
   if (int r = enter(ctx)) return r;
+  if (codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC) codec = BITAR_HIP_CODEC_DEFLATE;  // same decoder
   if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE &&
       codec != BITAR_HIP_CODEC_ZSTD)
     return fail(BITAR_HIP_NOT_IMPLEMENTED, "unknown codec");

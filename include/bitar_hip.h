@@ -40,8 +40,12 @@ enum bitar_hip_status {
  * RTE_COMP_ALGO_ZSTD path of reference src/config.cc:83-105 / BASELINE configs[5]). */
 enum bitar_hip_codec {
   BITAR_HIP_CODEC_LZ4 = 1,
-  BITAR_HIP_CODEC_DEFLATE = 2,
-  BITAR_HIP_CODEC_ZSTD = 3
+  BITAR_HIP_CODEC_DEFLATE = 2,         /* fixed-Huffman blocks (HuffmanEncoding::FIXED) */
+  BITAR_HIP_CODEC_ZSTD = 3,
+  BITAR_HIP_CODEC_DEFLATE_DYNAMIC = 4  /* dynamic Huffman (HuffmanEncoding::DYNAMIC, the
+                                          reference default, config.h:151); decoded like
+                                          DEFLATE.  Compress runs two kernels through a
+                                          stream-ordered scratch allocation. */
 };
 
 /* Per-segment marker written into sizes[] / produced[] when that segment's op failed

@@ -501,6 +501,9 @@ static void* bo_worker(void* arg) {
       else if (j->codec == BO_CODEC_ZSTD)
         r = bo_zstd_compress_block(j->in + off, len, j->slab + (uint64_t)i * j->stride, cap,
                                    &j->sizes[i]);
+      else if (j->codec == BO_CODEC_DEFLATE_DYN)
+        r = bo_deflate_dynamic_block(j->in + off, len, j->slab + (uint64_t)i * j->stride, cap,
+                                     &j->sizes[i]);
       else
         r = bo_deflate_fixed_block(j->in + off, len, j->slab + (uint64_t)i * j->stride, cap,
                                    &j->sizes[i]);
@@ -545,7 +548,8 @@ int bo_compress(int codec, const uint8_t* in, uint64_t n, uint32_t seg, uint8_t*
                 uint64_t slot_stride, uint32_t* sizes, uint32_t* nseg_out, int threads) {
   if (seg == 0) return BO_ERR_INVALID;
   if ((codec == BO_CODEC_LZ4 || codec == BO_CODEC_ZSTD) && seg > 65536u) return BO_ERR_INVALID;
-  if (codec != BO_CODEC_LZ4 && codec != BO_CODEC_DEFLATE && codec != BO_CODEC_ZSTD)
+  if (codec != BO_CODEC_LZ4 && codec != BO_CODEC_DEFLATE && codec != BO_CODEC_ZSTD &&
+      codec != BO_CODEC_DEFLATE_DYN)
     return BO_ERR_NOT_IMPLEMENTED;
   uint32_t nseg = (uint32_t)((n + seg - 1) / seg); /* device.cc:169-172 */
   *nseg_out = nseg;
@@ -563,7 +567,8 @@ int bo_decompress(int codec, const uint8_t* const* srcs, const uint32_t* sizes, 
   *out_size = 0;
   if (nseg == 0) return BO_OK; /* device.cc:244-246 */
   if (capacity < (uint64_t)nseg * seg) return BO_ERR_CAPACITY; /* device.cc:248-254 */
-  if (codec != BO_CODEC_LZ4 && codec != BO_CODEC_DEFLATE && codec != BO_CODEC_ZSTD)
+  if (codec != BO_CODEC_LZ4 && codec != BO_CODEC_DEFLATE && codec != BO_CODEC_ZSTD &&
+      codec != BO_CODEC_DEFLATE_DYN)
     return BO_ERR_NOT_IMPLEMENTED;
   bo_job j;
   memset(&j, 0, sizeof(j));

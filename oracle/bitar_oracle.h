@@ -47,7 +47,9 @@ enum {
   BO_ERR_NOT_IMPLEMENTED = -10
 };
 
-enum { BO_CODEC_LZ4 = 1, BO_CODEC_DEFLATE = 2, BO_CODEC_ZSTD = 3 };
+/* DEFLATE = fixed-Huffman blocks (HuffmanEncoding::FIXED); DEFLATE_DYN = dynamic Huffman
+ * (HuffmanEncoding::DYNAMIC, the reference default, config.h:151) */
+enum { BO_CODEC_LZ4 = 1, BO_CODEC_DEFLATE = 2, BO_CODEC_ZSTD = 3, BO_CODEC_DEFLATE_DYN = 4 };
 
 /* Configuration::UpdateCompressedSegSize (src/config.cc:59-73). */
 uint32_t bo_compressed_seg_size(uint32_t decompressed_seg_size);
@@ -72,6 +74,16 @@ int bo_inflate_raw(const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t ca
  * (the exact stream the HIP kernel emits). */
 int bo_deflate_fixed_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
                            uint32_t* csize);
+
+/* Deflate one segment with dynamic Huffman codes (bitar_deflate_dyn.c): the exact stream the
+ * HIP kernels deflate_dyn_parse_kernel + deflate_dyn_emit_kernel write (dynamic, fixed or
+ * stored block, whichever is smallest).  cap >= bo_deflate_bound(n). */
+int bo_deflate_dynamic_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
+                             uint32_t* csize);
+/* the block type that encoder chooses: 0 stored, 1 fixed, 2 dynamic (-1 on error) */
+int bo_deflate_dynamic_mode(const uint8_t* src, uint32_t n);
+/* length-limited Huffman code lengths as the dynamic encoder builds them */
+void bo_huff_lengths(const uint32_t* freq, int nsym, int maxlen, uint8_t* lens);
 
 /* ---- Zstandard (RFC 8878), bitar_zstd.c ------------------------------------------ */
 /* Decode one Zstandard frame (no dictionary; content checksum verified). */

@@ -112,7 +112,17 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
   CHECK(data.size() > 100000);
   auto host_in = std::make_shared<arrow::Buffer>(data.data(), static_cast<int64_t>(data.size()));
 
-  for (auto codec : {bitar::Codec::DEFLATE, bitar::Codec::LZ4, bitar::Codec::ZSTD}) {
+  // DEFLATE with the reference's default DYNAMIC Huffman (config.h:151) and with FIXED
+  struct Case {
+    bitar::Codec codec;
+    bitar::HuffmanEncoding huff;
+    const char* file;
+  };
+  for (const Case& cs : {Case{bitar::Codec::DEFLATE, bitar::HuffmanEncoding::DYNAMIC, "/deflate.segs"},
+                         Case{bitar::Codec::DEFLATE, bitar::HuffmanEncoding::FIXED, "/deflate_fixed.segs"},
+                         Case{bitar::Codec::LZ4, bitar::HuffmanEncoding::DEFAULT, "/lz4.segs"},
+                         Case{bitar::Codec::ZSTD, bitar::HuffmanEncoding::DEFAULT, "/zstd.segs"}}) {
+    const auto codec = cs.codec;
     const std::uint32_t seg = codec == bitar::Codec::DEFLATE ? 59460 : 65536;
     auto& dev = (*devs)[0];
     // not initialized yet -> Invalid (EntryGuard, device.cc:446-451)
@@ -124,10 +134,8 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
     auto& d = (*fresh)[0];
     auto cfg = MakeConfig(codec, seg);
     if (codec == bitar::Codec::DEFLATE) {
-      auto dyn = MakeConfig(codec, seg);
-      dyn->set_huffman_enc(bitar::HuffmanEncoding::DYNAMIC);
-      auto tmp = driver->GetDevices({(*ids)[0]});
-      CHECK((*tmp)[0]->Initialize(std::move(dyn)).IsInvalid());
+      CHECK(cfg->huffman_enc() == bitar::HuffmanEncoding::DYNAMIC);  // the reference default
+      cfg->set_huffman_enc(cs.huff);
     }
     CHECK_OK(d->Initialize(std::move(cfg)));
     CHECK(d->Compress(5, host_in).status().IsInvalid());  // qp out of range
@@ -139,10 +147,7 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
     const auto nseg = (data.size() + seg - 1) / seg;
     CHECK(comp->size() == nseg);
     for (const auto& b : *comp) CHECK(!b->is_cpu());
-    WriteSegments(outdir + (codec == bitar::Codec::DEFLATE ? "/deflate.segs"
-                            : codec == bitar::Codec::LZ4   ? "/lz4.segs"
-                                                           : "/zstd.segs"),
-                  *comp);
+    WriteSegments(outdir + cs.file, *comp);
 
     auto out = arrow::AllocateResizableBuffer(static_cast<int64_t>(nseg * seg));
     CHECK_OK(out.status());

@@ -15,6 +15,7 @@ ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "libbitar_oracle.so")
 CODEC_LZ4 = 1
 CODEC_DEFLATE = 2
 CODEC_ZSTD = 3
+CODEC_DEFLATE_DYN = 4
 
 BO_OK = 0
 BO_ERR_INVALID = -4
@@ -42,7 +43,8 @@ def lib():
         L.bo_zstd_bound.restype = ctypes.c_uint32
         L.bo_zstd_bound.argtypes = [ctypes.c_uint32]
         for name in ("bo_lz4_decompress_block", "bo_lz4_compress_block", "bo_inflate_raw",
-                     "bo_deflate_fixed_block", "bo_zstd_decompress", "bo_zstd_compress_block"):
+                     "bo_deflate_fixed_block", "bo_zstd_decompress", "bo_zstd_compress_block",
+                     "bo_deflate_dynamic_block"):
             f = getattr(L, name)
             f.restype = ctypes.c_int
             f.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32,
@@ -55,6 +57,10 @@ def lib():
         L.bo_decompress.argtypes = [ctypes.c_int, u8p, u8p, ctypes.c_uint32, ctypes.c_uint32,
                                     u8p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                     u8p, ctypes.c_int]
+        L.bo_deflate_dynamic_mode.restype = ctypes.c_int
+        L.bo_deflate_dynamic_mode.argtypes = [u8p, ctypes.c_uint32]
+        L.bo_huff_lengths.restype = None
+        L.bo_huff_lengths.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u8p]
         L.bo_fill.restype = None
         L.bo_fill.argtypes = [ctypes.c_int, ctypes.c_uint64, u8p, ctypes.c_uint64]
         _lib = L
@@ -107,6 +113,22 @@ def inflate(src, cap):
 
 def deflate_fixed(src):
     return _block(lib().bo_deflate_fixed_block, src, deflate_bound(len(src)))
+
+
+def deflate_dynamic(src):
+    return _block(lib().bo_deflate_dynamic_block, src, deflate_bound(len(src)))
+
+
+def deflate_dynamic_mode(src):
+    a = np.ascontiguousarray(np.frombuffer(bytes(src), dtype=np.uint8))
+    return lib().bo_deflate_dynamic_mode(_ptr(a), a.size)
+
+
+def huff_lengths(freq, maxlen):
+    f = np.ascontiguousarray(freq, dtype=np.uint32)
+    out = np.zeros(f.size, np.uint8)
+    lib().bo_huff_lengths(_ptr(f), f.size, maxlen, _ptr(out))
+    return out
 
 
 def zstd_bound(n):

@@ -53,11 +53,15 @@ def test_frontend_on_gpu(tmp_path):
     r = subprocess.run([BIN, "gpu", str(inp), str(tmp_path)], capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
-    segs = _segments(tmp_path / "deflate.segs")
     seg = 59460
-    assert len(segs) == (len(data) + seg - 1) // seg
-    for i, s in enumerate(segs):
-        assert zlib.decompress(s, -15) == data[i * seg:(i + 1) * seg]
+    # DYNAMIC (the reference default) is the oracle's dynamic stream; FIXED the fixed one
+    for name, enc in (("deflate.segs", O.deflate_dynamic), ("deflate_fixed.segs", O.deflate_fixed)):
+        segs = _segments(tmp_path / name)
+        assert len(segs) == (len(data) + seg - 1) // seg
+        for i, s in enumerate(segs):
+            plain = data[i * seg:(i + 1) * seg]
+            assert zlib.decompress(s, -15) == plain
+            assert enc(plain) == (0, s), (name, i)
     segs = _segments(tmp_path / "lz4.segs")
     seg = 65536
     assert len(segs) == (len(data) + seg - 1) // seg

@@ -108,3 +108,110 @@ def test_full_size_deflate_roundtrip(eng, kind):
         assert zlib.decompress(blob, -15) == plain
     del data, slab, out
     torch.cuda.empty_cache()
+
+
+# ---- dynamic Huffman (HuffmanEncoding::DYNAMIC, the reference default) ---------------------
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("seg", [59460, 65536, 2048, 100, 13, 8])
+def test_deflate_dynamic_bit_exact_vs_oracle(eng, kind, seg, inflate_decoder):
+    """deflate_dyn_parse_kernel + deflate_dyn_emit_kernel emit the oracle's exact stream
+    (dynamic, fixed or stored block, whichever is smallest); zlib decodes every segment and
+    our inflaters round-trip it."""
+    import bitar_amd
+    if inflate_decoder != 16 and seg != 59460:
+        pytest.skip("compress parity is decoder-independent: one decoder per extra size")
+    n = 3 * seg + seg // 3 + 1 if seg > 100 else 700
+    data = O.fill(kind, 93, n)
+    slab, stride, sizes = eng.compress(bitar_amd.CODEC_DEFLATE_DYNAMIC, up(data)[:n], seg)
+    eng.sync()
+    r, oslab, osizes = O.compress_segments(O.CODEC_DEFLATE_DYN, data, seg, stride)
+    assert r == 0
+    gsizes = down(sizes).astype(np.uint32)
+    assert np.array_equal(gsizes, osizes)
+    gslab = down(slab)
+    for i in range(gsizes.size):
+        a = gslab[i * stride:i * stride + gsizes[i]]
+        b = oslab[i * stride:i * stride + osizes[i]]
+        assert np.array_equal(a, b), f"segment {i}"
+        plain = data[i * seg:(i + 1) * seg].tobytes()
+        assert zlib.decompress(a.tobytes(), -15) == plain
+    out, prod = eng.decompress(bitar_amd.CODEC_DEFLATE_DYNAMIC, slab, stride, sizes, seg)
+    eng.sync()
+    assert np.array_equal(down(out)[:n], data)
+
+
+def test_deflate_dynamic_covers_every_block_type(eng, inflate_decoder):
+    """Inputs that make the encoder choose stored (random), fixed (tiny) and dynamic blocks,
+    in one ragged batch, including a 65536-B stored segment (two stored blocks)."""
+    import bitar_amd
+    if inflate_decoder != 16:
+        pytest.skip("one decoder suffices")
+    seg = 65536
+    parts = [O.fill(0, 1, seg), O.fill(1, 2, 40), O.fill(6, 3, seg), O.fill(3, 4, seg),
+             O.fill(0, 5, 5000), bytes([7]) * 1 + b"", O.fill(2, 6, 20000)]
+    modes = set()
+    for p in parts:
+        p = bytes(p)
+        modes.add(O.deflate_dynamic_mode(p))
+        data = np.frombuffer(p, np.uint8)
+        slab, stride, sizes = eng.compress(bitar_amd.CODEC_DEFLATE_DYNAMIC, up(data)[:len(p)], seg)
+        eng.sync()
+        g = down(slab)[:int(down(sizes)[0])].tobytes()
+        assert (0, g) == O.deflate_dynamic(p)
+        assert zlib.decompress(g, -15) == p
+    assert modes == {0, 1, 2}
+
+
+def test_deflate_dynamic_scattered_slots(eng, inflate_decoder):
+    """compress_scattered (the C++ slot pool's form) writes the same streams."""
+    import bitar_amd
+    if inflate_decoder != 16:
+        pytest.skip("one decoder suffices")
+    seg = 59460
+    n = 5 * seg + 99
+    data = O.fill(2, 8, n)
+    stride = bitar_amd.slot_size(bitar_amd.CODEC_DEFLATE_DYNAMIC, seg)
+    nseg = (n + seg - 1) // seg
+    slots = eng.empty(nseg * stride * 2)
+    order = [3, 0, 5, 1, 4, 2]  # slot k of segment i: a permuted, non-contiguous layout
+    ptrs = torch.tensor([slots.data_ptr() + order[i] * 2 * stride for i in range(nseg)],
+                        dtype=torch.int64).cuda()
+    sizes = eng.empty(nseg, dtype=torch.int32)
+    L = bitar_amd.lib()
+    import ctypes
+    bitar_amd.check(L.bitar_hip_compress_scattered(
+        eng.ctx, eng._stream(None), bitar_amd.CODEC_DEFLATE_DYNAMIC,
+        ctypes.c_void_p(up(data).data_ptr()), n, seg, ctypes.c_void_p(ptrs.data_ptr()), stride,
+        ctypes.c_void_p(sizes.data_ptr())))
+    eng.sync()
+    gs = down(sizes).astype(np.uint32)
+    s = down(slots)
+    for i in range(nseg):
+        plain = data[i * seg:(i + 1) * seg].tobytes()
+        blob = s[order[i] * 2 * stride:order[i] * 2 * stride + gs[i]].tobytes()
+        assert (0, blob) == O.deflate_dynamic(plain), i
+
+
+@pytest.mark.parametrize("kind", [1, 2])
+def test_full_size_deflate_dynamic_roundtrip(eng, kind, inflate_decoder):
+    """1 GiB at 59460-B segments with dynamic Huffman: round trip + zlib + oracle samples."""
+    import bitar_amd
+    if inflate_decoder == 32:
+        pytest.skip("lanes16 and wave decoders cover the full size")
+    n = 1 << 30
+    seg = 59460
+    data = eng.empty(n)
+    eng.fill(kind, 6, data)
+    slab, stride, sizes = eng.compress(bitar_amd.CODEC_DEFLATE_DYNAMIC, data, seg)
+    eng.sync()
+    out, prod = eng.decompress(bitar_amd.CODEC_DEFLATE_DYNAMIC, slab, stride, sizes, seg)
+    eng.sync()
+    assert torch.equal(out[:n], data)
+    gs = down(sizes).astype(np.uint32)
+    for i in (0, 1, 9000, gs.size - 1):
+        blob = down(slab[i * stride:i * stride + int(gs[i])]).tobytes()
+        plain = down(data[i * seg:min(n, (i + 1) * seg)]).tobytes()
+        assert zlib.decompress(blob, -15) == plain
+        assert (0, blob) == O.deflate_dynamic(plain)
+    del data, slab, out
+    torch.cuda.empty_cache()

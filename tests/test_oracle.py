@@ -246,3 +246,56 @@ def test_oracle_zstd_block_split_rule(kind):
     assert all(b[2] == 256 for b in blocks[:-1] if b[0] == 2)
     if kind in (1, 6):
         assert len(blocks) > 1  # the split path is exercised
+
+
+# ---- dynamic-Huffman DEFLATE (oracle/bitar_deflate_dyn.c) ----------------------------------
+def test_deflate_dynamic_zlib_decodes_every_kind():
+    import zlib
+    for kind in range(7):
+        for n in (1, 2, 12, 13, 64, 100, 4096, 59460, 65536):
+            d = O.fill(kind, 3, n).tobytes()
+            r, c = O.deflate_dynamic(d)
+            assert r == 0 and zlib.decompress(c, -15) == d, (kind, n)
+            r2, p = O.inflate(c, n)
+            assert r2 == 0 and p == d
+            assert len(c) <= O.deflate_bound(n)
+
+
+def test_deflate_dynamic_beats_fixed_on_compressible_data():
+    for kind in (1, 2, 5, 6):
+        d = O.fill(kind, 4, 59460).tobytes()
+        assert len(O.deflate_dynamic(d)[1]) < len(O.deflate_fixed(d)[1])
+    assert O.deflate_dynamic_mode(O.fill(0, 1, 59460).tobytes()) == 0   # random -> stored
+    assert O.deflate_dynamic_mode(O.fill(6, 1, 59460).tobytes()) == 2   # text -> dynamic
+    assert O.deflate_dynamic_mode(b"abc") == 1                          # tiny -> fixed
+
+
+def _kraft(lens, maxlen):
+    return sum(1 << (maxlen - int(x)) for x in lens if x)
+
+
+def test_huff_lengths_are_complete_and_limited():
+    """Length limiting (zlib's gen_bitlen scheme) on skewed (Fibonacci) and random
+    frequencies: every code complete (Kraft sum exactly 1), no length above the limit."""
+    rng = np.random.default_rng(1)
+    fib = [1, 1]
+    while len(fib) < 40:
+        fib.append(fib[-1] + fib[-2])
+    cases = [(np.array(fib[:30], np.uint32), 15), (np.array(fib[:19], np.uint32), 7)]
+    f = np.zeros(286, np.uint32)
+    f[:30] = fib[:30]
+    cases.append((f, 15))
+    for t in range(200):
+        nsym = int(rng.choice([19, 30, 286]))
+        ml = 7 if nsym == 19 else 15
+        f = np.zeros(nsym, np.uint32)
+        k = int(rng.integers(1, nsym + 1))
+        idx = rng.choice(nsym, k, replace=False)
+        f[idx] = (rng.pareto(0.5, k) * 3 + 1).astype(np.uint32) if t % 2 else rng.integers(1, 1000, k)
+        cases.append((f, ml))
+    for f, ml in cases:
+        lens = O.huff_lengths(f, ml)
+        assert lens.max() <= ml
+        assert _kraft(lens, ml) == 1 << ml
+        if (f > 0).sum() >= 2:
+            assert np.array_equal(lens > 0, f > 0)
