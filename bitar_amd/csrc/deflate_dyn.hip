@@ -27,6 +27,10 @@ namespace dyn {
 
 using namespace cmp;
 
+#ifndef BITAR_DYN_VARIANT
+#define BITAR_DYN_VARIANT 0  // timing experiments only (scripts/build_variant.sh)
+#endif
+
 constexpr uint32_t kPlanBytes = 2048;  // per segment: histograms + record count
 constexpr uint32_t kNLit = 286, kNDist = 30, kNCl = 19;
 constexpr uint32_t kPlanRecBytes = kNLit + kNDist;  // word index of the record byte count
@@ -60,9 +64,21 @@ __device__ __forceinline__ uint32_t fixed_len(uint32_t s) {
 }
 
 // ---- pass 1: records + histograms ---------------------------------------------------------
-struct RecOut : ByteOut {
-  uint32_t* lh;  // LDS literal/length histogram (286)
-  uint32_t* dh;  // LDS distance histogram (30)
+// Scratch per segment: [plan kPlanBytes][window masks kMaskBytes][match records ...].
+// Window w: 16 B = the lanes that start a selected match (u64) + the lanes that emit a
+// literal (u64); match k of the segment: one u32 = length symbol - 257 (5 bits) | its extra
+// bits (5) | distance symbol (5) | its extra bits (<= 10) -- the emit pass needs neither the
+// parse's coverage rule nor the symbol arithmetic again.
+constexpr uint32_t kMaskBytes = 16384;  // <= 1024 windows (n <= 65536)
+constexpr uint32_t kPlanWindows = kPlanRecBytes + 1;  // word index of the window count
+constexpr uint32_t kPlanTail = kPlanRecBytes + 2;     // word index of the tail start
+
+struct RecOut : ByteOut {  // the byte ring carries the match records
+  uint32_t* lh;          // LDS literal/length histogram (286)
+  uint32_t* dh;          // LDS distance histogram (30)
+  uint4* cst;            // LDS ring of 64 window mask pairs
+  GMEM uint4* cdst;      // mask area
+  uint32_t nwin, cflushed;
 
   __device__ __forceinline__ void window(const GMEM uint8_t*, const InRing&, const Window& W,
                                          uint32_t, uint32_t n) {
@@ -72,27 +88,41 @@ struct RecOut : ByteOut {
     const uint32_t pend = wave_incl_max(cl ? q + W.mlen : 0u);
     const bool covered = q < W.pos_in || (!cl && q < pend);
     const bool lit = !cl && !covered && q < n;
-    uint32_t nx, xv;
-    const uint32_t ls = len_sym(cl ? W.mlen : 3u, nx, xv);
-    const uint32_t ds = dist_sym(cl ? W.off : 1u, nx, xv);
+    const uint64_t litm = ballot(lit);
+    uint32_t lnx, lxv, dnx, dxv;
+    const uint32_t ls = len_sym(cl ? W.mlen : 3u, lnx, lxv);
+    const uint32_t ds = dist_sym(cl ? W.off : 1u, dnx, dxv);
     lds_order();
     if (lit) atomicAdd(&lh[W.byte], 1u);
     if (cl) {
       atomicAdd(&lh[257 + ls], 1u);
       atomicAdd(&dh[ds], 1u);
     }
+    if (lane == 0)
+      cst[nwin & 63u] = make_uint4((uint32_t)W.chain, (uint32_t)(W.chain >> 32), (uint32_t)litm,
+                                   (uint32_t)(litm >> 32));
     lds_order();
-    if (overflow) return;
+    ++nwin;
+    if (overflow || !W.chain) return;
     const uint32_t nm = (uint32_t)__builtin_popcountll(W.chain);
-    const uint32_t total = 8 + 4 * nm;
-    if (!room(total)) return;
+    if (!room(4 * nm)) return;
     const uint32_t rank = (uint32_t)__builtin_popcountll(W.chain & ((1ull << lane) - 1));
     uint32_t* r32 = reinterpret_cast<uint32_t*>(ring);
     lds_order();
-    if (lane < 2) r32[at(op + 4 * lane) >> 2] = lane ? (uint32_t)(W.chain >> 32) : (uint32_t)W.chain;
-    if (cl) r32[at(op + 8 + 4 * rank) >> 2] = W.mlen | (W.off << 16);
+    if (cl) r32[at(op + 4 * rank) >> 2] = ls | (lxv << 5) | (ds << 10) | (dxv << 15);
     lds_order();
-    op += total;
+    op += 4 * nm;
+  }
+  // window masks [cflushed, upto) to HBM, one window (16 B) per lane
+  __device__ __forceinline__ void flush_masks(uint32_t upto) {
+    const uint32_t lane = lane_id();
+    lds_order();
+    for (uint32_t w = cflushed + lane; w < upto; w += kWave) cdst[w] = cst[w & 63u];
+    cflushed = upto;
+  }
+  __device__ __forceinline__ void drain() {
+    ByteOut::drain();
+    flush_masks(nwin);
   }
   // the tail literals [s, s + n)
   __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I, uint32_t s,
@@ -144,19 +174,35 @@ __device__ void huff_lengths(const uint32_t* freq, uint32_t nsym, uint32_t maxle
   }
   lds_order();
   m = m < 2 ? 2u : m;
-  // leaves in (frequency, symbol) order: rank of every used symbol
-  for (uint32_t s0 = 0; s0 < nsym; s0 += kWave) {
-    const uint32_t s = s0 + lane;
-    const uint32_t fs = s < nsym ? T.fw[s] : 0u;
-    uint32_t r = 0;
-    for (uint32_t t = 0; t < nsym; ++t) {
-      const uint32_t ft = T.fw[t];
-      r += (ft != 0u && (ft < fs || (ft == fs && t < s))) ? 1u : 0u;
-    }
-    lds_order();
-    if (fs) T.leaf[r] = (uint16_t)s;
-    lds_order();
+  // leaves in (frequency, symbol) order: rank of every used symbol.  Keys (f << 9 | s) are
+  // unique; an unused symbol's key is ~0 (never below a used one).  Each lane holds the keys
+  // of symbols lane + 64 k in registers and counts the smaller keys of all symbols via
+  // readlane: no LDS round trip per comparison.
+  constexpr uint32_t kMaxChunks = (kNLit + kWave - 1) / kWave;  // 5
+  const uint32_t nch = (nsym + kWave - 1) / kWave;
+  uint32_t key[kMaxChunks], rank[kMaxChunks];
+#pragma unroll
+  for (uint32_t c = 0; c < kMaxChunks; ++c) {
+    const uint32_t s = c * kWave + lane;
+    const uint32_t f = c < nch && s < nsym ? T.fw[s] : 0u;
+    key[c] = f ? (f << 9) | s : ~0u;
+    rank[c] = 0;
   }
+  for (uint32_t c2 = 0; c2 < nch; ++c2) {
+    uint32_t kc = key[0];
+#pragma unroll
+    for (uint32_t c = 1; c < kMaxChunks; ++c) kc = c2 == c ? key[c] : kc;  // (c2 uniform)
+    for (uint32_t t = 0; t < kWave; ++t) {
+      const uint32_t kt = readlane(kc, t);
+#pragma unroll
+      for (uint32_t c = 0; c < kMaxChunks; ++c) rank[c] += kt < key[c] ? 1u : 0u;
+    }
+  }
+  lds_order();
+#pragma unroll
+  for (uint32_t c = 0; c < kMaxChunks; ++c)
+    if (key[c] != ~0u) T.leaf[rank[c]] = (uint16_t)(key[c] & 511u);
+  lds_order();
   if (lane == 0) {
     for (uint32_t k = 0; k < m; ++k) T.w[k] = T.fw[T.leaf[k]];
     uint32_t i = 0, j = m, next = m, no = 0;
@@ -209,33 +255,43 @@ __device__ void huff_lengths(const uint32_t* freq, uint32_t nsym, uint32_t maxle
   lds_order();
 }
 
-// canonical codes (RFC 1951 3.2.2), bit-reversed: tab[s] = code | len << 16
-__device__ void canon_codes(const uint8_t* lens, uint32_t n, uint32_t* tab, TreeLds& T) {
+// canonical codes (RFC 1951 3.2.2), bit-reversed: tab[s] = code | len << 16.  Lane-parallel:
+// a symbol's code = first code of its length + the number of earlier symbols of that length
+// (ballots per 64-symbol chunk, counts carried per length).
+__device__ void canon_codes(const uint8_t* lens, uint32_t n, uint32_t* tab) {
   const uint32_t lane = lane_id();
-  if (lane == 0) {
-    uint32_t bl[16];
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t cnt[16];  // per length: symbols so far (uniform)
 #pragma unroll
-    for (int b = 0; b < 16; ++b) bl[b] = 0;
-    for (uint32_t s = 0; s < n; ++s) {
-      const uint32_t l = lens[s];
+  for (int b = 0; b < 16; ++b) cnt[b] = 0;
+  lds_order();
+  for (uint32_t s0 = 0; s0 < n; s0 += kWave) {
+    const uint32_t s = s0 + lane;
+    const uint32_t l = s < n ? lens[s] : 0u;
 #pragma unroll
-      for (int b = 1; b < 16; ++b) bl[b] += l == (uint32_t)b ? 1u : 0u;
-    }
-    uint32_t code = 0;
+    for (int b = 1; b < 16; ++b) cnt[b] += (uint32_t)__builtin_popcountll(ballot(l == (uint32_t)b));
+  }
+  uint32_t first[16];
+  uint32_t code = 0;
+  first[0] = 0;
+#pragma unroll
+  for (int b = 1; b < 16; ++b) {
+    code = (code + (b > 1 ? cnt[b - 1] : 0u)) << 1;
+    first[b] = code;
+    cnt[b - 1] = 0;
+  }
+  cnt[15] = 0;
+  for (uint32_t s0 = 0; s0 < n; s0 += kWave) {
+    const uint32_t s = s0 + lane;
+    const uint32_t l = s < n ? lens[s] : 0u;
+    uint32_t c = 0;
 #pragma unroll
     for (int b = 1; b < 16; ++b) {
-      code = (code + (b > 1 ? bl[b - 1] : 0u)) << 1;
-      T.blc[b] = (uint16_t)code;
+      const uint64_t m = ballot(l == (uint32_t)b);
+      c = l == (uint32_t)b ? first[b] + cnt[b] + (uint32_t)__builtin_popcountll(m & lt) : c;
+      cnt[b] += (uint32_t)__builtin_popcountll(m);
     }
-    for (uint32_t s = 0; s < n; ++s) {
-      const uint32_t l = lens[s];
-      uint32_t c = 0;
-      if (l) {
-        c = T.blc[l];
-        T.blc[l] = (uint16_t)(c + 1);
-      }
-      tab[s] = (l ? __builtin_bitreverse32(c) >> (32 - l) : 0u) | (l << 16);
-    }
+    if (s < n) tab[s] = (l ? __builtin_bitreverse32(c) >> (32 - l) : 0u) | (l << 16);
   }
   lds_order();
 }
@@ -272,7 +328,10 @@ __device__ uint32_t rle_lens(const uint8_t* lens, uint32_t n, uint16_t* out) {
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return readlane(wave_incl_sum(v), 63); }
 
 // ---- pass 2 output: LDS bit ring of 64-bit lane contributions -----------------------------
-constexpr uint32_t kStageWords = 512, kStageMask = kStageWords - 1;
+constexpr uint32_t kB = 4;  // windows per emit step
+constexpr uint32_t kStageWords = 1024, kStageMask = kStageWords - 1;
+// one window adds <= 64 lanes x 45 bits = 90 words (+2 for the spill)
+constexpr uint32_t kFlushMargin = kB * 92 + 8;
 
 struct BitOut {
   uint32_t* stage;     // LDS, zero outside the pending range
@@ -292,24 +351,87 @@ struct BitOut {
     lds_order();
     wflushed = upto;
   }
+  __device__ __forceinline__ void or3(uint64_t bp, uint64_t val, uint32_t nb) {
+    const uint32_t w = (uint32_t)(bp >> 5), sh = (uint32_t)(bp & 31);
+    const uint64_t lo = val << sh;
+    const uint32_t w2 = sh && sh + nb > 64 ? (uint32_t)(val >> (64 - sh)) : 0u;
+    atomicOr(&stage[w & kStageMask], (uint32_t)lo);
+    atomicOr(&stage[(w + 1) & kStageMask], (uint32_t)(lo >> 32));
+    atomicOr(&stage[(w + 2) & kStageMask], w2);
+  }
   // append each lane's (val, nb) in lane order, nb <= 64
   __device__ __forceinline__ void put(uint64_t val, uint32_t nb) {
     if (overflow) return;
     const uint32_t incl = wave_incl_sum(nb);
     const uint32_t total = readlane(incl, 63);
     if ((bits + total + 7) / 8 > cap) { overflow = true; return; }
-    const uint64_t bp = bits + incl - nb;
-    const uint32_t w = (uint32_t)(bp >> 5), sh = (uint32_t)(bp & 31);
-    const uint64_t lo = val << sh;
-    const uint32_t w2 = sh && sh + nb > 64 ? (uint32_t)(val >> (64 - sh)) : 0u;
     lds_order();
-    atomicOr(&stage[w & kStageMask], (uint32_t)lo);
-    atomicOr(&stage[(w + 1) & kStageMask], (uint32_t)(lo >> 32));
-    atomicOr(&stage[(w + 2) & kStageMask], w2);
+    or3(bits + incl - nb, val, nb);
     lds_order();
     bits += total;
     const uint32_t full = (uint32_t)(bits >> 5);
-    if (full - wflushed >= kStageWords - 128) flush_words(full);  // a put adds <= 91 words
+    if (full - wflushed >= kStageWords - kFlushMargin) flush_words(full);
+  }
+  // kB windows at once: window k's lanes follow window k-1's (independent prefix sums)
+  __device__ __forceinline__ void put_multi(const uint64_t* val, const uint32_t* nb) {
+    if (overflow) return;
+    uint32_t incl[kB], total = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kB; ++k) incl[k] = wave_incl_sum(nb[k]);
+    uint64_t base[kB];
+#pragma unroll
+    for (uint32_t k = 0; k < kB; ++k) {
+      base[k] = bits + total;
+      total += readlane(incl[k], 63);
+    }
+    if ((bits + total + 7) / 8 > cap) { overflow = true; return; }
+    lds_order();
+#pragma unroll
+    for (uint32_t k = 0; k < kB; ++k) or3(base[k] + incl[k] - nb[k], val[k], nb[k]);
+    lds_order();
+    bits += total;
+    const uint32_t full = (uint32_t)(bits >> 5);
+    if (full - wflushed >= kStageWords - kFlushMargin) flush_words(full);
+  }
+};
+
+// A global byte range streamed through a 2 KiB LDS ring in 1 KiB rows (16 B per lane, the
+// next row prefetched into registers a whole row ahead): the emit pass's per-window reads
+// are LDS reads, never a dependent HBM round trip.  Byte k of the range (relative to the
+// 16-B aligned base) lives at ring[k & 2047] once ensure(k + 1) has run.
+struct RowRing {
+  const GMEM uint4* src16;  // 16-B aligned base of the range
+  uint32_t limit;           // bytes readable from src16 (blocks at or past it are not loaded)
+  uint8_t* ring;            // 2 KiB of LDS
+  uint32_t loaded;          // [0, loaded) committed; the ring holds [loaded - 2048, loaded)
+  uint4 nxt;                // the next row, in flight
+
+  __device__ __forceinline__ uint4 load_row(uint32_t r) const {
+    const uint32_t o = 1024u * r + 16u * lane_id();
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (o < limit) v = src16[o >> 4];
+    return v;
+  }
+  __device__ __forceinline__ void init(const GMEM uint4* base, uint32_t lim, uint8_t* lds) {
+    src16 = base;
+    limit = lim;
+    ring = lds;
+    loaded = 0;
+    nxt = load_row(0);
+  }
+  __device__ __forceinline__ void ensure(uint32_t end) {
+    while (loaded < end) {
+      const uint32_t r = loaded >> 10;
+      lds_order();
+      reinterpret_cast<uint4*>(ring)[((r & 1u) << 6) + lane_id()] = nxt;
+      lds_order();
+      loaded += 1024;
+      nxt = load_row(r + 1);
+    }
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t k) const { return ring[k & 2047u]; }
+  __device__ __forceinline__ uint32_t word(uint32_t k) const {  // k 4-aligned
+    return reinterpret_cast<const uint32_t*>(ring)[(k & 2047u) >> 2];
   }
 };
 
@@ -322,6 +444,7 @@ __global__ __launch_bounds__(64) void deflate_dyn_parse_kernel(
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
+  __shared__ __attribute__((aligned(16))) uint4 cst[64];
   __shared__ uint32_t hist[kNLit + kNDist];
   const uint32_t i_seg = blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
@@ -331,20 +454,29 @@ __global__ __launch_bounds__(64) void deflate_dyn_parse_kernel(
   GMEM uint8_t* scr = global_ptr(scratch + (uint64_t)i_seg * scr_stride);
   RecOut o;
   o.ring = obuf;
-  o.dst = scr + kPlanBytes;
-  o.cap = scr_stride - kPlanBytes;
+  o.dst = scr + kPlanBytes + kMaskBytes;
+  o.cap = scr_stride - kPlanBytes - kMaskBytes;
   o.op = 0;
   o.flushed = 0;
   o.overflow = false;
   o.lh = hist;
   o.dh = hist + kNLit;
-  parse(global_ptr(input + seg_off), n, global_ptr(input + n_total), table, inring, kMaxDist,
-        258u, o);
+  o.cst = cst;
+  o.cdst = reinterpret_cast<GMEM uint4*>(scr + kPlanBytes);
+  o.nwin = 0;
+  o.cflushed = 0;
+  const uint32_t tail = parse(global_ptr(input + seg_off), n, global_ptr(input + n_total), table,
+                             inring, kMaxDist, 258u, o);
   o.flush(o.op, true);
+  o.flush_masks(o.nwin);
   lds_order();
   GMEM uint32_t* plan = reinterpret_cast<GMEM uint32_t*>(scr);
   for (uint32_t k = lane_id(); k < kNLit + kNDist; k += kWave) plan[k] = hist[k];
-  if (lane_id() == 0) plan[kPlanRecBytes] = o.overflow ? 0xFFFFFFFFu : o.op;
+  if (lane_id() == 0) {
+    plan[kPlanRecBytes] = o.overflow ? 0xFFFFFFFFu : o.op;
+    plan[kPlanWindows] = o.nwin;
+    plan[kPlanTail] = tail;
+  }
   if (o.overflow && lane_id() == 0) atomicOr(err, 2u);
 }
 
@@ -362,8 +494,10 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
   __shared__ uint16_t cls[kNLit + kNDist + 4];
   __shared__ uint32_t clf[kNCl];
   // the tree scratch and the output bit ring share LDS: codes are built before any output
-  __shared__ __attribute__((aligned(16))) uint8_t pool[sizeof(TreeLds) > kStageWords * 4
-                                                           ? sizeof(TreeLds) : kStageWords * 4];
+  // (codes first; then the bit ring + the chain, record and input rings, 2 KiB each)
+  constexpr uint32_t kEmitLds = kStageWords * 4 + 3 * 2048;
+  __shared__ __attribute__((aligned(16))) uint8_t pool[sizeof(TreeLds) > kEmitLds
+                                                           ? sizeof(TreeLds) : kEmitLds];
   TreeLds& T = *reinterpret_cast<TreeLds*>(pool);
   const uint32_t lane = lane_id();
   const uint32_t i_seg = blockIdx.x;
@@ -385,8 +519,13 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
   uint8_t* ll = lens;
   uint8_t* dl = lens + kNLit;
   uint8_t* cll = lens + kNLit + kNDist;
+#if BITAR_DYN_VARIANT == 2  // timing experiment: no code construction (fixed codes)
+  for (uint32_t s = lane; s < kNLit + kNDist + kNCl; s += kWave) lens[s] = 8;
+  if (lane == 0) hist[0] = 0x7FFFFFFF;
+#else
   huff_lengths(hist, kNLit, 15, ll, T);
   huff_lengths(hist + kNLit, kNDist, 15, dl, T);
+#endif
   // HLIT / HDIST: trailing zero lengths trimmed
   uint32_t hlit = 257, hdist = 1;
   for (uint32_t s = lane; s < kNLit; s += kWave)
@@ -408,7 +547,9 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
   lds_order();
   for (uint32_t k = lane; k < ncl; k += kWave) atomicAdd(&clf[cls[k] & 31u], 1u);
   lds_order();
+#if BITAR_DYN_VARIANT != 2
   huff_lengths(clf, kNCl, 7, cll, T);
+#endif
   // the code-length code's lengths in transmission order, trailing zeros trimmed
   uint32_t hclen = 4;
   if (lane < kNCl && cll[kClo[lane]]) hclen = lane + 1;
@@ -458,16 +599,16 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
   }
   // codes
   if (mode == 2) {
-    canon_codes(ll, kNLit, ltab, T);
-    canon_codes(dl, kNDist, dtab, T);
-    canon_codes(cll, kNCl, ctab, T);
+    canon_codes(ll, kNLit, ltab);
+    canon_codes(dl, kNDist, dtab);
+    canon_codes(cll, kNCl, ctab);
   } else {
     uint8_t* fl = reinterpret_cast<uint8_t*>(T.w);  // 288 fixed lengths
     for (uint32_t s = lane; s < 288; s += kWave) fl[s] = (uint8_t)fixed_len(s);
     if (lane < kNDist) lens[kNLit + lane] = 5;
     lds_order();
-    canon_codes(fl, 288, ltab, T);
-    canon_codes(dl, kNDist, dtab, T);  // dl = 5 everywhere now
+    canon_codes(fl, 288, ltab);
+    canon_codes(dl, kNDist, dtab);  // dl = 5 everywhere now
   }
   // the bit ring (over the tree scratch): zero, then the block header
   uint32_t* stage = reinterpret_cast<uint32_t*>(pool);
@@ -508,49 +649,66 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
     hbits = (uint32_t)bp;
   }
   lds_order();
-  o.bits = readlane(hbits, 0);  // < kStageWords * 32 - 128 * 32: no flush needed yet
+  o.bits = readlane(hbits, 0);  // < kStageWords * 32 - the flush margin: no flush needed yet
 
-  // symbols, window by window from the records
-  const GMEM uint32_t* rec = reinterpret_cast<const GMEM uint32_t*>(scr + kPlanBytes);
-  uint32_t pos = 0, emitted = 0, rp = 0;
-  if (n >= kMfLimit + 1) {
-    const uint32_t last_start = n - kMfLimit;
-    for (uint32_t x = 0; x <= last_start; x += kWave) {
-      const uint64_t chain = (uint64_t)rec[rp] | ((uint64_t)rec[rp + 1] << 32);
-      const uint32_t q = x + lane;
-      const bool cl = (chain >> lane) & 1;
-      const uint32_t rank = (uint32_t)__builtin_popcountll(chain & ((1ull << lane) - 1));
-      const uint32_t r = cl ? rec[rp + 2 + rank] : 0x00010003u;
-      const uint32_t byte = q < n ? (uint32_t)in[q] : 0u;
-      const uint32_t mlen = r & 0xFFFFu, off = r >> 16;
-      const uint32_t pend = wave_incl_max(cl ? q + mlen : 0u);
-      const bool covered = q < pos || (!cl && q < pend);
-      const bool lit = !cl && !covered && q < n;
-      uint32_t lnx, lxv, dnx, dxv;
-      const uint32_t ls = len_sym(mlen, lnx, lxv);
-      const uint32_t ds = dist_sym(off, dnx, dxv);
+  // symbols, kB windows per step (independent LDS reads and prefix sums across the
+  // windows of a step); window masks, match records and input bytes stream through LDS rings
+  RowRing C, R, I;
+  const uint32_t s0 = (uint32_t)((uintptr_t)in & 15u);
+  const uint32_t nwin = plan[kPlanWindows];
+  uint32_t emitted = plan[kPlanTail];
+  {
+    uint8_t* rings = pool + kStageWords * 4;
+    C.init(reinterpret_cast<const GMEM uint4*>(scr + kPlanBytes), 16 * nwin, rings);
+    R.init(reinterpret_cast<const GMEM uint4*>(scr + kPlanBytes + kMaskBytes),
+           (plan[kPlanRecBytes] + 15u) & ~15u, rings + 2048);
+    const uint64_t span = (uint64_t)(global_ptr(input + n_total) - (in - s0));
+    I.init(reinterpret_cast<const GMEM uint4*>(in - s0),
+           (uint32_t)(span < (uint64_t)n + s0 ? span : (uint64_t)n + s0), rings + 4096);
+  }
+  if (BITAR_DYN_VARIANT == 1) emitted = n;  // timing experiment: no symbol emission
+  if (BITAR_DYN_VARIANT != 1) {
+    const uint64_t lt = (1ull << lane) - 1;
+    uint32_t rp = 0;  // record byte offset
+    for (uint32_t w0 = 0; w0 < nwin; w0 += kB) {
+      C.ensure(16 * (w0 + kB));
+      R.ensure(rp + 4 * kWave * kB);
+      I.ensure(s0 + kWave * (w0 + kB));
       lds_order();
-      const uint32_t lt = ltab[cl ? 257 + ls : byte];
-      const uint32_t dt = dtab[ds];
-      const uint32_t ln = lt >> 16, dn = dt >> 16;
-      const uint64_t mv = (uint64_t)(lt & 0xFFFFu) | ((uint64_t)lxv << ln) |
-                          ((uint64_t)(dt & 0xFFFFu) << (ln + lnx)) |
-                          ((uint64_t)dxv << (ln + lnx + dn));
-      const uint32_t mb = ln + lnx + dn + dnx;
-      o.put(cl ? mv : lit ? (uint64_t)(lt & 0xFFFFu) : 0ull, cl ? mb : lit ? ln : 0u);
-      if (chain) {
-        const uint32_t hl = highbit(chain);
-        pos = x + hl + readlane(mlen, hl);
+      uint64_t val[kB];
+      uint32_t nb[kB];
+      uint32_t rb = rp;
+#pragma unroll
+      for (uint32_t k = 0; k < kB; ++k) {
+        const uint32_t w = w0 + k;
+        const bool valid = w < nwin;
+        const uint64_t chain = valid ? (uint64_t)C.word(16 * w) | ((uint64_t)C.word(16 * w + 4) << 32) : 0ull;
+        const uint64_t litm = valid ? (uint64_t)C.word(16 * w + 8) | ((uint64_t)C.word(16 * w + 12) << 32) : 0ull;
+        const bool cl = (chain >> lane) & 1, lit = (litm >> lane) & 1;
+        const uint32_t r = R.word(rb + 4 * (uint32_t)__builtin_popcountll(chain & lt));
+        rb += 4 * (uint32_t)__builtin_popcountll(chain);
+        const uint32_t byte = I.byte(s0 + kWave * w + lane);
+        const uint32_t ls = r & 31u, lxv = (r >> 5) & 31u, ds = (r >> 10) & 31u, dxv = r >> 15;
+        const uint32_t lt_ = ltab[cl ? 257 + ls : byte];
+        const uint32_t dt = dtab[ds];
+        const uint32_t ln = lt_ >> 16, dn = dt >> 16;
+        const uint32_t lnx = len_extra_bits(ls), dnx = dist_extra_bits(ds);
+        const uint32_t lo = (lt_ & 0xFFFFu) | (lxv << ln);  // <= 20 bits
+        const uint64_t mv = (uint64_t)lo | ((uint64_t)((dt & 0xFFFFu) | (dxv << dn)) << (ln + lnx));
+        val[k] = cl ? mv : lit ? (uint64_t)(lt_ & 0xFFFFu) : 0ull;
+        nb[k] = cl ? ln + lnx + dn + dnx : lit ? ln : 0u;
       }
-      emitted = pos > x + kWave ? pos : x + kWave;
-      rp += 2 + (uint32_t)__builtin_popcountll(chain);
+      rp = rb;
+      o.put_multi(val, nb);
     }
   }
   // tail literals
   for (uint32_t k = emitted; k < n; k += kWave) {
     const uint32_t q = k + lane;
     const bool act = q < n;
-    const uint32_t b = act ? (uint32_t)in[q] : 0u;
+    I.ensure(s0 + k + kWave);
+    lds_order();
+    const uint32_t b = act ? I.byte(s0 + q) : 0u;
     lds_order();
     const uint32_t lt = ltab[b];
     o.put(act ? (uint64_t)(lt & 0xFFFFu) : 0ull, act ? (lt >> 16) : 0u);

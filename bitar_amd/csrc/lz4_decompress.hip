@@ -203,19 +203,21 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t cml = 4 + (mx ? 15u + b2 : cm4);
       const uint32_t colen = cL + cml;
       // eligible: at most one length byte each (< 255), <= 64 output bytes (so <= 60 literals),
-      // real offset, near, and (conservatively, as if this token opened the batch) not
-      // before the segment start
-      const bool csimple = (!lx || b1 < 255u) && (!mx || b2 < 255u) && colen <= 64u && coff != 0 && coff <= kNearOff && coff <= s.op + cL;
+      // a real offset (any distance: far sources are read back from HBM below), not before
+      // the segment start (conservatively, as if this token opened the batch)
+      const bool csimple = (!lx || b1 < 255u) && (!mx || b2 < 255u) && colen <= 64u && coff != 0 && coff <= s.op + cL;
       // walk record: next token lane (7 bits, <= 127 for an eligible token, see
       // kMaxEligibleNext; the walk stops at a lane >= 64, which was not parsed, after
       // consuming the sequence) | output length (255: not eligible, the walk's one compare
       // then stops; an ineligible token's wider nxt only ORs into those already-set bits).
-      // Sequence record: offset (12 bits; eligible
-      // offsets are <= kNearOff, and never 0) | literal count (6 bits) | token lane (6 bits)
-      // -- the output start goes into bits 24..29 after the walk.
+      // Sequence record: offset mod 4096 (12 bits) | literal count (6 bits) | token lane (6
+      // bits) | bit 30: offset beyond the ring -- the output start goes into bits 24..29
+      // after the walk; offsets >= 4096 (stock streams; ours stay <= 2560) get their high
+      // bits from the token lane below.
       const uint32_t nxt = lane + 3 + (lx ? 1u : 0u) + (mx ? 1u : 0u) + cL;
       const uint32_t pw = nxt | ((csimple ? colen : 255u) << 7);
-      const uint32_t pr = (coff & 4095u) | ((cL & 63u) << 12) | (lane << 18);
+      const uint32_t pr = (coff & 4095u) | ((cL & 63u) << 12) | (lane << 18) |
+                          (coff > kNearOff ? 0x40000000u : 0u);  // bit 30: far offset
       // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
       const uint32_t room = s.cap - s.op;
       const uint32_t lim = room < kBatchOut ? room : kBatchOut;
@@ -223,14 +225,19 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t out = walk_tokens(pw, pr, lim, k, vrec);
       if (out == 0) break;
       // every output byte takes the record of the latest sequence starting at or before it
-      const uint32_t key = wave_incl_max(vrec ? vrec | (lane << 24) : 0u);
-      // (3) sources: window literal / ring history / alias of an earlier byte of the batch
-      // (branch-free: every lane computes both forms).  bit31: alias (low 6 bits: the
-      // source lane); else an LDS byte address.
+      const uint32_t key = wave_incl_max(vrec ? (vrec & 0x00FFFFFFu) | (lane << 24) : 0u);
+      // (3) sources: window literal / ring history / HBM history (far) / alias of an earlier
+      // byte of the batch (branch-free: every lane computes every form).  bit31: alias (low 6
+      // bits: the source lane); bit30: far (low 16 bits: the output position); else an LDS
+      // byte address.
       const uint32_t ostart = key >> 24;
       const uint32_t seqlane = (key >> 18) & 63u;
       const uint32_t jL = (key >> 12) & 63u;
-      const uint32_t joff = key & 4095u;
+      uint32_t joff = key & 4095u;
+      // a sequence of the batch with an offset beyond the ring's reach (stock streams; ours
+      // stay <= 2560): only then the far-history machinery below (a wave-uniform branch)
+      const bool big = ballot(vrec >= 0x40000000u) != 0;
+      if (big) joff |= bpermute_lane(coff & ~4095u, seqlane);  // offsets >= 4096
       const uint32_t r = lane - ostart;
       const bool is_lit = r < jL;
       const uint32_t m = r - jL;
@@ -246,16 +253,28 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
       const uint32_t lit_addr = wrel + seqlane + 1 + (jL >= 15u ? 1u : 0u) + r;
       uint32_t st = is_lit ? lit_addr : srel >= 0 ? ((uint32_t)srel | 0x80000000u) : hist;
+      if (big && srel < -(int32_t)kNearOff && !is_lit)
+        st = (s.op + (uint32_t)srel) | 0x40000000u;  // far: the output position
       // pointer doubling until no lane of the batch aliases another (chains strictly descend)
       const uint64_t live = out >= 64 ? ~0ull : (1ull << out) - 1;  // lanes of the batch
       while (ballot((int32_t)st < 0) & live) {
         const uint32_t other = bpermute_lane(st, st & 63u);
         st = (st & 0x80000000u) ? other : st;
       }
-      // (4) one gather, one store
+      // (4) one gather (LDS, or HBM for far history), one store
       lds_order();
-      const uint8_t g = lds[st & 0x3FFFu];
-      ring[(base + s.op + lane) & kRingMask] = g;
+      uint32_t g = lds[st & 0x3FFFu];
+      if (big) {
+        const bool gfar = (st >> 30) == 1u && lane < out;
+        const uint64_t farm = ballot(gfar);
+        // history only in HBM: make this wave's flushed stores visible to its loads
+        if (farm && (ballot((st & 0xFFFFu) >= s.fenced) & farm)) {
+          global_fence_wave();
+          s.fenced = s.flushed;
+        }
+        if (gfar) g = s.dst[st & 0xFFFFu];
+      }
+      ring[(base + s.op + lane) & kRingMask] = (uint8_t)g;
       lds_order();
       s.ip += k;
       s.op += out;

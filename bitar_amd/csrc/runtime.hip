@@ -299,8 +299,9 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
                        in, n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
   else if (codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC) {
     // pass 1 (parse -> records + histograms) and pass 2 (codes + emit) through a
-    // stream-ordered scratch of 2 KiB plan + one slot per segment (deflate_dyn.hip)
-    const uint64_t scr_stride = bitar_hip_slot_size(BITAR_HIP_CODEC_DEFLATE, seg) + 2048u;
+    // stream-ordered scratch per segment (deflate_dyn.hip)
+    // per segment: 2 KiB plan + 16 KiB of window masks + match records (<= one slot)
+    const uint64_t scr_stride = bitar_hip_slot_size(BITAR_HIP_CODEC_DEFLATE, seg) + 2048u + 16384u;
     void* scratch = nullptr;
     HIP_TRY(hipMallocAsync(&scratch, nseg * scr_stride, s), "scratch allocation");
     hipLaunchKernelGGL(bitar_hip::deflate_dyn_parse_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,

@@ -241,8 +241,9 @@ __device__ __forceinline__ uint32_t chain_fast(uint64_t& m, uint64_t extm, uint3
 
 // The window-scan parse over one segment; hands each window to E::window and the tail to
 // E::sequence.
+// Returns where the tail literals start (the emitter's pending_from).
 template <class E>
-__device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const GMEM uint8_t* in_end,
+__device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, const GMEM uint8_t* in_end,
                                       uint16_t* table, uint8_t* inring, uint32_t max_dist,
                                       uint32_t max_mlen, E& em) {
   const uint32_t lane = lane_id();
@@ -433,6 +434,7 @@ __device__ __forceinline__ void parse(const GMEM uint8_t* in, uint32_t n, const 
   }
   const uint32_t t0 = em.pending_from(anchor, emitted);
   if (t0 < n) em.sequence(in, I, t0, n - t0, 0, 0);
+  return t0;
 }
 
 }  // namespace cmp

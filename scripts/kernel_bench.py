@@ -21,8 +21,8 @@ def main():
     import bitar_amd
     eng = bitar_amd.Engine(0)
     codec = {"lz4": bitar_amd.CODEC_LZ4, "deflate": bitar_amd.CODEC_DEFLATE,
-             "zstd": bitar_amd.CODEC_ZSTD}[a.codec]
-    seg = a.seg or (59460 if a.codec == "deflate" else 65536)
+             "zstd": bitar_amd.CODEC_ZSTD, "deflate_dyn": bitar_amd.CODEC_DEFLATE_DYNAMIC}[a.codec]
+    seg = a.seg or (59460 if a.codec.startswith("deflate") else 65536)
     n = a.bytes
     nseg = (n + seg - 1) // seg
     stride = bitar_amd.slot_size(codec, seg)
