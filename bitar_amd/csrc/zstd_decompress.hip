@@ -453,6 +453,87 @@ __device__ __forceinline__ bool huf_stream(State& s, uint8_t* win, Tabs& t, uint
   return b.bitpos == 0;
 }
 
+// The speculative form of huf_stream: every lane decodes "a symbol starting at bit P - lane"
+// (its table index = the `log` bits below that position, bits below the stream start read as
+// zero) with one LDS table lookup, and a scalar walk follows the real code chain through the
+// candidates (one v_readlane + one v_writelane per symbol, the symbol dropped into the lane
+// of its output byte); 64 output bytes are stored at once.  Same result and the same
+// acceptance rule (the stream consumed exactly) as huf_stream.
+__device__ __forceinline__ uint32_t huf_walk(uint32_t ev, uint32_t c0, uint32_t cmax, uint32_t& k,
+                                             uint32_t& outv) {
+  uint32_t c, e, nb, m0_saved;
+  __asm__ volatile(
+      "s_mov_b32 %[m0s], m0\n"
+      "s_mov_b32 %[k], 0\n"
+      "s_mov_b32 m0, %[c0]\n"
+      "L_hw_%=:\n"
+      "s_cmp_ge_u32 %[k], 64\n"
+      "s_cbranch_scc1 L_hd_%=\n"
+      "s_cmp_ge_u32 m0, %[cmax]\n"
+      "s_cbranch_scc1 L_hd_%=\n"
+      "v_readlane_b32 %[e], %[ev], %[k]\n"
+      "v_writelane_b32 %[ov], %[e], m0\n"
+      "s_lshr_b32 %[nb], %[e], 8\n"
+      "s_add_u32 m0, m0, 1\n"
+      "s_add_u32 %[k], %[k], %[nb]\n"
+      "s_branch L_hw_%=\n"
+      "L_hd_%=:\n"
+      "s_mov_b32 %[c], m0\n"
+      "s_mov_b32 m0, %[m0s]\n"
+      : [k] "=&s"(k), [c] "=&s"(c), [e] "=&s"(e), [nb] "=&s"(nb), [m0s] "=&s"(m0_saved),
+        [ov] "+v"(outv)
+      : [ev] "v"(ev), [c0] "s"(c0), [cmax] "s"(cmax)
+      : "scc");
+  return c;
+}
+
+__device__ __forceinline__ bool huf_stream_fast(State& s, uint8_t* win, Tabs& t, uint32_t log,
+                                                uint32_t start, uint32_t len, GMEM uint8_t* out,
+                                                uint32_t n) {
+  if (len == 0) return false;
+  const uint32_t lane = lane_id();
+  const uint32_t last = load_le(s, win, start + len - 1, 1);
+  if (last == 0) return false;
+  int32_t P = (int32_t)((len - 1) * 8 + hb32(last));  // bits [0, P) remain
+  const uint64_t sabs = (uint64_t)(uintptr_t)(s.src + start);
+  const uint32_t mask = (1u << log) - 1;
+  uint32_t produced = 0, cnt = 0, outv = 0;
+  while (produced + cnt < n) {
+    // stage the bytes holding bits [P - 64 - log, P) (+ a dword of slack), window placed so
+    // that the backward reader keeps finding them in it
+    const int32_t lo_bit = P - 64 - (int32_t)log;
+    const uint32_t lo = lo_bit > 0 ? (uint32_t)lo_bit >> 3 : 0u;
+    const uint32_t hi = (uint32_t)(P + 7) >> 3;  // <= len
+    const uint64_t alo = sabs + lo, ahi = sabs + hi + 8;
+    if (alo < s.wb || ahi > s.wb + kWin) {
+      const uint64_t want = ahi > kWin ? ahi - kWin + 16 : 0ull;
+      refill_abs(s, win, want > alo ? alo : want);
+    }
+    const uint32_t wbase = (uint32_t)(sabs - s.wb);  // window index of stream byte 0 (mod 2^32)
+    // candidate lane: the `log` bits starting at bit b = P - lane - log
+    const int32_t b = P - (int32_t)lane - (int32_t)log;
+    const uint32_t bb = b > 0 ? (uint32_t)b : 0u;
+    const uint32_t wi = wbase + (bb >> 3);
+    lds_order();
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(win + (wi & ~3u));
+    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(win + (wi & ~3u) + 4);
+    const uint32_t v = funnel(w0, w1, wi & 3u);
+    const uint32_t bits = b >= 0 ? v >> (bb & 7u) : (-b < 32 ? v << (uint32_t)(-b) : 0u);
+    const uint32_t ev = t.huf[bits & mask];
+    uint32_t k;
+    const uint32_t rem = n - produced;
+    cnt = huf_walk(ev, cnt, rem < 64u ? rem : 64u, k, outv);
+    P -= (int32_t)k;
+    if (cnt == 64) {
+      out[produced + lane] = (uint8_t)outv;
+      produced += 64;
+      cnt = 0;
+    }
+  }
+  if (cnt && lane < cnt) out[produced + lane] = (uint8_t)outv;
+  return P == 0;
+}
+
 // ---- output helpers -------------------------------------------------------------------------
 __device__ __forceinline__ void out_fill(State& s, uint8_t* ring, uint32_t v, uint32_t n) {
   const uintptr_t base = (uintptr_t)s.dst;
@@ -649,7 +730,7 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
       return false;
     }
     if (nstreams == 1) {
-      if (!huf_stream(s, win, t, fr.huf_log, cs, cl, lit_tail, regen)) return false;
+      if (!huf_stream_fast(s, win, t, fr.huf_log, cs, cl, lit_tail, regen)) return false;
     } else {
       if (cl < 6) return false;
       const uint32_t j = load_le(s, win, cs, 4);
@@ -659,10 +740,10 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
       const uint32_t qq = (regen + 3) / 4;
       if (3 * qq > regen) return false;
       const uint32_t st = cs + 6;
-      if (!huf_stream(s, win, t, fr.huf_log, st, s1, lit_tail, qq)) return false;
-      if (!huf_stream(s, win, t, fr.huf_log, st + s1, s2, lit_tail + qq, qq)) return false;
-      if (!huf_stream(s, win, t, fr.huf_log, st + s1 + s2, s3, lit_tail + 2 * qq, qq)) return false;
-      if (!huf_stream(s, win, t, fr.huf_log, st + s1 + s2 + s3, s4, lit_tail + 3 * qq,
+      if (!huf_stream_fast(s, win, t, fr.huf_log, st, s1, lit_tail, qq)) return false;
+      if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1, s2, lit_tail + qq, qq)) return false;
+      if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1 + s2, s3, lit_tail + 2 * qq, qq)) return false;
+      if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1 + s2 + s3, s4, lit_tail + 3 * qq,
                       regen - 3 * qq)) return false;
     }
     global_fence_wave();  // the executor reads back what the streams wrote
@@ -780,69 +861,6 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
       co = 0;
       lq = 0;
     };
-    // general sequence loop: any table size (cells in LDS), the bit-exact Bwd reader
-    auto run = [&]() __attribute__((always_inline)) -> bool {
-      Bwd b;
-      if (q >= end || !bwd_init(s, win, b, q, end - q)) return false;
-      uint32_t sll = bwd_read(s, win, b, fr.al[0]);
-      uint32_t sof = bwd_read(s, win, b, fr.al[1]);
-      uint32_t sml = bwd_read(s, win, b, fr.al[2]);
-      for (uint32_t k = 0; k < nseq; ++k) {
-        const uint32_t cll = cell(t.fse[0], sll), cof = cell(t.fse[1], sof), cml = cell(t.fse[2], sml);
-        const uint32_t llc = cll & 0xFFu, ofc = cof & 0xFFu, mlc = cml & 0xFFu;
-        if (llc > 35 || mlc > 52 || ofc > 31) return false;
-        const uint32_t ofv = uniform((1u << ofc) + bwd_read(s, win, b, ofc));
-        const uint32_t mle = readlane(mlt, mlc), lle = readlane(llt, llc);
-        const uint32_t ml = uniform((mle & 0xFFFFFFu) + bwd_read(s, win, b, mle >> 24));
-        const uint32_t ll = uniform((lle & 0xFFFFFFu) + bwd_read(s, win, b, lle >> 24));
-        if (k + 1 < nseq) {
-          sll = uniform((cll >> 16) + bwd_read(s, win, b, (cll >> 8) & 0xFFu));
-          sml = uniform((cml >> 16) + bwd_read(s, win, b, (cml >> 8) & 0xFFu));
-          sof = uniform((cof >> 16) + bwd_read(s, win, b, (cof >> 8) & 0xFFu));
-        }
-        uint32_t off;
-        if (ofv > 3) {
-          off = ofv - 3;
-          fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
-        } else {
-          const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
-          if (idx == 1) {
-            off = fr.rep0;
-          } else if (idx == 2) {
-            off = fr.rep1;
-            fr.rep1 = fr.rep0; fr.rep0 = off;
-          } else if (idx == 3) {
-            off = fr.rep2;
-            fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
-          } else {
-            off = fr.rep0 - 1;
-            if (off == 0) return false;
-            fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
-          }
-        }
-        const uint32_t opv = s.op + co;  // output position including the pending chunk
-        // also keeps the output behind the unread Huffman literals in the slot tail
-        if (lp + ll > regen || (uint64_t)opv + ml + (regen - lp) > s.cap) return false;
-        if (off == 0 || off > opv + ll) return false;
-        const uint32_t ol = ll + ml;
-        if (ol <= kWave && off <= kNearOff) {
-          if (co + ol > kWave) exec();
-          if (lane - co < ol) {
-            rec = co | (ll << 8) | (lq << 16);
-            roff = off;
-          }
-          co += ol;
-          lq += ll;
-          lp += ll;
-        } else {
-          exec();
-          copy_lits(ll);
-          match_copy(s, ring, off, ml);
-        }
-      }
-      exec();
-      return b.bitpos == 0;
-    };
     // fast sequence loop for tables of <= 64 cells (every predefined one): the tables live in
     // registers, lane u = cell u packed as baseline (17 bits) | extra-bit count << 17 |
     // state bits << 22 | next-state base << 25 (offset table: the code in place of the
@@ -921,9 +939,74 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
       exec();
       return fb.remaining(q) == 0;
     };
+    // the same loop for larger tables (libzstd's custom FSE tables, accuracy <= 9): the
+    // three cells come from LDS (issued together), baselines from the llt / mlt registers
+    auto fast_lds = [&]() __attribute__((always_inline)) -> bool {
+      FastBits fb;
+      if (!fb.init(s, q, end)) return false;
+      uint32_t sll = fb.read(fr.al[0]), sof = fb.read(fr.al[1]), sml = fb.read(fr.al[2]);
+      for (uint32_t k = 0; k < nseq; ++k) {
+        fb.reload(s, q);
+        lds_order();
+        const uint32_t cll = uniform(t.fse[0][sll]), cof = uniform(t.fse[1][sof]),
+                       cml = uniform(t.fse[2][sml]);
+        const uint32_t ofc = cof & 0xFFu;
+        const uint32_t ofv = (1u << ofc) + fb.read(ofc);
+        const uint32_t mle = readlane(mlt, cml & 0xFFu);
+        const uint32_t ml = (mle & 0xFFFFFFu) + fb.read(mle >> 24);
+        if (fb.used > 31) fb.reload(s, q);
+        const uint32_t lle = readlane(llt, cll & 0xFFu);
+        const uint32_t ll = (lle & 0xFFFFFFu) + fb.read(lle >> 24);
+        if (k + 1 < nseq) {
+          sll = (cll >> 16) + fb.read((cll >> 8) & 0xFFu);
+          sml = (cml >> 16) + fb.read((cml >> 8) & 0xFFu);
+          sof = (cof >> 16) + fb.read((cof >> 8) & 0xFFu);
+        }
+        uint32_t off;
+        if (ofv > 3) {
+          off = ofv - 3;
+          fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+        } else {
+          const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
+          if (idx == 1) {
+            off = fr.rep0;
+          } else if (idx == 2) {
+            off = fr.rep1;
+            fr.rep1 = fr.rep0; fr.rep0 = off;
+          } else if (idx == 3) {
+            off = fr.rep2;
+            fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+          } else {
+            off = fr.rep0 - 1;
+            if (off == 0) return false;
+            fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
+          }
+        }
+        const uint32_t opv = s.op + co;
+        if (lp + ll > regen || (uint64_t)opv + ml + (regen - lp) > s.cap) return false;
+        if (off == 0 || off > opv + ll) return false;
+        const uint32_t ol = ll + ml;
+        if (ol <= kWave && off <= kNearOff) {
+          if (co + ol > kWave) exec();
+          if (lane - co < ol) {
+            rec = co | (ll << 8) | (lq << 16);
+            roff = off;
+          }
+          co += ol;
+          lq += ll;
+          lp += ll;
+        } else {
+          exec();
+          copy_lits(ll);
+          match_copy(s, ring, off, ml);
+        }
+      }
+      exec();
+      return fb.remaining(q) == 0;
+    };
     ZP_BEGIN(tq);
     ZP_ADD(11, nseq);
-    if (!(rt ? fast() : run())) return false;
+    if (!(rt ? fast() : fast_lds())) return false;
     ZP_END(4, tq);
   } else if (q != end) {
     return false;
