@@ -17,6 +17,8 @@
 //   Literal runs >= kLongLit bypass the ring and stream HBM -> HBM (wave_copy_global).
 #include "stream_ring.hip.h"
 
+#include <type_traits>
+
 namespace bitar_hip {
 
 
@@ -134,6 +136,18 @@ __device__ __forceinline__ uint32_t walk_tokens(uint32_t pw, uint32_t pr, uint32
 
 }  // namespace lz4d
 
+// Two instantiations, launched back to back by the runtime:
+//   FARK = false  every segment; batches admit offsets within the ring only (our own streams
+//                 never go beyond it).  A segment whose next sequence could be batched only
+//                 with far history (stock streams: offsets up to 65535) is deferred
+//                 (produced = kDefer) as soon as that is seen.
+//   FARK = true   the deferred segments only (the others exit at once): FAR batches read far
+//                 history back from HBM, and stay FAR while they meet it.
+// Keeping the far machinery out of the first kernel keeps its batch path as short as before
+// (measured: 4-8 % on our own streams when both share one kernel).
+constexpr uint32_t kDefer = 0xFFFFFFFEu;
+
+template <bool FARK>
 __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
@@ -144,6 +158,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   uint8_t* ring = lds + kWin;
   const uint32_t i = blockIdx.x;
   if (i >= nseg) return;
+  if (FARK && produced[i] != kDefer) return;
 
   State s;
   s.src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
@@ -164,6 +179,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   const uint32_t lane = lane_id();
   const uint32_t base = (uint32_t)(uintptr_t)s.dst;  // ring index = absolute address & mask
   const uint32_t src_lo = (uint32_t)(uintptr_t)s.src;
+  bool want_far = false, stay_far = false;
   while (ok) {
     // ---- batch fast path: up to kBatchOut output bytes of short sequences per step ------
     // 1. every lane l decodes "a token at stream position ip+l" from the LDS window
@@ -180,8 +196,11 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     // Bytes past the batch are written too: their ring slots are >= kRing - kBatchOut
     // behind the output, older than any near source and already flushed, and are rewritten
     // before use.
-    for (;;) {
-      if (s.ip + kBatchIn > s.csize) break;
+    // one batch; FAR = false admits offsets within the ring only (the common case, no far
+    // bookkeeping), FAR = true any offset (far history read from HBM); returns the output
+    // byte count, 0 if the first token does not qualify
+    auto batch = [&](auto far_tag) __attribute__((always_inline)) -> uint32_t {
+      constexpr bool FAR = decltype(far_tag)::value;
       if (s.op + kBatchOut - s.flushed > kFlushAt) flush(s, ring, s.op, false);
       uint32_t wrel = src_lo + s.ip - (uint32_t)s.wb;  // window index of ip (mod 2^32)
       if (wrel > kWin - kBatchIn) {
@@ -203,29 +222,34 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t cml = 4 + (mx ? 15u + b2 : cm4);
       const uint32_t colen = cL + cml;
       // eligible: at most one length byte each (< 255), <= 64 output bytes (so <= 60 literals),
-      // a real offset (any distance: far sources are read back from HBM below), not before
-      // the segment start (conservatively, as if this token opened the batch)
-      const bool csimple = (!lx || b1 < 255u) && (!mx || b2 < 255u) && colen <= 64u && coff != 0 && coff <= s.op + cL;
+      // a real offset (within the ring, or any distance in a FAR batch: far sources are read
+      // back from HBM below), not before the segment start (conservatively, as if this token
+      // opened the batch)
+      const bool cfar = (!lx || b1 < 255u) && (!mx || b2 < 255u) && colen <= 64u && coff != 0 &&
+                        coff <= s.op + cL;
+      const bool csimple = cfar && (FAR || coff <= kNearOff);
       // walk record: next token lane (7 bits, <= 127 for an eligible token, see
       // kMaxEligibleNext; the walk stops at a lane >= 64, which was not parsed, after
       // consuming the sequence) | output length (255: not eligible, the walk's one compare
       // then stops; an ineligible token's wider nxt only ORs into those already-set bits).
       // Sequence record: offset mod 4096 (12 bits) | literal count (6 bits) | token lane (6
-      // bits) | bit 30: offset beyond the ring -- the output start goes into bits 24..29
-      // after the walk; offsets >= 4096 (stock streams; ours stay <= 2560) get their high
-      // bits from the token lane below.
+      // bits) -- the output start goes into bits 24..29 after the walk; offsets >= 4096 (FAR
+      // batches) get their high bits from the token lane below.
       const uint32_t nxt = lane + 3 + (lx ? 1u : 0u) + (mx ? 1u : 0u) + cL;
       const uint32_t pw = nxt | ((csimple ? colen : 255u) << 7);
-      const uint32_t pr = (coff & 4095u) | ((cL & 63u) << 12) | (lane << 18) |
-                          (coff > kNearOff ? 0x40000000u : 0u);  // bit 30: far offset
+      const uint32_t pr = (coff & 4095u) | ((cL & 63u) << 12) | (lane << 18);
       // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
       const uint32_t room = s.cap - s.op;
       const uint32_t lim = room < kBatchOut ? room : kBatchOut;
       uint32_t k, vrec = 0;
       const uint32_t out = walk_tokens(pw, pr, lim, k, vrec);
-      if (out == 0) break;
+      if (out == 0) {
+        // the first token qualifies only for a FAR batch: worth trying one
+        if (!FAR) want_far = (ballot(cfar) & 1ull) != 0;
+        return 0u;
+      }
       // every output byte takes the record of the latest sequence starting at or before it
-      const uint32_t key = wave_incl_max(vrec ? (vrec & 0x00FFFFFFu) | (lane << 24) : 0u);
+      const uint32_t key = wave_incl_max(vrec ? vrec | (lane << 24) : 0u);
       // (3) sources: window literal / ring history / HBM history (far) / alias of an earlier
       // byte of the batch (branch-free: every lane computes every form).  bit31: alias (low 6
       // bits: the source lane); bit30: far (low 16 bits: the output position); else an LDS
@@ -234,9 +258,9 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t seqlane = (key >> 18) & 63u;
       const uint32_t jL = (key >> 12) & 63u;
       uint32_t joff = key & 4095u;
-      // a sequence of the batch with an offset beyond the ring's reach (stock streams; ours
-      // stay <= 2560): only then the far-history machinery below (a wave-uniform branch)
-      const bool big = ballot(vrec >= 0x40000000u) != 0;
+      // FAR batches (entered only where a near batch could not start: stock streams with
+      // offsets beyond the ring's reach; ours stay <= 2560) read far history from HBM
+      const bool big = FAR;
       if (big) joff |= bpermute_lane(coff & ~4095u, seqlane);  // offsets >= 4096
       const uint32_t r = lane - ostart;
       const bool is_lit = r < jL;
@@ -273,12 +297,31 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
           s.fenced = s.flushed;
         }
         if (gfar) g = s.dst[st & 0xFFFFu];
+        stay_far = farm != 0;  // keep to FAR batches while they meet far history
       }
       ring[(base + s.op + lane) & kRingMask] = (uint8_t)g;
       lds_order();
       s.ip += k;
       s.op += out;
+      return out;
+    };
+    for (;;) {
+      if (s.ip + kBatchIn > s.csize) break;
+      if constexpr (FARK) {
+        if (stay_far) {
+          if (batch(std::true_type{})) continue;
+          stay_far = false;
+        }
+        want_far = false;
+        if (batch(std::false_type{})) continue;
+        if (!want_far || !batch(std::true_type{})) break;
+      } else {
+        want_far = false;
+        if (batch(std::false_type{})) continue;
+        break;
+      }
     }
+    if (!FARK && want_far) break;  // defer the segment to the FAR kernel
     // ---- general path: one sequence, any shape -----------------------------------------
     if (s.ip >= s.csize) { ok = false; break; }
     const uint32_t token = sv.get(s, win, s.ip);
@@ -301,7 +344,9 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     if ((uint64_t)s.op + m > s.cap) { ok = false; break; }
     match_copy(s, ring, off, m);
   }
-  if (ok) {
+  if (!FARK && want_far) {
+    if (lane_id() == 0) produced[i] = kDefer;
+  } else if (ok) {
     flush(s, ring, s.op, true);
     if (lane_id() == 0) produced[i] = s.op;
   } else if (lane_id() == 0) {
@@ -309,5 +354,12 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     atomicOr(err, 1u);
   }
 }
+
+template __global__ void lz4_decompress_kernel<false>(const uint8_t* const*, const uint8_t*,
+                                                     uint64_t, const uint32_t*, uint32_t,
+                                                     uint32_t, uint8_t*, uint32_t*, uint32_t*);
+template __global__ void lz4_decompress_kernel<true>(const uint8_t* const*, const uint8_t*,
+                                                    uint64_t, const uint32_t*, uint32_t, uint32_t,
+                                                    uint8_t*, uint32_t*, uint32_t*);
 
 }  // namespace bitar_hip

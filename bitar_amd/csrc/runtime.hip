@@ -18,6 +18,7 @@
 namespace bitar_hip {
 __global__ void lz4_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
                                     uint8_t* const*, uint32_t*, uint32_t*);
+template <bool FARK>
 __global__ void lz4_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                       const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
                                       uint32_t*);
@@ -408,8 +409,14 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
   const auto* slab = static_cast<const uint8_t*>(d_slab);
   auto* out = static_cast<uint8_t*>(d_out);
   if (codec == BITAR_HIP_CODEC_LZ4)
-    hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
-                       stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s));
+  {
+    // near-history kernel over every segment, then the far-history kernel over the segments
+    // it deferred (lz4_decompress.hip)
+    hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<false>, dim3(nseg), dim3(64), 0, s, srcs,
+                       slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s));
+    hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<true>, dim3(nseg), dim3(64), 0, s, srcs,
+                       slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s));
+  }
   else if (codec == BITAR_HIP_CODEC_DEFLATE) {
     // lane-per-segment decoder for stored / fixed-Huffman streams first; the wave decoder
     // then takes the segments it deferred (inflate_lanes.hip)
