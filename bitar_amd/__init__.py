@@ -17,6 +17,7 @@ CODEC_DEFLATE = 2
 CODEC_ZSTD = 3
 CODEC_DEFLATE_DYNAMIC = 4  # HuffmanEncoding::DYNAMIC (decoded as CODEC_DEFLATE)
 SEGMENT_ERROR = 0xFFFFFFFF
+CHECKSUM_CRC32, CHECKSUM_ADLER32, CHECKSUM_CRC32_ADLER32 = 1, 2, 3
 MAX_SEG_SIZE = 65536
 
 # negated arrow::StatusCode (reference src/include/util.h:157-205)
@@ -71,6 +72,7 @@ def lib():
         "bitar_hip_pack": (i32, [vp, vp, vp, u64, vp, u32, vp, vp]),
         "bitar_hip_fill": (i32, [vp, vp, i32, u64, vp, u64]),
         "bitar_hip_fill_at": (i32, [vp, vp, i32, u64, u64, vp, u64]),
+        "bitar_hip_checksum": (i32, [vp, vp, u32, vp, u64, u32, vp, u32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -88,7 +90,7 @@ ABI_SYMBOLS = ("bitar_hip_abi_version", "bitar_hip_last_error", "bitar_hip_devic
                "bitar_hip_compress", "bitar_hip_compress_scattered", "bitar_hip_pointer_info",
                "bitar_hip_decompress", "bitar_hip_decompress_slab",
                "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_pack_lz4f", "bitar_hip_fill",
-               "bitar_hip_fill_at")
+               "bitar_hip_fill_at", "bitar_hip_checksum")
 
 
 def check(rc):
@@ -192,6 +194,13 @@ class Engine:
         n = out.numel() if n is None else n
         check(lib().bitar_hip_fill_at(self.ctx, self._stream(stream), kind, seed, offset,
                                       _ptr(out), n))
+
+    def checksum(self, kind, data, seg, sums, n=None, lens=None, nseg=None, stream=None):
+        """per-segment CRC32 / Adler32 (uint64 tensor `sums`) of uncompressed data"""
+        n = data.numel() if n is None else n
+        nseg = (n + seg - 1) // seg if nseg is None else nseg
+        check(lib().bitar_hip_checksum(self.ctx, self._stream(stream), kind, _ptr(data), n, seg,
+                                       _ptr(lens), nseg, _ptr(sums)))
 
     def sync(self, stream=None):
         s = self._stream(stream) if stream is not False else None

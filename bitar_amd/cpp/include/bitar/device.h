@@ -85,6 +85,12 @@ class CompressDevice {
   [[nodiscard]] std::uint64_t slot_size() const noexcept { return slot_size_; }
   [[nodiscard]] void* stream(std::uint16_t queue_pair_id) const;
 
+  /// \brief Per-segment checksums of the last Compress (over its input) or Decompress (over
+  /// its output) on \p queue_pair_id, when the configuration asks for a checksum type: the
+  /// values DPDK leaves in rte_comp_op::input_chksum / output_chksum (CRC32 in bits 0..31,
+  /// Adler32 in bits 32..63 for CRC32_ADLER32).  Empty when no checksum is configured.
+  [[nodiscard]] const std::vector<std::uint64_t>& checksums(std::uint16_t queue_pair_id) const;
+
   virtual ~CompressDevice();
 
  protected:
@@ -98,6 +104,9 @@ class CompressDevice {
   }
 
   virtual arrow::Status set_configuration(std::unique_ptr<Configuration<Class>> configuration);
+
+  /// The checksum to compute per segment (BITAR_HIP_CHECKSUM_*), 0 for none.
+  [[nodiscard]] virtual std::uint32_t checksum_kind() const { return 0; }
 
   [[nodiscard]] auto state() const noexcept { return state_; }
   void set_state(internal::DeviceState state) { state_ = state; }
@@ -155,6 +164,7 @@ class HipCompressDevice : public HipGfx950CompressDevice {
   arrow::Status ValidateConfiguration() override;
   arrow::Status set_configuration(
       std::unique_ptr<Configuration<Class_HIP_GFX950>> configuration) override;
+  [[nodiscard]] std::uint32_t checksum_kind() const override;
 
   friend arrow::Result<HipGfx950CompressDevice*>
   DeviceManager::Create<Class_HIP_GFX950>(std::uint8_t, std::vector<std::uint32_t>);

@@ -108,6 +108,10 @@ struct QueuePairMemory {
   std::size_t table_cap = 0;
   void* d_stage = nullptr;
   std::uint64_t stage_cap = 0;
+  std::uint64_t* d_sums = nullptr;  // per-segment checksums (device, then pinned host)
+  std::uint64_t* h_sums = nullptr;
+  std::size_t sums_cap = 0;
+  std::vector<std::uint64_t> checksums;  // of the last call
 
   ~QueuePairMemory() {
     if (!ctx) return;
@@ -117,6 +121,25 @@ struct QueuePairMemory {
     if (d_sizes) (void)bitar_hip_free(ctx, d_sizes);
     if (d_prod) (void)bitar_hip_free(ctx, d_prod);
     if (d_stage) (void)bitar_hip_free(ctx, d_stage);
+    if (d_sums) (void)bitar_hip_free(ctx, d_sums);
+    if (h_sums) (void)bitar_hip_host_free(ctx, h_sums);
+  }
+
+  arrow::Status Sums(std::size_t n) {
+    if (n <= sums_cap) return arrow::Status::OK();
+    if (d_sums) (void)bitar_hip_free(ctx, d_sums);
+    if (h_sums) (void)bitar_hip_host_free(ctx, h_sums);
+    d_sums = nullptr;
+    h_sums = nullptr;
+    sums_cap = 0;
+    const std::size_t cap = std::max<std::size_t>(n, 1024);
+    void* p = nullptr;
+    BITAR_ABI(bitar_hip_alloc(ctx, cap * 8, &p), "checksum table");
+    d_sums = static_cast<std::uint64_t*>(p);
+    BITAR_ABI(bitar_hip_host_alloc(ctx, cap * 8, &p), "checksum table");
+    h_sums = static_cast<std::uint64_t*>(p);
+    sums_cap = cap;
+    return arrow::Status::OK();
   }
 
   arrow::Status Tables(std::size_t n) {
@@ -258,6 +281,13 @@ void* CompressDevice<Class, Enable>::stream(std::uint16_t queue_pair_id) const {
 }
 
 template <typename Class, typename Enable>
+const std::vector<std::uint64_t>& CompressDevice<Class, Enable>::checksums(
+    std::uint16_t queue_pair_id) const {
+  static const std::vector<std::uint64_t> kNone;
+  return queue_pair_id < qp_memory_.size() ? qp_memory_[queue_pair_id]->checksums : kNone;
+}
+
+template <typename Class, typename Enable>
 arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
     std::uint16_t queue_pair_id, const std::shared_ptr<arrow::Buffer>& decompressed_buffer) {
   BufferVector compressed_buffers;
@@ -301,7 +331,16 @@ arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
                                       reinterpret_cast<void* const*>(m->d_ptrs), slot_size_,
                                       m->d_sizes);
   if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sizes, m->d_sizes, 4ull * nseg, m->stream);
+  // the checksum of the uncompressed input (DPDK input_chksum of a compress op)
+  const std::uint32_t ck = checksum_kind();
+  if (rc == 0 && ck) {
+    st = m->Sums(nseg);
+    if (!st.ok()) return release(st);
+    rc = bitar_hip_checksum(ctx_, m->stream, ck, d_in, n, seg, nullptr, nseg, m->d_sums);
+    if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sums, m->d_sums, 8ull * nseg, m->stream);
+  }
   if (rc == 0) rc = bitar_hip_sync(ctx_, m->stream);
+  if (rc == 0) m->checksums.assign(m->h_sums, ck ? m->h_sums + nseg : m->h_sums);
   if (rc != 0) {
     return release(internal::FromAbi(
         rc, "Failed to compress via queue pair " + std::to_string(queue_pair_id) +
@@ -375,10 +414,19 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
                                 m->d_prod);
   if (rc == 0)
     rc = bitar_hip_memcpy(ctx_, m->h_sizes, m->d_prod, 4ull * nseg, m->stream);
+  // the checksum of the decompressed output (DPDK output_chksum of a decompress op)
+  const std::uint32_t ck = checksum_kind();
+  if (rc == 0 && ck) {
+    ARROW_RETURN_NOT_OK(m->Sums(nseg));
+    rc = bitar_hip_checksum(ctx_, m->stream, ck, d_out, static_cast<std::uint64_t>(min_capacity),
+                            seg, m->d_prod, nseg, m->d_sums);
+    if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sums, m->d_sums, 8ull * nseg, m->stream);
+  }
   if (rc == 0 && !out_on_dev)
     rc = bitar_hip_memcpy(ctx_, reinterpret_cast<void*>(out_addr), d_out,
                           static_cast<std::uint64_t>(min_capacity), m->stream);
   if (rc == 0) rc = bitar_hip_sync(ctx_, m->stream);
+  if (rc == 0) m->checksums.assign(m->h_sums, ck ? m->h_sums + nseg : m->h_sums);
   if (rc != 0) {
     return internal::FromAbi(rc, "Failed to decompress via queue pair " +
                                      std::to_string(queue_pair_id) + " of compress device " +
@@ -484,12 +532,19 @@ arrow::Status HipCompressDevice::ValidateConfiguration() {
   const auto* hip_configuration = dynamic_cast<HipConfiguration*>(configuration().get());
   if (ARROW_PREDICT_FALSE(hip_configuration == nullptr))
     return arrow::Status::Invalid("Invalid configuration for HipCompressDevice");
-  if (hip_configuration->checksum_type() != ChecksumType::NONE)
-    return arrow::Status::NotImplemented("checksum type ",
-                                         ToString(hip_configuration->checksum_type()),
-                                         " is not supported by compress device of type ",
-                                         kHipConfigurationTypeName);
+  // every rte_comp_checksum_type is supported (checksum.hip); see checksums()
   return HipGfx950CompressDevice::ValidateConfiguration();
+}
+
+std::uint32_t HipCompressDevice::checksum_kind() const {
+  const auto* c = dynamic_cast<const HipConfiguration*>(configuration().get());
+  if (!c) return 0;
+  switch (c->checksum_type()) {
+    case ChecksumType::CRC32: return BITAR_HIP_CHECKSUM_CRC32;
+    case ChecksumType::ADLER32: return BITAR_HIP_CHECKSUM_ADLER32;
+    case ChecksumType::CRC32_ADLER32: return BITAR_HIP_CHECKSUM_CRC32_ADLER32;
+    default: return 0;
+  }
 }
 
 arrow::Status HipCompressDevice::set_configuration(

@@ -43,6 +43,8 @@ __global__ void deflate_dyn_parse_kernel(const uint8_t*, uint64_t, uint32_t, uin
 __global__ void deflate_dyn_emit_kernel(const uint8_t*, uint64_t, uint32_t, const uint8_t*,
                                         uint64_t, uint8_t*, uint64_t, uint8_t* const*, uint32_t*,
                                         uint32_t*);
+__global__ void checksum_kernel(uint32_t, const uint8_t*, uint64_t, uint32_t, const uint32_t*,
+                                uint32_t, uint64_t*);
 __global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t, uint64_t*, uint32_t*);
 __global__ void pack_kernel(const uint8_t*, uint64_t, const uint32_t*, const uint64_t*, uint32_t,
                             uint8_t*);
@@ -550,6 +552,23 @@ int bitar_hip_pack_lz4f(bitar_hip_ctx* ctx, void* stream, const void* d_in, uint
                        nseg, static_cast<uint8_t*>(d_frame));
     HIP_TRY(hipGetLastError(), "lz4f pack launch");
   }
+  return 0;
+}
+
+int bitar_hip_checksum(bitar_hip_ctx* ctx, void* stream, uint32_t kind, const void* d_data,
+                       uint64_t n, uint32_t seg, const uint32_t* d_lens, uint32_t nseg,
+                       uint64_t* d_sums) {
+  if (int r = enter(ctx)) return r;
+  if (kind < BITAR_HIP_CHECKSUM_CRC32 || kind > BITAR_HIP_CHECKSUM_CRC32_ADLER32)
+    return fail(BITAR_HIP_INVALID, "checksum kind must be CRC32, ADLER32 or CRC32_ADLER32");
+  if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
+  if (!d_lens && nseg != (uint32_t)((n + seg - 1) / seg))
+    return fail(BITAR_HIP_INVALID, "nseg must be ceil(n / seg) without a length array");
+  if (!nseg) return 0;
+  if (!d_data || !d_sums) return fail(BITAR_HIP_INVALID, "null buffer");
+  hipLaunchKernelGGL(bitar_hip::checksum_kernel, dim3(nseg), dim3(64), 0, pick_stream(ctx, stream),
+                     kind, static_cast<const uint8_t*>(d_data), n, seg, d_lens, nseg, d_sums);
+  HIP_TRY(hipGetLastError(), "checksum launch");
   return 0;
 }
 

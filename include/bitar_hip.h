@@ -175,6 +175,23 @@ int bitar_hip_fill(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed, vo
 int bitar_hip_fill_at(bitar_hip_ctx* ctx, void* stream, int kind, uint64_t seed,
                       uint64_t offset, void* d_out, uint64_t n);
 
+/* Checksum types (rte_comp_checksum_type, reference src/include/config.h:169-182). */
+enum bitar_hip_checksum_kind {
+  BITAR_HIP_CHECKSUM_CRC32 = 1,         /* zlib / ISO-HDLC CRC-32 */
+  BITAR_HIP_CHECKSUM_ADLER32 = 2,       /* RFC 1950 Adler-32 */
+  BITAR_HIP_CHECKSUM_CRC32_ADLER32 = 3  /* CRC-32 in bits 0..31, Adler-32 in bits 32..63 */
+};
+
+/* Per-segment checksum of uncompressed data -- what the reference's xforms ask the engine to
+ * compute over an op's uncompressed side (checksum_type in compress_xform / decompress_xform,
+ * reference src/config.cc:83-105): segment i starts at d_data + i*seg and holds d_lens[i]
+ * bytes (a decompress's d_produced; BITAR_HIP_SEGMENT_ERROR gives 0), or, with d_lens NULL,
+ * min(seg, n - i*seg) bytes (a compress's input; then nseg must be ceil(n / seg)).
+ * d_sums[i] (uint64) receives the checksum.  Asynchronous on `stream`. */
+int bitar_hip_checksum(bitar_hip_ctx* ctx, void* stream, uint32_t kind, const void* d_data,
+                       uint64_t n, uint32_t seg, const uint32_t* d_lens, uint32_t nseg,
+                       uint64_t* d_sums);
+
 /* Where `ptr` lives: *kind = 0 pageable host, 1 pinned host, 2 device memory (then *device
  * is its ordinal).  Replaces rte_mem_virt2iova() residency assumptions (memory.cc:388). */
 int bitar_hip_pointer_info(const void* ptr, int* kind, int* device);

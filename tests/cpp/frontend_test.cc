@@ -254,6 +254,32 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
     CHECK(d->Recycle(async_out[0]) == async_out[0].size());
     CHECK(d->Recycle(async_out[1]) == async_out[1].size());
   }
+  // checksum_type (config.h:169-182): per-segment CRC32 | Adler32 << 32 of the uncompressed
+  // side of each call -- the compress input and the decompress output (written for the
+  // Python side to check against zlib)
+  {
+    auto fresh = driver->GetDevices({(*ids)[0]});
+    CHECK_OK(fresh.status());
+    auto& d = (*fresh)[0];
+    const std::uint32_t seg = 65536;
+    auto cfg = MakeConfig(bitar::Codec::LZ4, seg);
+    cfg->set_checksum_type(bitar::ChecksumType::CRC32_ADLER32);
+    CHECK_OK(d->Initialize(std::move(cfg)));
+    auto comp = d->Compress(0, host_in);
+    CHECK_OK(comp.status());
+    const auto nseg = (data.size() + seg - 1) / seg;
+    const std::vector<std::uint64_t> cs = d->checksums(0);
+    CHECK(cs.size() == nseg);
+    if (comp.ok()) {
+      auto o = arrow::AllocateResizableBuffer(static_cast<int64_t>(nseg * seg));
+      std::unique_ptr<arrow::ResizableBuffer> out = std::move(*o);
+      CHECK_OK(d->Decompress(1, *comp, out));
+      CHECK(d->checksums(1) == cs);  // round trip: same uncompressed bytes
+      std::ofstream f(outdir + "/checksums.bin", std::ios::binary);
+      f.write(reinterpret_cast<const char*>(cs.data()), static_cast<std::streamsize>(8 * cs.size()));
+      CHECK(d->Recycle(*comp) == comp->size());
+    }
+  }
   // empty input -> empty vector (device.cc:161-164); empty vector -> OK
   auto& d0 = (*devs)[0];
   CHECK_OK(d0->Initialize(MakeConfig(bitar::Codec::LZ4, 65536)));

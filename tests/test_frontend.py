@@ -11,6 +11,8 @@ import struct
 import subprocess
 import zlib
 
+import numpy as np
+
 import pytest
 
 import oracle_lib as O
@@ -68,6 +70,12 @@ def test_frontend_on_gpu(tmp_path):
     for i, s in enumerate(segs):
         rc, plain = O.lz4_decompress(s, seg)
         assert rc == 0 and plain == data[i * seg:(i + 1) * seg]
+    # configured checksums: CRC32 | Adler32 << 32 of every 64 KiB segment (vs zlib)
+    cs = np.fromfile(tmp_path / "checksums.bin", dtype=np.uint64)
+    assert cs.size == (len(data) + 65535) // 65536
+    for i, v in enumerate(cs.tolist()):
+        part = data[i * 65536:(i + 1) * 65536]
+        assert v == zlib.crc32(part) | (zlib.adler32(part) << 32), i
     segs = _segments(tmp_path / "zstd.segs")
     assert len(segs) == (len(data) + seg - 1) // seg
     for i, s in enumerate(segs):

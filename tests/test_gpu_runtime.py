@@ -200,3 +200,49 @@ def test_lz4_mutations_match_oracle(eng):
                 n_bad += 1
                 assert prod[k] == 0xFFFFFFFF, (lo + k, r, int(prod[k]))
         assert ok == (n_bad == 0)
+
+
+@pytest.mark.parametrize("kind", [0, 1, 6])
+@pytest.mark.parametrize("seg", [65536, 59460, 4096, 100, 1])
+def test_checksums_match_zlib(eng, kind, seg):
+    """bitar_hip_checksum: per-segment CRC32 / Adler32 / both (DPDK's CRC32_ADLER32 layout)
+    equal zlib's, over contiguous segments (a compress's input) and over segments of given
+    lengths (a decompress's produced sizes, SEGMENT_ERROR -> 0)."""
+    import zlib
+    import bitar_amd
+    n = 3 * seg + seg // 2 + 1 if seg > 1 else 77
+    data = O.fill(kind, 5, n)
+    d = up(data)[:n]
+    nseg = (n + seg - 1) // seg
+    for ck in (1, 2, 3):
+        sums = eng.empty(nseg, dtype=torch.int64)
+        eng.checksum(ck, d, seg, sums, n=n)
+        got = down(sums).view(np.uint64)
+        for i in range(nseg):
+            part = data[i * seg:(i + 1) * seg].tobytes()
+            c, a = zlib.crc32(part), zlib.adler32(part)
+            want = c if ck == 1 else a if ck == 2 else c | (a << 32)
+            assert int(got[i]) == want, (ck, i)
+    # per-segment lengths (shorter than seg, zero, and a failed segment)
+    lens = np.array([min(seg, (7 * i + 3) % (seg + 1)) for i in range(nseg)], np.uint32)
+    lens[0] = 0
+    if nseg > 2:
+        lens[2] = 0xFFFFFFFF
+    dl = torch.from_numpy(lens.view(np.int32)).cuda()
+    sums = eng.empty(nseg, dtype=torch.int64)
+    eng.checksum(3, d, seg, sums, n=n, lens=dl, nseg=nseg)
+    got = down(sums).view(np.uint64)
+    for i in range(nseg):
+        if lens[i] == 0xFFFFFFFF:
+            assert int(got[i]) == 0
+            continue
+        part = data[i * seg:i * seg + int(lens[i])].tobytes()
+        assert int(got[i]) == zlib.crc32(part) | (zlib.adler32(part) << 32), i
+
+
+def test_checksum_rejects_bad_kind(eng):
+    import bitar_amd
+    d = eng.empty(100)
+    s = eng.empty(1, dtype=torch.int64)
+    with pytest.raises(bitar_amd.BitarError):
+        eng.checksum(4, d, 100, s)
