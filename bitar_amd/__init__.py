@@ -73,6 +73,7 @@ def lib():
         "bitar_hip_fill": (i32, [vp, vp, i32, u64, vp, u64]),
         "bitar_hip_fill_at": (i32, [vp, vp, i32, u64, u64, vp, u64]),
         "bitar_hip_checksum": (i32, [vp, vp, u32, vp, u64, u32, vp, u32, vp]),
+        "bitar_hip_copy_batch": (i32, [vp, vp, vp, vp, vp, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -90,7 +91,7 @@ ABI_SYMBOLS = ("bitar_hip_abi_version", "bitar_hip_last_error", "bitar_hip_devic
                "bitar_hip_compress", "bitar_hip_compress_scattered", "bitar_hip_pointer_info",
                "bitar_hip_decompress", "bitar_hip_decompress_slab",
                "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_pack_lz4f", "bitar_hip_fill",
-               "bitar_hip_fill_at", "bitar_hip_checksum")
+               "bitar_hip_fill_at", "bitar_hip_checksum", "bitar_hip_copy_batch")
 
 
 def check(rc):
@@ -201,6 +202,11 @@ class Engine:
         nseg = (n + seg - 1) // seg if nseg is None else nseg
         check(lib().bitar_hip_checksum(self.ctx, self._stream(stream), kind, _ptr(data), n, seg,
                                        _ptr(lens), nseg, _ptr(sums)))
+
+    def copy_batch(self, srcs, dsts, sizes, n, stream=None):
+        """entry i: sizes[i] bytes from srcs[i] to dsts[i] (int64 / int32 device tensors)"""
+        check(lib().bitar_hip_copy_batch(self.ctx, self._stream(stream), _ptr(srcs), _ptr(dsts),
+                                         _ptr(sizes), n))
 
     def sync(self, stream=None):
         s = self._stream(stream) if stream is not False else None

@@ -112,6 +112,8 @@ struct QueuePairMemory {
   std::uint64_t* h_sums = nullptr;
   std::size_t sums_cap = 0;
   std::vector<std::uint64_t> checksums;  // of the last call
+  void* d_chain = nullptr;  // chained ops (max_sgl_segs > 1): one stream per op
+  std::uint64_t chain_cap = 0;
 
   ~QueuePairMemory() {
     if (!ctx) return;
@@ -123,6 +125,17 @@ struct QueuePairMemory {
     if (d_stage) (void)bitar_hip_free(ctx, d_stage);
     if (d_sums) (void)bitar_hip_free(ctx, d_sums);
     if (h_sums) (void)bitar_hip_host_free(ctx, h_sums);
+    if (d_chain) (void)bitar_hip_free(ctx, d_chain);
+  }
+
+  arrow::Status Chain(std::uint64_t bytes) {
+    if (bytes <= chain_cap) return arrow::Status::OK();
+    if (d_chain) (void)bitar_hip_free(ctx, d_chain);
+    d_chain = nullptr;
+    chain_cap = 0;
+    BITAR_ABI(bitar_hip_alloc(ctx, bytes, &d_chain), "qp chain scratch");
+    chain_cap = bytes;
+    return arrow::Status::OK();
   }
 
   arrow::Status Sums(std::size_t n) {
@@ -321,38 +334,88 @@ arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
     device_memory_->PutAll(slots);
     return st;
   };
-  auto st = m->Tables(nseg);
-  if (!st.ok()) return release(st);
-  for (std::uint32_t i = 0; i < nseg; ++i)
-    m->h_ptrs[i] = static_cast<std::uint64_t>(reinterpret_cast<uintptr_t>(slots[i]));
-  int rc = bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 8ull * nseg, m->stream);
-  if (rc == 0)
-    rc = bitar_hip_compress_scattered(ctx_, m->stream, codec, d_in, n, seg,
-                                      reinterpret_cast<void* const*>(m->d_ptrs), slot_size_,
-                                      m->d_sizes);
-  if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sizes, m->d_sizes, 4ull * nseg, m->stream);
-  // the checksum of the uncompressed input (DPDK input_chksum of a compress op)
-  const std::uint32_t ck = checksum_kind();
-  if (rc == 0 && ck) {
-    st = m->Sums(nseg);
-    if (!st.ok()) return release(st);
-    rc = bitar_hip_checksum(ctx_, m->stream, ck, d_in, n, seg, nullptr, nseg, m->d_sums);
-    if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sums, m->d_sums, 8ull * nseg, m->stream);
-  }
-  if (rc == 0) rc = bitar_hip_sync(ctx_, m->stream);
-  if (rc == 0) m->checksums.assign(m->h_sums, ck ? m->h_sums + nseg : m->h_sums);
-  if (rc != 0) {
+  auto failed = [&](int rc) {
     return release(internal::FromAbi(
         rc, "Failed to compress via queue pair " + std::to_string(queue_pair_id) +
                 " of compress device " + std::to_string(device_id_)));
+  };
+  // an op covers k segments (max_sgl_segs, reference memory.cc:359-399); k == 1 compresses
+  // each segment straight into its slot, k > 1 compresses the op as one stream into the
+  // queue pair's chain scratch and then spreads it over the op's slots (the dst mbuf chain,
+  // memory.cc:401-425), slot_size() bytes per slot
+  const std::uint32_t k = configuration_->max_sgl_segs();
+  const std::uint64_t opseg = std::uint64_t{k} * seg;
+  const auto nops = static_cast<std::uint32_t>((n + opseg - 1) / opseg);
+  const std::uint64_t stride = k > 1 ? bitar_hip_slot_size(codec, static_cast<std::uint32_t>(opseg)) : 0;
+  auto st = m->Tables(k > 1 ? 2ull * nseg + nops : nseg);
+  if (st.ok() && k > 1) st = m->Chain(stride * nops);
+  if (!st.ok()) return release(st);
+  int rc = 0;
+  if (k == 1) {
+    for (std::uint32_t i = 0; i < nseg; ++i)
+      m->h_ptrs[i] = static_cast<std::uint64_t>(reinterpret_cast<uintptr_t>(slots[i]));
+    rc = bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 8ull * nseg, m->stream);
+    if (rc == 0)
+      rc = bitar_hip_compress_scattered(ctx_, m->stream, codec, d_in, n, seg,
+                                        reinterpret_cast<void* const*>(m->d_ptrs), slot_size_,
+                                        m->d_sizes);
+  } else {
+    rc = bitar_hip_compress(ctx_, m->stream, codec, d_in, n, static_cast<std::uint32_t>(opseg),
+                            m->d_chain, stride, m->d_sizes);
+  }
+  if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sizes, m->d_sizes, 4ull * nops, m->stream);
+  // the checksum of the uncompressed input of each op (DPDK input_chksum of a compress op)
+  const std::uint32_t ck = checksum_kind();
+  if (rc == 0 && ck) {
+    st = m->Sums(nops);
+    if (!st.ok()) return release(st);
+    rc = bitar_hip_checksum(ctx_, m->stream, ck, d_in, n, static_cast<std::uint32_t>(opseg),
+                            nullptr, nops, m->d_sums);
+    if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sums, m->d_sums, 8ull * nops, m->stream);
+  }
+  if (rc == 0) rc = bitar_hip_sync(ctx_, m->stream);
+  if (rc != 0) return failed(rc);
+  m->checksums.assign(m->h_sums, ck ? m->h_sums + nops : m->h_sums);
+  for (std::uint32_t j = 0; j < nops; ++j) {
+    const std::uint64_t cap = (k == 1 ? 1 : std::min<std::uint64_t>(k, nseg - std::uint64_t{j} * k)) * slot_size_;
+    if (m->h_sizes[j] == BITAR_HIP_SEGMENT_ERROR || m->h_sizes[j] > cap)
+      return release(arrow::Status::IOError("Compress data output is larger than allocated buffer"));
   }
   auto mm = hip_memory_manager(device_id_);
   compressed_buffers.reserve(nseg);
-  for (std::uint32_t i = 0; i < nseg; ++i) {
-    if (m->h_sizes[i] == BITAR_HIP_SEGMENT_ERROR)
-      return release(arrow::Status::IOError("Compress data output is larger than allocated buffer"));
-    compressed_buffers.emplace_back(std::make_unique<arrow::Buffer>(slots[i], m->h_sizes[i], mm));
+  if (k == 1) {
+    for (std::uint32_t i = 0; i < nseg; ++i)
+      compressed_buffers.emplace_back(std::make_unique<arrow::Buffer>(slots[i], m->h_sizes[i], mm));
+    return compressed_buffers;
   }
+  // spread op j's stream over its slots: slot i of the op holds bytes [i*L, (i+1)*L); the
+  // op's trailing slots may stay empty and are returned as empty buffers, so that Decompress
+  // regroups exactly k buffers per op (the reference returns only the non-empty ones,
+  // device.cc:183-195, and then groups by k regardless)
+  const std::uint64_t L = slot_size_;
+  std::vector<std::uint32_t> piece(nseg, 0);
+  std::uint32_t e = 0;
+  auto* chain = static_cast<std::uint8_t*>(m->d_chain);
+  for (std::uint32_t i = 0; i < nseg; ++i) {
+    const std::uint32_t j = i / k;
+    const std::uint64_t at = std::uint64_t{i % k} * L;
+    const std::uint64_t size = m->h_sizes[j];
+    piece[i] = static_cast<std::uint32_t>(size > at ? std::min(L, size - at) : 0);
+    if (piece[i] == 0) continue;
+    m->h_ptrs[e] = reinterpret_cast<std::uint64_t>(chain + j * stride + at);
+    m->h_ptrs[nseg + e] = reinterpret_cast<std::uint64_t>(slots[i]);
+    m->h_sizes[nops + e] = piece[i];
+    ++e;
+  }
+  rc = bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 16ull * nseg, m->stream);
+  if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->d_sizes, m->h_sizes + nops, 4ull * e, m->stream);
+  if (rc == 0)
+    rc = bitar_hip_copy_batch(ctx_, m->stream, reinterpret_cast<const void* const*>(m->d_ptrs),
+                              reinterpret_cast<void* const*>(m->d_ptrs + nseg), m->d_sizes, e);
+  if (rc == 0) rc = bitar_hip_sync(ctx_, m->stream);
+  if (rc != 0) return failed(rc);
+  for (std::uint32_t i = 0; i < nseg; ++i)
+    compressed_buffers.emplace_back(std::make_unique<arrow::Buffer>(slots[i], piece[i], mm));
   return compressed_buffers;
 }
 
@@ -377,7 +440,13 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
 
   const auto nseg = static_cast<std::uint32_t>(compressed_buffers.size());
   const auto codec = internal::AbiCodec(*configuration_);
-  ARROW_RETURN_NOT_OK(m->Tables(nseg));
+  // op j decompresses buffers [j*k, (j+1)*k) as one stream into k segments of the output
+  // (max_sgl_segs = k, reference memory.cc:432-505); k > 1 first joins the op's buffers in
+  // the queue pair's chain scratch (the src mbuf chain)
+  const std::uint32_t k = configuration_->max_sgl_segs();
+  const std::uint64_t opseg = std::uint64_t{k} * seg;
+  const std::uint32_t nops = (nseg + k - 1) / k, nfull = nseg / k, tail = nseg % k;
+  ARROW_RETURN_NOT_OK(m->Tables(k > 1 ? 2ull * nseg + nops : nseg));
 
   // sources: HBM buffers in place; host buffers staged behind the output area
   std::uint64_t host_bytes = 0;
@@ -394,6 +463,8 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
   std::uint64_t off = out_bytes;
   for (std::uint32_t i = 0; i < nseg; ++i) {
     const auto& b = compressed_buffers[i];
+    if (static_cast<std::uint64_t>(b->size()) >= BITAR_HIP_SEGMENT_ERROR)
+      return arrow::Status::Invalid("compressed buffer ", i, " is too large");
     m->h_sizes[i] = static_cast<std::uint32_t>(b->size());
     if (on_dev[i]) {
       m->h_ptrs[i] = b->address();
@@ -406,34 +477,77 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
     }
   }
   void* d_out = out_on_dev ? reinterpret_cast<void*>(out_addr) : m->d_stage;
-  BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 8ull * nseg, m->stream), "tables");
-  BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_sizes, m->h_sizes, 4ull * nseg, m->stream), "tables");
-  int rc = bitar_hip_decompress(ctx_, m->stream, codec,
-                                reinterpret_cast<const void* const*>(m->d_ptrs), m->d_sizes,
-                                nseg, seg, d_out, static_cast<std::uint64_t>(min_capacity),
-                                m->d_prod);
+  int rc = 0;
+  std::uint32_t nunits = nseg;  // ops, one produced size / checksum each
+  std::uint64_t unit = seg;
+  if (k == 1) {
+    BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 8ull * nseg, m->stream), "tables");
+    BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_sizes, m->h_sizes, 4ull * nseg, m->stream), "tables");
+    rc = bitar_hip_decompress(ctx_, m->stream, codec,
+                              reinterpret_cast<const void* const*>(m->d_ptrs), m->d_sizes, nseg,
+                              seg, d_out, static_cast<std::uint64_t>(min_capacity), m->d_prod);
+  } else {
+    nunits = nops;
+    unit = opseg;
+    // op j's stream = its buffers back to back at chain + base_j (16-B aligned bases)
+    std::uint64_t total = 0;
+    std::vector<std::uint64_t> base(nops);
+    for (std::uint32_t j = 0; j < nops; ++j) {
+      base[j] = total;
+      std::uint64_t len = 0;
+      for (std::uint32_t i = j * k; i < std::min(nseg, (j + 1) * k); ++i) len += m->h_sizes[i];
+      if (len >= BITAR_HIP_SEGMENT_ERROR)
+        return arrow::Status::Invalid("compressed op ", j, " is too large");
+      m->h_sizes[nseg + j] = static_cast<std::uint32_t>(len);
+      total = (total + len + 15) & ~15ull;
+    }
+    ARROW_RETURN_NOT_OK(m->Chain(std::max<std::uint64_t>(total, 16)));
+    auto* chain = static_cast<std::uint8_t*>(m->d_chain);
+    for (std::uint32_t j = 0; j < nops; ++j) {
+      std::uint64_t at = base[j];
+      m->h_ptrs[2ull * nseg + j] = reinterpret_cast<std::uint64_t>(chain + at);
+      for (std::uint32_t i = j * k; i < std::min(nseg, (j + 1) * k); ++i) {
+        m->h_ptrs[nseg + i] = reinterpret_cast<std::uint64_t>(chain + at);
+        at += m->h_sizes[i];
+      }
+    }
+    BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 8ull * (2ull * nseg + nops), m->stream),
+              "tables");
+    BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_sizes, m->h_sizes, 4ull * (nseg + nops), m->stream),
+              "tables");
+    const auto* ops = reinterpret_cast<const void* const*>(m->d_ptrs + 2ull * nseg);
+    rc = bitar_hip_copy_batch(ctx_, m->stream, reinterpret_cast<const void* const*>(m->d_ptrs),
+                              reinterpret_cast<void* const*>(m->d_ptrs + nseg), m->d_sizes, nseg);
+    if (rc == 0 && nfull)
+      rc = bitar_hip_decompress(ctx_, m->stream, codec, ops, m->d_sizes + nseg, nfull,
+                                static_cast<std::uint32_t>(opseg), d_out, nfull * opseg, m->d_prod);
+    if (rc == 0 && tail)  // the last op covers the remaining tail < k buffers
+      rc = bitar_hip_decompress(ctx_, m->stream, codec, ops + nfull, m->d_sizes + nseg + nfull, 1,
+                                tail * seg, static_cast<std::uint8_t*>(d_out) + nfull * opseg,
+                                std::uint64_t{tail} * seg, m->d_prod + nfull);
+  }
   if (rc == 0)
-    rc = bitar_hip_memcpy(ctx_, m->h_sizes, m->d_prod, 4ull * nseg, m->stream);
-  // the checksum of the decompressed output (DPDK output_chksum of a decompress op)
+    rc = bitar_hip_memcpy(ctx_, m->h_sizes, m->d_prod, 4ull * nunits, m->stream);
+  // the checksum of the decompressed output of each op (DPDK output_chksum)
   const std::uint32_t ck = checksum_kind();
   if (rc == 0 && ck) {
-    ARROW_RETURN_NOT_OK(m->Sums(nseg));
+    ARROW_RETURN_NOT_OK(m->Sums(nunits));
     rc = bitar_hip_checksum(ctx_, m->stream, ck, d_out, static_cast<std::uint64_t>(min_capacity),
-                            seg, m->d_prod, nseg, m->d_sums);
-    if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sums, m->d_sums, 8ull * nseg, m->stream);
+                            static_cast<std::uint32_t>(unit), m->d_prod, nunits, m->d_sums);
+    if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sums, m->d_sums, 8ull * nunits, m->stream);
   }
   if (rc == 0 && !out_on_dev)
     rc = bitar_hip_memcpy(ctx_, reinterpret_cast<void*>(out_addr), d_out,
                           static_cast<std::uint64_t>(min_capacity), m->stream);
   if (rc == 0) rc = bitar_hip_sync(ctx_, m->stream);
-  if (rc == 0) m->checksums.assign(m->h_sums, ck ? m->h_sums + nseg : m->h_sums);
+  if (rc == 0) m->checksums.assign(m->h_sums, ck ? m->h_sums + nunits : m->h_sums);
   if (rc != 0) {
     return internal::FromAbi(rc, "Failed to decompress via queue pair " +
                                      std::to_string(queue_pair_id) + " of compress device " +
                                      std::to_string(device_id_));
   }
   std::int64_t total = 0;
-  for (std::uint32_t i = 0; i < nseg; ++i) {
+  for (std::uint32_t i = 0; i < nunits; ++i) {
     if (m->h_sizes[i] == BITAR_HIP_SEGMENT_ERROR)
       return arrow::Status::IOError("Some operations have failed");
     total += m->h_sizes[i];
@@ -483,8 +597,13 @@ arrow::Status CompressDevice<Class, Enable>::ValidateConfiguration() {
     return arrow::Status::NotImplemented("Compress device ", +device_id_,
                                          " does not support the codec");
   if (configuration_->max_sgl_segs() < 1) configuration_->set_max_sgl_segs(1);
-  if (configuration_->max_sgl_segs() > 1)
-    return arrow::Status::Invalid("Compress device does not support chained mbufs.");
+  // chained ops: an op of max_sgl_segs segments is one stream, so it must fit a segment
+  // kernel (the reference asks the PMD for RTE_COMP_FF_OOP_SGL_IN_SGL_OUT, device.cc:377-380)
+  if (std::uint64_t{configuration_->max_sgl_segs()} * configuration_->decompressed_seg_size() >
+      internal::kMaxSegSize32) {
+    return arrow::Status::Invalid("Compress device does not support chained mbufs of more than ",
+                                  internal::kMaxSegSize32, " bytes per operation.");
+  }
   if (configuration_->decompressed_seg_size() < internal::kMinSegSize ||
       configuration_->decompressed_seg_size() > internal::kMaxSegSize32) {
     return arrow::Status::Invalid("decompressed_seg_size is not in the range of [",

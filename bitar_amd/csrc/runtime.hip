@@ -49,6 +49,7 @@ __global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t, uint64_t*
 __global__ void pack_kernel(const uint8_t*, uint64_t, const uint32_t*, const uint64_t*, uint32_t,
                             uint8_t*);
 __global__ void fill_kernel(int, uint64_t, uint64_t, uint8_t*, uint64_t);
+__global__ void copy_batch_kernel(const uint8_t* const*, uint8_t* const*, const uint32_t*, uint32_t);
 __global__ void lz4f_sizes_kernel(const uint32_t*, uint32_t, uint64_t, uint32_t, uint32_t*);
 __global__ void lz4f_pack_kernel(const uint8_t*, uint64_t, uint32_t, const uint8_t*, uint64_t,
                                  const uint32_t*, const uint64_t*, uint32_t, uint8_t*);
@@ -522,6 +523,19 @@ int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_
                        nseg, static_cast<uint8_t*>(d_frame));
     HIP_TRY(hipGetLastError(), "pack launch");
   }
+  return 0;
+}
+
+int bitar_hip_copy_batch(bitar_hip_ctx* ctx, void* stream, const void* const* d_srcs,
+                         void* const* d_dsts, const uint32_t* d_sizes, uint32_t n) {
+  if (int r = enter(ctx)) return r;
+  if (n == 0) return 0;
+  if (!d_srcs || !d_dsts || !d_sizes) return fail(BITAR_HIP_INVALID, "null buffer");
+  hipStream_t s = pick_stream(ctx, stream);
+  hipLaunchKernelGGL(bitar_hip::copy_batch_kernel, dim3(n), dim3(64), 0, s,
+                     reinterpret_cast<const uint8_t* const*>(d_srcs),
+                     reinterpret_cast<uint8_t* const*>(d_dsts), d_sizes, n);
+  HIP_TRY(hipGetLastError(), "copy batch launch");
   return 0;
 }
 

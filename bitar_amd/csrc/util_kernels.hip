@@ -71,6 +71,18 @@ __global__ __launch_bounds__(64) void pack_kernel(const uint8_t* __restrict__ sl
   wave_copy_global(global_ptr(frame + offsets[i]), global_ptr(slab + (uint64_t)i * stride), len);
 }
 
+// Batched copy: entry i moves sizes[i] bytes from srcs[i] to dsts[i]; one wave per entry.
+// Splits a chained op's output over its slots and joins chained inputs (max_sgl_segs > 1).
+__global__ __launch_bounds__(64) void copy_batch_kernel(const uint8_t* const* __restrict__ srcs,
+                                                        uint8_t* const* __restrict__ dsts,
+                                                        const uint32_t* __restrict__ sizes,
+                                                        uint32_t n) {
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  const uint32_t len = sizes[i];
+  if (len) wave_copy_global(global_ptr(dsts[i]), global_ptr(srcs[i]), len);
+}
+
 // LZ4 frame data blocks (lz4 frame format, independent blocks): framed size of block i =
 // 4-byte size field + the compressed block, or the raw slice when it did not shrink (a
 // compressed block may not exceed the frame's maximum block size).

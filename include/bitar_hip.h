@@ -152,6 +152,15 @@ int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream);
 int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_t slot_stride,
                    const uint32_t* d_sizes, uint32_t nseg, uint64_t* d_offsets, void* d_frame);
 
+/* Batched device-to-device copy: entry i moves d_sizes[i] bytes from d_srcs[i] to d_dsts[i]
+ * (device arrays of n device pointers / sizes; any alignment, ranges must not overlap).
+ * Asynchronous on `stream`.  The front-end's chained operations (max_sgl_segs > 1) use it to
+ * spread one op's compressed stream over its pool slots and to join a chained input: the
+ * mbuf chains the reference builds with rte_pktmbuf_chain (src/memory.cc:60-100, 380-425,
+ * 459-500). */
+int bitar_hip_copy_batch(bitar_hip_ctx* ctx, void* stream, const void* const* d_srcs,
+                         void* const* d_dsts, const uint32_t* d_sizes, uint32_t n);
+
 /* The data blocks of an LZ4 frame (LZ4 frame format, block independence) from LZ4 segments
  * of n input bytes (d_in, segment size seg <= 65536, so the frame's maximum block size is
  * 64 KiB): block i = LE32 size + the compressed block, or LE32(len | 1<<31) + the raw input

@@ -280,6 +280,60 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
       CHECK(d->Recycle(*comp) == comp->size());
     }
   }
+  // chained ops (max_sgl_segs = 4, reference memory.cc:350-505): one stream per 4 segments,
+  // spread over 4 slots (trailing ones empty); Decompress regroups 4 buffers per op; one
+  // checksum per op; an op larger than 64 KiB is refused
+  for (const auto codec : {bitar::Codec::LZ4, bitar::Codec::DEFLATE, bitar::Codec::ZSTD}) {
+    const std::uint32_t seg = 16384, k = 4;
+    {
+      auto fresh = driver->GetDevices({(*ids)[0]});
+      CHECK_OK(fresh.status());
+      auto cfg = MakeConfig(codec, seg * 2);
+      cfg->set_max_sgl_segs(k);
+      CHECK((*fresh)[0]->Initialize(std::move(cfg)).IsInvalid());
+    }
+    auto fresh = driver->GetDevices({(*ids)[0]});
+    CHECK_OK(fresh.status());
+    auto& d = (*fresh)[0];
+    auto cfg = MakeConfig(codec, seg);
+    cfg->set_max_sgl_segs(k);
+    cfg->set_checksum_type(bitar::ChecksumType::CRC32);
+    CHECK_OK(d->Initialize(std::move(cfg)));
+    auto comp = d->Compress(0, host_in);
+    CHECK_OK(comp.status());
+    if (!comp.ok()) continue;
+    const auto nseg = (data.size() + seg - 1) / seg;
+    const auto nops = (nseg + k - 1) / k;
+    CHECK(comp->size() == nseg);
+    CHECK(d->checksums(0).size() == nops);
+    const std::vector<std::uint64_t> cs = d->checksums(0);
+    WriteSegments(outdir + (codec == bitar::Codec::LZ4       ? "/sgl_lz4.segs"
+                            : codec == bitar::Codec::DEFLATE ? "/sgl_deflate.segs"
+                                                             : "/sgl_zstd.segs"),
+                  *comp);
+    auto o = arrow::AllocateResizableBuffer(static_cast<int64_t>(nseg * seg));
+    std::unique_ptr<arrow::ResizableBuffer> out = std::move(*o);
+    CHECK_OK(d->Decompress(1, *comp, out));
+    CHECK(out->size() == static_cast<int64_t>(data.size()) &&
+          std::memcmp(out->data(), data.data(), data.size()) == 0);
+    CHECK(d->checksums(1) == cs);
+    // HBM in and out
+    auto dev_in = arrow::Buffer::Copy(host_in, bitar::hip_memory_manager(0));
+    CHECK_OK(dev_in.status());
+    auto comp2 = d->Compress(1, *dev_in);
+    CHECK_OK(comp2.status());
+    auto dev_out = bitar::AllocateResizableDeviceBuffer(static_cast<int64_t>(nseg * seg), 0);
+    std::unique_ptr<arrow::ResizableBuffer> dout = std::move(*dev_out);
+    CHECK_OK(d->Decompress(0, *comp2, dout));
+    auto back = arrow::Buffer::Copy(std::shared_ptr<arrow::Buffer>(std::move(dout)),
+                                    arrow::default_cpu_memory_manager());
+    CHECK_OK(back.status());
+    if (back.ok())
+      CHECK((*back)->size() == static_cast<int64_t>(data.size()) &&
+            std::memcmp((*back)->data(), data.data(), data.size()) == 0);
+    CHECK(d->Recycle(*comp) == comp->size());
+    CHECK(d->Recycle(*comp2) == comp2->size());
+  }
   // empty input -> empty vector (device.cc:161-164); empty vector -> OK
   auto& d0 = (*devs)[0];
   CHECK_OK(d0->Initialize(MakeConfig(bitar::Codec::LZ4, 65536)));

@@ -81,6 +81,24 @@ def test_frontend_on_gpu(tmp_path):
     for i, s in enumerate(segs):
         rc, plain = O.zstd_decompress(s, seg)
         assert rc == 0 and plain == data[i * seg:(i + 1) * seg]
+    # chained ops (max_sgl_segs = 4 over 16 KiB segments): the 4 buffers of op j joined are
+    # one stream of input bytes [j*64Ki, (j+1)*64Ki), the oracle's own encoding of them
+    seg, k = 16384, 4
+    for name, enc, dec in (("sgl_lz4.segs", O.lz4_compress, O.lz4_decompress),
+                           ("sgl_deflate.segs", O.deflate_dynamic, None),
+                           ("sgl_zstd.segs", O.zstd_compress, O.zstd_decompress)):
+        segs = _segments(tmp_path / name)
+        assert len(segs) == (len(data) + seg - 1) // seg, name
+        for j in range(0, len(segs), k):
+            stream = b"".join(segs[j:j + k])
+            plain = data[j * seg:(j + k) * seg]
+            assert all(len(p) > 0 for p in segs[j:j + k][:1])
+            if dec is None:
+                assert zlib.decompress(stream, -15) == plain
+            else:
+                rc, got = dec(stream, k * seg)
+                assert rc == 0 and got == plain, (name, j)
+            assert enc(plain) == (0, stream), (name, j)
 
 
 @pytest.mark.gpu

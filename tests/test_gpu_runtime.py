@@ -246,3 +246,29 @@ def test_checksum_rejects_bad_kind(eng):
     s = eng.empty(1, dtype=torch.int64)
     with pytest.raises(bitar_amd.BitarError):
         eng.checksum(4, d, 100, s)
+
+
+def test_copy_batch_any_alignment(eng):
+    """bitar_hip_copy_batch (chained ops' split / join): entries of any size and alignment,
+    zero-size entries, neighbours untouched."""
+    rng = np.random.default_rng(3)
+    src = up(rng.integers(0, 256, 1 << 20, dtype=np.uint8))
+    dst = eng.empty(1 << 20)
+    dst.zero_()
+    base_s, base_d = src.data_ptr(), dst.data_ptr()
+    entries, at = [], 0
+    for k in range(300):
+        n = int(rng.choice([0, 1, 15, 16, 17, 63, 64, 1000, 4096, 5000]))
+        so = int(rng.integers(0, (1 << 20) - n))
+        entries.append((so, at, n))
+        at += n + int(rng.integers(1, 40))
+    srcs = torch.tensor([base_s + e[0] for e in entries], dtype=torch.int64).cuda()
+    dsts = torch.tensor([base_d + e[1] for e in entries], dtype=torch.int64).cuda()
+    sizes = torch.tensor([e[2] for e in entries], dtype=torch.int32).cuda()
+    eng.copy_batch(srcs, dsts, sizes, len(entries))
+    eng.sync()
+    s, d = down(src), down(dst)
+    want = np.zeros_like(d)
+    for so, do, n in entries:
+        want[do:do + n] = s[so:so + n]
+    assert np.array_equal(d, want)
