@@ -162,7 +162,7 @@ def run_job(eng, codec_name, kind, job_bytes, seg, nstreams, steps, warmup, worl
             "local": local, "job_bytes": job_bytes}
 
 
-def kernel_lines(codec_name, r, traffic_json):
+def kernel_lines(codec_name, r, traffic_json, leg="headline"):
     """roofline of the dominant kernel + per-kernel averages.  Durations are HIP events
     bracketing each launch on its own stream; algorithmic bytes per launch =
     U + C (+ 4 B per segment for compress) of the part that launch covered."""
@@ -179,7 +179,8 @@ def kernel_lines(codec_name, r, traffic_json):
     traffic = None
     try:
         with open(traffic_json) as f:
-            traffic = json.load(f).get(dominant[0])
+            # per-launch HBM bytes of this leg's kernel, from its own PMC passes
+            traffic = json.load(f).get(f"{leg}/{dominant[0]}")
     except (OSError, ValueError):
         pass
     roof = {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 2),
@@ -191,8 +192,8 @@ def kernel_lines(codec_name, r, traffic_json):
     return roof, kernels
 
 
-def leg_summary(name, r, world, steps, traffic_json, workload):
-    roof, kern = kernel_lines(name, r, traffic_json)
+def leg_summary(name, r, world, steps, traffic_json, workload, leg=None):
+    roof, kern = kernel_lines(name, r, traffic_json, leg or name)
     U = float(r["job_bytes"])
     return {"workload": workload,
             "value": round(U * steps / r["elapsed"] / GIB, 3), "unit": "GiB/s",
@@ -511,7 +512,7 @@ def main():
             "zlib1_raw_deflate_59460": stock[1]["deflate"],
             "libzstd1_on_arrow_kind2": stock[1]["zstd"]}
     if rb is not None:
-        s = leg_summary("lz4", rb, world, args.steps, args.traffic_json,
+        s = leg_summary("lz4", rb, world, args.steps, args.traffic_json, leg="recordbatch", workload=
                         f"BASELINE configs[3]: {args.record_bytes >> 30} GiB Arrow record-batch "
                         f"job, 64 KiB chunks, round-robin batches of 256 chunks over {world} "
                         f"GPU(s), {args.streams} concurrent queue-pair streams per GPU, LZ4 "

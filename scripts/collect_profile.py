@@ -40,24 +40,37 @@ def per_kernel(path):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+LEGS = ("headline", "zstd", "deflate", "deflate_dyn")
+# the kernels each leg is about (every pass also runs the headline's LZ4 kernels)
+LEG_KERNELS = {"headline": ("lz4_",), "zstd": ("zstd_",),
+               "deflate": ("deflate_compress", "inflate"),
+               "deflate_dyn": ("deflate_dyn_", "inflate")}
+
+
 def main():
     tag, rdir = sys.argv[1], sys.argv[2]
     out = os.path.join(ROOT, "gpurun_out")
     rdir = os.path.join(ROOT, rdir)
     os.makedirs(rdir, exist_ok=True)
     shutil.copy(os.path.join(out, f"bench_{tag}.json"), os.path.join(rdir, "bench.json"))
-    shutil.copy(os.path.join(out, f"prof_{tag}", "trace_kernel_stats.csv"),
-                os.path.join(rdir, "kernel_stats.csv"))
-    fetch = per_kernel(os.path.join(out, f"pmc_{tag}_FETCH_SIZE", "pmc_counter_collection.csv"))
-    write = per_kernel(os.path.join(out, f"pmc_{tag}_WRITE_SIZE", "pmc_counter_collection.csv"))
     traffic, lines = {}, []
-    for k in sorted(set(fetch) | set(write)):
-        f_kib, w_kib = fetch.get(k, 0.0), write.get(k, 0.0)
-        x = FETCH_FACTOR.get(k, 2.0)
-        b = (x * f_kib + w_kib) * 1024.0
-        traffic[k] = round(b)
-        lines.append(f"{k:28s} FETCH_SIZE {f_kib:14.1f} KiB (x{x:g} = {x * f_kib * 1024:.4g} B)  "
-                     f"WRITE_SIZE {w_kib:14.1f} KiB  -> {b:.4g} B per launch")
+    for leg in LEGS:
+        prof = os.path.join(out, f"prof_{tag}_{leg}", "trace_kernel_stats.csv")
+        if not os.path.exists(prof):
+            continue
+        shutil.copy(prof, os.path.join(rdir, f"kernel_stats_{leg}.csv"))
+        fetch = per_kernel(os.path.join(out, f"pmc_{tag}_{leg}_FETCH_SIZE", "pmc_counter_collection.csv"))
+        write = per_kernel(os.path.join(out, f"pmc_{tag}_{leg}_WRITE_SIZE", "pmc_counter_collection.csv"))
+        for k in sorted(set(fetch) | set(write)):
+            if not k.startswith(LEG_KERNELS[leg]):
+                continue
+            f_kib, w_kib = fetch.get(k, 0.0), write.get(k, 0.0)
+            x = FETCH_FACTOR.get(k, 2.0)
+            b = (x * f_kib + w_kib) * 1024.0
+            traffic[f"{leg}/{k}"] = round(b)
+            lines.append(f"{leg + '/' + k:40s} FETCH_SIZE {f_kib:14.1f} KiB (x{x:g} = "
+                         f"{x * f_kib * 1024:.4g} B)  WRITE_SIZE {w_kib:14.1f} KiB  -> {b:.4g} B "
+                         f"per launch")
     with open(os.path.join(rdir, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
     with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:

@@ -9,11 +9,16 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { echo bench failed; tail -30 gpurun_out/bench_${TAG}.err; exit 1; }
 cat gpurun_out/bench_${TAG}.json
 if [ -n "$PROFILE" ]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o trace --output-format csv -- \
-    python3 bench.py --no-cpu-baseline --no-secondary ${BENCH_ARGS} > gpurun_out/prof_${TAG}.log 2>&1 || { echo prof failed; tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
-  for ctr in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 600 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${TAG}_$ctr -o pmc --output-format csv -- \
-      python3 bench.py --no-cpu-baseline --no-secondary --steps 2 --warmup 1 ${BENCH_ARGS} > gpurun_out/pmc_${TAG}_$ctr.log 2>&1 || { echo pmc $ctr failed; tail -30 gpurun_out/pmc_${TAG}_$ctr.log; exit 1; }
+  # one kernel-trace pass and one pass per PMC counter for each leg on its own (--only), so a
+  # kernel's averages never mix launches of different legs (the record-batch leg also runs
+  # lz4_compress_kernel, the stock-decode leg lz4_decompress_kernel, ...)
+  for leg in ${PROF_LEGS:-headline zstd deflate deflate_dyn}; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$leg -o trace --output-format csv -- \
+      python3 bench.py --only $leg ${BENCH_ARGS} > gpurun_out/prof_${TAG}_$leg.log 2>&1 || { echo prof $leg failed; tail -30 gpurun_out/prof_${TAG}_$leg.log; exit 1; }
+    for ctr in FETCH_SIZE WRITE_SIZE; do
+      timeout -k 10 300 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${TAG}_${leg}_$ctr -o pmc --output-format csv -- \
+        python3 bench.py --only $leg --steps 2 --warmup 1 ${BENCH_ARGS} > gpurun_out/pmc_${TAG}_${leg}_$ctr.log 2>&1 || { echo pmc $leg $ctr failed; tail -30 gpurun_out/pmc_${TAG}_${leg}_$ctr.log; exit 1; }
+    done
   done
-  find gpurun_out/prof_${TAG} gpurun_out/pmc_${TAG}_* -name "*.csv" | head -20
+  find gpurun_out/prof_${TAG}_* gpurun_out/pmc_${TAG}_* -name "*stats.csv" | head -20
 fi
