@@ -30,8 +30,10 @@ __global__ void inflate_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
 template <uint32_t L>
 __global__ void inflate_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                      const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
-__global__ void zstd_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
-                                     uint8_t* const*, uint32_t*, uint32_t*);
+__global__ void zstd_parse_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint2*);
+__global__ void zstd_entropy_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
+                                    const uint2*, uint8_t*, uint64_t, uint8_t* const*, uint32_t*,
+                                    uint32_t*);
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                        const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                        uint32_t*, uint32_t*, uint32_t);
@@ -233,8 +235,8 @@ uint64_t bitar_hip_slot_size(uint32_t codec, uint32_t seg) {
     bound = (uint64_t)seg + seg / 255u + 16u;           // LZ4_compressBound
   else if (codec == BITAR_HIP_CODEC_DEFLATE || codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC)
     bound = ((uint64_t)seg * 9 + 7) / 8 + 16u;          // fixed Huffman, 9 bits/literal
-  else if (codec == BITAR_HIP_CODEC_ZSTD)  // oracle bo_zstd_bound: blocks of <= 256 sequences
-    bound = (uint64_t)seg + 7u + 3u * ((uint64_t)seg / 1024u + 2u) + 8u + 512u;
+  else if (codec == BITAR_HIP_CODEC_ZSTD)  // oracle bo_zstd_bound: one block, raw if larger
+    bound = (uint64_t)seg + 7u + 3u + 8u + 512u;
   else
     return 0;
   return (bound + 255u) & ~(uint64_t)255u;
@@ -317,9 +319,24 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
     HIP_TRY(hipFreeAsync(scratch, s), "scratch release");
     HIP_TRY(le, "compress launch");
   }
-  else
-    hipLaunchKernelGGL(bitar_hip::zstd_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
-                       n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
+  else {
+    // pass 1 (parse -> literals + sequence records) and pass 2 (entropy coding) through a
+    // stream-ordered scratch: per segment the literal area + records (zstd_compress.hip),
+    // then {nlit, nseq} per segment
+    const uint64_t scr_stride = ((uint64_t)seg + 15u & ~15ull) + 8ull * (seg / 4u + 2u) + 255u & ~255ull;
+    void* scratch = nullptr;
+    HIP_TRY(hipMallocAsync(&scratch, nseg * scr_stride + nseg * 8u, s), "scratch allocation");
+    auto* scr = static_cast<uint8_t*>(scratch);
+    auto* meta = reinterpret_cast<uint2*>(scr + nseg * scr_stride);
+    hipLaunchKernelGGL(bitar_hip::zstd_parse_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in, n,
+                       seg, scr, scr_stride, meta);
+    hipLaunchKernelGGL(bitar_hip::zstd_entropy_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
+                       n, seg, scr, scr_stride, meta, slab, slot_stride, dsts, d_sizes,
+                       err_word(ctx, s));
+    const hipError_t le = hipGetLastError();
+    HIP_TRY(hipFreeAsync(scratch, s), "scratch release");
+    HIP_TRY(le, "compress launch");
+  }
   HIP_TRY(hipGetLastError(), "compress launch");
   return 0;
 }

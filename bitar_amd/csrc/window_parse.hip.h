@@ -242,12 +242,19 @@ __device__ __forceinline__ uint32_t chain_fast(uint64_t& m, uint64_t extm, uint3
 // The window-scan parse over one segment; hands each window to E::window and the tail to
 // E::sequence.
 // Returns where the tail literals start (the emitter's pending_from).
-template <class E>
+// REP (the Zstd parse, oracle BO_PARSE_REP): a history h of the parse's 3 most recent distinct
+// match distances (initially 1 4 8), fixed per window; every position first tries p - h0,
+// p - h1, p - h2 (the first whose 4 bytes agree), then its hash candidate; a position with
+// only a hash match does not start a match when one of the next kRepAhead positions holds a
+// repeat match.
+constexpr uint32_t kRepAhead = 3;
+template <class E, bool REP = false>
 __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, const GMEM uint8_t* in_end,
                                       uint16_t* table, uint8_t* inring, uint32_t max_dist,
                                       uint32_t max_mlen, E& em) {
   const uint32_t lane = lane_id();
   uint32_t anchor = 0, emitted = 0;
+  uint32_t h0 = 1, h1 = 4, h2 = 8;  // REP: the distance history (uniform)
   InRing I;
   I.ring = inring;
   I.in_lo = (uint32_t)(uintptr_t)in;
@@ -290,7 +297,18 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       // Table and ring accesses are issued on all lanes (no exec-mask branches: the scalar
       // unit is the bottleneck).  Lanes past last_start exist only in the final window;
       // their table writes are never looked up again.
-      const uint32_t cand = table[h];
+      uint32_t cand = table[h];
+      bool isrep = false;
+      if constexpr (REP) {
+        // repeat candidates, read from the ring (h <= max_dist: every p - h >= x - kMaxDist is
+        // staged); their 4 bytes against the position's
+        const uint32_t r0 = I.dword(p - h0), r1 = I.dword(p - h1), r2 = I.dword(p - h2);
+        const bool k0 = act && h0 <= p && r0 == v.x;
+        const bool k1 = act && h1 <= p && r1 == v.x;
+        const bool k2 = act && h2 <= p && r2 == v.x;
+        isrep = k0 || k1 || k2;
+        cand = k0 ? p - h0 : k1 ? p - h1 : k2 ? p - h2 : cand;
+      }
       lds_order();
       table[h] = (uint16_t)p;
       lds_order();
@@ -316,7 +334,14 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       const uint32_t pos_in = pos;
       const uint32_t start = pos > x ? pos - x : 0u;
       // (len >= kMinMatch implies pre; ballots of single compares, see wave.hip.h)
-      const uint64_t valid = ballot(len >= kMinMatch) & (start < kWave ? ~0ull << start : 0ull);
+      uint64_t valid = ballot(len >= kMinMatch) & (start < kWave ? ~0ull << start : 0ull);
+      if constexpr (REP) {  // a hash-only match gives way to a repeat match just ahead
+        const uint64_t repm = ballot(isrep);
+        uint64_t ahead = 0;
+#pragma unroll
+        for (uint32_t k = 1; k <= kRepAhead; ++k) ahead |= repm >> k;
+        valid &= ~(~repm & ahead);
+      }
       const uint64_t extm = valid & ballot(len == kPreExt) & ballot(lim > kPreExt);
       uint64_t chain = 0;
       uint32_t mlen_v = len;
@@ -380,6 +405,27 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
         m = e < kWave ? valid & (~0ull << e) : 0ull;
       }
       if (chain) pos = x + e;
+      if constexpr (REP) {  // the history after this window's matches, in order
+        const uint32_t offv = p - cand;
+        uint64_t cm = chain;
+        while (cm) {
+          const uint32_t l = (uint32_t)__builtin_ctzll(cm);
+          cm &= cm - 1;
+          const uint32_t d = readlane(offv, l);
+          if (d == h1) {
+            h1 = h0;
+            h0 = d;
+          } else if (d == h2) {
+            h2 = h1;
+            h1 = h0;
+            h0 = d;
+          } else if (d != h0) {
+            h2 = h1;
+            h1 = h0;
+            h0 = d;
+          }
+        }
+      }
       Window W;
       W.x = x;
       W.chain = chain;

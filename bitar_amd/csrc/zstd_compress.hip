@@ -1,21 +1,32 @@
-// zstd_compress.hip -- Zstandard (RFC 8878) frame per segment, one wavefront per segment
-// (gfx950): zstd_compress_kernel, BASELINE configs[5].
+// zstd_compress.hip -- Zstandard (RFC 8878) frame per segment, level-1 class (gfx950):
+// BASELINE configs[4] / [5].  The frame is exactly the one the oracle's bo_zstd_compress_block
+// (oracle/bitar_zstd.c) writes: single-segment header with the content size, ONE block
+// (compressed, or raw when that is not smaller), Huffman literals (1 or 4 streams, direct or
+// FSE-compressed weights) or raw / RLE ones, repeat offsets, and per-table RLE /
+// FSE_Compressed / predefined sequence codes chosen by integer cost estimates.
 //
-// The frame is exactly the one the oracle's bo_zstd_compress_block (oracle/bitar_zstd.c)
-// writes: single-segment frame header with the content size, then blocks of <= 256
-// sequences found by the shared window-scan parse (window_parse.hip.h, restated by
-// bo_window_parse), each block = raw literals section + sequences coded with the predefined
-// FSE distributions (RFC 8878 3.1.1.3.2.2), offsets as Offset_Value = distance + 3 (no
-// repeat offsets); a block that does not shrink is stored raw.
+// Two launches, one wavefront per segment each, through a scratch area per segment
+// (kLitCap literal bytes, then 8-byte sequence records):
+//   zstd_parse_kernel    the window-scan parse (window_parse.hip.h) in its repeat-offset
+//                        form (REP): literal bytes staged in LDS and flushed to the literal
+//                        area, one {literal length | distance << 17, match length} record
+//                        per match; per segment {nlit, nseq} in the meta array.
+//   zstd_entropy_kernel  literal histograms per stream quarter, code lengths
+//                        (huffman.hip.h), weights, stream sizes; repeat-offset codes by a
+//                        scalar scan of the records; sequence code histograms, table
+//                        choice and FSE tables (one lane); then the literal streams and the
+//                        sequence bitstream, each lane placing its bit field by a prefix
+//                        sum into the LDS output ring.
+#include "huffman.hip.h"
 #include "window_parse.hip.h"
 
 namespace bitar_hip {
 
 namespace zse {
 
-constexpr uint32_t kMaxSeq = 256;  // sequences per block (oracle ZS_MAX_SEQ)
+using namespace cmp;
 
-// ---- predefined distributions and code tables (RFC 8878 3.1.1.3.2.1-2) ---------------------
+// ---- code tables (RFC 8878 3.1.1.3.2.1-2) ----------------------------------------------------
 constexpr uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,   7,   8,   9,    10,   11,
                                   12, 13, 14, 15, 16, 18, 20,  22,  24,  28,   32,   40,
                                   48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384,
@@ -30,8 +41,7 @@ constexpr uint32_t kMLBase[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13,   
 constexpr uint8_t kMLBits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                  0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1,
                                  2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-constexpr uint8_t kOFBits[29] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14,
-                                 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28};
+// predefined distributions (accuracy logs 6 / 5 / 6)
 constexpr int16_t kLLNorm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
                                  2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
 constexpr int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
@@ -39,183 +49,92 @@ constexpr int16_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1,
                                  1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
 constexpr int16_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
                                  1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+// 256 * log2(1 + i / 64), rounded (oracle kLog2Frac)
+constexpr uint8_t kLog2Frac[64] = {
+    0,   6,   11,  17,  22,  28,  33,  38,  44,  49,  54,  59,  63,  68,  73,  78,
+    82,  87,  92,  96,  100, 105, 109, 113, 118, 122, 126, 130, 134, 138, 142, 146,
+    150, 154, 157, 161, 165, 169, 172, 176, 179, 183, 186, 190, 193, 197, 200, 203,
+    207, 210, 213, 216, 220, 223, 226, 229, 232, 235, 238, 241, 244, 247, 250, 253};
 
-// FSE compression table of one predefined distribution (FSE_buildCTable; the oracle's
-// zs_build_ctable): state[] = next-state table, per symbol {deltaNbBits, deltaFindState |
-// extra-bit count << 16}.
-struct CTab {
-  uint16_t state[64];
-  uint2 sym[64];
+struct Tabs {
+  uint8_t ll_bits[36], ml_bits[53];
+  uint8_t ll_code[64], ml_code[128];  // ZSTD_LLcode below 64 / ZSTD_MLcode of ml - 3 below 128
+  int16_t ll_norm[36], ml_norm[53], of_norm[29];
+  uint8_t log2frac[64];
 };
-
-constexpr CTab build_ctab(const int16_t* norm, uint32_t max_sym, uint32_t al,
-                          const uint8_t* extra) {
-  CTab c{};
-  const uint32_t size = 1u << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
-  uint32_t high = size - 1;
-  uint8_t sym_at[64] = {};
-  uint32_t cumul[65] = {};
-  for (uint32_t s = 1; s <= max_sym + 1; ++s) {
-    if (norm[s - 1] == -1) {
-      cumul[s] = cumul[s - 1] + 1;
-      sym_at[high--] = (uint8_t)(s - 1);
-    } else {
-      cumul[s] = cumul[s - 1] + (uint32_t)norm[s - 1];
-    }
+constexpr Tabs build_tabs() {
+  Tabs t{};
+  for (uint32_t i = 0; i < 36; ++i) {
+    t.ll_bits[i] = kLLBits[i];
+    t.ll_norm[i] = kLLNorm[i];
   }
-  uint32_t pos = 0;
-  for (uint32_t s = 0; s <= max_sym; ++s)
-    for (int i = 0; i < norm[s]; ++i) {
-      sym_at[pos] = (uint8_t)s;
-      do {
-        pos = (pos + step) & mask;
-      } while (pos > high);
-    }
-  for (uint32_t u = 0; u < size; ++u) c.state[cumul[sym_at[u]]++] = (uint16_t)(size + u);
-  int32_t total = 0;
-  for (uint32_t s = 0; s <= max_sym; ++s) {
-    int32_t dnb = 0, dfs = 0;
-    if (norm[s] == 0) {
-      dnb = (int32_t)(((al + 1) << 16) - size);
-    } else if (norm[s] == -1 || norm[s] == 1) {
-      dnb = (int32_t)((al << 16) - size);
-      dfs = total - 1;
-      total += 1;
-    } else {
-      uint32_t hb = 0;  // highbit(norm - 1)
-      for (uint32_t v = (uint32_t)norm[s] - 1; v > 1; v >>= 1) ++hb;
-      const uint32_t mbo = al - hb;
-      const uint32_t msp = (uint32_t)norm[s] << mbo;
-      dnb = (int32_t)((mbo << 16) - msp);
-      dfs = total - norm[s];
-      total += norm[s];
-    }
-    c.sym[s] = uint2{(uint32_t)dnb, ((uint32_t)dfs & 0xFFFFu) | ((uint32_t)extra[s] << 16)};
+  for (uint32_t i = 0; i < 53; ++i) {
+    t.ml_bits[i] = kMLBits[i];
+    t.ml_norm[i] = kMLNorm[i];
   }
-  return c;
-}
-
-// code of a literal length < 64 / of a match length - 3 < 128 (ZSTD_LLcode / ZSTD_MLcode;
-// longer lengths: highbit + 19 / + 36)
-struct Codes {
-  uint8_t ll[64];
-  uint8_t ml[128];
-};
-constexpr Codes build_codes() {
-  Codes t{};
+  for (uint32_t i = 0; i < 29; ++i) t.of_norm[i] = kOFNorm[i];
+  for (uint32_t i = 0; i < 64; ++i) t.log2frac[i] = kLog2Frac[i];
   for (uint32_t v = 0; v < 64; ++v) {
     uint32_t c = 35;
     while (kLLBase[c] > v) --c;
-    t.ll[v] = (uint8_t)c;
+    t.ll_code[v] = (uint8_t)c;
   }
   for (uint32_t v = 0; v < 128; ++v) {
     uint32_t c = 52;
     while (kMLBase[c] > v + 3) --c;
-    t.ml[v] = (uint8_t)c;
+    t.ml_code[v] = (uint8_t)c;
   }
   return t;
 }
-
-__constant__ CTab kCtLL = build_ctab(kLLNorm, 35, 6, kLLBits);
-__constant__ CTab kCtML = build_ctab(kMLNorm, 52, 6, kMLBits);
-__constant__ CTab kCtOF = build_ctab(kOFNorm, 28, 5, kOFBits);
-__constant__ Codes kCodes = build_codes();
+__constant__ Tabs kT = build_tabs();
 
 __device__ __forceinline__ uint32_t hb32(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
+__device__ __forceinline__ uint32_t ll_code(uint32_t ll) { return ll < 64 ? kT.ll_code[ll] : hb32(ll) + 19u; }
+__device__ __forceinline__ uint32_t ml_code(uint32_t ml) {  // ml >= 3
+  const uint32_t b = ml - 3;
+  return b < 128 ? kT.ml_code[b] : hb32(b) + 36u;
+}
 
+// ---- scratch layout --------------------------------------------------------------------------
+__host__ __device__ constexpr uint64_t lit_cap(uint32_t seg) { return ((uint64_t)seg + 15u) & ~15ull; }
+__host__ __device__ constexpr uint64_t scratch_stride(uint32_t seg) {
+  return (lit_cap(seg) + 8ull * (seg / 4u + 2u) + 255u) & ~255ull;
+}
 
+// ---- pass 1: the parse, literals + sequence records ---------------------------------------
+struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the literal area
+  GMEM uint2* seqs;
+  uint32_t nseq;
 
-using cmp::InRing;
-using cmp::Window;
-using cmp::kObuf;
-using cmp::kObufMask;
-
-// Emitter, per parsed window: literal lanes write their byte straight into the literal
-// section (placed by mbcnt), staged in the LDS output ring; match lanes append {literal
-// length, offset, match length} to a 2 KiB LDS table; a block closes right after its 256th
-// match (the window is split at that lane).
-struct ZstdOut : cmp::ByteOut {
-  uint2* seqs;              // LDS, kMaxSeq records {ll | offset_value << 16, match length}
-  uint32_t* ew;             // LDS, 4 x 64: per-chain symbol transforms / state bits
-  const uint8_t* tabs;      // LDS, the OF / ML / LL next-state tables at 0 / 64 / 128
-  const GMEM uint8_t* src;  // the segment's input (raw blocks are copied from it)
-  uint32_t blk;             // output offset of the open block's header
-  uint32_t in0;             // input position the open block starts at
-  uint32_t nlit, nseq;
-
-  __device__ __forceinline__ void begin_block(uint32_t in_pos) {
-    blk = op;
-    in0 = in_pos;
-    nlit = 0;
-    nseq = 0;
-    // block header (3) + raw-literals header (3), patched in HBM when the block closes
-    if (room(6)) op += 6;
-  }
-
-  // literal bytes [s, s + len) of the input, appended to the literal section
+  // literal bytes [s, s + len) of the input, appended to the literal area
   __device__ __forceinline__ void literals(const GMEM uint8_t* in, const InRing& I, uint32_t s,
                                            uint32_t len) {
-    if (overflow || !len) return;
+    if (!len) return;
     const uint32_t lane = lane_id();
     if (len <= 256 && s >= I.lo) {
       for (uint32_t k = 0; k < len; k += kWave) {
         const uint32_t step = len - k < kWave ? len - k : kWave;
-        if (!room(step)) return;
+        room(step);
         lds_order();
         const uint32_t b = I.byte(s + k + (lane < step ? lane : 0u));
         put(b, step);
       }
     } else {  // long run (or not in the input ring): drain the ring, then HBM -> HBM
-      if ((uint64_t)op + len > cap) {
-        overflow = true;
-        return;
-      }
       flush(op, true);
       wave_copy_global(dst + op, in + s, len);
       op += len;
       flushed = op;
     }
-    nlit += len;
   }
-
-  // the literal tail of the segment (and the whole segment when it is too short to parse)
   __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I, uint32_t s,
                                            uint32_t len, uint32_t, uint32_t) {
     literals(in, I, s, len);
   }
-  // literals are written window by window: the tail starts where output stopped
   __device__ __forceinline__ uint32_t pending_from(uint32_t, uint32_t emitted) const {
     return emitted;
   }
-
-  // the literal lanes `litm` and match lanes `chm` of one window
-  __device__ __forceinline__ void part(const Window& W, uint32_t ll, uint64_t litm, uint64_t chm) {
-    const uint32_t lane = lane_id();
-    const uint32_t nl = (uint32_t)__builtin_popcountll(litm);
-    if (nl) {
-      if (!room(nl)) return;
-      const uint32_t li = __builtin_amdgcn_mbcnt_hi((uint32_t)(litm >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)litm, 0u));
-      lds_order();
-      ring[(litm >> lane) & 1 ? at(op + li) : kObuf + lane] = (uint8_t)W.byte;
-      lds_order();
-      op += nl;
-      nlit += nl;
-    }
-    const uint32_t ns = (uint32_t)__builtin_popcountll(chm);
-    if (ns) {
-      const uint32_t si = __builtin_amdgcn_mbcnt_hi((uint32_t)(chm >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)chm, 0u));
-      lds_order();
-      if ((chm >> lane) & 1) seqs[nseq + si] = uint2{ll | ((W.off + 3u) << 16), W.mlen};
-      lds_order();
-      nseq += ns;
-    }
-  }
-
   __device__ __forceinline__ void window(const GMEM uint8_t*, const InRing&, const Window& W,
                                          uint32_t anchor, uint32_t n) {
-    if (overflow) return;
     const uint32_t lane = lane_id();
     const uint32_t q = W.x + lane;
     const bool cl = (W.chain >> lane) & 1;
@@ -226,29 +145,316 @@ struct ZstdOut : cmp::ByteOut {
     const uint32_t ll = q - lit_start;  // chain lanes: their literal length
     const bool lit = !cl && q >= W.pos_in && q >= end_incl && q < n;
     const uint64_t litm = ballot(lit);
-    const uint32_t cnt = (uint32_t)__builtin_popcountll(W.chain);
-    if (nseq + cnt < kMaxSeq) {
-      part(W, ll, litm, W.chain);
-      return;
+    const uint32_t nl = (uint32_t)__builtin_popcountll(litm);
+    if (nl) {
+      room(nl);
+      const uint32_t li = __builtin_amdgcn_mbcnt_hi((uint32_t)(litm >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)litm, 0u));
+      lds_order();
+      ring[lit ? at(op + li) : kObuf + lane] = (uint8_t)W.byte;
+      lds_order();
+      op += nl;
     }
-    // the block's last match is the (kMaxSeq - nseq)-th chain lane: split the window there
-    uint64_t m = W.chain;
-    for (uint32_t r = kMaxSeq - nseq - 1; r; --r) m &= m - 1;
-    const uint32_t ls = (uint32_t)__builtin_ctzll(m);
-    const uint64_t lo = ls == 63 ? ~0ull : (2ull << ls) - 1;
-    part(W, ll, litm & lo, W.chain & lo);
-    const uint32_t end = W.x + ls + readlane(W.mlen, ls);
-    close_block(false, end);
-    begin_block(end);
-    part(W, ll, litm & ~lo, W.chain & ~lo);
+    if (W.chain) {
+      const uint32_t si = __builtin_amdgcn_mbcnt_hi((uint32_t)(W.chain >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)W.chain, 0u));
+      if (cl) seqs[nseq + si] = make_uint2(ll | (W.off << 17), W.mlen);
+      nseq += (uint32_t)__builtin_popcountll(W.chain);
+    }
   }
+};
 
-  // OR the lanes' bit fields (v, nb), in DESCENDING lane order, into the bitstream that
-  // starts at output byte p0; bits = bits written so far; zeroed = first ring byte not yet
-  // cleared for the bitstream
-  __device__ __forceinline__ void put_bits(uint64_t v, uint32_t nb, uint32_t p0, uint32_t& bits,
-                                           uint32_t& zeroed) {
+// ---- pass 2: entropy coding ------------------------------------------------------------------
+// FSE state tables in LDS: literal lengths at 0 (<= 512 states), offsets at 512 (<= 256),
+// match lengths at 768 (<= 512); entry kTabDummy = 0 serves the idle lanes of the chain walk.
+constexpr uint32_t kTabLL = 0, kTabOF = 512, kTabML = 768, kTabDummy = 1280;
+
+struct EntLds {
+  uint32_t hq[4][256];     // literal histograms per stream quarter
+  uint32_t hist[256];      // all literals
+  huf::TreeLds T;
+  uint8_t len[256];        // code lengths
+  uint8_t w[256];          // weights
+  uint32_t code[256];      // code | length << 16
+  uint8_t desc[192];       // Huffman tree description; then modes + table descriptions
+  uint8_t tmp[256];        // serial bit writer output (weights FSE form, table descriptions)
+  uint32_t sh[3][64];      // sequence code histograms: LL, OF, ML
+  int16_t norm[64];
+  uint16_t tabs[kTabDummy + 1];
+  uint32_t tr[3][64];      // per symbol: deltaNbBits | deltaFindState << 20 (12-bit signed)
+  uint8_t sym_at[512];
+  uint16_t nxt[64];
+  uint32_t ew[4 * kWave];  // per 64 sequences: chain transforms / state bits
+  uint32_t u[16];          // lane-0 results: sizes, modes, accuracy logs
+  uint32_t wk[32];         // lane-0 work: weight counts, code ranges
+};
+
+// 256 * log2(x), x >= 1
+__device__ __forceinline__ uint32_t log2fix(uint32_t x) {
+  const uint32_t hb = hb32(x);
+  const uint32_t f = (hb >= 6 ? x >> (hb - 6) : x << (6 - hb)) & 63u;
+  return (hb << 8) + kT.log2frac[f];
+}
+
+// oracle zs_table_log (total >= 2, max_sym >= 1)
+__device__ uint32_t table_log(uint32_t max_log, uint32_t total, uint32_t max_sym) {
+  int tl = (int)max_log;
+  const int src_bits = (int)hb32(total - 1) - 2;
+  if (src_bits < tl) tl = src_bits;
+  const int a = (int)hb32(total) + 1, b = (int)hb32(max_sym) + 2;
+  const int mb = a < b ? a : b;
+  if (mb > tl) tl = mb;
+  if (tl < 5) tl = 5;
+  if (tl > (int)max_log) tl = (int)max_log;
+  return (uint32_t)tl;
+}
+
+// oracle zs_normalize (lane-serial)
+__device__ void normalize(const uint32_t* cnt, uint32_t max_sym, uint32_t total, uint32_t tl,
+                          int16_t* norm) {
+  const uint32_t size = 1u << tl;
+  int32_t sum = 0;
+  for (uint32_t s = 0; s <= max_sym; ++s) {
+    uint32_t v = 0;
+    if (cnt[s]) {
+      v = (cnt[s] * size + total / 2) / total;
+      if (v == 0) v = 1;
+    }
+    norm[s] = (int16_t)v;
+    sum += (int32_t)v;
+  }
+  int32_t delta = (int32_t)size - sum;
+  if (delta > 0) {
+    uint32_t best = 0;
+    for (uint32_t s = 1; s <= max_sym; ++s) if (cnt[s] > cnt[best]) best = s;
+    norm[best] = (int16_t)(norm[best] + delta);
+  }
+  while (delta < 0) {
+    uint32_t best = 0;
+    for (uint32_t s = 1; s <= max_sym; ++s) if (norm[s] > norm[best]) best = s;
+    int32_t take = norm[best] - 1;
+    if (take > -delta) take = -delta;
+    norm[best] = (int16_t)(norm[best] - take);
+    delta += take;
+  }
+}
+
+// lane-serial forward bit writer into LDS bytes (BIT_CStream)
+struct SBits {
+  uint8_t* out;
+  uint32_t pos;
+  uint64_t acc;
+  uint32_t nb;
+  __device__ __forceinline__ void add(uint64_t v, uint32_t n) {
+    if (!n) return;
+    acc |= (v & ((1ull << n) - 1)) << nb;
+    nb += n;
+    while (nb >= 8) {
+      out[pos++] = (uint8_t)acc;
+      acc >>= 8;
+      nb -= 8;
+    }
+  }
+  __device__ __forceinline__ void pad() {
+    if (nb) {
+      out[pos++] = (uint8_t)acc;
+      acc = 0;
+      nb = 0;
+    }
+  }
+};
+
+// oracle zs_write_ncount
+__device__ uint32_t write_ncount(SBits& w, const int16_t* norm, uint32_t max_sym, uint32_t tl) {
+  const uint32_t p0 = w.pos;
+  w.add(tl - 5, 4);
+  int remaining = (1 << tl) + 1, threshold = 1 << tl;
+  uint32_t nbits = tl + 1, s = 0;
+  bool prev0 = false;
+  while (s <= max_sym && remaining > 1) {
+    if (prev0) {
+      uint32_t start = s;
+      while (norm[s] == 0) ++s;
+      while (s >= start + 3) {
+        w.add(3, 2);
+        start += 3;
+      }
+      w.add(s - start, 2);
+    }
+    int count = norm[s++];
+    const int mx = (2 * threshold - 1) - remaining;
+    remaining -= count < 0 ? -count : count;
+    ++count;
+    if (count >= threshold) count += mx;
+    w.add((uint32_t)count, nbits - (count < mx ? 1u : 0u));
+    prev0 = count == 1;
+    while (remaining < threshold) {
+      --nbits;
+      threshold >>= 1;
+    }
+  }
+  w.pad();
+  return w.pos - p0;
+}
+
+// oracle zs_build_ctable (lane-serial): state table at st, per-symbol transforms at tr
+__device__ void build_ctable(const int16_t* norm, uint32_t max_sym, uint32_t al, uint16_t* st,
+                             uint32_t* tr, uint8_t* sym_at, uint16_t* cumul) {
+  const uint32_t size = 1u << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+  uint32_t high = size - 1;
+  cumul[0] = 0;
+  for (uint32_t s = 1; s <= max_sym + 1; ++s) {
+    if (norm[s - 1] == -1) {
+      cumul[s] = (uint16_t)(cumul[s - 1] + 1);
+      sym_at[high--] = (uint8_t)(s - 1);
+    } else {
+      cumul[s] = (uint16_t)(cumul[s - 1] + norm[s - 1]);
+    }
+  }
+  uint32_t pos = 0;
+  for (uint32_t s = 0; s <= max_sym; ++s)
+    for (int i = 0; i < norm[s]; ++i) {
+      sym_at[pos] = (uint8_t)s;
+      do {
+        pos = (pos + step) & mask;
+      } while (pos > high);
+    }
+  for (uint32_t u = 0; u < size; ++u) st[cumul[sym_at[u]]++] = (uint16_t)(size + u);
+  int32_t total = 0;
+  for (uint32_t s = 0; s <= max_sym; ++s) {
+    int32_t dnb, dfs = 0;
+    if (norm[s] == 0) {
+      dnb = (int32_t)(((al + 1) << 16) - size);
+    } else if (norm[s] == -1 || norm[s] == 1) {
+      dnb = (int32_t)((al << 16) - size);
+      dfs = total - 1;
+      total += 1;
+    } else {
+      const uint32_t mbo = al - hb32((uint32_t)norm[s] - 1);
+      const uint32_t msp = (uint32_t)norm[s] << mbo;
+      dnb = (int32_t)((mbo << 16) - msp);
+      dfs = total - norm[s];
+      total += norm[s];
+    }
+    tr[s] = (uint32_t)dnb | ((uint32_t)dfs << 20);
+  }
+}
+
+__device__ __forceinline__ uint32_t tr_d(uint32_t e) { return e & 0xFFFFFu; }
+__device__ __forceinline__ int32_t tr_f(uint32_t e) { return (int32_t)e >> 20; }
+
+// FSE_initCState2 / FSE_encodeSymbol over an LDS table (lane-serial)
+__device__ __forceinline__ uint32_t enc_init(const uint16_t* st, const uint32_t* tr, uint32_t s) {
+  const uint32_t d = tr_d(tr[s]);
+  const uint32_t nbo = (d + (1u << 15)) >> 16;
+  const uint32_t val = (nbo << 16) - d;
+  return st[(int32_t)(val >> nbo) + tr_f(tr[s])];
+}
+__device__ __forceinline__ uint32_t enc_sym(SBits& w, const uint16_t* st, const uint32_t* tr,
+                                            uint32_t state, uint32_t s) {
+  const uint32_t nbo = (state + tr_d(tr[s])) >> 16;
+  w.add(state, nbo);
+  return st[(int32_t)(state >> nbo) + tr_f(tr[s])];
+}
+
+// Huffman weights in FSE form into L.tmp (oracle zs_weights_fse); 0 if not codable
+__device__ uint32_t weights_fse(EntLds& L, uint32_t nw) {
+  if (nw < 2) return 0;
+  uint32_t* cnt = L.wk;
+  for (uint32_t k = 0; k < 13; ++k) cnt[k] = 0;
+  uint32_t max_w = 0, distinct = 0;
+  for (uint32_t i = 0; i < nw; ++i) {
+    const uint32_t x = L.w[i];
+    if (!cnt[x]++) ++distinct;
+    if (x > max_w) max_w = x;
+  }
+  if (distinct < 2) return 0;
+  const uint32_t tl = table_log(6, nw, max_w);
+  int16_t* norm = L.norm;
+  normalize(cnt, max_w, nw, tl, norm);
+  SBits bw{L.tmp + 1, 0, 0, 0};
+  write_ncount(bw, norm, max_w, tl);
+  uint16_t* st = L.tabs;
+  uint32_t* tr = L.tr[0];
+  build_ctable(norm, max_w, tl, st, tr, L.sym_at, L.nxt);
+  uint32_t s1, s2;
+  int32_t i = (int32_t)nw;
+  if (nw & 1) {
+    s1 = enc_init(st, tr, L.w[--i]);
+    s2 = enc_init(st, tr, L.w[--i]);
+    s1 = enc_sym(bw, st, tr, s1, L.w[--i]);
+  } else {
+    s2 = enc_init(st, tr, L.w[--i]);
+    s1 = enc_init(st, tr, L.w[--i]);
+  }
+  while (i > 0) {
+    s2 = enc_sym(bw, st, tr, s2, L.w[--i]);
+    s1 = enc_sym(bw, st, tr, s1, L.w[--i]);
+    if (bw.pos > 200) return 0;  // far past the 128-byte limit: give up early
+  }
+  bw.add(s2, tl);
+  bw.add(s1, tl);
+  bw.add(1, 1);
+  bw.pad();
+  if (bw.pos >= 128) return 0;
+  L.tmp[0] = (uint8_t)bw.pos;
+  return bw.pos + 1;
+}
+
+// one sequence table (oracle zs_choose), lane-serial; t: 0 LL, 1 OF, 2 ML.  Appends its
+// description to w, builds its state table / transforms, returns mode | al << 8 (RLE: al 0)
+__device__ uint32_t choose_table(EntLds& L, uint32_t t, uint32_t nseq, SBits& w) {
+  const uint32_t* cnt = L.sh[t];
+  const uint32_t nsym = t == 0 ? 36u : t == 1 ? 32u : 53u;
+  uint32_t max_sym = 0, distinct = 0;
+  for (uint32_t s = 0; s < nsym; ++s)
+    if (cnt[s]) {
+      ++distinct;
+      max_sym = s;
+    }
+  uint16_t* st = L.tabs + (t == 0 ? kTabLL : t == 1 ? kTabOF : kTabML);
+  uint32_t* tr = L.tr[t];
+  if (distinct == 1) {  // RLE: no state, no bits
+    w.add(max_sym, 8);
+    tr[max_sym] = 0;
+    st[0] = 0;
+    return 1u;
+  }
+  const int16_t* def = t == 0 ? kT.ll_norm : t == 1 ? kT.of_norm : kT.ml_norm;
+  const uint32_t def_al = t == 1 ? 5u : 6u, def_max = t == 0 ? 35u : t == 1 ? 28u : 52u;
+  uint32_t cost_pre = 0;
+  for (uint32_t s = 0; s <= max_sym; ++s) {
+    if (!cnt[s]) continue;
+    const uint32_t nd = def[s] == -1 ? 1u : (uint32_t)def[s];
+    cost_pre += cnt[s] * ((def_al << 8) - log2fix(nd));
+  }
+  const uint32_t tl = table_log(t == 1 ? 8u : 9u, nseq, max_sym);
+  int16_t* norm = L.norm;
+  normalize(cnt, max_sym, nseq, tl, norm);
+  uint32_t cost_fse = 0;
+  for (uint32_t s = 0; s <= max_sym; ++s)
+    if (cnt[s]) cost_fse += cnt[s] * ((tl << 8) - log2fix((uint32_t)norm[s]));
+  SBits tw{L.tmp, 0, 0, 0};
+  const uint32_t nb = write_ncount(tw, norm, max_sym, tl);
+  cost_fse += nb * 8u * 256u;
+  if (cost_fse < cost_pre) {
+    for (uint32_t k = 0; k < nb; ++k) w.add(L.tmp[k], 8);
+    build_ctable(norm, max_sym, tl, st, tr, L.sym_at, L.nxt);
+    return 2u | (tl << 8);
+  }
+  // predefined: its distribution (with "less than 1" symbols)
+  build_ctable(def, def_max, def_al, st, tr, L.sym_at, L.nxt);
+  return 0u | (def_al << 8);
+}
+
+struct EntOut : ByteOut {
+  // OR the lanes' bit fields (v0 of n0 bits, then v1 of n1 bits; n0 + n1 <= 96), in
+  // DESCENDING lane order, into the bitstream that starts at output byte p0; bits = bits
+  // written so far; zeroed = first ring byte not yet cleared for the bitstream
+  __device__ __forceinline__ void put_bits(uint64_t v0, uint32_t n0, uint64_t v1, uint32_t n1,
+                                           uint32_t p0, uint32_t& bits, uint32_t& zeroed) {
     const uint32_t lane = lane_id();
+    const uint32_t nb = n0 + n1;
     const uint32_t incl = wave_incl_sum(nb);
     const uint32_t total = readlane(incl, 63);
     op = p0 + (bits >> 3);
@@ -258,196 +464,427 @@ struct ZstdOut : cmp::ByteOut {
     for (uint32_t b = zeroed + lane; b < end; b += kWave) ring[at(b)] = 0;
     if (end > zeroed) zeroed = end;
     const uint32_t pos = bits + total - incl;  // lanes above come first
-    const uint32_t a = ((((uint32_t)(uintptr_t)dst + p0) & kObufMask) << 3) + pos;
+    const uint32_t base = (((uint32_t)(uintptr_t)dst + p0) & kObufMask) << 3;
     const uint32_t wmask = kObufMask >> 2;
-    const uint32_t w = (a >> 5) & wmask, sh = a & 31u;
-    const uint32_t x0 = (uint32_t)(v << sh);
-    const uint32_t x1 = (uint32_t)((v << sh) >> 32);
-    const uint32_t x2 = sh ? (uint32_t)(v >> (64 - sh)) : 0u;
     uint32_t* r32 = reinterpret_cast<uint32_t*>(ring);
+    auto place = [&](uint64_t v, uint32_t a) {
+      const uint32_t wi = (a >> 5) & wmask, sh = a & 31u;
+      const uint32_t x0 = (uint32_t)(v << sh);
+      const uint32_t x1 = (uint32_t)((v << sh) >> 32);
+      const uint32_t x2 = sh ? (uint32_t)(v >> (64 - sh)) : 0u;
+      if (x0) atomicOr(&r32[wi], x0);
+      if (x1) atomicOr(&r32[(wi + 1) & wmask], x1);
+      if (x2) atomicOr(&r32[(wi + 2) & wmask], x2);
+    };
     lds_order();
-    atomicOr(&r32[w], x0);
-    atomicOr(&r32[(w + 1) & wmask], x1);
-    atomicOr(&r32[(w + 2) & wmask], x2);
+    if (n0) place(v0 & (n0 >= 64 ? ~0ull : (1ull << n0) - 1), base + pos);
+    if (n1) place(v1 & (n1 >= 64 ? ~0ull : (1ull << n1) - 1), base + pos + n0);
     lds_order();
     bits += total;
     op = p0 + (bits >> 3);
   }
 
-  // The sequences bitstream of the open block (nseq >= 1), oracle zs_close_block.  Per 64
-  // sequences (highest first): every lane computes its sequence's codes and symbol
-  // transforms and stores them chain-major in LDS (ew[4 k + c]: c = 0 OF, 1 ML, 2 LL,
-  // deltaNbBits | deltaFindState << 24); then lanes 0..2 walk the three FSE state chains on
-  // the vector ALU, one chain per lane, sequence 63 down to 0, each step one LDS read of the
-  // transform and one of the chain's state table (tabs), writing the state bits back over
-  // the transform; finally every lane assembles its sequence's field (state bits + extra
-  // bits, <= 61 bits), placed by a prefix sum.  The walk costs a few scalar instructions per
-  // sequence: the scalar unit stays with the parse, which every wave of the CU shares.
-  __device__ __forceinline__ void encode_sequences() {
-    const uint32_t lane = lane_id();
-    const uint32_t p0 = op;
-    uint32_t bits = 0, zeroed = p0;
-    uint32_t st = 0;  // lane c < 3: the state of chain c
-    const uint32_t top = nseq - 1;
-    // chain of this lane: its table base in tabs (lanes >= 3 walk a dummy chain whose
-    // reads stay inside the tables and whose writes go to ew[4 k + 3])
-    const uint32_t cl = lane < 3 ? lane : 3u;
-    const uint32_t tb = cl == 0 ? 0u : cl == 1 ? 64u : cl == 2 ? 128u : 192u;
-    for (int32_t c = (int32_t)(top >> 6); c >= 0; --c) {
-      const uint32_t j = (uint32_t)c * kWave + lane;
-      const bool act = j < nseq;
+  // bytes from LDS (lane-parallel), n <= 256
+  __device__ __forceinline__ void put_lds(const uint8_t* src, uint32_t n) {
+    for (uint32_t k = 0; k < n; k += kWave) {
+      const uint32_t step = n - k < kWave ? n - k : kWave;
+      if (!room(step)) return;
       lds_order();
-      const uint2 rec = seqs[act ? j : top];
-      const uint32_t ll = rec.x & 0xFFFFu, of = rec.x >> 16, mlb = rec.y - 3u;
-      const uint32_t llc = ll < 64 ? kCodes.ll[ll] : hb32(ll) + 19u;
-      const uint32_t mlc = mlb < 128 ? kCodes.ml[mlb] : hb32(mlb) + 36u;
-      const uint32_t ofc = hb32(of);
-      const uint2 eLL = kCtLL.sym[llc], eML = kCtML.sym[mlc], eOF = kCtOF.sym[ofc];
-      auto pack = [](uint2 e) { return e.x | (e.y << 24); };  // d < 2^19, f in [-64, 64)
-      ew[4 * lane + 0] = pack(eOF);
-      ew[4 * lane + 1] = pack(eML);
-      ew[4 * lane + 2] = pack(eLL);
-      ew[4 * lane + 3] = 0u;
-      lds_order();
-      int32_t k = 63;
-      if (c == (int32_t)(top >> 6)) {  // the last sequence initialises the three states
-        k = (int32_t)(top & 63u);
-        const uint32_t e = ew[4 * (uint32_t)k + cl];
-        const uint32_t d = e & 0xFFFFFFu;
-        const int32_t f = (int32_t)e >> 24;
-        const uint32_t nbo = (d + (1u << 15)) >> 16;
-        const uint32_t val = (nbo << 16) - d;
-        st = tabs[(tb + (uint32_t)((int32_t)(val >> nbo) + f)) & 255u];
-        lds_order();
-        ew[4 * (uint32_t)k + cl] = 0u;  // no state bits
-        --k;
-      }
-      for (; k >= 0; --k) {
-        lds_order();
-        const uint32_t e = ew[4 * (uint32_t)k + cl];
-        const uint32_t nb = (st + (e & 0xFFFFFFu)) >> 16;
-        const uint32_t out = st & ((1u << nb) - 1u);
-        st = tabs[(tb + (uint32_t)((int32_t)(st >> nb) + ((int32_t)e >> 24))) & 255u];
-        ew[4 * (uint32_t)k + cl] = out | (nb << 24);
-      }
-      lds_order();
-      const uint32_t w0 = ew[4 * lane + 0], w1 = ew[4 * lane + 1], w2 = ew[4 * lane + 2];
-      const uint32_t nof = w0 >> 24, nml = w1 >> 24, nll = w2 >> 24;
-      const uint32_t stb = ((w0 & 0xFFFFFFu) | ((w1 & 0xFFFFFFu) << nof) |
-                            ((w2 & 0xFFFFFFu) << (nof + nml))) & 0xFFFFFFu;
-      // each lane's field: state bits, then literal-length, match-length and offset extras
-      const uint32_t stn = nof + nml + nll;
-      const uint32_t llb = eLL.y >> 16, mlbits = eML.y >> 16;
-      const uint64_t llx = ll & ((1u << llb) - 1u);
-      const uint64_t mlx = mlb & ((1u << mlbits) - 1u);
-      const uint64_t ofx = of & ((1u << ofc) - 1u);
-      uint64_t v = (uint64_t)stb | (llx << stn) | (mlx << (stn + llb)) |
-                   (ofx << (stn + llb + mlbits));
-      uint32_t nb = stn + llb + mlbits + ofc;
-      if (!act) {
-        v = 0;
-        nb = 0;
-      }
-      put_bits(v, nb, p0, bits, zeroed);
-      if (overflow) return;
+      const uint32_t b = src[k + (lane_id() < step ? lane_id() : 0u)];
+      put(b, step);
     }
-    // final states (ML, OF, LL: the decoder reads LL first) and the end mark
-    const uint32_t sOF = readlane(st, 0), sML = readlane(st, 1), sLL = readlane(st, 2);
-    const uint32_t fin = (sML & 63u) | ((sOF & 31u) << 6) | ((sLL & 63u) << 11) | (1u << 17);
-    put_bits(lane == 0 ? fin : 0u, lane == 0 ? 18u : 0u, p0, bits, zeroed);
-    op = p0 + ((bits + 7) >> 3);
-  }
-
-  // close the open block; in_end = input position it ends at (oracle zs_close_block)
-  __device__ __forceinline__ void close_block(bool last, uint32_t in_end) {
-    if (overflow) return;
-    const uint32_t lane = lane_id();
-    // Number_of_Sequences (1 or 2 bytes) + Symbol_Compression_Modes (0: all predefined)
-    const uint32_t nh = nseq == 0 ? 1u : nseq < 128 ? 2u : 3u;
-    if (!room(nh)) return;
-    const uint32_t b0 = nseq < 128 ? nseq : (nseq >> 8) + 128u;
-    const uint32_t b1 = nseq < 128 ? 0u : nseq & 0xFFu;
-    lds_order();
-    if (lane < nh) ring[at(op + lane)] = (uint8_t)(lane == 0 ? b0 : lane == 1 ? b1 : 0u);
-    lds_order();
-    op += nh;
-    if (nseq) encode_sequences();
-    if (overflow) return;
-    const uint32_t csz = op - (blk + 3), raw = in_end - in0;
-    uint32_t hdr;
-    const bool stored = csz >= raw;
-    if (stored) {  // did not shrink: the block's input, raw
-      if (flushed < blk) flush(blk, true);  // bytes before the block are still staged
-      global_fence_wave();                  // earlier stores to this range land first
-      wave_copy_global(dst + blk + 3, src + in0, raw);
-      op = blk + 3 + raw;
-      flushed = op;
-      hdr = (last ? 1u : 0u) | (raw << 3);
-    } else {
-      flush(op, true);
-      hdr = (last ? 1u : 0u) | (2u << 1) | (csz << 3);
-    }
-    global_fence_wave();
-    // block header; compressed blocks also get their raw-literals header (20-bit size)
-    uint32_t hb = 0;
-    if (lane < 3) hb = hdr >> (8 * lane);
-    else if (lane == 3) hb = (3u << 2) | ((nlit & 15u) << 4);
-    else if (lane == 4) hb = nlit >> 4;
-    else if (lane == 5) hb = nlit >> 12;
-    if (lane < (stored ? 3u : 6u)) dst[blk + lane] = (uint8_t)hb;
   }
 };
 
 }  // namespace zse
 
-__global__ __launch_bounds__(64) void zstd_compress_kernel(
-    const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
-    uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
-    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
+__global__ __launch_bounds__(64) void zstd_parse_kernel(const uint8_t* __restrict__ input,
+                                                        uint64_t n_total, uint32_t seg,
+                                                        uint8_t* __restrict__ scratch,
+                                                        uint64_t sstride,
+                                                        uint2* __restrict__ meta) {
   using namespace cmp;
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];  // + trash bytes
-  __shared__ __attribute__((aligned(16))) uint2 seqs[zse::kMaxSeq];
-  __shared__ __attribute__((aligned(16))) uint32_t ew[4 * kWave];
-  __shared__ __attribute__((aligned(16))) uint8_t tabs[256];
+  const uint32_t i_seg = blockIdx.x;
+  const uint64_t seg_off = (uint64_t)i_seg * seg;
+  if (seg_off >= n_total) return;
+  const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
+  zse::SeqCollect o;
+  o.ring = obuf;
+  o.dst = global_ptr(scratch + (uint64_t)i_seg * sstride);
+  o.cap = zse::lit_cap(seg);
+  o.op = 0;
+  o.flushed = 0;
+  o.overflow = false;
+  o.seqs = reinterpret_cast<GMEM uint2*>(o.dst + zse::lit_cap(seg));
+  o.nseq = 0;
+  const GMEM uint8_t* in = global_ptr(input + seg_off);
+  parse<zse::SeqCollect, true>(in, n, global_ptr(input + n_total), table, inring, kMaxDist,
+                               0xFFFFFFFFu, o);
+  o.flush(o.op, true);
+  if (lane_id() == 0) meta[i_seg] = make_uint2(o.op, o.nseq);
+}
+
+__global__ __launch_bounds__(64) void zstd_entropy_kernel(
+    const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
+    uint8_t* __restrict__ scratch, uint64_t sstride, const uint2* __restrict__ meta,
+    uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
+    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
+  using namespace cmp;
+  using namespace zse;
+  __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
+  __shared__ __attribute__((aligned(16))) EntLds L;
   const uint32_t i_seg = blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
   const uint32_t lane = lane_id();
-  zse::ZstdOut o;
+  const GMEM uint8_t* src = global_ptr(input + seg_off);
+  GMEM uint8_t* lits = global_ptr(scratch + (uint64_t)i_seg * sstride);
+  GMEM uint2* seqs = reinterpret_cast<GMEM uint2*>(lits + lit_cap(seg));
+  const uint2 mt = meta[i_seg];
+  const uint32_t nlit = mt.x, nseq = mt.y;
+  EntOut o;
   o.ring = obuf;
   o.dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
   o.cap = slot_stride;
   o.op = 0;
   o.flushed = 0;
   o.overflow = false;
-  o.seqs = seqs;
-  o.ew = ew;
-  o.tabs = tabs;
-  tabs[lane] = (uint8_t)zse::kCtOF.state[lane & 31u];
-  tabs[64 + lane] = (uint8_t)zse::kCtML.state[lane];
-  tabs[128 + lane] = (uint8_t)zse::kCtLL.state[lane];
-  tabs[192 + lane] = 0;
-  o.src = global_ptr(input + seg_off);
   // frame header: magic, Single_Segment with the content size (1 byte below 256, else 2)
   const uint32_t fh = n < 256 ? 6u : 7u;
   const uint32_t fcs = n < 256 ? n : n - 256u;
   const uint32_t hb = lane < 4 ? (0xFD2FB528u >> (8 * lane)) & 0xFFu
                       : lane == 4 ? (n < 256 ? 0x20u : 0x60u)
                       : lane == 5 ? fcs & 0xFFu : fcs >> 8;
-  if (lane < fh) obuf[o.at(lane)] = (uint8_t)hb;
+  o.put(hb, fh);
+  const uint32_t blk = o.op;
+  o.op += 3;  // block header, written last
+
+  // ---- literal histograms per stream quarter ----
+  for (uint32_t k = lane; k < 5 * 256; k += kWave) (&L.hq[0][0])[k] = 0;
   lds_order();
-  o.op = fh;
-  o.begin_block(0);
-  parse(o.src, n, global_ptr(input + n_total), table, inring, kMaxDist, 0xFFFFFFFFu, o);
-  o.close_block(true, n);
-  o.flush(o.op, true);
-  if (lane == 0) {
-    sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : o.op;
-    if (o.overflow) atomicOr(err, 2u);
+  const uint32_t qs = (nlit + 3) / 4;
+  for (uint32_t b0 = 0; b0 < nlit; b0 += 16u * kWave) {
+    const uint32_t at = b0 + 16u * lane;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (at < nlit) v = *reinterpret_cast<const GMEM uint4*>(lits + at);
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t idx = at + j;
+      if (idx < nlit) {
+        const uint32_t q = (idx >= qs ? 1u : 0u) + (idx >= 2 * qs ? 1u : 0u) + (idx >= 3 * qs ? 1u : 0u);
+        atomicAdd(&L.hq[q][(wv[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
+      }
+    }
   }
+  lds_order();
+  uint32_t distinct = 0;
+  for (uint32_t s0 = 0; s0 < 256; s0 += kWave) {
+    const uint32_t s = s0 + lane;
+    const uint32_t t = L.hq[0][s] + L.hq[1][s] + L.hq[2][s] + L.hq[3][s];
+    L.hist[s] = t;
+    distinct += (uint32_t)__builtin_popcountll(ballot(t != 0));
+  }
+  lds_order();
+
+  // ---- literals section ----
+  bool huff = false;
+  uint32_t ns = 1, dsz = 0, hs = 0, total = 0;
+  uint32_t sbytes[4] = {0, 0, 0, 0};
+  if (nlit > 0 && distinct > 1) {
+    huf::huff_lengths(L.hist, 256, 11, L.len, L.T);
+    // max length, highest used symbol, weights
+    uint32_t lmax = 0, msym = 0;
+    for (uint32_t s0 = 0; s0 < 256; s0 += kWave) {
+      const uint32_t l = L.len[s0 + lane];
+      lmax = max(lmax, l);
+      const uint64_t used = ballot(l != 0);
+      if (used) msym = s0 + 63u - (uint32_t)__builtin_clzll(used);
+    }
+    for (uint32_t d = 1; d < 64; d <<= 1) lmax = max(lmax, (uint32_t)__shfl_xor((int)lmax, (int)d, 64));
+    lmax = readlane(lmax, 0);
+    for (uint32_t s0 = 0; s0 < 256; s0 += kWave) {
+      const uint32_t l = L.len[s0 + lane];
+      L.w[s0 + lane] = (uint8_t)(l ? lmax + 1 - l : 0u);
+    }
+    // stream sizes from the quarter histograms
+    ns = nlit < 256 ? 1u : 4u;
+    uint32_t bq[4] = {0, 0, 0, 0};
+    for (uint32_t s0 = 0; s0 < 256; s0 += kWave) {
+      const uint32_t s = s0 + lane, l = L.len[s];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) bq[q] += L.hq[q][s] * l;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) bq[q] = readlane(wave_incl_sum(bq[q]), 63);
+    if (ns == 1) {
+      sbytes[0] = (bq[0] + bq[1] + bq[2] + bq[3] + 8) >> 3;
+    } else {
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) sbytes[q] = (bq[q] + 8) >> 3;
+    }
+    lds_order();
+    if (lane == 0) {
+      // codes: table ranges by increasing weight, then symbol (HUF_readDTableX1)
+      uint32_t* start = L.wk;
+      uint32_t* rc = L.wk + 16;
+      uint32_t next = 0;
+      for (uint32_t k = 0; k < 13; ++k) rc[k] = 0;
+      for (uint32_t s = 0; s < 256; ++s)
+        if (L.len[s]) rc[L.w[s]]++;
+      for (uint32_t k = 1; k <= lmax; ++k) {
+        start[k] = next;
+        next += rc[k] << (k - 1);
+      }
+      for (uint32_t s = 0; s < 256; ++s) {
+        const uint32_t l = L.len[s];
+        if (!l) {
+          L.code[s] = 0;
+          continue;
+        }
+        const uint32_t wt = L.w[s];
+        L.code[s] = (start[wt] >> (wt - 1)) | (l << 16);
+        start[wt] += 1u << (wt - 1);
+      }
+      // tree description: direct when possible and not larger than the FSE form
+      const uint32_t nw = msym;
+      const uint32_t fsz = weights_fse(L, nw);
+      const uint32_t direct = nw <= 128 ? 1 + (nw + 1) / 2 : 0u;
+      uint32_t d = 0;
+      if (direct && (!fsz || direct <= fsz)) {
+        L.desc[0] = (uint8_t)(127 + nw);
+        for (uint32_t i = 0; i < nw; i += 2)
+          L.desc[1 + i / 2] = (uint8_t)((L.w[i] << 4) | (i + 1 < nw ? L.w[i + 1] : 0u));
+        d = direct;
+      } else if (fsz) {
+        for (uint32_t k = 0; k < fsz; ++k) L.desc[k] = L.tmp[k];
+        d = fsz;
+      }
+      L.u[0] = d;
+    }
+    lds_order();
+    dsz = L.u[0];
+    if (dsz) {
+      total = dsz + (ns == 4 ? 6u : 0u) + sbytes[0] + sbytes[1] + sbytes[2] + sbytes[3];
+      const int32_t limit = (int32_t)nlit - (int32_t)((nlit >> 6) + 2);
+      huff = (int32_t)total < limit;
+    }
+  }
+  if (huff) {
+    hs = ns == 1 || nlit < 1024 ? 3u : nlit < 16384 ? 4u : 5u;
+    const uint32_t sf = ns == 1 ? 0u : nlit < 1024 ? 1u : nlit < 16384 ? 2u : 3u;
+    const uint64_t h = 2u | (sf << 2) | ((uint64_t)nlit << 4) |
+                       ((uint64_t)total << (hs == 3 ? 14 : hs == 4 ? 18 : 22));
+    o.room(hs);
+    o.put((uint32_t)(h >> (8 * (lane < 8 ? lane : 0u))) & 0xFFu, hs);
+    o.put_lds(L.desc, dsz);
+    if (ns == 4) {
+      const uint32_t j = lane >> 1;
+      const uint32_t sv = j == 0 ? sbytes[0] : j == 1 ? sbytes[1] : sbytes[2];
+      o.room(6);
+      o.put((lane & 1) ? sv >> 8 : sv & 0xFFu, 6);
+    }
+    // the streams: symbols from the last, 64 per step (the highest index first)
+    for (uint32_t k = 0; k < ns && !o.overflow; ++k) {
+      const uint32_t a = ns == 1 ? 0u : k * qs;
+      const uint32_t b = ns == 1 ? nlit : (k == 3 ? nlit : (k + 1) * qs);
+      const uint32_t p0 = o.op;
+      uint32_t bits = 0, zeroed = p0;
+      for (int32_t e = (int32_t)b; e > (int32_t)a && !o.overflow; e -= (int32_t)kWave) {
+        const int32_t idx = e - (int32_t)kWave + (int32_t)lane;
+        const bool act = idx >= (int32_t)a;
+        const uint32_t sym = act ? (uint32_t)lits[idx] : 0u;
+        lds_order();
+        const uint32_t cw = L.code[sym];
+        o.put_bits(act ? (cw & 0xFFFFu) : 0u, act ? cw >> 16 : 0u, 0, 0, p0, bits, zeroed);
+      }
+      o.put_bits(lane == 0 ? 1u : 0u, lane == 0 ? 1u : 0u, 0, 0, p0, bits, zeroed);  // end mark
+      o.op = p0 + ((bits + 7) >> 3);
+    }
+  } else if (nlit > 0 && distinct == 1) {  // RLE
+    const uint32_t h = nlit < 32 ? 1u | (nlit << 3)
+                       : nlit < 4096 ? 1u | (1u << 2) | ((nlit & 15u) << 4) | ((nlit >> 4) << 8)
+                                     : 1u | (3u << 2) | ((nlit & 15u) << 4) | ((nlit >> 4) << 8);
+    const uint32_t hsz = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
+    const uint32_t byte0 = lits[0];
+    o.room(hsz + 1);
+    o.put(lane < hsz ? (h >> (8 * lane)) & 0xFFu : byte0, hsz + 1);
+  } else {  // raw
+    const uint32_t h = nlit < 32 ? (nlit << 3)
+                       : nlit < 4096 ? (1u << 2) | ((nlit & 15u) << 4) | ((nlit >> 4) << 8)
+                                     : (3u << 2) | ((nlit & 15u) << 4) | ((nlit >> 4) << 8);
+    const uint32_t hsz = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
+    o.room(hsz);
+    o.put((h >> (8 * (lane < 4 ? lane : 0u))) & 0xFFu, hsz);
+    if (nlit) {
+      if ((uint64_t)o.op + nlit > o.cap) {
+        o.overflow = true;
+      } else {
+        o.flush(o.op, true);
+        wave_copy_global(o.dst + o.op, lits, nlit);
+        o.op += nlit;
+        o.flushed = o.op;
+      }
+    }
+  }
+
+  // ---- sequences section ----
+  if (!o.overflow) {
+    const uint32_t nh = nseq < 128 ? 1u : 2u;
+    o.room(nh);
+    o.put(nh == 1 ? nseq : lane == 0 ? (nseq >> 8) + 128u : nseq & 0xFFu, nh);
+  }
+  if (nseq && !o.overflow) {
+    // repeat offsets (RFC 8878 3.1.2.5) by a scalar scan, codes, histograms; the records
+    // become {literal length | offset value << 17, match length}
+    for (uint32_t k = lane; k < 3 * 64; k += kWave) (&L.sh[0][0])[k] = 0;
+    lds_order();
+    uint32_t r0 = 1, r1 = 4, r2 = 8;
+    for (uint32_t c0 = 0; c0 < nseq; c0 += kWave) {
+      const uint32_t j = c0 + lane;
+      const bool act = j < nseq;
+      const uint2 rec = act ? seqs[j] : make_uint2(0, 3);
+      const uint32_t ll = rec.x & 0x1FFFFu, off = rec.x >> 17, ml = rec.y;
+      const uint32_t cnt = nseq - c0 < kWave ? nseq - c0 : kWave;
+      uint32_t ov = 0;
+      for (uint32_t k = 0; k < cnt; ++k) {
+        const uint32_t lk = readlane(ll, k), o_ = readlane(off, k);
+        uint32_t v;
+        if (lk) v = o_ == r0 ? 1u : o_ == r1 ? 2u : o_ == r2 ? 3u : o_ + 3u;
+        else v = o_ == r1 ? 1u : o_ == r2 ? 2u : o_ == r0 - 1u ? 3u : o_ + 3u;
+        const uint32_t idx = v > 3 ? 3u : v - 1u + (lk ? 0u : 1u);
+        if (idx == 3) {
+          r2 = r1;
+          r1 = r0;
+          r0 = o_;
+        } else if (idx == 1) {
+          r1 = r0;
+          r0 = o_;
+        } else if (idx == 2) {
+          r2 = r1;
+          r1 = r0;
+          r0 = o_;
+        }
+        ov = writelane(ov, v, k);
+      }
+      if (act) {
+        atomicAdd(&L.sh[0][ll_code(ll)], 1u);
+        atomicAdd(&L.sh[1][hb32(ov)], 1u);
+        atomicAdd(&L.sh[2][ml_code(ml)], 1u);
+        seqs[j] = make_uint2(ll | (ov << 17), ml);
+      }
+    }
+    lds_order();
+    // tables (one lane): modes byte + descriptions in L.desc, states / transforms
+    if (lane == 0) {
+      SBits w{L.desc + 1, 0, 0, 0};
+      const uint32_t mll = choose_table(L, 0, nseq, w);
+      const uint32_t mof = choose_table(L, 1, nseq, w);
+      const uint32_t mml = choose_table(L, 2, nseq, w);
+      L.desc[0] = (uint8_t)(((mll & 3u) << 6) | ((mof & 3u) << 4) | ((mml & 3u) << 2));
+      L.u[1] = w.pos + 1;
+      L.u[2] = mll >> 8;
+      L.u[3] = mof >> 8;
+      L.u[4] = mml >> 8;
+      L.tabs[kTabDummy] = 0;
+    }
+    lds_order();
+    o.put_lds(L.desc, L.u[1]);
+    const uint32_t al_ll = L.u[2], al_of = L.u[3], al_ml = L.u[4];
+    // the bitstream, last sequence first (oracle bo_zstd_compress_block).  Per 64 sequences
+    // (highest first): every lane stores its sequence's three symbol transforms; lanes 0..2
+    // walk the OF / ML / LL state chains, sequence 63 down to 0, writing the state bits back
+    // over the transforms; then every lane places its field (states, then LL, ML, OF extra
+    // bits) by a prefix sum.
+    const uint32_t p0 = o.op;
+    uint32_t bits = 0, zeroed = p0;
+    uint32_t st = 0;  // lane c < 3: the state of chain c (OF, ML, LL)
+    const uint32_t top = nseq - 1;
+    const uint32_t cl = lane < 3 ? lane : 3u;
+    const uint32_t tb = cl == 0 ? kTabOF : cl == 1 ? kTabML : cl == 2 ? kTabLL : kTabDummy;
+    for (int32_t c = (int32_t)(top >> 6); c >= 0 && !o.overflow; --c) {
+      const uint32_t j = (uint32_t)c * kWave + lane;
+      const bool act = j < nseq;
+      lds_order();
+      const uint2 rec = seqs[act ? j : top];
+      const uint32_t ll = rec.x & 0x1FFFFu, ov = rec.x >> 17, mlb = rec.y - 3u;
+      const uint32_t llc = ll_code(ll), mlc = ml_code(rec.y), ofc = hb32(ov);
+      L.ew[4 * lane + 0] = L.tr[1][ofc];
+      L.ew[4 * lane + 1] = L.tr[2][mlc];
+      L.ew[4 * lane + 2] = L.tr[0][llc];
+      L.ew[4 * lane + 3] = 0u;
+      lds_order();
+      int32_t k = 63;
+      if (c == (int32_t)(top >> 6)) {  // the last sequence initialises the three states
+        k = (int32_t)(top & 63u);
+        const uint32_t e = L.ew[4 * (uint32_t)k + cl];
+        const uint32_t d = tr_d(e);
+        const uint32_t nbo = (d + (1u << 15)) >> 16;
+        const uint32_t val = (nbo << 16) - d;
+        st = L.tabs[tb + (uint32_t)((int32_t)(val >> nbo) + tr_f(e))];
+        lds_order();
+        L.ew[4 * (uint32_t)k + cl] = 0u;  // no state bits
+        --k;
+      }
+      for (; k >= 0; --k) {
+        lds_order();
+        const uint32_t e = L.ew[4 * (uint32_t)k + cl];
+        const uint32_t nb = (st + tr_d(e)) >> 16;
+        const uint32_t out = st & ((1u << nb) - 1u);
+        st = L.tabs[tb + (uint32_t)((int32_t)(st >> nb) + tr_f(e))];
+        L.ew[4 * (uint32_t)k + cl] = out | (nb << 24);
+      }
+      lds_order();
+      const uint32_t w0 = L.ew[4 * lane + 0], w1 = L.ew[4 * lane + 1], w2 = L.ew[4 * lane + 2];
+      const uint32_t nof = w0 >> 24, nml = w1 >> 24, nll = w2 >> 24;
+      const uint64_t stb = (uint64_t)(w0 & 0xFFFFFFu) | ((uint64_t)(w1 & 0xFFFFFFu) << nof) |
+                           ((uint64_t)(w2 & 0xFFFFFFu) << (nof + nml));
+      const uint32_t stn = nof + nml + nll;
+      const uint32_t llb = kT.ll_bits[llc], mlbits = kT.ml_bits[mlc];
+      // part 0: state bits + literal-length extra (<= 26 + 16); part 1: match-length extra,
+      // then offset extra (<= 16 + 16)
+      const uint64_t f0 = stb | ((uint64_t)(ll & ((1u << llb) - 1u)) << stn);
+      const uint64_t f1 = (uint64_t)(mlb & ((1u << mlbits) - 1u)) |
+                          ((uint64_t)(ov & ((1u << ofc) - 1u)) << mlbits);
+      o.put_bits(act ? f0 : 0u, act ? stn + llb : 0u, act ? f1 : 0u, act ? mlbits + ofc : 0u,
+                 p0, bits, zeroed);
+    }
+    if (!o.overflow) {
+      // final states (ML, OF, LL: the decoder reads LL first) and the end mark
+      const uint32_t sOF = readlane(st, 0), sML = readlane(st, 1), sLL = readlane(st, 2);
+      const uint64_t fin = (uint64_t)(sML & ((1u << al_ml) - 1u)) |
+                           ((uint64_t)(sOF & ((1u << al_of) - 1u)) << al_ml) |
+                           ((uint64_t)(sLL & ((1u << al_ll) - 1u)) << (al_ml + al_of)) |
+                           (1ull << (al_ml + al_of + al_ll));
+      const uint32_t fn = al_ml + al_of + al_ll + 1;
+      o.put_bits(lane == 0 ? fin : 0u, lane == 0 ? fn : 0u, 0, 0, p0, bits, zeroed);
+      o.op = p0 + ((bits + 7) >> 3);
+    }
+  }
+
+  // ---- the block: compressed, or raw when that is not smaller ----
+  const bool stored = o.overflow || o.op - (blk + 3) >= n;
+  uint32_t hdr;
+  if (stored) {
+    o.overflow = false;
+    if (o.flushed < blk) o.flush(blk, true);  // the frame header is still staged
+    global_fence_wave();                       // earlier stores to this range land first
+    wave_copy_global(o.dst + blk + 3, src, n);
+    o.op = blk + 3 + n;
+    o.flushed = o.op;
+    hdr = 1u | (n << 3);
+  } else {
+    hdr = 1u | (2u << 1) | ((o.op - (blk + 3)) << 3);
+    o.flush(o.op, true);
+  }
+  global_fence_wave();
+  if (lane < 3) o.dst[blk + lane] = (uint8_t)(hdr >> (8 * lane));
+  if (lane == 0) sizes[i_seg] = o.op;
+  (void)err;
 }
 
 }  // namespace bitar_hip

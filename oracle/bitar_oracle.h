@@ -104,6 +104,9 @@ typedef void (*bo_emit_fn)(void* ctx, uint32_t lit_start, uint32_t lit_len, uint
 void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t max_mlen,
                      bo_emit_fn emit, void* ctx);
 #define BO_MAX_DIST_ALL 2560u
+#define BO_PARSE_REP 1u
+void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t max_mlen,
+                           uint32_t flags, bo_emit_fn emit, void* ctx);
 
 /* ---- segment-level restatement of CompressDevice ------------------------------- */
 /* Compress (device.cc:156-238): cut `in` into ceil(n/seg) segments in order, compress each

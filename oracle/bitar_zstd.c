@@ -602,22 +602,159 @@ done:
 }
 
 /* ================================================================================ */
-/* encoder: the frame the HIP kernel emits                                            */
+/* encoder: the frame the HIP kernels write (zstd_compress.hip)                       */
 /* ================================================================================ */
-#define ZS_MAX_SEQ 256u /* sequences per block (the kernel keeps a block's sequences in 2 KiB of LDS) */
+/* One frame per segment: single-segment header with the content size, then ONE block (a
+ * segment is <= 64 KiB, below the 128 KiB block limit), compressed or -- when that is not
+ * smaller than the input -- raw.  Inside the compressed block:
+ *
+ *   parse      the bitar window-scan parse (bo_window_parse, distance <= 2560);
+ *   offsets    repeat offsets (RFC 8878 3.1.2.5, history 1 4 8): a match whose distance is
+ *              in the history is coded as its repeat code, else as distance + 3;
+ *   literals   nlit == 0: raw; one distinct byte: RLE; else Huffman (code lengths by
+ *              bo_huff_lengths limited to 11 bits; weights direct when <= 128 are sent and
+ *              not larger than their FSE form, else FSE-compressed with two interleaved
+ *              states), 1 stream below 256 literals, else 4; raw when the Huffman section
+ *              is not at least nlit/64 + 2 bytes smaller;
+ *   sequences  per table (literal lengths, offsets, match lengths): one distinct code ->
+ *              RLE; else FSE_Compressed with counts normalized by zs_normalize when its
+ *              estimated size (fixed-point log2 costs + table description) is below the
+ *              predefined distribution's, else predefined.
+ * Every choice is integer arithmetic, so the kernels reproduce it bit for bit. */
+
+/* 256 * log2(1 + i / 64), rounded */
+static const uint8_t kLog2Frac[64] = {
+    0,   6,   11,  17,  22,  28,  33,  38,  44,  49,  54,  59,  63,  68,  73,  78,
+    82,  87,  92,  96,  100, 105, 109, 113, 118, 122, 126, 130, 134, 138, 142, 146,
+    150, 154, 157, 161, 165, 169, 172, 176, 179, 183, 186, 190, 193, 197, 200, 203,
+    207, 210, 213, 216, 220, 223, 226, 229, 232, 235, 238, 241, 244, 247, 250, 253};
+
+/* 256 * log2(x) in fixed point, x >= 1 */
+static uint32_t zs_log2fix(uint32_t x) {
+  const uint32_t hb = zs_highbit(x);
+  const uint32_t f = (hb >= 6 ? x >> (hb - 6) : x << (6 - hb)) & 63u;
+  return (hb << 8) + kLog2Frac[f];
+}
+
+/* FSE table log for `total` symbols of alphabet [0, max_sym] (FSE_optimalTableLog's rule):
+ * at most the source size's bits - 2, at least what the alphabet and source need, in
+ * [5, max_log].  total >= 2, max_sym >= 1. */
+static uint32_t zs_table_log(uint32_t max_log, uint32_t total, uint32_t max_sym) {
+  int tl = (int)max_log;
+  const int src_bits = (int)zs_highbit(total - 1) - 2;
+  if (src_bits < tl) tl = src_bits;
+  const int a = (int)zs_highbit(total) + 1, b = (int)zs_highbit(max_sym) + 2;
+  const int min_bits = a < b ? a : b;
+  if (min_bits > tl) tl = min_bits;
+  if (tl < 5) tl = 5;
+  if (tl > (int)max_log) tl = (int)max_log;
+  return (uint32_t)tl;
+}
+
+/* counts -> normalized counts summing to 2^tl: rounded shares, at least 1 per used symbol;
+ * a shortfall goes to the most frequent symbol, an excess is taken from the largest
+ * normalized counts (first symbol on ties) down to 1 */
+static void zs_normalize(const uint32_t* cnt, uint32_t max_sym, uint32_t total, uint32_t tl,
+                         int16_t* norm) {
+  const uint32_t size = 1u << tl;
+  int32_t sum = 0;
+  for (uint32_t s = 0; s <= max_sym; ++s) {
+    uint32_t v = 0;
+    if (cnt[s]) {
+      v = (cnt[s] * size + total / 2) / total;
+      if (v == 0) v = 1;
+    }
+    norm[s] = (int16_t)v;
+    sum += (int32_t)v;
+  }
+  int32_t delta = (int32_t)size - sum;
+  if (delta > 0) {
+    uint32_t best = 0;
+    for (uint32_t s = 1; s <= max_sym; ++s) if (cnt[s] > cnt[best]) best = s;
+    norm[best] = (int16_t)(norm[best] + delta);
+  }
+  while (delta < 0) {
+    uint32_t best = 0;
+    for (uint32_t s = 1; s <= max_sym; ++s) if (norm[s] > norm[best]) best = s;
+    int32_t take = norm[best] - 1;
+    if (take > -delta) take = -delta;
+    norm[best] = (int16_t)(norm[best] - take);
+    delta += take;
+  }
+}
+
+typedef struct {  /* forward bit writer (BIT_CStream) */
+  uint8_t* out;
+  uint32_t pos, cap;
+  uint64_t acc;
+  uint32_t nb;
+  int err;
+} zs_bw;
+
+static void zs_bw_add(zs_bw* w, uint64_t v, uint32_t n) {
+  if (n == 0) return;
+  w->acc |= (v & ((1ull << n) - 1)) << w->nb;
+  w->nb += n;
+  while (w->nb >= 8) {
+    if (w->pos >= w->cap) { w->err = 1; return; }
+    w->out[w->pos++] = (uint8_t)w->acc;
+    w->acc >>= 8;
+    w->nb -= 8;
+  }
+}
+/* pad to a byte boundary (no end mark) */
+static void zs_bw_pad(zs_bw* w) {
+  if (w->nb) {
+    if (w->pos >= w->cap) { w->err = 1; return; }
+    w->out[w->pos++] = (uint8_t)w->acc;
+    w->acc = 0;
+    w->nb = 0;
+  }
+}
+static void zs_bw_close(zs_bw* w) {
+  zs_bw_add(w, 1, 1);  /* end mark */
+  zs_bw_pad(w);
+}
+
+/* FSE_writeNCount: the table description of norm[0..max_sym]; returns its size in bytes */
+static uint32_t zs_write_ncount(zs_bw* w, const int16_t* norm, uint32_t max_sym, uint32_t tl) {
+  const uint32_t p0 = w->pos;
+  zs_bw_add(w, tl - 5, 4);
+  int remaining = (1 << tl) + 1, threshold = 1 << tl;
+  uint32_t nbits = tl + 1, s = 0;
+  int prev0 = 0;
+  while (s <= max_sym && remaining > 1) {
+    if (prev0) {
+      uint32_t start = s;
+      while (norm[s] == 0) ++s;
+      while (s >= start + 3) { zs_bw_add(w, 3, 2); start += 3; }
+      zs_bw_add(w, s - start, 2);
+    }
+    int count = norm[s++];
+    const int max = (2 * threshold - 1) - remaining;
+    remaining -= count < 0 ? -count : count;
+    ++count;
+    if (count >= threshold) count += max;
+    zs_bw_add(w, (uint32_t)count, nbits - (count < max ? 1u : 0u));
+    prev0 = count == 1;
+    while (remaining < threshold) { --nbits; threshold >>= 1; }
+  }
+  zs_bw_pad(w);
+  return w->pos - p0;
+}
 
 typedef struct {
-  uint16_t state[1u << 6];
+  uint16_t state[1u << 9];
   int32_t dnb[64];   /* deltaNbBits */
   int32_t dfs[64];   /* deltaFindState */
   uint32_t al;
 } zs_ctable;
 
-/* FSE_buildCTable for a normalized distribution */
+/* FSE_buildCTable for a normalized distribution (-1 = "less than 1" allowed) */
 static void zs_build_ctable(zs_ctable* c, const int16_t* norm, uint32_t max_sym, uint32_t al) {
   const uint32_t size = 1u << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
   uint32_t high = size - 1;
-  uint8_t sym_at[64];
+  uint8_t sym_at[1u << 9];
   uint32_t cumul[65];
   cumul[0] = 0;
   for (uint32_t s = 1; s <= max_sym + 1; ++s) {
@@ -655,35 +792,7 @@ static void zs_build_ctable(zs_ctable* c, const int16_t* norm, uint32_t max_sym,
   c->al = al;
 }
 
-typedef struct {  /* forward bit writer (BIT_CStream) */
-  uint8_t* out;
-  uint32_t pos, cap;
-  uint64_t acc;
-  uint32_t nb;
-  int err;
-} zs_bw;
-
-static void zs_bw_add(zs_bw* w, uint64_t v, uint32_t n) {
-  if (n == 0) return;
-  w->acc |= (v & ((1ull << n) - 1)) << w->nb;
-  w->nb += n;
-  while (w->nb >= 8) {
-    if (w->pos >= w->cap) { w->err = 1; return; }
-    w->out[w->pos++] = (uint8_t)w->acc;
-    w->acc >>= 8;
-    w->nb -= 8;
-  }
-}
-static void zs_bw_close(zs_bw* w) {
-  zs_bw_add(w, 1, 1);  /* end mark */
-  if (w->nb) {
-    if (w->pos >= w->cap) { w->err = 1; return; }
-    w->out[w->pos++] = (uint8_t)w->acc;
-    w->acc = 0;
-    w->nb = 0;
-  }
-}
-static void zs_enc_init(const zs_ctable* c, uint32_t* st, uint32_t s) {
+static void zs_enc_init(const zs_ctable* c, uint32_t* st, uint32_t s) {  /* FSE_initCState2 */
   const uint32_t nbo = (uint32_t)((c->dnb[s] + (1 << 15)) >> 16);
   const uint32_t value = (nbo << 16) - (uint32_t)c->dnb[s];
   *st = c->state[(value >> nbo) + c->dfs[s]];
@@ -705,152 +814,380 @@ uint32_t bo_zstd_ml_code(uint32_t ml) {  /* ml >= 3 */
   return c;
 }
 
+/* ---- literals section ---- */
+static void zs_lit_header(uint8_t* d, uint32_t type, uint32_t n, uint32_t* hsz) {
+  if (n < 32) {
+    d[0] = (uint8_t)(type | (n << 3));
+    *hsz = 1;
+  } else if (n < 4096) {
+    d[0] = (uint8_t)(type | (1u << 2) | ((n & 15u) << 4));
+    d[1] = (uint8_t)(n >> 4);
+    *hsz = 2;
+  } else {
+    d[0] = (uint8_t)(type | (3u << 2) | ((n & 15u) << 4));
+    d[1] = (uint8_t)(n >> 4);
+    d[2] = (uint8_t)(n >> 12);
+    *hsz = 3;
+  }
+}
+
+/* Huffman tree description of weights w[0..nw-1] (FSE form); 0 if it cannot be FSE-coded
+ * (fewer than 2 weights, one distinct weight, or >= 128 bytes).  out: >= 128 bytes. */
+static uint32_t zs_weights_fse(const uint8_t* w, uint32_t nw, uint8_t* out) {
+  if (nw < 2) return 0;
+  uint32_t cnt[13] = {0}, max_w = 0, distinct = 0;
+  for (uint32_t i = 0; i < nw; ++i) {
+    if (!cnt[w[i]]++) ++distinct;
+    if (w[i] > max_w) max_w = w[i];
+  }
+  if (distinct < 2) return 0;
+  const uint32_t tl = zs_table_log(6, nw, max_w);
+  int16_t norm[13];
+  zs_normalize(cnt, max_w, nw, tl, norm);
+  uint8_t buf[512];
+  zs_bw bw = {buf + 1, 0, 500, 0, 0, 0};
+  zs_write_ncount(&bw, norm, max_w, tl);
+  zs_ctable ct;
+  zs_build_ctable(&ct, norm, max_w, tl);
+  /* FSE_compress_usingCTable: weights from the last, two states, state 1 flushed last */
+  uint32_t s1, s2;
+  int32_t i = (int32_t)nw;
+  if (nw & 1) {
+    zs_enc_init(&ct, &s1, w[--i]);
+    zs_enc_init(&ct, &s2, w[--i]);
+    zs_enc_sym(&bw, &ct, &s1, w[--i]);
+  } else {
+    zs_enc_init(&ct, &s2, w[--i]);
+    zs_enc_init(&ct, &s1, w[--i]);
+  }
+  while (i > 0) {
+    zs_enc_sym(&bw, &ct, &s2, w[--i]);
+    zs_enc_sym(&bw, &ct, &s1, w[--i]);
+  }
+  zs_bw_add(&bw, s2, tl);
+  zs_bw_add(&bw, s1, tl);
+  zs_bw_close(&bw);
+  if (bw.err || bw.pos >= 128) return 0;
+  buf[0] = (uint8_t)bw.pos;
+  memcpy(out, buf, bw.pos + 1);
+  return bw.pos + 1;
+}
+
+/* literals section of lit[0..n) into d; returns its size */
+static uint32_t zs_literals(const uint8_t* lit, uint32_t n, uint8_t* d, uint32_t cap, int* err) {
+  uint32_t hist[256] = {0}, distinct = 0, hsz;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!hist[lit[i]]++) ++distinct;
+  if (n == 0 || distinct > 1) {
+    if (n > 0) {
+      /* ---- Huffman ---- */
+      uint8_t len[256];
+      bo_huff_lengths(hist, 256, 11, len);
+      uint32_t L = 0, max_sym = 0;
+      for (uint32_t s = 0; s < 256; ++s) {
+        if (len[s] > L) L = len[s];
+        if (len[s]) max_sym = s;
+      }
+      uint8_t w[256];
+      uint32_t rank_cnt[13] = {0};
+      for (uint32_t s = 0; s < 256; ++s) {
+        w[s] = len[s] ? (uint8_t)(L + 1 - len[s]) : 0;
+        if (len[s]) rank_cnt[w[s]]++;
+      }
+      /* codes: table index ranges by increasing weight, then symbol (HUF_readDTableX1) */
+      uint32_t start[13], next = 0, code[256];
+      for (uint32_t k = 1; k <= L; ++k) {
+        start[k] = next;
+        next += rank_cnt[k] << (k - 1);
+      }
+      for (uint32_t s = 0; s < 256; ++s) {
+        if (!len[s]) continue;
+        code[s] = start[w[s]] >> (w[s] - 1);
+        start[w[s]] += 1u << (w[s] - 1);
+      }
+      /* tree description */
+      uint8_t desc[130];
+      uint32_t dsz = 0;
+      const uint32_t nw = max_sym;
+      const uint32_t fsz = zs_weights_fse(w, nw, desc);
+      const uint32_t direct = nw <= 128 ? 1 + (nw + 1) / 2 : 0;
+      if (direct && (!fsz || direct <= fsz)) {
+        desc[0] = (uint8_t)(127 + nw);
+        for (uint32_t i = 0; i < nw; i += 2)
+          desc[1 + i / 2] = (uint8_t)((w[i] << 4) | (i + 1 < nw ? w[i + 1] : 0));
+        dsz = direct;
+      } else {
+        dsz = fsz;
+      }
+      if (dsz) {
+        const uint32_t ns = n < 256 ? 1 : 4, q = (n + 3) / 4;
+        uint32_t bytes[4] = {0}, total = dsz + (ns == 4 ? 6 : 0);
+        for (uint32_t k = 0; k < ns; ++k) {
+          const uint32_t a = ns == 1 ? 0 : k * q, b = ns == 1 ? n : (k == 3 ? n : (k + 1) * q);
+          uint64_t bits = 0;
+          for (uint32_t i = a; i < b; ++i) bits += len[lit[i]];
+          bytes[k] = (uint32_t)((bits + 1 + 7) / 8);
+          total += bytes[k];
+        }
+        const int32_t limit = (int32_t)n - (int32_t)((n >> 6) + 2);
+        if ((int32_t)total < limit) {
+          const uint32_t hs = ns == 1 || n < 1024 ? 3 : n < 16384 ? 4 : 5;
+          if (hs + total > cap) { *err = 1; return 0; }
+          const uint32_t sf = ns == 1 ? 0 : n < 1024 ? 1 : n < 16384 ? 2 : 3;
+          const uint64_t h = 2u | (sf << 2) |
+                             ((uint64_t)n << 4) | ((uint64_t)total << (hs == 3 ? 14 : hs == 4 ? 18 : 22));
+          for (uint32_t k = 0; k < hs; ++k) d[k] = (uint8_t)(h >> (8 * k));
+          uint32_t p = hs;
+          memcpy(d + p, desc, dsz);
+          p += dsz;
+          if (ns == 4) {
+            for (uint32_t k = 0; k < 3; ++k) {
+              d[p + 2 * k] = (uint8_t)bytes[k];
+              d[p + 2 * k + 1] = (uint8_t)(bytes[k] >> 8);
+            }
+            p += 6;
+          }
+          for (uint32_t k = 0; k < ns; ++k) {
+            const uint32_t a = ns == 1 ? 0 : k * q, b = ns == 1 ? n : (k == 3 ? n : (k + 1) * q);
+            zs_bw bw = {d, p, cap, 0, 0, 0};
+            for (uint32_t i = b; i-- > a;) zs_bw_add(&bw, code[lit[i]], len[lit[i]]);
+            zs_bw_close(&bw);
+            if (bw.err) { *err = 1; return 0; }
+            p = bw.pos;
+          }
+          return p;
+        }
+      }
+    }
+    /* ---- raw ---- */
+    zs_lit_header(d, 0, n, &hsz);
+    if (hsz + n > cap) { *err = 1; return 0; }
+    memcpy(d + hsz, lit, n);
+    return hsz + n;
+  }
+  /* ---- RLE ---- */
+  zs_lit_header(d, 1, n, &hsz);
+  d[hsz] = lit[0];
+  return hsz + 1;
+}
+
+/* ---- sequences section ---- */
 typedef struct {
-  const uint8_t* src;
-  uint8_t* dst;
-  uint32_t cap, op;
-  int err;
-  uint32_t blk;        /* output offset of the current block header */
-  uint32_t in0;        /* input position the current block starts at */
-  uint32_t in;         /* input consumed so far */
+  uint32_t mode;   /* 0 predefined, 1 RLE, 2 FSE_Compressed */
+  uint32_t rle;    /* the symbol of an RLE table */
+  zs_ctable ct;
+} zs_seqtab;
+
+/* choose and describe one table (codes[0..nseq)); appends the description to w */
+static void zs_choose(zs_seqtab* t, const uint8_t* codes, uint32_t nseq, uint32_t max_code,
+                      uint32_t max_log, const int16_t* def, uint32_t def_max, uint32_t def_al,
+                      zs_bw* w) {
+  uint32_t cnt[64] = {0}, max_sym = 0, distinct = 0;
+  for (uint32_t i = 0; i < nseq; ++i) {
+    if (!cnt[codes[i]]++) ++distinct;
+    if (codes[i] > max_sym) max_sym = codes[i];
+  }
+  (void)max_code;
+  if (distinct == 1) {
+    t->mode = 1;
+    t->rle = max_sym;
+    zs_bw_add(w, max_sym, 8);
+    return;
+  }
+  /* estimated bits (x256) of the symbols' FSE states under each distribution */
+  uint64_t cost_pre = 0;
+  for (uint32_t s = 0; s <= max_sym; ++s) {
+    if (!cnt[s]) continue;
+    const uint32_t nd = def[s] == -1 ? 1u : (uint32_t)def[s];
+    cost_pre += (uint64_t)cnt[s] * ((def_al << 8) - zs_log2fix(nd));
+  }
+  const uint32_t tl = zs_table_log(max_log, nseq, max_sym);
+  int16_t norm[64];
+  zs_normalize(cnt, max_sym, nseq, tl, norm);
+  uint64_t cost_fse = 0;
+  for (uint32_t s = 0; s <= max_sym; ++s)
+    if (cnt[s]) cost_fse += (uint64_t)cnt[s] * ((tl << 8) - zs_log2fix((uint32_t)norm[s]));
+  uint8_t tmp[128];
+  zs_bw tw = {tmp, 0, sizeof tmp, 0, 0, 0};
+  const uint32_t nb = zs_write_ncount(&tw, norm, max_sym, tl);
+  cost_fse += (uint64_t)nb * 8 * 256;
+  if (cost_fse < cost_pre) {
+    t->mode = 2;
+    for (uint32_t k = 0; k < nb; ++k) zs_bw_add(w, tmp[k], 8);
+    zs_build_ctable(&t->ct, norm, max_sym, tl);
+  } else {
+    t->mode = 0;
+    zs_build_ctable(&t->ct, def, def_max, def_al);
+  }
+}
+
+typedef struct {
+  uint8_t* lit;
   uint32_t nlit;
   uint32_t nseq;
-  uint32_t ll[ZS_MAX_SEQ], ml[ZS_MAX_SEQ], of[ZS_MAX_SEQ];
-  zs_ctable ct_ll, ct_ml, ct_of;
-} zs_enc;
+  uint32_t* ll;
+  uint32_t* ml;
+  uint32_t* off;
+} zs_parsed;
 
-static void zs_begin_block(zs_enc* e) {
-  e->blk = e->op;
-  e->in0 = e->in;
-  e->op += 3 + 3;  /* block header + 3-byte raw-literals header */
-  e->nlit = 0;
-  e->nseq = 0;
-  if (e->op > e->cap) e->err = 1;
-}
-
-static void zs_close_block(zs_enc* e, uint32_t last) {
-  if (e->err) return;
-  const uint32_t nlit = e->nlit, nseq = e->nseq;
-  uint8_t* d = e->dst;
-  const uint32_t lh = e->blk + 3;
-  d[lh] = (uint8_t)((3u << 2) | ((nlit & 15u) << 4));  /* raw literals, 20-bit size */
-  d[lh + 1] = (uint8_t)(nlit >> 4);
-  d[lh + 2] = (uint8_t)(nlit >> 12);
-  uint32_t p = e->op;
-  if (p + 3 > e->cap) { e->err = 1; return; }
-  if (nseq < 128) {
-    d[p++] = (uint8_t)nseq;
-  } else {
-    d[p++] = (uint8_t)((nseq >> 8) + 128);
-    d[p++] = (uint8_t)nseq;
-  }
-  if (nseq) {
-    d[p++] = 0;  /* LL, OF, ML: predefined distributions */
-    zs_bw w = {d, p, e->cap, 0, 0, 0};
-    uint32_t sml, sof, sll;
-    const uint32_t k = nseq - 1;
-    const uint32_t llc = bo_zstd_ll_code(e->ll[k]), mlc = bo_zstd_ml_code(e->ml[k]),
-                   ofc = zs_highbit(e->of[k]);
-    zs_enc_init(&e->ct_ml, &sml, mlc);
-    zs_enc_init(&e->ct_of, &sof, ofc);
-    zs_enc_init(&e->ct_ll, &sll, llc);
-    zs_bw_add(&w, e->ll[k], kLLBits[llc]);
-    zs_bw_add(&w, e->ml[k] - 3, kMLBits[mlc]);
-    zs_bw_add(&w, e->of[k], ofc);
-    for (uint32_t j = nseq - 1; j-- > 0;) {
-      const uint32_t lc = bo_zstd_ll_code(e->ll[j]), mc = bo_zstd_ml_code(e->ml[j]),
-                     oc = zs_highbit(e->of[j]);
-      zs_enc_sym(&w, &e->ct_of, &sof, oc);
-      zs_enc_sym(&w, &e->ct_ml, &sml, mc);
-      zs_enc_sym(&w, &e->ct_ll, &sll, lc);
-      zs_bw_add(&w, e->ll[j], kLLBits[lc]);
-      zs_bw_add(&w, e->ml[j] - 3, kMLBits[mc]);
-      zs_bw_add(&w, e->of[j], oc);
-    }
-    zs_bw_add(&w, sml, e->ct_ml.al);
-    zs_bw_add(&w, sof, e->ct_of.al);
-    zs_bw_add(&w, sll, e->ct_ll.al);
-    zs_bw_close(&w);
-    if (w.err) { e->err = 1; return; }
-    p = w.pos;
-  }
-  const uint32_t csz = p - (e->blk + 3), raw = e->in - e->in0;
-  uint32_t hdr;
-  if (csz >= raw) {  /* did not shrink: store the block's input raw */
-    if (e->blk + 3 + raw > e->cap) { e->err = 1; return; }
-    memcpy(d + e->blk + 3, e->src + e->in0, raw);
-    hdr = last | (0u << 1) | (raw << 3);
-    p = e->blk + 3 + raw;
-  } else {
-    hdr = last | (2u << 1) | (csz << 3);
-  }
-  d[e->blk] = (uint8_t)hdr;
-  d[e->blk + 1] = (uint8_t)(hdr >> 8);
-  d[e->blk + 2] = (uint8_t)(hdr >> 16);
-  e->op = p;
-}
-
-static void zs_emit(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t off, uint32_t mlen) {
-  zs_enc* e = (zs_enc*)vctx;
-  if (e->err) return;
-  if (e->op + lit_len > e->cap) { e->err = 1; return; }
-  memcpy(e->dst + e->op, e->src + lit_start, lit_len);
-  e->op += lit_len;
-  e->nlit += lit_len;
-  e->in += lit_len;
+static void zs_collect(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t off,
+                       uint32_t mlen) {
+  zs_parsed* z = (zs_parsed*)vctx;
+  (void)lit_start;
+  z->nlit += lit_len;  /* bytes are gathered from the positions afterwards */
   if (mlen) {
-    e->ll[e->nseq] = lit_len;
-    e->ml[e->nseq] = mlen;
-    e->of[e->nseq] = off + 3;  /* Offset_Value: no repeat offsets */
-    e->nseq++;
-    e->in += mlen;
-    /* a block ends right after its ZS_MAX_SEQ-th match: the literals that follow belong to
-     * the next block, so the kernel writes every literal byte as soon as it is parsed */
-    if (e->nseq == ZS_MAX_SEQ) {
-      zs_close_block(e, 0);
-      zs_begin_block(e);
-    }
+    z->ll[z->nseq] = lit_len;
+    z->ml[z->nseq] = mlen;
+    z->off[z->nseq] = off;
+    z->nseq++;
   }
 }
 
 uint32_t bo_zstd_bound(uint32_t n) {
-  /* frame header 4+1+2, then per block of input: 3-byte header + at most the raw input
-   * (a block never grows: it is stored raw instead) -- blocks split only at sequence
-   * boundaries, at most n/4/ZS_MAX_SEQ+1 of them.  The +512: a block is written compressed
-   * before it is judged, and its compressed form may exceed its raw size by < 2 B per
-   * sequence (<= 17 state + 16 literal-length + 12 offset bits vs a >= 4-byte match) plus
-   * its headers. */
-  return n + 7 + 3 * (n / (4 * ZS_MAX_SEQ) + 2) + 8 + 512;
+  /* frame header 4+1+2 + block header 3 + at most the raw input (a block that does not
+   * shrink is stored raw); the slack covers the kernels' staging */
+  return n + 7 + 3 + 8 + 512;
 }
 
 int bo_zstd_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
                            uint32_t* csize) {
   if (n > 65536 || cap < bo_zstd_bound(n)) return BO_ERR_INVALID;
-  zs_enc* e = (zs_enc*)calloc(1, sizeof(zs_enc));
-  if (!e) return BO_ERR_OUT_OF_MEMORY;
-  e->src = src;
-  e->dst = dst;
-  e->cap = cap;
-  zs_build_ctable(&e->ct_ll, kLLDefault, 35, ZS_LL_AL);
-  zs_build_ctable(&e->ct_ml, kMLDefault, 52, ZS_ML_AL);
-  zs_build_ctable(&e->ct_of, kOFDefault, 28, ZS_OF_AL);
-  /* frame header: magic, single segment, content size (1 byte below 256, else 2 bytes) */
-  dst[0] = 0x28; dst[1] = 0xB5; dst[2] = 0x2F; dst[3] = 0xFD;
-  if (n < 256) {
-    dst[4] = 0x20;
-    dst[5] = (uint8_t)n;
-    e->op = 6;
-  } else {
-    dst[4] = 0x60;
-    dst[5] = (uint8_t)(n - 256);
-    dst[6] = (uint8_t)((n - 256) >> 8);
-    e->op = 7;
+  const uint32_t maxseq = n / 4 + 2;
+  zs_parsed z = {0};
+  z.lit = (uint8_t*)malloc(n + 1);
+  z.ll = (uint32_t*)malloc(4u * maxseq);
+  z.ml = (uint32_t*)malloc(4u * maxseq);
+  z.off = (uint32_t*)malloc(4u * maxseq);
+  uint8_t* codes = (uint8_t*)malloc(3u * maxseq);
+  uint32_t* ov = (uint32_t*)malloc(4u * maxseq);
+  int rc = BO_ERR_OUT_OF_MEMORY;
+  if (!z.lit || !z.ll || !z.ml || !z.off || !codes || !ov) goto out;
+  bo_window_parse_flags(src, n, BO_MAX_DIST_ALL, 0xFFFFFFFFu, BO_PARSE_REP, zs_collect, &z);
+  {
+    /* literal bytes: everything outside the matches */
+    uint32_t ip = 0, lp = 0;
+    for (uint32_t i = 0; i < z.nseq; ++i) {
+      memcpy(z.lit + lp, src + ip, z.ll[i]);
+      lp += z.ll[i];
+      ip += z.ll[i] + z.ml[i];
+    }
+    memcpy(z.lit + lp, src + ip, n - ip);
+    lp += n - ip;
+    if (lp != z.nlit) { rc = BO_ERR_IO; goto out; }
   }
-  zs_begin_block(e);
-  bo_window_parse(src, n, BO_MAX_DIST_ALL, 0xFFFFFFFFu, zs_emit, e);
-  zs_close_block(e, 1);
-  const int rc = e->err ? BO_ERR_IO : BO_OK;
-  if (!e->err) *csize = e->op;
-  free(e);
+  /* repeat offsets (RFC 8878 3.1.2.5) */
+  {
+    uint32_t r0 = 1, r1 = 4, r2 = 8;
+    for (uint32_t i = 0; i < z.nseq; ++i) {
+      const uint32_t o = z.off[i];
+      uint32_t v;
+      if (z.ll[i]) {
+        v = o == r0 ? 1 : o == r1 ? 2 : o == r2 ? 3 : o + 3;
+      } else {
+        v = o == r1 ? 1 : o == r2 ? 2 : o == r0 - 1 ? 3 : o + 3;
+      }
+      ov[i] = v;
+      const uint32_t idx = v > 3 ? 3 : v - 1 + (z.ll[i] ? 0 : 1);  /* 3: a new offset */
+      if (v > 3 || idx == 3) {
+        r2 = r1;
+        r1 = r0;
+        r0 = o;
+      } else if (idx == 1) {
+        r1 = r0;
+        r0 = o;
+      } else if (idx == 2) {
+        r2 = r1;
+        r1 = r0;
+        r0 = o;
+      }
+    }
+  }
+  {
+    uint32_t op;
+    /* frame header: magic, Single_Segment with the content size (1 byte below 256, else 2) */
+    dst[0] = 0x28; dst[1] = 0xB5; dst[2] = 0x2F; dst[3] = 0xFD;
+    if (n < 256) {
+      dst[4] = 0x20;
+      dst[5] = (uint8_t)n;
+      op = 6;
+    } else {
+      dst[4] = 0x60;
+      dst[5] = (uint8_t)(n - 256);
+      dst[6] = (uint8_t)((n - 256) >> 8);
+      op = 7;
+    }
+    const uint32_t blk = op;
+    int err = 0;
+    uint32_t p = blk + 3;
+    p += zs_literals(z.lit, z.nlit, dst + p, cap - p, &err);
+    if (!err && p + 4 <= cap) {
+      const uint32_t nseq = z.nseq;
+      if (nseq < 128) {
+        dst[p++] = (uint8_t)nseq;
+      } else {
+        dst[p++] = (uint8_t)((nseq >> 8) + 128);
+        dst[p++] = (uint8_t)nseq;
+      }
+      if (nseq) {
+        uint8_t* llc = codes;
+        uint8_t* mlc = codes + maxseq;
+        uint8_t* ofc = codes + 2 * maxseq;
+        for (uint32_t i = 0; i < nseq; ++i) {
+          llc[i] = (uint8_t)bo_zstd_ll_code(z.ll[i]);
+          mlc[i] = (uint8_t)bo_zstd_ml_code(z.ml[i]);
+          ofc[i] = (uint8_t)zs_highbit(ov[i]);
+        }
+        const uint32_t mp = p++;  /* Symbol_Compression_Modes */
+        zs_bw w = {dst, p, cap, 0, 0, 0};
+        static zs_seqtab tll, tof, tml;  /* (large: not on the stack) */
+        zs_choose(&tll, llc, nseq, 35, 9, kLLDefault, 35, ZS_LL_AL, &w);
+        zs_choose(&tof, ofc, nseq, 31, 8, kOFDefault, 28, ZS_OF_AL, &w);
+        zs_choose(&tml, mlc, nseq, 52, 9, kMLDefault, 52, ZS_ML_AL, &w);
+        dst[mp] = (uint8_t)((tll.mode << 6) | (tof.mode << 4) | (tml.mode << 2));
+        /* the bitstream: last sequence first */
+        uint32_t sml = 0, sof = 0, sll = 0;
+        const uint32_t k = nseq - 1;
+        if (tml.mode != 1) zs_enc_init(&tml.ct, &sml, mlc[k]);
+        if (tof.mode != 1) zs_enc_init(&tof.ct, &sof, ofc[k]);
+        if (tll.mode != 1) zs_enc_init(&tll.ct, &sll, llc[k]);
+        zs_bw_add(&w, z.ll[k], kLLBits[llc[k]]);
+        zs_bw_add(&w, z.ml[k] - 3, kMLBits[mlc[k]]);
+        zs_bw_add(&w, ov[k], ofc[k]);
+        for (uint32_t j = nseq - 1; j-- > 0;) {
+          if (tof.mode != 1) zs_enc_sym(&w, &tof.ct, &sof, ofc[j]);
+          if (tml.mode != 1) zs_enc_sym(&w, &tml.ct, &sml, mlc[j]);
+          if (tll.mode != 1) zs_enc_sym(&w, &tll.ct, &sll, llc[j]);
+          zs_bw_add(&w, z.ll[j], kLLBits[llc[j]]);
+          zs_bw_add(&w, z.ml[j] - 3, kMLBits[mlc[j]]);
+          zs_bw_add(&w, ov[j], ofc[j]);
+        }
+        if (tml.mode != 1) zs_bw_add(&w, sml, tml.ct.al);
+        if (tof.mode != 1) zs_bw_add(&w, sof, tof.ct.al);
+        if (tll.mode != 1) zs_bw_add(&w, sll, tll.ct.al);
+        zs_bw_close(&w);
+        err |= w.err;
+        p = w.pos;
+      }
+    } else {
+      err = 1;
+    }
+    if (err) { rc = BO_ERR_IO; goto out; }
+    const uint32_t csz = p - (blk + 3);
+    uint32_t hdr;
+    if (csz >= n) {  /* did not shrink: one raw block */
+      memcpy(dst + blk + 3, src, n);
+      hdr = 1u | (0u << 1) | (n << 3);
+      p = blk + 3 + n;
+    } else {
+      hdr = 1u | (2u << 1) | (csz << 3);
+    }
+    dst[blk] = (uint8_t)hdr;
+    dst[blk + 1] = (uint8_t)(hdr >> 8);
+    dst[blk + 2] = (uint8_t)(hdr >> 16);
+    *csize = p;
+    rc = BO_OK;
+  }
+out:
+  free(z.lit); free(z.ll); free(z.ml); free(z.off); free(codes); free(ov);
   return rc;
 }

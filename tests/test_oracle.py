@@ -214,38 +214,101 @@ def test_oracle_zstd_rejects_malformed():
             break
 
 
-def _zstd_blocks(frame):
-    """(type, size, nseq) of every block of a single-segment frame the oracle wrote."""
+def _zstd_info(frame):
+    """Structure of a single-segment, single-block frame the oracle wrote: block type, and
+    for a compressed block the literal section (type, streams, sizes, Huffman description
+    header byte) and the sequence section (count, table modes)."""
     fh = 6 if frame[4] == 0x20 else 7
-    p, out = fh, []
-    while True:
-        h = frame[p] | (frame[p + 1] << 8) | (frame[p + 2] << 16)
-        last, btype, bsize = h & 1, (h >> 1) & 3, h >> 3
-        nseq = None
-        if btype == 2:
-            lsz = (frame[p + 3] >> 4) | (frame[p + 4] << 4) | (frame[p + 5] << 12)
-            q = p + 6 + lsz
-            nseq = frame[q] if frame[q] < 128 else ((frame[q] - 128) << 8) + frame[q + 1]
-        out.append((btype, bsize, nseq))
-        p += 3 + bsize
-        if last:
-            break
-    assert p == len(frame)
-    return out
+    p = fh
+    h = frame[p] | (frame[p + 1] << 8) | (frame[p + 2] << 16)
+    last, btype, bsize = h & 1, (h >> 1) & 3, h >> 3
+    assert last == 1 and p + 3 + (bsize if btype != 1 else 1) == len(frame)
+    info = {"block": btype, "bsize": bsize}
+    if btype != 2:
+        return info
+    p += 3
+    b0 = frame[p]
+    lt, sf = b0 & 3, (b0 >> 2) & 3
+    if lt < 2:
+        if sf in (0, 2):
+            reg, hs = b0 >> 3, 1
+        elif sf == 1:
+            reg, hs = (b0 >> 4) + (frame[p + 1] << 4), 2
+        else:
+            reg, hs = (b0 >> 4) + (frame[p + 1] << 4) + (frame[p + 2] << 12), 3
+        lsz, streams, desc = hs + (reg if lt == 0 else 1), 0, None
+    else:
+        hs = 3 if sf <= 1 else 4 if sf == 2 else 5
+        c = int.from_bytes(frame[p:p + hs], "little")
+        bits = 10 if hs == 3 else 14 if hs == 4 else 18
+        reg, cs = (c >> 4) & ((1 << bits) - 1), c >> (4 + bits)
+        lsz, streams, desc = hs + cs, 1 if sf == 0 else 4, frame[p + hs]
+    q = p + lsz
+    nseq = frame[q]
+    if nseq >= 128:
+        nseq, q = ((nseq - 128) << 8) + frame[q + 1], q + 2
+    else:
+        q += 1
+    modes = None
+    if nseq:
+        m = frame[q]
+        modes = (m >> 6, (m >> 4) & 3, (m >> 2) & 3)
+    info.update(lit_type=lt, nlit=reg, lit_bytes=lsz, streams=streams, huf_desc=desc,
+                nseq=nseq, modes=modes)
+    return info
 
 
-@pytest.mark.parametrize("kind", [1, 2, 3, 4, 6])
-def test_oracle_zstd_block_split_rule(kind):
-    """Blocks close right after their 256th sequence; a block that does not shrink is raw."""
-    data = O.fill(kind, 11, 65536).tobytes()
-    r, frame = O.zstd_compress(data)
-    assert r == 0
-    blocks = _zstd_blocks(frame)
-    assert all(b[0] in (0, 2) for b in blocks)
-    assert all(b[2] is None or b[2] <= 256 for b in blocks)
-    assert all(b[2] == 256 for b in blocks[:-1] if b[0] == 2)
-    if kind in (1, 6):
-        assert len(blocks) > 1  # the split path is exercised
+def test_oracle_zstd_frame_structure():
+    """One block per segment (raw when it does not shrink); literals raw / RLE / Huffman with
+    1 stream below 256 literals, else 4; FSE-compressed Huffman weights when more than 128
+    would be sent directly; repeat-offset / FSE table modes on structured input."""
+    rnd = O.fill(0, 1, 65536).tobytes()
+    r, f = O.zstd_compress(rnd)
+    assert r == 0 and _zstd_info(f)["block"] == 0 and len(f) == 7 + 3 + 65536
+    # one distinct literal byte: RLE literals
+    i = _zstd_info(O.zstd_compress(b"\x07" * 5000)[1])
+    assert i["block"] == 2 and i["lit_type"] == 1
+    # text: Huffman, 1 stream below 256 literals, else 4
+    text = O.fill(6, 3, 2000).tobytes()
+    i = _zstd_info(O.zstd_compress(text[:600])[1])
+    assert i["block"] == 2 and i["lit_type"] == 2 and i["streams"] == 1 and i["nlit"] < 256
+    i = _zstd_info(O.zstd_compress(text)[1])
+    assert i["lit_type"] == 2 and i["streams"] == 4 and i["nlit"] >= 256
+    rng = np.random.default_rng(5)
+    # 16 equiprobable byte values: every weight equal -> not FSE-codable -> direct weights
+    small = bytes(rng.integers(0, 16, 30000).astype(np.uint8))
+    i = _zstd_info(O.zstd_compress(small)[1])
+    assert i["lit_type"] == 2 and i["huf_desc"] == 127 + 15
+    # skewed bytes across the whole range: > 128 weights -> FSE-compressed (byte < 128)
+    p = 0.5 ** (1 + np.arange(256) % 9)
+    skew = bytes(rng.choice(256, size=30000, p=p / p.sum()).astype(np.uint8))
+    i = _zstd_info(O.zstd_compress(skew)[1])
+    assert i["lit_type"] == 2 and i["huf_desc"] < 128
+    col = O.fill(5, 1, 65536).tobytes()  # int64 column: sequences on FSE tables
+    i = _zstd_info(O.zstd_compress(col)[1])
+    assert i["block"] == 2 and i["nseq"] > 1000 and 2 in i["modes"]
+
+
+def test_oracle_zstd_ratio_vs_libzstd1():
+    """The level-1-class encoder: on the Arrow-like kind-2 input (all four 1 MiB columns) and
+    the Silesia-style kind 1, at least 95 % of libzstd level 1's ratio on the same segments."""
+    Z = _libzstd()
+    Z.ZSTD_compress.restype = ctypes.c_size_t
+    Z.ZSTD_compressBound.restype = ctypes.c_size_t
+    seg = 65536
+    for kind, n in ((2, 4 << 20), (1, 3 << 20)):
+        data = O.fill(kind, 1000, n).tobytes()
+        ours = theirs = 0
+        out = ctypes.create_string_buffer(int(Z.ZSTD_compressBound(seg)))
+        for i in range(0, n, seg):
+            s = data[i:i + seg]
+            r, f = O.zstd_compress(s)
+            assert r == 0
+            ours += len(f)
+            c = Z.ZSTD_compress(out, len(out), s, len(s), 1)
+            assert not Z.ZSTD_isError(c)
+            theirs += c
+        assert n / ours >= 0.95 * (n / theirs), (kind, n / ours, n / theirs)
 
 
 # ---- dynamic-Huffman DEFLATE (oracle/bitar_deflate_dyn.c) ----------------------------------
