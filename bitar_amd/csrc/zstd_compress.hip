@@ -26,6 +26,15 @@ namespace zse {
 
 using namespace cmp;
 
+#ifndef BITAR_ZSTD_STOP
+#define BITAR_ZSTD_STOP 0  // timing experiments only: end the entropy kernel after phase k
+#endif
+#define ZSE_PHASE(k)                             \
+  if constexpr (BITAR_ZSTD_STOP == (k)) {        \
+    if (lane == 0) sizes[i_seg] = 16u;           \
+    return;                                      \
+  }
+
 // ---- code tables (RFC 8878 3.1.1.3.2.1-2) ----------------------------------------------------
 constexpr uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,   7,   8,   9,    10,   11,
                                   12, 13, 14, 15, 16, 18, 20,  22,  24,  28,   32,   40,
@@ -187,6 +196,7 @@ struct EntLds {
   uint32_t ew[4 * kWave];  // per 64 sequences: chain transforms / state bits
   uint32_t u[16];          // lane-0 results: sizes, modes, accuracy logs
   uint32_t wk[32];         // lane-0 work: weight counts, code ranges
+  alignas(16) uint8_t lst[16 * kWave];  // literal block being encoded (16-B stores)
 };
 
 // 256 * log2(x), x >= 1
@@ -591,6 +601,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
   }
   lds_order();
 
+  ZSE_PHASE(1)
   // ---- literals section ----
   bool huff = false;
   uint32_t ns = 1, dsz = 0, hs = 0, total = 0;
@@ -674,6 +685,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       huff = (int32_t)total < limit;
     }
   }
+  ZSE_PHASE(2)
   if (huff) {
     hs = ns == 1 || nlit < 1024 ? 3u : nlit < 16384 ? 4u : 5u;
     const uint32_t sf = ns == 1 ? 0u : nlit < 1024 ? 1u : nlit < 16384 ? 2u : 3u;
@@ -694,13 +706,29 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       const uint32_t b = ns == 1 ? nlit : (k == 3 ? nlit : (k + 1) * qs);
       const uint32_t p0 = o.op;
       uint32_t bits = 0, zeroed = p0;
-      for (int32_t e = (int32_t)b; e > (int32_t)a && !o.overflow; e -= (int32_t)kWave) {
-        const int32_t idx = e - (int32_t)kWave + (int32_t)lane;
-        const bool act = idx >= (int32_t)a;
-        const uint32_t sym = act ? (uint32_t)lits[idx] : 0u;
+      // 1 KiB blocks of aligned 16-B groups, staged in LDS, the next one loaded during the
+      // current one
+      const GMEM uint4* l16 = reinterpret_cast<const GMEM uint4*>(lits);
+      const int32_t gA = (int32_t)(a >> 4), gB = (int32_t)((b + 15) >> 4);
+      int32_t g0 = gB - (int32_t)kWave;
+      uint4 blkv = make_uint4(0, 0, 0, 0);
+      if (g0 + (int32_t)lane >= gA) blkv = l16[g0 + (int32_t)lane];
+      for (;;) {
         lds_order();
-        const uint32_t cw = L.code[sym];
-        o.put_bits(act ? (cw & 0xFFFFu) : 0u, act ? cw >> 16 : 0u, 0, 0, p0, bits, zeroed);
+        reinterpret_cast<uint4*>(L.lst)[lane] = blkv;
+        const int32_t g1 = g0 - (int32_t)kWave;
+        if (g0 > gA && g1 + (int32_t)lane >= gA) blkv = l16[g1 + (int32_t)lane];
+        const int32_t lo = max((int32_t)a, 16 * g0), hi = min((int32_t)b, 16 * (g0 + (int32_t)kWave));
+        for (int32_t e = hi; e > lo && !o.overflow; e -= (int32_t)kWave) {
+          const int32_t idx = e - (int32_t)kWave + (int32_t)lane;
+          const bool act = idx >= lo;
+          lds_order();
+          const uint32_t sym = act ? L.lst[idx - 16 * g0] : 0u;
+          const uint32_t cw = L.code[sym];
+          o.put_bits(act ? (cw & 0xFFFFu) : 0u, act ? cw >> 16 : 0u, 0, 0, p0, bits, zeroed);
+        }
+        if (g0 <= gA || o.overflow) break;
+        g0 = g1;
       }
       o.put_bits(lane == 0 ? 1u : 0u, lane == 0 ? 1u : 0u, 0, 0, p0, bits, zeroed);  // end mark
       o.op = p0 + ((bits + 7) >> 3);
@@ -732,6 +760,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     }
   }
 
+  ZSE_PHASE(3)
   // ---- sequences section ----
   if (!o.overflow) {
     const uint32_t nh = nseq < 128 ? 1u : 2u;
@@ -739,38 +768,44 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     o.put(nh == 1 ? nseq : lane == 0 ? (nseq >> 8) + 128u : nseq & 0xFFu, nh);
   }
   if (nseq && !o.overflow) {
-    // repeat offsets (RFC 8878 3.1.2.5) by a scalar scan, codes, histograms; the records
-    // become {literal length | offset value << 17, match length}
+    // repeat offsets (RFC 8878 3.1.2.5), codes, histograms; the records become {literal
+    // length | offset value << 17, match length}.  The history is scanned lane-parallel,
+    // 64 sequences per step: after sequence i, r0 = o_i; r1 = o_{j-1} for the last j <= i
+    // that is not a plain repeat of r0 (ll_j > 0 && o_j == o_{j-1}); r2 = r1 before the last
+    // k <= i that is neither such a repeat nor a repeat of r1 (prefix maxima + bpermute)
     for (uint32_t k = lane; k < 3 * 64; k += kWave) (&L.sh[0][0])[k] = 0;
     lds_order();
-    uint32_t r0 = 1, r1 = 4, r2 = 8;
+    uint32_t c0r = 1, c1r = 4, c2r = 8;  // the history before the step (uniform)
+    uint2 nrec = lane < nseq ? seqs[lane] : make_uint2(0, 3);
     for (uint32_t c0 = 0; c0 < nseq; c0 += kWave) {
       const uint32_t j = c0 + lane;
       const bool act = j < nseq;
-      const uint2 rec = act ? seqs[j] : make_uint2(0, 3);
-      const uint32_t ll = rec.x & 0x1FFFFu, off = rec.x >> 17, ml = rec.y;
+      const uint2 rec = nrec;
+      if (c0 + kWave + lane < nseq) nrec = seqs[c0 + kWave + lane];  // prefetch the next step
+      const uint32_t ll = rec.x & 0x1FFFFu, o = rec.x >> 17, ml = rec.y;
       const uint32_t cnt = nseq - c0 < kWave ? nseq - c0 : kWave;
-      uint32_t ov = 0;
-      for (uint32_t k = 0; k < cnt; ++k) {
-        const uint32_t lk = readlane(ll, k), o_ = readlane(off, k);
-        uint32_t v;
-        if (lk) v = o_ == r0 ? 1u : o_ == r1 ? 2u : o_ == r2 ? 3u : o_ + 3u;
-        else v = o_ == r1 ? 1u : o_ == r2 ? 2u : o_ == r0 - 1u ? 3u : o_ + 3u;
-        const uint32_t idx = v > 3 ? 3u : v - 1u + (lk ? 0u : 1u);
-        if (idx == 3) {
-          r2 = r1;
-          r1 = r0;
-          r0 = o_;
-        } else if (idx == 1) {
-          r1 = r0;
-          r0 = o_;
-        } else if (idx == 2) {
-          r2 = r1;
-          r1 = r0;
-          r0 = o_;
-        }
-        ov = writelane(ov, v, k);
-      }
+      // (every cross-lane op runs on all 64 lanes: a DPP or bpermute source lane that is
+      // off in EXEC reads as 0)
+      const uint32_t so = wave_shr1(o);
+      const uint32_t oprev = lane == 0 ? c0r : so;                      // r0 before
+      const bool same = !act || (ll != 0 && o == oprev);
+      const uint32_t mj = wave_incl_max(same ? 0u : lane + 1);
+      const uint32_t p1 = bpermute(oprev, mj ? mj - 1 : 0u);
+      const uint32_t r1a = mj ? p1 : c1r;                               // r1 after
+      const uint32_t s1 = wave_shr1(r1a);
+      const uint32_t r1b = lane == 0 ? c1r : s1;                        // r1 before
+      const bool ev = !same && o != r1b;
+      const uint32_t mk = wave_incl_max(ev ? lane + 1 : 0u);
+      const uint32_t p2 = bpermute(r1b, mk ? mk - 1 : 0u);
+      const uint32_t r2a = mk ? p2 : c2r;                               // r2 after
+      const uint32_t s2 = wave_shr1(r2a);
+      const uint32_t r2b = lane == 0 ? c2r : s2;                        // r2 before
+      uint32_t ov;
+      if (ll) ov = o == oprev ? 1u : o == r1b ? 2u : o == r2b ? 3u : o + 3u;
+      else ov = o == r1b ? 1u : o == r2b ? 2u : o == oprev - 1u ? 3u : o + 3u;
+      c0r = readlane(o, cnt - 1);
+      c1r = readlane(r1a, cnt - 1);
+      c2r = readlane(r2a, cnt - 1);
       if (act) {
         atomicAdd(&L.sh[0][ll_code(ll)], 1u);
         atomicAdd(&L.sh[1][hb32(ov)], 1u);
@@ -779,6 +814,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       }
     }
     lds_order();
+    ZSE_PHASE(4)
     // tables (one lane): modes byte + descriptions in L.desc, states / transforms
     if (lane == 0) {
       SBits w{L.desc + 1, 0, 0, 0};
@@ -793,6 +829,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       L.tabs[kTabDummy] = 0;
     }
     lds_order();
+    ZSE_PHASE(5)
     o.put_lds(L.desc, L.u[1]);
     const uint32_t al_ll = L.u[2], al_of = L.u[3], al_ml = L.u[4];
     // the bitstream, last sequence first (oracle bo_zstd_compress_block).  Per 64 sequences
@@ -806,22 +843,26 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     const uint32_t top = nseq - 1;
     const uint32_t cl = lane < 3 ? lane : 3u;
     const uint32_t tb = cl == 0 ? kTabOF : cl == 1 ? kTabML : cl == 2 ? kTabLL : kTabDummy;
+    uint2 prec = seqs[(top >> 6) * kWave + lane < nseq ? (top >> 6) * kWave + lane : top];
     for (int32_t c = (int32_t)(top >> 6); c >= 0 && !o.overflow; --c) {
       const uint32_t j = (uint32_t)c * kWave + lane;
       const bool act = j < nseq;
-      lds_order();
-      const uint2 rec = seqs[act ? j : top];
+      const uint2 rec = prec;
+      if (c > 0) prec = seqs[(uint32_t)(c - 1) * kWave + lane];  // prefetch the next step
       const uint32_t ll = rec.x & 0x1FFFFu, ov = rec.x >> 17, mlb = rec.y - 3u;
       const uint32_t llc = ll_code(ll), mlc = ml_code(rec.y), ofc = hb32(ov);
-      L.ew[4 * lane + 0] = L.tr[1][ofc];
-      L.ew[4 * lane + 1] = L.tr[2][mlc];
-      L.ew[4 * lane + 2] = L.tr[0][llc];
-      L.ew[4 * lane + 3] = 0u;
       lds_order();
+      const uint32_t eOF = L.tr[1][ofc], eML = L.tr[2][mlc], eLL = L.tr[0][llc];
+      // the chain lane's transform of sequence k: readlanes (no LDS round trip on the
+      // state chain, whose only memory access is the state table)
+      auto tr_of = [&](uint32_t k) __attribute__((always_inline)) {
+        const uint32_t a = readlane(eOF, k), b = readlane(eML, k), d = readlane(eLL, k);
+        return cl == 0 ? a : cl == 1 ? b : cl == 2 ? d : 0u;
+      };
       int32_t k = 63;
       if (c == (int32_t)(top >> 6)) {  // the last sequence initialises the three states
         k = (int32_t)(top & 63u);
-        const uint32_t e = L.ew[4 * (uint32_t)k + cl];
+        const uint32_t e = tr_of((uint32_t)k);
         const uint32_t d = tr_d(e);
         const uint32_t nbo = (d + (1u << 15)) >> 16;
         const uint32_t val = (nbo << 16) - d;
@@ -831,10 +872,10 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
         --k;
       }
       for (; k >= 0; --k) {
-        lds_order();
-        const uint32_t e = L.ew[4 * (uint32_t)k + cl];
+        const uint32_t e = tr_of((uint32_t)k);
         const uint32_t nb = (st + tr_d(e)) >> 16;
         const uint32_t out = st & ((1u << nb) - 1u);
+        lds_order();
         st = L.tabs[tb + (uint32_t)((int32_t)(st >> nb) + tr_f(e))];
         L.ew[4 * (uint32_t)k + cl] = out | (nb << 24);
       }

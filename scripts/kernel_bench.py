@@ -47,8 +47,11 @@ def main():
             if r:
                 tc.append(e[0].elapsed_time(e[1]))
                 td.append(e[1].elapsed_time(e[2]))
-        eng.sync()
-        ok = bool(torch.equal(out[:n], data))
+        try:
+            eng.sync()
+            ok = bool(torch.equal(out[:n], data))
+        except bitar_amd.BitarError:  # (timing variants that cut the encoder short)
+            ok = False
         C = int(sizes.to(torch.int64).sum().item())
         tcm, tdm = min(tc), min(td)
         print(json.dumps({"kind": kind, "codec": a.codec, "ratio": round(n / C, 3), "ok": ok,
