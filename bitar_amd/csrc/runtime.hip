@@ -36,7 +36,11 @@ __global__ void zstd_entropy_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*
                                     uint32_t*);
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                        const uint32_t*, uint32_t, uint32_t, uint8_t*,
-                                       uint32_t*, uint32_t*, uint32_t);
+                                       uint32_t*, uint32_t*, uint32_t, uint8_t*);
+template <uint32_t L>
+__global__ void zstd_handoff_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
+                                    const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
+                                    const uint8_t*, uint32_t*);
 template <uint32_t L>
 __global__ void zstd_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                   const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
@@ -472,9 +476,21 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
         hipLaunchKernelGGL(bitar_hip::zstd_lanes_kernel<8>, g, dim3(64), 0, s, srcs, slab,
                            stride, d_sizes, nseg, seg, out, d_produced);
     }
+    // the wave decoder hands the sequence sections of its frames' last blocks to the lane
+    // executor through a stream-ordered scratch (zstd_decompress.hip kHand*: 6 KiB per
+    // segment)
+    constexpr uint64_t kHandStride = 4ull * (16 + 3 * 512);
+    void* hscr = nullptr;
+    HIP_TRY(hipMallocAsync(&hscr, (uint64_t)nseg * kHandStride, s), "scratch allocation");
     hipLaunchKernelGGL(bitar_hip::zstd_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs,
                        slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
-                       L ? 1u : 0u);
+                       L ? 1u : 0u, static_cast<uint8_t*>(hscr));
+    hipLaunchKernelGGL(bitar_hip::zstd_handoff_kernel<16>, dim3((nseg + 15) / 16), dim3(64), 0, s,
+                       srcs, slab, stride, d_sizes, nseg, seg, out, d_produced,
+                       static_cast<const uint8_t*>(hscr), err_word(ctx, s));
+    const hipError_t le = hipGetLastError();
+    HIP_TRY(hipFreeAsync(hscr, s), "scratch release");
+    HIP_TRY(le, "decompress launch");
   }
   HIP_TRY(hipGetLastError(), "decompress launch");
   return 0;

@@ -405,25 +405,23 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
         m = e < kWave ? valid & (~0ull << e) : 0ull;
       }
       if (chain) pos = x + e;
-      if constexpr (REP) {  // the history after this window's matches, in order
-        const uint32_t offv = p - cand;
-        uint64_t cm = chain;
-        while (cm) {
-          const uint32_t l = (uint32_t)__builtin_ctzll(cm);
-          cm &= cm - 1;
-          const uint32_t d = readlane(offv, l);
-          if (d == h1) {
-            h1 = h0;
-            h0 = d;
-          } else if (d == h2) {
-            h2 = h1;
-            h1 = h0;
-            h0 = d;
-          } else if (d != h0) {
-            h2 = h1;
-            h1 = h0;
-            h0 = d;
-          }
+      if constexpr (REP) {
+        // the history after this window's matches: the 3 most recently used distinct
+        // distances (move-to-front) of [h2, h1, h0, the chain's distances in lane order],
+        // found by ballots instead of a per-match scalar loop
+        if (chain) {
+          const uint32_t offv = p - cand;
+          const uint32_t n0 = readlane(offv, highbit(chain));
+          const uint64_t m1 = chain & ballot(offv != n0);
+          const uint32_t o1 = h0 != n0 ? h0 : h1;  // first old distance unlike n0
+          const uint32_t n1 = m1 ? readlane(offv, highbit(m1)) : o1;
+          const uint64_t m2 = m1 & ballot(offv != n1);
+          // first old distance unlike n0 and n1
+          const uint32_t o2 = h0 != n0 && h0 != n1 ? h0 : h1 != n0 && h1 != n1 ? h1 : h2;
+          const uint32_t n2 = m2 ? readlane(offv, highbit(m2)) : o2;
+          h0 = n0;
+          h1 = n1;
+          h2 = n2;
         }
       }
       Window W;

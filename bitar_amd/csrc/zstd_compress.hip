@@ -96,12 +96,15 @@ constexpr Tabs build_tabs() {
   return t;
 }
 __constant__ Tabs kT = build_tabs();
+// the entropy kernel's copy in LDS: a __constant__ read compiles to a global load whose
+// latency would sit on every dependent step
+__shared__ __attribute__((aligned(16))) Tabs sT;
 
 __device__ __forceinline__ uint32_t hb32(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
-__device__ __forceinline__ uint32_t ll_code(uint32_t ll) { return ll < 64 ? kT.ll_code[ll] : hb32(ll) + 19u; }
+__device__ __forceinline__ uint32_t ll_code(uint32_t ll) { return ll < 64 ? sT.ll_code[ll] : hb32(ll) + 19u; }
 __device__ __forceinline__ uint32_t ml_code(uint32_t ml) {  // ml >= 3
   const uint32_t b = ml - 3;
-  return b < 128 ? kT.ml_code[b] : hb32(b) + 36u;
+  return b < 128 ? sT.ml_code[b] : hb32(b) + 36u;
 }
 
 // ---- scratch layout --------------------------------------------------------------------------
@@ -179,31 +182,32 @@ struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the lit
 constexpr uint32_t kTabLL = 0, kTabOF = 512, kTabML = 768, kTabDummy = 1280;
 
 struct EntLds {
-  uint32_t hq[4][256];     // literal histograms per stream quarter
-  uint32_t hist[256];      // all literals
-  huf::TreeLds T;
+  uint32_t hist[256];      // literal histogram
   uint8_t len[256];        // code lengths
   uint8_t w[256];          // weights
-  uint32_t code[256];      // code | length << 16
   uint8_t desc[192];       // Huffman tree description; then modes + table descriptions
   uint8_t tmp[256];        // serial bit writer output (weights FSE form, table descriptions)
-  uint32_t sh[3][64];      // sequence code histograms: LL, OF, ML
   int16_t norm[64];
   uint16_t tabs[kTabDummy + 1];
   uint32_t tr[3][64];      // per symbol: deltaNbBits | deltaFindState << 20 (12-bit signed)
   uint8_t sym_at[512];
   uint16_t nxt[64];
-  uint32_t ew[4 * kWave];  // per 64 sequences: chain transforms / state bits
   uint32_t u[16];          // lane-0 results: sizes, modes, accuracy logs
   uint32_t wk[32];         // lane-0 work: weight counts, code ranges
-  alignas(16) uint8_t lst[16 * kWave];  // literal block being encoded (16-B stores)
+  union {                  // by phase
+    huf::TreeLds T;        // code lengths
+    struct {
+      uint32_t code[256];                 // code | length << 16
+      alignas(16) uint8_t lst[16 * kWave];  // literal block being encoded (16-B stores)
+    } E;
+    uint32_t sh[3][64];    // sequence code histograms: LL, OF, ML
+  };
 };
-
 // 256 * log2(x), x >= 1
 __device__ __forceinline__ uint32_t log2fix(uint32_t x) {
   const uint32_t hb = hb32(x);
   const uint32_t f = (hb >= 6 ? x >> (hb - 6) : x << (6 - hb)) & 63u;
-  return (hb << 8) + kT.log2frac[f];
+  return (hb << 8) + sT.log2frac[f];
 }
 
 // oracle zs_table_log (total >= 2, max_sym >= 1)
@@ -430,7 +434,7 @@ __device__ uint32_t choose_table(EntLds& L, uint32_t t, uint32_t nseq, SBits& w)
     st[0] = 0;
     return 1u;
   }
-  const int16_t* def = t == 0 ? kT.ll_norm : t == 1 ? kT.of_norm : kT.ml_norm;
+  const int16_t* def = t == 0 ? sT.ll_norm : t == 1 ? sT.of_norm : sT.ml_norm;
   const uint32_t def_al = t == 1 ? 5u : 6u, def_max = t == 0 ? 35u : t == 1 ? 28u : 52u;
   uint32_t cost_pre = 0;
   for (uint32_t s = 0; s <= max_sym; ++s) {
@@ -554,6 +558,9 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
   const GMEM uint8_t* src = global_ptr(input + seg_off);
   GMEM uint8_t* lits = global_ptr(scratch + (uint64_t)i_seg * sstride);
   GMEM uint2* seqs = reinterpret_cast<GMEM uint2*>(lits + lit_cap(seg));
+  for (uint32_t k = lane; k < sizeof(Tabs); k += kWave)
+    reinterpret_cast<uint8_t*>(&sT)[k] = reinterpret_cast<const uint8_t*>(&kT)[k];
+  lds_order();
   const uint2 mt = meta[i_seg];
   const uint32_t nlit = mt.x, nseq = mt.y;
   EntOut o;
@@ -573,8 +580,8 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
   const uint32_t blk = o.op;
   o.op += 3;  // block header, written last
 
-  // ---- literal histograms per stream quarter ----
-  for (uint32_t k = lane; k < 5 * 256; k += kWave) (&L.hq[0][0])[k] = 0;
+  // ---- literal histogram ----
+  for (uint32_t k = lane; k < 256; k += kWave) L.hist[k] = 0;
   lds_order();
   const uint32_t qs = (nlit + 3) / 4;
   for (uint32_t b0 = 0; b0 < nlit; b0 += 16u * kWave) {
@@ -583,22 +590,13 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     if (at < nlit) v = *reinterpret_cast<const GMEM uint4*>(lits + at);
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) {
-      const uint32_t idx = at + j;
-      if (idx < nlit) {
-        const uint32_t q = (idx >= qs ? 1u : 0u) + (idx >= 2 * qs ? 1u : 0u) + (idx >= 3 * qs ? 1u : 0u);
-        atomicAdd(&L.hq[q][(wv[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
-      }
-    }
+    for (uint32_t j = 0; j < 16; ++j)
+      if (at + j < nlit) atomicAdd(&L.hist[(wv[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
   }
   lds_order();
   uint32_t distinct = 0;
-  for (uint32_t s0 = 0; s0 < 256; s0 += kWave) {
-    const uint32_t s = s0 + lane;
-    const uint32_t t = L.hq[0][s] + L.hq[1][s] + L.hq[2][s] + L.hq[3][s];
-    L.hist[s] = t;
-    distinct += (uint32_t)__builtin_popcountll(ballot(t != 0));
-  }
+  for (uint32_t s0 = 0; s0 < 256; s0 += kWave)
+    distinct += (uint32_t)__builtin_popcountll(ballot(L.hist[s0 + lane] != 0));
   lds_order();
 
   ZSE_PHASE(1)
@@ -622,13 +620,24 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       const uint32_t l = L.len[s0 + lane];
       L.w[s0 + lane] = (uint8_t)(l ? lmax + 1 - l : 0u);
     }
-    // stream sizes from the quarter histograms
+    // stream sizes: the code lengths of each quarter's literals (a second read of them)
     ns = nlit < 256 ? 1u : 4u;
     uint32_t bq[4] = {0, 0, 0, 0};
-    for (uint32_t s0 = 0; s0 < 256; s0 += kWave) {
-      const uint32_t s = s0 + lane, l = L.len[s];
+    lds_order();
+    for (uint32_t b0 = 0; b0 < nlit; b0 += 16u * kWave) {
+      const uint32_t at = b0 + 16u * lane;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (at < nlit) v = *reinterpret_cast<const GMEM uint4*>(lits + at);
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (uint32_t q = 0; q < 4; ++q) bq[q] += L.hq[q][s] * l;
+      for (uint32_t j = 0; j < 16; ++j) {
+        const uint32_t idx = at + j;
+        const uint32_t l = idx < nlit ? (uint32_t)L.len[(wv[j >> 2] >> (8 * (j & 3))) & 0xFFu] : 0u;
+        bq[0] += idx < qs ? l : 0u;
+        bq[1] += idx >= qs && idx < 2 * qs ? l : 0u;
+        bq[2] += idx >= 2 * qs && idx < 3 * qs ? l : 0u;
+        bq[3] += idx >= 3 * qs ? l : 0u;
+      }
     }
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) bq[q] = readlane(wave_incl_sum(bq[q]), 63);
@@ -654,11 +663,11 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       for (uint32_t s = 0; s < 256; ++s) {
         const uint32_t l = L.len[s];
         if (!l) {
-          L.code[s] = 0;
+          L.E.code[s] = 0;
           continue;
         }
         const uint32_t wt = L.w[s];
-        L.code[s] = (start[wt] >> (wt - 1)) | (l << 16);
+        L.E.code[s] = (start[wt] >> (wt - 1)) | (l << 16);
         start[wt] += 1u << (wt - 1);
       }
       // tree description: direct when possible and not larger than the FSE form
@@ -715,7 +724,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       if (g0 + (int32_t)lane >= gA) blkv = l16[g0 + (int32_t)lane];
       for (;;) {
         lds_order();
-        reinterpret_cast<uint4*>(L.lst)[lane] = blkv;
+        reinterpret_cast<uint4*>(L.E.lst)[lane] = blkv;
         const int32_t g1 = g0 - (int32_t)kWave;
         if (g0 > gA && g1 + (int32_t)lane >= gA) blkv = l16[g1 + (int32_t)lane];
         const int32_t lo = max((int32_t)a, 16 * g0), hi = min((int32_t)b, 16 * (g0 + (int32_t)kWave));
@@ -723,8 +732,8 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
           const int32_t idx = e - (int32_t)kWave + (int32_t)lane;
           const bool act = idx >= lo;
           lds_order();
-          const uint32_t sym = act ? L.lst[idx - 16 * g0] : 0u;
-          const uint32_t cw = L.code[sym];
+          const uint32_t sym = act ? L.E.lst[idx - 16 * g0] : 0u;
+          const uint32_t cw = L.E.code[sym];
           o.put_bits(act ? (cw & 0xFFFFu) : 0u, act ? cw >> 16 : 0u, 0, 0, p0, bits, zeroed);
         }
         if (g0 <= gA || o.overflow) break;
@@ -843,6 +852,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     const uint32_t top = nseq - 1;
     const uint32_t cl = lane < 3 ? lane : 3u;
     const uint32_t tb = cl == 0 ? kTabOF : cl == 1 ? kTabML : cl == 2 ? kTabLL : kTabDummy;
+    const uint32_t m_of = cl == 0 ? ~0u : 0u, m_ml = cl == 1 ? ~0u : 0u, m_ll = cl == 2 ? ~0u : 0u;
     uint2 prec = seqs[(top >> 6) * kWave + lane < nseq ? (top >> 6) * kWave + lane : top];
     for (int32_t c = (int32_t)(top >> 6); c >= 0 && !o.overflow; --c) {
       const uint32_t j = (uint32_t)c * kWave + lane;
@@ -855,10 +865,12 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       const uint32_t eOF = L.tr[1][ofc], eML = L.tr[2][mlc], eLL = L.tr[0][llc];
       // the chain lane's transform of sequence k: readlanes (no LDS round trip on the
       // state chain, whose only memory access is the state table)
-      auto tr_of = [&](uint32_t k) __attribute__((always_inline)) {
-        const uint32_t a = readlane(eOF, k), b = readlane(eML, k), d = readlane(eLL, k);
-        return cl == 0 ? a : cl == 1 ? b : cl == 2 ? d : 0u;
+      auto tr_of = [&](uint32_t k) __attribute__((always_inline)) {  // (no branches)
+        return (readlane(eOF, k) & m_of) | (readlane(eML, k) & m_ml) | (readlane(eLL, k) & m_ll);
       };
+      // per sequence lane: each chain's state bits | their count << 24 (written by
+      // writelane: no LDS store on the chain)
+      uint32_t w0 = 0, w1 = 0, w2 = 0;
       int32_t k = 63;
       if (c == (int32_t)(top >> 6)) {  // the last sequence initialises the three states
         k = (int32_t)(top & 63u);
@@ -866,33 +878,39 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
         const uint32_t d = tr_d(e);
         const uint32_t nbo = (d + (1u << 15)) >> 16;
         const uint32_t val = (nbo << 16) - d;
-        st = L.tabs[tb + (uint32_t)((int32_t)(val >> nbo) + tr_f(e))];
         lds_order();
-        L.ew[4 * (uint32_t)k + cl] = 0u;  // no state bits
+        st = L.tabs[tb + (uint32_t)((int32_t)(val >> nbo) + tr_f(e))];  // no state bits
         --k;
       }
+#ifdef BITAR_ZSTD_NOWALK
+      k = -1;
+#endif
       for (; k >= 0; --k) {
         const uint32_t e = tr_of((uint32_t)k);
         const uint32_t nb = (st + tr_d(e)) >> 16;
-        const uint32_t out = st & ((1u << nb) - 1u);
+        const uint32_t out = (st & ((1u << nb) - 1u)) | (nb << 24);
         lds_order();
         st = L.tabs[tb + (uint32_t)((int32_t)(st >> nb) + tr_f(e))];
-        L.ew[4 * (uint32_t)k + cl] = out | (nb << 24);
+        w0 = writelane(w0, readlane(out, 0), (uint32_t)k);
+        w1 = writelane(w1, readlane(out, 1), (uint32_t)k);
+        w2 = writelane(w2, readlane(out, 2), (uint32_t)k);
       }
-      lds_order();
-      const uint32_t w0 = L.ew[4 * lane + 0], w1 = L.ew[4 * lane + 1], w2 = L.ew[4 * lane + 2];
       const uint32_t nof = w0 >> 24, nml = w1 >> 24, nll = w2 >> 24;
       const uint64_t stb = (uint64_t)(w0 & 0xFFFFFFu) | ((uint64_t)(w1 & 0xFFFFFFu) << nof) |
                            ((uint64_t)(w2 & 0xFFFFFFu) << (nof + nml));
       const uint32_t stn = nof + nml + nll;
-      const uint32_t llb = kT.ll_bits[llc], mlbits = kT.ml_bits[mlc];
+      const uint32_t llb = sT.ll_bits[llc], mlbits = sT.ml_bits[mlc];
       // part 0: state bits + literal-length extra (<= 26 + 16); part 1: match-length extra,
       // then offset extra (<= 16 + 16)
       const uint64_t f0 = stb | ((uint64_t)(ll & ((1u << llb) - 1u)) << stn);
       const uint64_t f1 = (uint64_t)(mlb & ((1u << mlbits) - 1u)) |
                           ((uint64_t)(ov & ((1u << ofc) - 1u)) << mlbits);
+#ifndef BITAR_ZSTD_NOPUT
       o.put_bits(act ? f0 : 0u, act ? stn + llb : 0u, act ? f1 : 0u, act ? mlbits + ofc : 0u,
                  p0, bits, zeroed);
+#else
+      if (lane == 0) L.u[8] += (uint32_t)f0 + (uint32_t)f1;
+#endif
     }
     if (!o.overflow) {
       // final states (ML, OF, LL: the decoder reads LL first) and the end mark

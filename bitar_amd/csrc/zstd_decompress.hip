@@ -664,6 +664,13 @@ __device__ __forceinline__ void exec_chunk(State& s, uint8_t* win, uint8_t* ring
   s.op += co;
 }
 
+// Hand-off to the lane-per-segment sequence executor (zstd_lanes.hip zstd_handoff_kernel):
+// per segment kHandStride bytes of scratch = a record of kHandRec words, then the LL, OF and
+// ML decode cells (kHandCells words each, the LDS cell format sym | nbits << 8 | base << 16)
+constexpr uint32_t kHandRec = 16, kHandCells = 512, kHandMinSeq = 16;
+constexpr uint64_t kHandStride = 4ull * (kHandRec + 3 * kHandCells);
+constexpr uint32_t kHanded = 0xFFFFFFFDu;  // produced[i] while the executor owns segment i
+
 struct Frame {
   uint32_t rep0, rep1, rep2;
   uint32_t al[3];      // accuracy logs of the LL / OF / ML tables
@@ -673,8 +680,11 @@ struct Frame {
 };
 
 // one compressed block at stream [p, p + len)
-__device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr, uint32_t p,
-                      uint32_t len) {
+// 0: malformed, 1: decoded, 2: handed off (the sequences of the frame's last block go to the
+// lane executor: hand != null, last block, no checksum, >= kHandMinSeq sequences)
+__device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr, uint32_t p,
+                      uint32_t len, GMEM uint32_t* hand, bool last_block, uint32_t fsz,
+                      uint32_t fcs) {
   const uint32_t lane = lane_id();
   p = uniform(p);
   len = uniform(len);
@@ -686,65 +696,65 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
   uint32_t regen, csz = 0, hsz, nstreams = 1;
   if (lt < 2) {
     if (sf == 0 || sf == 2) { regen = b0 >> 3; hsz = 1; }
-    else if (sf == 1) { if (len < 2) return false; regen = load_le(s, win, p, 2) >> 4; hsz = 2; }
-    else { if (len < 3) return false; regen = load_le(s, win, p, 3) >> 4; hsz = 3; }
+    else if (sf == 1) { if (len < 2) return 0; regen = load_le(s, win, p, 2) >> 4; hsz = 2; }
+    else { if (len < 3) return 0; regen = load_le(s, win, p, 3) >> 4; hsz = 3; }
   } else {
     if (sf <= 1) {
-      if (len < 3) return false;
+      if (len < 3) return 0;
       const uint32_t c = load_le(s, win, p, 3);
       regen = (c >> 4) & 0x3FFu; csz = (c >> 14) & 0x3FFu; hsz = 3; nstreams = sf == 0 ? 1 : 4;
     } else if (sf == 2) {
-      if (len < 4) return false;
+      if (len < 4) return 0;
       const uint32_t c = load_le(s, win, p, 4);
       regen = (c >> 4) & 0x3FFFu; csz = (c >> 18) & 0x3FFFu; hsz = 4; nstreams = 4;
     } else {
-      if (len < 5) return false;
+      if (len < 5) return 0;
       const uint64_t c = (uint64_t)load_le(s, win, p, 4) | ((uint64_t)load_le(s, win, p + 4, 1) << 32);
       regen = (uint32_t)(c >> 4) & 0x3FFFFu; csz = (uint32_t)(c >> 22) & 0x3FFFFu; hsz = 5; nstreams = 4;
     }
   }
-  if (regen > (128u << 10) || regen > s.cap - s.op) return false;
+  if (regen > (128u << 10) || regen > s.cap - s.op) return 0;
   uint32_t q = p + hsz;
   // where the literals come from: the stream (raw), one byte (RLE), or the slot tail
   uint32_t lit_stream = 0, lit_byte = 0;
   GMEM uint8_t* lit_tail = s.dst + (s.cap - regen);
   if (lt == 0) {
-    if (q + regen > end) return false;
+    if (q + regen > end) return 0;
     lit_stream = q;
     q += regen;
   } else if (lt == 1) {
-    if (q + 1 > end) return false;
+    if (q + 1 > end) return 0;
     lit_byte = load_le(s, win, q, 1);
     q += 1;
   } else {
-    if (q + csz > end) return false;
+    if (q + csz > end) return 0;
     uint32_t cs = q, cl = csz;
     if (lt == 2) {
       uint32_t log;
       const int n = huf_read(s, win, t, cs, cl, log);
-      if (n < 0) return false;
+      if (n < 0) return 0;
       fr.huf_log = log;
       cs += (uint32_t)n;
       cl -= (uint32_t)n;
     } else if (!fr.huf_log) {
-      return false;
+      return 0;
     }
     if (nstreams == 1) {
-      if (!huf_stream_fast(s, win, t, fr.huf_log, cs, cl, lit_tail, regen)) return false;
+      if (!huf_stream_fast(s, win, t, fr.huf_log, cs, cl, lit_tail, regen)) return 0;
     } else {
-      if (cl < 6) return false;
+      if (cl < 6) return 0;
       const uint32_t j = load_le(s, win, cs, 4);
       const uint32_t s1 = j & 0xFFFFu, s2 = j >> 16, s3 = load_le(s, win, cs + 4, 2);
-      if (6ull + s1 + s2 + s3 > cl) return false;
+      if (6ull + s1 + s2 + s3 > cl) return 0;
       const uint32_t s4 = cl - 6 - s1 - s2 - s3;
       const uint32_t qq = (regen + 3) / 4;
-      if (3 * qq > regen) return false;
+      if (3 * qq > regen) return 0;
       const uint32_t st = cs + 6;
-      if (!huf_stream_fast(s, win, t, fr.huf_log, st, s1, lit_tail, qq)) return false;
-      if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1, s2, lit_tail + qq, qq)) return false;
-      if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1 + s2, s3, lit_tail + 2 * qq, qq)) return false;
+      if (!huf_stream_fast(s, win, t, fr.huf_log, st, s1, lit_tail, qq)) return 0;
+      if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1, s2, lit_tail + qq, qq)) return 0;
+      if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1 + s2, s3, lit_tail + 2 * qq, qq)) return 0;
       if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1 + s2 + s3, s4, lit_tail + 3 * qq,
-                      regen - 3 * qq)) return false;
+                      regen - 3 * qq)) return 0;
     }
     global_fence_wave();  // the executor reads back what the streams wrote
     q += csz;
@@ -763,26 +773,26 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
     lp += n;
   };
   // ---- sequences section ----
-  if (q >= end) return false;
+  if (q >= end) return 0;
   uint32_t nseq = load_le(s, win, q, 1);
   if (nseq < 128) {
     q += 1;
   } else if (nseq < 255) {
-    if (q + 2 > end) return false;
+    if (q + 2 > end) return 0;
     nseq = ((nseq - 128) << 8) + load_le(s, win, q + 1, 1);
     q += 2;
   } else {
-    if (q + 3 > end) return false;
+    if (q + 3 > end) return 0;
     nseq = load_le(s, win, q + 1, 2) + 0x7F00u;
     q += 3;
   }
   ZP_END(2, th);
   if (nseq) {
-    if (q >= end) return false;
+    if (q >= end) return 0;
     ZP_BEGIN(tm);
     const uint32_t modes = load_le(s, win, q, 1);
     q += 1;
-    if (modes & 3u) return false;
+    if (modes & 3u) return 0;
     // tables in order LL, OF, ML (unrolled: fr.al / fr.have stay in registers)
 #pragma unroll
     for (uint32_t k = 0; k < 3; ++k) {
@@ -798,14 +808,14 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
           if (lane <= dmax)
             t.norm[lane] = k == 0 ? kLLDefault[lane] : k == 1 ? kOFDefault[lane] : kMLDefault[lane];
           lds_order();
-          if (!fse_build(t, cells, dmax, dal)) return false;
+          if (!fse_build(t, cells, dmax, dal)) return 0;
           fr.pre[k] = true;
         }
         fr.al[k] = dal;
       } else if (mode == 1) {
-        if (q >= end) return false;
+        if (q >= end) return 0;
         const uint32_t sy = load_le(s, win, q, 1);
-        if (sy > maxs) return false;
+        if (sy > maxs) return 0;
         fse_rle(cells, sy);
         fr.pre[k] = false;
         fr.al[k] = 0;
@@ -813,18 +823,36 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
       } else if (mode == 2) {
         uint32_t ms = maxs, al;
         const int n = read_ncount(s, win, t, q, end - q, ms, al, maxal);
-        if (n < 0) return false;
+        if (n < 0) return 0;
         fr.pre[k] = false;
-        if (!fse_build(t, cells, ms, al)) return false;
+        if (!fse_build(t, cells, ms, al)) return 0;
         fr.al[k] = al;
         q += (uint32_t)n;
       } else if (!fr.have[k]) {
-        return false;
+        return 0;
       }
       fr.have[k] = true;
     }
-    if (q >= end) return false;
+    if (q >= end) return 0;
     ZP_END(3, tm);
+    if (hand && last_block && nseq >= kHandMinSeq) {
+      // everything before this block is output; the executor continues from s.op
+      flush(s, ring, s.op, true);
+      global_fence_wave();
+#pragma unroll
+      for (uint32_t k = 0; k < 3; ++k) {
+        const uint32_t nc = 1u << fr.al[k];
+        lds_order();
+        for (uint32_t u = lane; u < nc; u += kWave) hand[kHandRec + k * kHandCells + u] = t.fse[k][u];
+      }
+      const uint32_t rv = lane == 0 ? q : lane == 1 ? end : lane == 2 ? nseq
+                          : lane == 3 ? fr.al[0] | (fr.al[1] << 8) | (fr.al[2] << 16) | (lt << 24)
+                          : lane == 4 ? (lt == 0 ? lit_stream : lit_byte)
+                          : lane == 5 ? regen : lane == 6 ? s.op : lane == 7 ? fr.rep0
+                          : lane == 8 ? fr.rep1 : lane == 9 ? fr.rep2 : lane == 10 ? fsz : fcs;
+      if (lane < 12) hand[lane] = rv;
+      return 2;
+    }
     // FSE tables of <= 64 cells (every predefined one) move into registers: lane u holds cell
     // u and a state lookup is one v_readlane instead of an LDS round trip
     const bool rt = fr.al[0] <= 6 && fr.al[1] <= 6 && fr.al[2] <= 6;
@@ -878,7 +906,7 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
         info[k] = bv | (((c >> 8) & 7u) << 22) | (((c >> 16) & 63u) << 25);
       }
       FastBits fb;
-      if (!fb.init(s, q, end)) return false;
+      if (!fb.init(s, q, end)) return 0;
       uint32_t sll = fb.read(fr.al[0]), sof = fb.read(fr.al[1]), sml = fb.read(fr.al[2]);
       for (uint32_t k = 0; k < nseq; ++k) {
         fb.reload(s, q);
@@ -910,13 +938,13 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
             fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
           } else {
             off = fr.rep0 - 1;
-            if (off == 0) return false;
+            if (off == 0) return 0;
             fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
           }
         }
         const uint32_t opv = s.op + co;
-        if (lp + ll > regen || (uint64_t)opv + ml + (regen - lp) > s.cap) return false;
-        if (off == 0 || off > opv + ll) return false;
+        if (lp + ll > regen || (uint64_t)opv + ml + (regen - lp) > s.cap) return 0;
+        if (off == 0 || off > opv + ll) return 0;
         const uint32_t ol = ll + ml;
         if (ol <= kWave && off <= kNearOff) {
           if (co + ol > kWave) exec();
@@ -943,7 +971,7 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
     // three cells come from LDS (issued together), baselines from the llt / mlt registers
     auto fast_lds = [&]() __attribute__((always_inline)) -> bool {
       FastBits fb;
-      if (!fb.init(s, q, end)) return false;
+      if (!fb.init(s, q, end)) return 0;
       uint32_t sll = fb.read(fr.al[0]), sof = fb.read(fr.al[1]), sml = fb.read(fr.al[2]);
       for (uint32_t k = 0; k < nseq; ++k) {
         fb.reload(s, q);
@@ -978,13 +1006,13 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
             fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
           } else {
             off = fr.rep0 - 1;
-            if (off == 0) return false;
+            if (off == 0) return 0;
             fr.rep2 = fr.rep1; fr.rep1 = fr.rep0; fr.rep0 = off;
           }
         }
         const uint32_t opv = s.op + co;
-        if (lp + ll > regen || (uint64_t)opv + ml + (regen - lp) > s.cap) return false;
-        if (off == 0 || off > opv + ll) return false;
+        if (lp + ll > regen || (uint64_t)opv + ml + (regen - lp) > s.cap) return 0;
+        if (off == 0 || off > opv + ll) return 0;
         const uint32_t ol = ll + ml;
         if (ol <= kWave && off <= kNearOff) {
           if (co + ol > kWave) exec();
@@ -1006,14 +1034,14 @@ __device__ __forceinline__ bool block(State& s, uint8_t* win, uint8_t* ring, Tab
     };
     ZP_BEGIN(tq);
     ZP_ADD(11, nseq);
-    if (!(rt ? fast() : fast_lds())) return false;
+    if (!(rt ? fast() : fast_lds())) return 0;
     ZP_END(4, tq);
   } else if (q != end) {
-    return false;
+    return 0;
   }
-  if ((uint64_t)s.op + (regen - lp) > s.cap) return false;
+  if ((uint64_t)s.op + (regen - lp) > s.cap) return 0;
   copy_lits(regen - lp);
-  return true;
+  return 1;
 }
 
 // XXH64 of the first n output bytes (already flushed to HBM and fenced), low 32 bits
@@ -1087,7 +1115,7 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
-    uint32_t defer_only) {
+    uint32_t defer_only, uint8_t* __restrict__ hscr) {
   using namespace zsd;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
   __shared__ __attribute__((aligned(16))) Tabs t;
@@ -1143,7 +1171,9 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     fr.have[0] = fr.have[1] = fr.have[2] = false;
     fr.pre[0] = fr.pre[1] = fr.pre[2] = false;
     fr.huf_log = 0;
-    bool bad = false, last = false;
+    bool bad = false, last = false, handed = false;
+    GMEM uint32_t* hand = hscr && !cks ? global_ptr(reinterpret_cast<uint32_t*>(hscr + (uint64_t)i * kHandStride))
+                                       : nullptr;
     while (!last) {
       if (p + 3 > cs) { bad = true; break; }
       const uint32_t bh = load_le(s, win, p, 3);
@@ -1166,7 +1196,9 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
       } else if (type == 2) {
         if (bsz > (128u << 10) || p + bsz > cs) { bad = true; break; }
         ZP_BEGIN(tb);
-        if (!block(s, win, ring, t, fr, p, bsz)) { bad = true; break; }
+        const int r = block(s, win, ring, t, fr, p, bsz, hand, last, fsz, (uint32_t)fcs);
+        if (r == 0) { bad = true; break; }
+        if (r == 2) { handed = true; break; }
         ZP_END(1, tb);
         ZP_ADD(13, 1);
         p += bsz;
@@ -1176,6 +1208,10 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
       }
     }
     if (bad) break;
+    if (handed) {  // the executor finishes the frame (and its final checks)
+      if (lane_id() == 0) produced[i] = kHanded;
+      return;
+    }
     flush(s, ring, s.op, true);
     if (cks) {
       if (p + 4 > cs) break;

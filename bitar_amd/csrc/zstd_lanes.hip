@@ -374,6 +374,146 @@ __global__ __launch_bounds__(64) void zstd_lanes_kernel(
   }
 }
 
+// ---- the lane executor of handed-off sequence sections ---------------------------------------
+// zstd_decompress_kernel decodes a frame up to the sequence section of its last block (the
+// literals -- Huffman-coded ones into the tail of the output slot --, the three decode
+// tables, the repeat offsets) and hands the rest over (zstd_decompress.hip kHand*): here
+// every lane runs one segment's sequence loop, its decode cells read from the scratch
+// (L2-resident, 6 KiB per segment), with the wave kernel's acceptance checks, then the final
+// frame checks.  kHand* mirror zstd_decompress.hip.
+namespace zsh {
+constexpr uint32_t kHandRec = 16, kHandCells = 512;
+constexpr uint64_t kHandStride = 4ull * (kHandRec + 3 * kHandCells);
+constexpr uint32_t kHanded = 0xFFFFFFFDu;
+}  // namespace zsh
+
+template <uint32_t L>
+__global__ __launch_bounds__(64) void zstd_handoff_kernel(
+    const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
+    uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
+    uint8_t* __restrict__ out, uint32_t* __restrict__ produced,
+    const uint8_t* __restrict__ hscr, uint32_t* __restrict__ err) {
+  using namespace zsl;
+  using namespace zsh;
+  // baseline | extra-bit count << 24 of every literal-length / match-length code
+  __shared__ uint32_t llt[64], mlt[64];
+  const uint32_t lane = lane_id();
+  llt[lane] = lane < 36 ? kLLBase[lane] | ((uint32_t)kLLBits[lane] << 24) : 0u;
+  mlt[lane] = lane < 53 ? kMLBase[lane] | ((uint32_t)kMLBits[lane] << 24) : 0u;
+  lds_order();
+  const uint32_t i = blockIdx.x * L + lane;
+  if (lane >= L || i >= nseg || produced[i] != kHanded) return;
+  const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kHandStride));
+  const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
+  GMEM uint8_t* dst = global_ptr(out + (uint64_t)i * seg);
+  const uint32_t cs = csizes[i];
+  const uint32_t q = h[0], end = h[1], nseq = h[2], w3 = h[3], litv = h[4], regen = h[5];
+  uint32_t op = h[6];
+  uint32_t r0 = h[7], r1 = h[8], r2 = h[9];
+  const uint32_t fsz = h[10], fcs = h[11];
+  const uint32_t al0 = w3 & 0xFFu, al1 = (w3 >> 8) & 0xFFu, al2 = (w3 >> 16) & 0xFFu,
+                 lt = w3 >> 24;
+  const GMEM uint32_t* tll = h + kHandRec;
+  const GMEM uint32_t* tof = tll + kHandCells;
+  const GMEM uint32_t* tml = tof + kHandCells;
+  const uint32_t cap = seg;
+  const uint32_t capw = fsz ? fcs : cap;  // wildcopies stay inside the content size
+  // Huffman literals sit at the slot tail [cap - regen, cap): writes stay below the unread
+  // part of it
+  const GMEM uint8_t* tail = dst + (cap - regen);
+  uint32_t lp = 0;
+  auto limit = [&]() __attribute__((always_inline)) { return lt == 2 ? cap - (regen - lp) : capw; };
+  auto lits = [&](uint32_t n) __attribute__((always_inline)) {
+    if (n == 0) return;
+    if (lt == 0) {
+      copy_lits(dst + op, src + litv + lp, n, op + n + 16 <= capw && litv + lp + n + 16 <= cs);
+    } else if (lt == 1) {
+      const uint64_t w = 0x0101010101010101ull * (litv & 0xFFu);
+      if (op + n + 8 <= capw) {
+        for (uint32_t j = 0; j < n; j += 8) st8(dst + op + j, w);
+      } else {
+        for (uint32_t j = 0; j < n; ++j) dst[op + j] = (uint8_t)litv;
+      }
+    } else {
+      copy_lits(dst + op, tail + lp, n, op + n + 16 <= cap - (regen - lp) && lp + n + 16 <= regen);
+    }
+  };
+  bool ok = true;
+  Bits b;
+  b.ptr = (int32_t)end - 8;
+  b.load(src, q);
+  const uint32_t lastb = (uint32_t)(b.C >> 56);
+  if (lastb == 0) ok = false;
+  if (ok) {
+    b.used = 8 - (31u - (uint32_t)__builtin_clz(lastb));
+    uint32_t sll = b.read(al0), sof = b.read(al1), sml = b.read(al2);
+    for (uint32_t k = 0; k < nseq; ++k) {
+      b.reload(src, q);
+      const uint32_t cll = tll[sll], cof = tof[sof], cml = tml[sml];
+      const uint32_t ofc = cof & 0xFFu;
+      const uint32_t ofv = (1u << ofc) + b.read(ofc);
+      const uint32_t mle = mlt[cml & 63u];
+      const uint32_t ml = (mle & 0xFFFFFFu) + b.read(mle >> 24);
+      if (b.used > 20) b.reload(src, q);  // <= 16 extra + 26 state bits follow
+      const uint32_t lle = llt[cll & 63u];
+      const uint32_t ll = (lle & 0xFFFFFFu) + b.read(lle >> 24);
+      if (k + 1 < nseq) {
+        sll = (cll >> 16) + b.read((cll >> 8) & 0xFFu);
+        sml = (cml >> 16) + b.read((cml >> 8) & 0xFFu);
+        sof = (cof >> 16) + b.read((cof >> 8) & 0xFFu);
+      }
+      // repeat offsets in select form (no exec-mask branches)
+      const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
+      const uint32_t off = ofv > 3 ? ofv - 3 : idx == 1 ? r0 : idx == 2 ? r1 : idx == 3 ? r2 : r0 - 1;
+      const bool shift2 = ofv > 3 || idx >= 3, shift1 = ofv > 3 || idx >= 2;
+      const uint32_t c0 = r0, c1 = r1, c2 = r2;
+      r2 = shift2 ? c1 : c2;
+      r1 = shift1 ? c0 : c1;
+      r0 = off;
+      if (lp + ll > regen || (uint64_t)op + ml + (regen - lp) > cap || off == 0 ||
+          off > op + ll) {
+        ok = false;
+        break;
+      }
+      lits(ll);
+      op += ll;
+      lp += ll;
+      copy_match(dst + op, off, ml, op + ml + 32 <= limit());
+      op += ml;
+    }
+    if (ok && b.remaining(q) != 0) ok = false;
+  }
+  if (ok && (uint64_t)op + (regen - lp) > cap) ok = false;
+  if (ok) {
+    const uint32_t n = regen - lp;
+    if (lt == 2) {  // the tail literals may overlap their destination: forward, 8 B only
+                    // where the gap allows
+      const uint32_t gap = (cap - (regen - lp)) - op;
+      if (gap >= 8) {
+        uint32_t j = 0;
+        for (; j + 8 <= n; j += 8) st8(dst + op + j, ld8(tail + lp + j));
+        for (; j < n; ++j) dst[op + j] = tail[lp + j];
+      } else {
+        for (uint32_t j = 0; j < n; ++j) dst[op + j] = tail[lp + j];
+      }
+    } else {
+      lits(n);
+    }
+    op += n;
+    ok = end == cs && (!fsz || fcs == op);
+  }
+  if (ok) {
+    produced[i] = op;
+  } else {
+    produced[i] = 0xFFFFFFFFu;
+    atomicOr(err, 1u);
+  }
+}
+
+template __global__ void zstd_handoff_kernel<16>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                                 const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                                 uint32_t*, const uint8_t*, uint32_t*);
+
 template __global__ void zstd_lanes_kernel<64>(const uint8_t* const*, const uint8_t*, uint64_t,
                                                const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                                uint32_t*);
