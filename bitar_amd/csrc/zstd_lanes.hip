@@ -439,17 +439,48 @@ __global__ __launch_bounds__(64) void zstd_handoff_kernel(
     }
   };
   bool ok = true;
-  Bits b;
+  // backward bit reader with the 8 bytes below its window loaded one reload ahead (the
+  // reload is a shift, its load's latency hides behind a sequence)
+  struct PBits {
+    uint64_t C, N;
+    uint32_t used;
+    int32_t ptr;
+    __device__ __forceinline__ static uint64_t at(const GMEM uint8_t* s, int32_t a, uint32_t q) {
+      const int32_t lo = (int32_t)q - 8;
+      const uint64_t v = ld8(s + (a < lo ? lo : a));
+      const int32_t below = (int32_t)q - a;
+      return below <= 0 ? v : below >= 8 ? 0ull : v & (~0ull << (8 * (uint32_t)below));
+    }
+    __device__ __forceinline__ void reload(const GMEM uint8_t* s, uint32_t q) {
+      const uint32_t sb = used >> 3;
+      if (sb) {
+        C = sb == 8 ? N : (C << (8 * sb)) | (N >> (64 - 8 * sb));
+        used &= 7u;
+        ptr -= (int32_t)sb;
+        N = at(s, ptr - 8, q);
+      }
+    }
+    __device__ __forceinline__ uint32_t read(uint32_t n) {
+      const uint32_t sh = (64 - used - n) & 63u;
+      const uint32_t v = (uint32_t)(C >> sh) & ((1u << n) - 1u);
+      used += n;
+      return v;
+    }
+    __device__ __forceinline__ int32_t remaining(uint32_t q) const {
+      return 8 * (ptr - (int32_t)q) + 64 - (int32_t)used;
+    }
+  } b;
   b.ptr = (int32_t)end - 8;
-  b.load(src, q);
+  b.C = PBits::at(src, b.ptr, q);
+  b.N = PBits::at(src, b.ptr - 8, q);
   const uint32_t lastb = (uint32_t)(b.C >> 56);
   if (lastb == 0) ok = false;
   if (ok) {
     b.used = 8 - (31u - (uint32_t)__builtin_clz(lastb));
     uint32_t sll = b.read(al0), sof = b.read(al1), sml = b.read(al2);
+    uint32_t cll = tll[sll], cof = tof[sof], cml = tml[sml];
     for (uint32_t k = 0; k < nseq; ++k) {
       b.reload(src, q);
-      const uint32_t cll = tll[sll], cof = tof[sof], cml = tml[sml];
       const uint32_t ofc = cof & 0xFFu;
       const uint32_t ofv = (1u << ofc) + b.read(ofc);
       const uint32_t mle = mlt[cml & 63u];
@@ -457,10 +488,13 @@ __global__ __launch_bounds__(64) void zstd_handoff_kernel(
       if (b.used > 20) b.reload(src, q);  // <= 16 extra + 26 state bits follow
       const uint32_t lle = llt[cll & 63u];
       const uint32_t ll = (lle & 0xFFFFFFu) + b.read(lle >> 24);
-      if (k + 1 < nseq) {
+      if (k + 1 < nseq) {  // the next cells load while this sequence is copied
         sll = (cll >> 16) + b.read((cll >> 8) & 0xFFu);
         sml = (cml >> 16) + b.read((cml >> 8) & 0xFFu);
         sof = (cof >> 16) + b.read((cof >> 8) & 0xFFu);
+        cll = tll[sll];
+        cof = tof[sof];
+        cml = tml[sml];
       }
       // repeat offsets in select form (no exec-mask branches)
       const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
