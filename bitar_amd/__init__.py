@@ -74,6 +74,7 @@ def lib():
         "bitar_hip_fill_at": (i32, [vp, vp, i32, u64, u64, vp, u64]),
         "bitar_hip_checksum": (i32, [vp, vp, u32, vp, u64, u32, vp, u32, vp]),
         "bitar_hip_copy_batch": (i32, [vp, vp, vp, vp, vp, u32]),
+        "bitar_hip_lz4_chain": (i32, [vp, vp, vp, u32, vp, u32, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -91,7 +92,8 @@ ABI_SYMBOLS = ("bitar_hip_abi_version", "bitar_hip_last_error", "bitar_hip_devic
                "bitar_hip_compress", "bitar_hip_compress_scattered", "bitar_hip_pointer_info",
                "bitar_hip_decompress", "bitar_hip_decompress_slab",
                "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_pack_lz4f", "bitar_hip_fill",
-               "bitar_hip_fill_at", "bitar_hip_checksum", "bitar_hip_copy_batch")
+               "bitar_hip_fill_at", "bitar_hip_checksum", "bitar_hip_copy_batch",
+               "bitar_hip_lz4_chain")
 
 
 def check(rc):

@@ -60,6 +60,17 @@ struct Piece {
   bool raw;
 };
 
+// one frame of a stock stream (the unit the stock writers emit per buffer)
+struct Frame {
+  uint64_t offset = 0, csize = 0;  // the whole frame
+  uint64_t content = 0;            // declared content size (has_content)
+  bool has_content = false;
+  bool linked = false;             // LZ4: blocks depend on the previous ones
+  bool content_checksum = false;   // LZ4: XXH32 of the content follows the EndMark
+  uint32_t checksum = 0;
+  std::vector<Piece> blocks;       // LZ4 data blocks
+};
+
 class HipCodec : public arrow::util::Codec {
  public:
   HipCodec(arrow::Compression::type type, int device, bitar_hip_ctx* ctx)
@@ -118,8 +129,14 @@ class HipCodec : public arrow::util::Codec {
     BITAR_ABI(bitar_hip_sync(ctx_, nullptr), "segment codec");
     return arrow::Status::OK();
   }
-  arrow::Result<std::vector<Piece>> WalkZstd(const uint8_t* p, uint64_t n) const;
-  arrow::Result<std::vector<Piece>> WalkLz4f(const uint8_t* p, uint64_t n) const;
+  arrow::Result<std::vector<Frame>> WalkZstd(const uint8_t* p, uint64_t n) const;
+  arrow::Result<std::vector<Frame>> WalkLz4f(const uint8_t* p, uint64_t n) const;
+  arrow::Result<int64_t> DecompressZstd(const std::vector<Frame>& frames, const uint8_t* d_in,
+                                        int64_t output_buffer_len, uint8_t* output);
+  arrow::Result<int64_t> DecompressLz4f(const std::vector<Frame>& frames, const uint8_t* d_in,
+                                        uint64_t n, int64_t output_buffer_len, uint8_t* output);
+  // the frame's independent 64 KiB blocks, in parallel, to dout; returns the content size
+  arrow::Result<uint64_t> Lz4Independent(const Frame& f, const uint8_t* d_in, uint8_t* dout);
 
   arrow::Compression::type type_;
   int device_;
@@ -208,12 +225,14 @@ arrow::Result<int64_t> HipCodec::Compress(int64_t input_len, const uint8_t* inpu
   return static_cast<int64_t>(total);
 }
 
-// Zstandard frames: each must state its content size (== kSeg except the last, <= kSeg)
-arrow::Result<std::vector<Piece>> HipCodec::WalkZstd(const uint8_t* p, uint64_t n) const {
-  std::vector<Piece> v;
+// Zstandard frames (any content size; a frame without one only as the stream's single
+// frame, sized by the caller's output buffer)
+arrow::Result<std::vector<Frame>> HipCodec::WalkZstd(const uint8_t* p, uint64_t n) const {
+  std::vector<Frame> v;
   uint64_t pos = 0;
   while (pos < n) {
-    const uint64_t start = pos;
+    Frame f;
+    f.offset = pos;
     if (n - pos < 6 || Rd32(p + pos) != kZstdMagic)
       return arrow::Status::NotImplemented("not a Zstandard frame at offset ", pos);
     pos += 4;
@@ -224,11 +243,10 @@ arrow::Result<std::vector<Piece>> HipCodec::WalkZstd(const uint8_t* p, uint64_t 
     if (!single) pos += 1;
     const uint32_t fsz = fcs_flag == 0 ? (single ? 1u : 0u) : fcs_flag == 1 ? 2u
                          : fcs_flag == 2 ? 4u : 8u;
-    if (fsz == 0) return arrow::Status::NotImplemented("Zstandard frame without content size");
     if (pos + fsz > n) return arrow::Status::Invalid("truncated Zstandard frame header");
-    uint64_t fcs = 0;
-    for (uint32_t k = 0; k < fsz; ++k) fcs |= uint64_t(p[pos + k]) << (8 * k);
-    if (fsz == 2) fcs += 256;
+    for (uint32_t k = 0; k < fsz; ++k) f.content |= uint64_t(p[pos + k]) << (8 * k);
+    if (fsz == 2) f.content += 256;
+    f.has_content = fsz != 0;
     pos += fsz;
     for (bool last = false; !last;) {
       if (pos + 3 > n) return arrow::Status::Invalid("truncated Zstandard block header");
@@ -240,33 +258,38 @@ arrow::Result<std::vector<Piece>> HipCodec::WalkZstd(const uint8_t* p, uint64_t 
     }
     if ((fhd >> 2) & 1u) pos += 4;  // content checksum (verified on the device)
     if (pos > n) return arrow::Status::Invalid("truncated Zstandard frame");
-    if (fcs > kSeg) return arrow::Status::NotImplemented("Zstandard frame larger than 64 KiB");
-    v.push_back({start, static_cast<uint32_t>(pos - start), static_cast<uint32_t>(fcs), false});
+    f.csize = pos - f.offset;
+    v.push_back(f);
   }
-  for (size_t i = 0; i + 1 < v.size(); ++i)
-    if (v[i].content != kSeg)
-      return arrow::Status::NotImplemented("Zstandard frames of other than 64 KiB content");
   return v;
 }
 
-// LZ4 frames: version 01, independent blocks of <= 64 KiB, no block / content checksums
-arrow::Result<std::vector<Piece>> HipCodec::WalkLz4f(const uint8_t* p, uint64_t n) const {
-  std::vector<Piece> v;
+// LZ4 frames: version 01, blocks of <= 64 KiB (independent or linked), optional block
+// checksums, content size and content checksum (both checksums verified here: XXH32)
+arrow::Result<std::vector<Frame>> HipCodec::WalkLz4f(const uint8_t* p, uint64_t n) const {
+  std::vector<Frame> v;
   uint64_t pos = 0;
   while (pos < n) {
+    Frame f;
+    f.offset = pos;
     if (n - pos < 7 || Rd32(p + pos) != kLz4fMagic)
       return arrow::Status::NotImplemented("not an LZ4 frame at offset ", pos);
     const uint32_t flg = p[pos + 4], bd = p[pos + 5];
     if ((flg >> 6) != 1) return arrow::Status::Invalid("LZ4 frame version");
-    if (!((flg >> 5) & 1)) return arrow::Status::NotImplemented("LZ4 frame with linked blocks");
-    if ((flg >> 4) & 1) return arrow::Status::NotImplemented("LZ4 block checksums");
-    if ((flg >> 2) & 1) return arrow::Status::NotImplemented("LZ4 content checksum");
+    f.linked = !((flg >> 5) & 1);
+    const bool block_cks = (flg >> 4) & 1;
+    f.content_checksum = (flg >> 2) & 1;
     if (flg & 1) return arrow::Status::NotImplemented("LZ4 dictionary id");
     if (((bd >> 4) & 7) != 4) return arrow::Status::NotImplemented("LZ4 blocks larger than 64 KiB");
-    const uint64_t dlen = 2 + (((flg >> 3) & 1) ? 8 : 0);
+    const bool has_size = (flg >> 3) & 1;
+    const uint64_t dlen = 2 + (has_size ? 8 : 0);
     if (pos + 4 + dlen + 1 > n) return arrow::Status::Invalid("truncated LZ4 frame header");
     if (((Xxh32(p + pos + 4, dlen, 0) >> 8) & 0xFF) != p[pos + 4 + dlen])
       return arrow::Status::Invalid("LZ4 frame header checksum");
+    if (has_size) {
+      f.has_content = true;
+      for (int k = 0; k < 8; ++k) f.content |= uint64_t(p[pos + 6 + k]) << (8 * k);
+    }
     pos += 4 + dlen + 1;
     for (;;) {
       if (pos + 4 > n) return arrow::Status::Invalid("truncated LZ4 frame");
@@ -275,9 +298,21 @@ arrow::Result<std::vector<Piece>> HipCodec::WalkLz4f(const uint8_t* p, uint64_t 
       if (bs == 0) break;  // EndMark
       const uint32_t len = bs & 0x7FFFFFFFu;
       if (len > kSeg || pos + len > n) return arrow::Status::Invalid("bad LZ4 block size");
-      v.push_back({pos, len, 0, (bs >> 31) != 0});
-      pos += len;
+      if (block_cks) {
+        if (pos + len + 4 > n) return arrow::Status::Invalid("truncated LZ4 block checksum");
+        if (Xxh32(p + pos, len, 0) != Rd32(p + pos + len))
+          return arrow::Status::IOError("LZ4 block checksum mismatch");
+      }
+      f.blocks.push_back({pos, len, 0, (bs >> 31) != 0});
+      pos += len + (block_cks ? 4 : 0);
     }
+    if (f.content_checksum) {
+      if (pos + 4 > n) return arrow::Status::Invalid("truncated LZ4 content checksum");
+      f.checksum = Rd32(p + pos);
+      pos += 4;
+    }
+    f.csize = pos - f.offset;
+    v.push_back(std::move(f));
   }
   return v;
 }
@@ -288,7 +323,7 @@ arrow::Result<int64_t> HipCodec::Decompress(int64_t input_len, const uint8_t* in
   if (input_len < 0 || output_buffer_len < 0) return arrow::Status::Invalid("negative length");
   const uint64_t n = static_cast<uint64_t>(input_len);
   const bool zstd = type_ == arrow::Compression::ZSTD;
-  const bool in_dev = OnDevice(input), out_dev = OnDevice(output);
+  const bool in_dev = OnDevice(input);
   // the header walk needs the bytes on the host
   std::vector<uint8_t> host;
   const uint8_t* hp = input;
@@ -298,68 +333,179 @@ arrow::Result<int64_t> HipCodec::Decompress(int64_t input_len, const uint8_t* in
     ARROW_RETURN_NOT_OK(Sync());
     hp = host.data();
   }
-  std::vector<Piece> pieces;
+  std::vector<Frame> frames;
   if (zstd) {
-    ARROW_ASSIGN_OR_RAISE(pieces, WalkZstd(hp, n));
+    ARROW_ASSIGN_OR_RAISE(frames, WalkZstd(hp, n));
   } else {
-    ARROW_ASSIGN_OR_RAISE(pieces, WalkLz4f(hp, n));
+    ARROW_ASSIGN_OR_RAISE(frames, WalkLz4f(hp, n));
   }
-  const uint64_t nseg = pieces.size();
-  if (nseg == 0) return 0;
-  if (nseg > 0x7FFFFFFFull) return arrow::Status::Invalid("too many segments");
+  if (frames.empty()) return 0;
   const uint8_t* d_in = input;
   if (!in_dev) {
     ARROW_RETURN_NOT_OK(Reserve(d_in_, c_in_, n + 16));
     ARROW_RETURN_NOT_OK(Copy(d_in_, input, n));
     d_in = static_cast<const uint8_t*>(d_in_);
   }
-  // a stored LZ4 block decodes as an empty one (a lone 0x00 token) and is copied after
-  ARROW_RETURN_NOT_OK(Reserve(d_aux_, c_aux_, std::max<uint64_t>(nseg * 4, 16)));
+  if (zstd) return DecompressZstd(frames, d_in, output_buffer_len, output);
+  return DecompressLz4f(frames, d_in, n, output_buffer_len, output);
+}
+
+// Zstandard: every frame is one segment of the wave decoder; segments are as large as the
+// largest frame (frames of 64 KiB, the shape this codec writes, are the common case)
+arrow::Result<int64_t> HipCodec::DecompressZstd(const std::vector<Frame>& frames,
+                                                const uint8_t* d_in, int64_t output_buffer_len,
+                                                uint8_t* output) {
+  const uint64_t nseg = frames.size();
+  if (nseg > 0x7FFFFFFFull) return arrow::Status::Invalid("too many segments");
+  uint64_t seg = 0;
+  for (const Frame& f : frames) {
+    if (!f.has_content && nseg > 1)
+      return arrow::Status::NotImplemented("Zstandard frames without content size");
+    const uint64_t c = f.has_content ? f.content : static_cast<uint64_t>(output_buffer_len);
+    seg = std::max(seg, c);
+  }
+  seg = std::max<uint64_t>((seg + 15) & ~15ull, 16);
+  if (seg > (1ull << 30)) return arrow::Status::NotImplemented("Zstandard frame larger than 1 GiB");
+  std::vector<const uint8_t*> srcs(nseg);
+  std::vector<uint32_t> csz(nseg);
+  for (uint64_t i = 0; i < nseg; ++i) {
+    srcs[i] = d_in + frames[i].offset;
+    csz[i] = static_cast<uint32_t>(frames[i].csize);
+  }
+  ARROW_RETURN_NOT_OK(Reserve(d_srcs_, c_srcs_, nseg * sizeof(void*)));
+  ARROW_RETURN_NOT_OK(Reserve(d_sizes_, c_sizes_, nseg * 4));
+  ARROW_RETURN_NOT_OK(Reserve(d_off_, c_off_, nseg * 4));  // produced sizes
+  ARROW_RETURN_NOT_OK(Reserve(d_out_, c_out_, nseg * seg));
+  ARROW_RETURN_NOT_OK(Copy(d_srcs_, srcs.data(), nseg * sizeof(void*)));
+  ARROW_RETURN_NOT_OK(Copy(d_sizes_, csz.data(), nseg * 4));
+  auto* dout = static_cast<uint8_t*>(d_out_);
+  BITAR_ABI(bitar_hip_decompress(ctx_, nullptr, BITAR_HIP_CODEC_ZSTD,
+                                 reinterpret_cast<const void* const*>(d_srcs_),
+                                 static_cast<const uint32_t*>(d_sizes_),
+                                 static_cast<uint32_t>(nseg), static_cast<uint32_t>(seg), dout,
+                                 nseg * seg, static_cast<uint32_t*>(d_off_)),
+            "bitar_hip_decompress");
+  std::vector<uint32_t> prod(nseg);
+  ARROW_RETURN_NOT_OK(Copy(prod.data(), d_off_, nseg * 4));
+  ARROW_RETURN_NOT_OK(Sync());
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < nseg; ++i) {
+    if (frames[i].has_content && prod[i] != frames[i].content)
+      return arrow::Status::IOError("Zstandard frame ", i, " decoded to a wrong size");
+    total += prod[i];
+  }
+  if (total > static_cast<uint64_t>(output_buffer_len))
+    return arrow::Status::Invalid("decompressed size ", total, " exceeds the output buffer (",
+                                  output_buffer_len, ")");
+  // frame i's output sits at i * seg: gather them back to back
+  uint64_t at = 0;
+  for (uint64_t i = 0; i < nseg; ++i) {
+    ARROW_RETURN_NOT_OK(Copy(output + at, dout + i * seg, prod[i]));
+    at += prod[i];
+  }
+  ARROW_RETURN_NOT_OK(Sync());
+  return static_cast<int64_t>(total);
+}
+
+arrow::Result<uint64_t> HipCodec::Lz4Independent(const Frame& f, const uint8_t* d_in,
+                                                 uint8_t* dout) {
+  const uint64_t nseg = f.blocks.size();
+  if (nseg == 0) return 0;
+  // a stored block decodes as an empty one (a lone 0x00 token) and is copied after
+  ARROW_RETURN_NOT_OK(Reserve(d_aux_, c_aux_, 16));
   static const uint8_t kEmptyBlock[16] = {0};
   ARROW_RETURN_NOT_OK(Copy(d_aux_, kEmptyBlock, 16));
   const uint8_t* empty = static_cast<const uint8_t*>(d_aux_);
   std::vector<const uint8_t*> srcs(nseg);
   std::vector<uint32_t> csz(nseg);
   for (uint64_t i = 0; i < nseg; ++i) {
-    const bool raw = pieces[i].raw;
-    srcs[i] = raw ? empty : d_in + pieces[i].offset;
-    csz[i] = raw ? 1u : pieces[i].csize;
+    const bool raw = f.blocks[i].raw;
+    srcs[i] = raw ? empty : d_in + f.blocks[i].offset;
+    csz[i] = raw ? 1u : f.blocks[i].csize;
   }
   ARROW_RETURN_NOT_OK(Reserve(d_srcs_, c_srcs_, nseg * sizeof(void*)));
   ARROW_RETURN_NOT_OK(Reserve(d_sizes_, c_sizes_, nseg * 4));
   ARROW_RETURN_NOT_OK(Reserve(d_off_, c_off_, nseg * 4));  // produced sizes
-  ARROW_RETURN_NOT_OK(Reserve(d_out_, c_out_, nseg * kSeg));
   ARROW_RETURN_NOT_OK(Copy(d_srcs_, srcs.data(), nseg * sizeof(void*)));
   ARROW_RETURN_NOT_OK(Copy(d_sizes_, csz.data(), nseg * 4));
-  auto* dout = static_cast<uint8_t*>(d_out_);
-  BITAR_ABI(bitar_hip_decompress(ctx_, nullptr, zstd ? BITAR_HIP_CODEC_ZSTD : BITAR_HIP_CODEC_LZ4,
+  BITAR_ABI(bitar_hip_decompress(ctx_, nullptr, BITAR_HIP_CODEC_LZ4,
                                  reinterpret_cast<const void* const*>(d_srcs_),
                                  static_cast<const uint32_t*>(d_sizes_),
                                  static_cast<uint32_t>(nseg), kSeg, dout, nseg * kSeg,
                                  static_cast<uint32_t*>(d_off_)),
             "bitar_hip_decompress");
   for (uint64_t i = 0; i < nseg; ++i)
-    if (pieces[i].raw)
-      ARROW_RETURN_NOT_OK(Copy(dout + i * kSeg, d_in + pieces[i].offset, pieces[i].csize));
+    if (f.blocks[i].raw)
+      ARROW_RETURN_NOT_OK(Copy(dout + i * kSeg, d_in + f.blocks[i].offset, f.blocks[i].csize));
   ARROW_RETURN_NOT_OK(Sync());
   std::vector<uint32_t> prod(nseg);
   ARROW_RETURN_NOT_OK(Copy(prod.data(), d_off_, nseg * 4));
   ARROW_RETURN_NOT_OK(Sync());
   uint64_t total = 0;
   for (uint64_t i = 0; i < nseg; ++i) {
-    const uint32_t got = pieces[i].raw ? pieces[i].csize : prod[i];
-    if (zstd && got != pieces[i].content)
-      return arrow::Status::IOError("Zstandard frame ", i, " decoded to a wrong size");
+    const uint32_t got = f.blocks[i].raw ? f.blocks[i].csize : prod[i];
     if (i + 1 < nseg && got != kSeg)
       return arrow::Status::NotImplemented("LZ4 frame blocks of other than 64 KiB");
     total += got;
   }
-  if (total > static_cast<uint64_t>(output_buffer_len))
-    return arrow::Status::Invalid("decompressed size ", total, " exceeds the output buffer (",
-                                  output_buffer_len, ")");
+  return total;
+}
+
+// LZ4 frames in order: independent blocks decode in parallel (one segment each), linked
+// ones in order on one wavefront (bitar_hip_lz4_chain); content checksums checked (XXH32)
+arrow::Result<int64_t> HipCodec::DecompressLz4f(const std::vector<Frame>& frames,
+                                                const uint8_t* d_in, uint64_t n,
+                                                int64_t output_buffer_len, uint8_t* output) {
+  const uint64_t cap = static_cast<uint64_t>(output_buffer_len);
+  uint64_t most = 0;  // staging: the output, plus a full last block of slack
+  for (const Frame& f : frames) most += f.blocks.size() * kSeg;
+  ARROW_RETURN_NOT_OK(Reserve(d_out_, c_out_, std::max<uint64_t>(std::min(most, cap + kSeg), 16)));
+  auto* dout = static_cast<uint8_t*>(d_out_);
+  uint64_t total = 0;
+  for (const Frame& f : frames) {
+    uint64_t got = 0;
+    if (f.blocks.empty()) {
+      got = 0;
+    } else if (!f.linked) {
+      if (total + f.blocks.size() * kSeg > c_out_)
+        return arrow::Status::Invalid("LZ4 stream exceeds the output buffer");
+      ARROW_ASSIGN_OR_RAISE(got, Lz4Independent(f, d_in, dout + total));
+    } else {
+      std::vector<uint32_t> tab(2 * f.blocks.size());
+      for (size_t b = 0; b < f.blocks.size(); ++b) {
+        tab[2 * b] = static_cast<uint32_t>(f.blocks[b].offset);
+        tab[2 * b + 1] = f.blocks[b].csize | (f.blocks[b].raw ? 0x80000000u : 0u);
+      }
+      ARROW_RETURN_NOT_OK(Reserve(d_srcs_, c_srcs_, tab.size() * 4));
+      ARROW_RETURN_NOT_OK(Reserve(d_off_, c_off_, 4));
+      ARROW_RETURN_NOT_OK(Copy(d_srcs_, tab.data(), tab.size() * 4));
+      BITAR_ABI(bitar_hip_lz4_chain(ctx_, nullptr, d_in, static_cast<uint32_t>(n),
+                                    static_cast<const uint32_t*>(d_srcs_),
+                                    static_cast<uint32_t>(f.blocks.size()), dout + total,
+                                    c_out_ - total, static_cast<uint32_t*>(d_off_)),
+                "bitar_hip_lz4_chain");
+      ARROW_RETURN_NOT_OK(Sync());
+      uint32_t prod = 0;
+      ARROW_RETURN_NOT_OK(Copy(&prod, d_off_, 4));
+      ARROW_RETURN_NOT_OK(Sync());
+      got = prod;
+    }
+    if (f.has_content && got != f.content)
+      return arrow::Status::IOError("LZ4 frame decoded to a wrong size");
+    if (total + got > cap)
+      return arrow::Status::Invalid("decompressed size exceeds the output buffer (",
+                                    output_buffer_len, ")");
+    if (f.content_checksum) {
+      std::vector<uint8_t> back(got);
+      ARROW_RETURN_NOT_OK(Copy(back.data(), dout + total, got));
+      ARROW_RETURN_NOT_OK(Sync());
+      if (Xxh32(back.data(), got, 0) != f.checksum)
+        return arrow::Status::IOError("LZ4 content checksum mismatch");
+    }
+    total += got;
+  }
   ARROW_RETURN_NOT_OK(Copy(output, dout, total));
   ARROW_RETURN_NOT_OK(Sync());
-  (void)out_dev;  // bitar_hip_memcpy handles host and device destinations alike
   return static_cast<int64_t>(total);
 }
 

@@ -55,6 +55,8 @@ __global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t, uint64_t*
 __global__ void pack_kernel(const uint8_t*, uint64_t, const uint32_t*, const uint64_t*, uint32_t,
                             uint8_t*);
 __global__ void fill_kernel(int, uint64_t, uint64_t, uint8_t*, uint64_t);
+__global__ void lz4_chain_kernel(const uint8_t*, uint32_t, const uint32_t*, uint32_t, uint8_t*,
+                                 uint32_t, uint32_t*, uint32_t*);
 __global__ void copy_batch_kernel(const uint8_t* const*, uint8_t* const*, const uint32_t*, uint32_t);
 __global__ void lz4f_sizes_kernel(const uint32_t*, uint32_t, uint64_t, uint32_t, uint32_t*);
 __global__ void lz4f_pack_kernel(const uint8_t*, uint64_t, uint32_t, const uint8_t*, uint64_t,
@@ -109,6 +111,7 @@ hipStream_t pick_stream(bitar_hip_ctx*, void* stream) {
 }
 
 constexpr uint32_t kMaxSeg = BITAR_HIP_MAX_SEG_SIZE;
+constexpr uint32_t kMaxZstdFrame = 1u << 30;
 
 // index of the error word of `stream`; words run out only after 1000+ distinct foreign
 // streams, after which they share the NULL stream's word (still correct, merely coarser)
@@ -420,7 +423,11 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
       codec != BITAR_HIP_CODEC_ZSTD)
     return fail(BITAR_HIP_NOT_IMPLEMENTED, "unknown codec");
   if (nseg == 0) return 0;  // reference device.cc:244-246
-  if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
+  // Zstd: a segment may be a whole stock frame of up to kMaxZstdFrame bytes (the wave
+  // decoder reads far history from HBM; the Arrow adapter decodes stock IPC bodies so)
+  const uint32_t max_seg = codec == BITAR_HIP_CODEC_ZSTD ? kMaxZstdFrame : kMaxSeg;
+  if (seg == 0 || seg > max_seg)
+    return fail(BITAR_HIP_INVALID, "seg must be in [1, " + std::to_string(max_seg) + "]");
   if (capacity < (uint64_t)nseg * seg)  // reference device.cc:248-254
     return fail(BITAR_HIP_CAPACITY_ERROR,
                 "The decompressed_buffer is required to be >= " +
@@ -556,6 +563,21 @@ int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_
                        nseg, static_cast<uint8_t*>(d_frame));
     HIP_TRY(hipGetLastError(), "pack launch");
   }
+  return 0;
+}
+
+int bitar_hip_lz4_chain(bitar_hip_ctx* ctx, void* stream, const void* d_src, uint32_t src_len,
+                        const uint32_t* d_blocks, uint32_t nblocks, void* d_out,
+                        uint64_t capacity, uint32_t* d_produced) {
+  if (int r = enter(ctx)) return r;
+  if (!d_src || !d_blocks || !d_out || !d_produced) return fail(BITAR_HIP_INVALID, "null buffer");
+  if (capacity > 0xFFFFFFFFull) capacity = 0xFFFFFFFFull;
+  hipStream_t s = pick_stream(ctx, stream);
+  hipLaunchKernelGGL(bitar_hip::lz4_chain_kernel, dim3(1), dim3(64), 0, s,
+                     static_cast<const uint8_t*>(d_src), src_len, d_blocks, nblocks,
+                     static_cast<uint8_t*>(d_out), (uint32_t)capacity, d_produced,
+                     err_word(ctx, s));
+  HIP_TRY(hipGetLastError(), "lz4 chain launch");
   return 0;
 }
 

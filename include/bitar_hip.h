@@ -122,7 +122,8 @@ int bitar_hip_compress_scattered(bitar_hip_ctx* ctx, void* stream, uint32_t code
 /* Decompress nseg segments.  d_srcs[i] (a device array of device pointers) holds
  * d_sizes[i] compressed bytes; segment i inflates into d_out + i*seg and d_produced[i]
  * receives its size.  Requires capacity >= nseg*seg, else BITAR_HIP_CAPACITY_ERROR
- * (reference device.cc:248-254).  Asynchronous on `stream`.
+ * (reference device.cc:248-254).  seg <= 65536, except for Zstd: <= 2^30, so that a whole
+ * stock frame of any content size can be one segment.  Asynchronous on `stream`.
  * Replaces one CompressDevice::Decompress call (reference src/device.cc:240-318,
  * src/memory.cc:432-505). */
 int bitar_hip_decompress(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
@@ -151,6 +152,18 @@ int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream);
  * d_frame is NULL. */
 int bitar_hip_pack(bitar_hip_ctx* ctx, void* stream, const void* d_slab, uint64_t slot_stride,
                    const uint32_t* d_sizes, uint32_t nseg, uint64_t* d_offsets, void* d_frame);
+
+/* LZ4 frame with LINKED blocks (LZ4 frame format Block_Independence = 0, the liblz4 and
+ * Arrow LZ4_FRAME default): the blocks of ONE frame decode in order on one wavefront, each
+ * block's matches reaching into the output of the blocks before it.  d_blocks holds nblocks
+ * pairs {offset of the block's data in d_src, size | 1u << 31 for a stored block}; the
+ * output goes to d_out (capacity bytes) and *d_produced receives its total size, or
+ * BITAR_HIP_SEGMENT_ERROR (then the next sync returns BITAR_HIP_IO_ERROR).  Asynchronous on
+ * `stream`.  Frame / block checksums are the caller's (XXH32).  Used by the Arrow util::Codec
+ * adapter for stock IPC bodies. */
+int bitar_hip_lz4_chain(bitar_hip_ctx* ctx, void* stream, const void* d_src, uint32_t src_len,
+                        const uint32_t* d_blocks, uint32_t nblocks, void* d_out,
+                        uint64_t capacity, uint32_t* d_produced);
 
 /* Batched device-to-device copy: entry i moves d_sizes[i] bytes from d_srcs[i] to d_dsts[i]
  * (device arrays of n device pointers / sizes; any alignment, ranges must not overlap).

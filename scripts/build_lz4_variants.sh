@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/../bitar_amd"
 dir=$1
 mkdir -p build_lzv lib/variants
-for f in runtime inflate compress util_kernels zstd_decompress zstd_compress zstd_lanes inflate_lanes deflate_dyn checksum; do
+for f in runtime inflate compress util_kernels zstd_decompress zstd_compress zstd_lanes inflate_lanes deflate_dyn checksum lz4_chain; do
   [ -f build_lzv/$f.o ] || /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics -c csrc/$f.hip -o build_lzv/$f.o &
 done
 wait

@@ -6,6 +6,7 @@ GPU: Compress / Decompress / Recycle / async through a real device; every compre
 segment it returns must decode with the third-party decoder (zlib for DEFLATE, the pinned
 oracle for LZ4 and Zstd) to the matching input slice.
 """
+import ctypes
 import os
 import struct
 import subprocess
@@ -101,6 +102,72 @@ def test_frontend_on_gpu(tmp_path):
             assert enc(plain) == (0, stream), (name, j)
 
 
+def _lz4f_compress(plain, independent, block_checksum, content_checksum, content_size):
+    """liblz4's frame API with explicit preferences (LZ4F_compressFrame)."""
+    L = ctypes.CDLL("liblz4.so.1")
+
+    class FrameInfo(ctypes.Structure):
+        _fields_ = [("blockSizeID", ctypes.c_int), ("blockMode", ctypes.c_int),
+                    ("contentChecksumFlag", ctypes.c_int), ("frameType", ctypes.c_int),
+                    ("contentSize", ctypes.c_ulonglong), ("dictID", ctypes.c_uint),
+                    ("blockChecksumFlag", ctypes.c_int)]
+
+    class Prefs(ctypes.Structure):
+        _fields_ = [("frameInfo", FrameInfo), ("compressionLevel", ctypes.c_int),
+                    ("autoFlush", ctypes.c_uint), ("favorDecSpeed", ctypes.c_uint),
+                    ("reserved", ctypes.c_uint * 3)]
+
+    p = Prefs()
+    p.frameInfo.blockSizeID = 4  # 64 KiB
+    p.frameInfo.blockMode = 1 if independent else 0
+    p.frameInfo.contentChecksumFlag = int(content_checksum)
+    p.frameInfo.blockChecksumFlag = int(block_checksum)
+    p.frameInfo.contentSize = len(plain) if content_size else 0
+    L.LZ4F_compressFrameBound.restype = ctypes.c_size_t
+    L.LZ4F_compressFrame.restype = ctypes.c_size_t
+    cap = L.LZ4F_compressFrameBound(ctypes.c_size_t(len(plain)), ctypes.byref(p))
+    out = ctypes.create_string_buffer(cap)
+    r = L.LZ4F_compressFrame(out, ctypes.c_size_t(cap), plain, ctypes.c_size_t(len(plain)),
+                             ctypes.byref(p))
+    assert r < cap
+    return out.raw[:r]
+
+
+def _stock_streams(pa):
+    """(kind, stream, plain): the per-buffer frames pyarrow's codecs write (Arrow's default
+    LZ4F preferences: linked 64 KiB blocks; zstd level 1 frames of the whole buffer) for the
+    column buffers of an Arrow-like table, and liblz4 / libzstd frames with checksums and
+    content sizes."""
+    out = []
+    cols = [O.fill(2, 31, 300000).tobytes(), O.fill(6, 32, 200000).tobytes(),
+            O.fill(5, 33, 1 << 20).tobytes(), O.fill(0, 34, 70000).tobytes(), b"x" * 5]
+    for plain in cols:
+        out.append(("zstd", pa.Codec("zstd").compress(plain).to_pybytes(), plain))
+        out.append(("lz4f", pa.Codec("lz4").compress(plain).to_pybytes(), plain))
+    plain = cols[0]
+    for ind, bc, cc, cs in ((True, True, True, True), (False, True, True, False),
+                            (False, False, True, True), (True, False, False, False)):
+        out.append(("lz4f", _lz4f_compress(plain, ind, bc, cc, cs), plain))
+    try:
+        Z = ctypes.CDLL("libzstd.so.1")
+        Z.ZSTD_createCCtx.restype = ctypes.c_void_p
+        Z.ZSTD_CCtx_setParameter.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        Z.ZSTD_compress2.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_void_p, ctypes.c_size_t]
+        Z.ZSTD_compress2.restype = ctypes.c_size_t
+        cc = Z.ZSTD_createCCtx()
+        for level, cks in ((1, 1), (3, 0), (9, 1)):
+            Z.ZSTD_CCtx_setParameter(cc, 100, level)
+            Z.ZSTD_CCtx_setParameter(cc, 201, cks)  # checksum flag
+            buf = ctypes.create_string_buffer(len(plain) + 4096)
+            r = Z.ZSTD_compress2(cc, buf, len(buf), plain, len(plain))
+            assert r < len(buf)
+            out.append(("zstd", buf.raw[:r], plain))
+    except OSError:
+        pass
+    return out
+
+
 @pytest.mark.gpu
 def test_arrow_codec_adapter_on_gpu(tmp_path):
     """bitar::MakeArrowCodec (ZSTD, LZ4_FRAME): GPU round trips and stock-codec decoding are
@@ -113,9 +180,19 @@ def test_arrow_codec_adapter_on_gpu(tmp_path):
     data = O.fill(O.KIND_MIXED, 5, 9 * 65536 + 1234).tobytes()
     inp = tmp_path / "input.bin"
     inp.write_bytes(data)
+    # stock streams for the GPU decoder (DecompressZstd / DecompressLz4f of arrow_codec.cc)
+    man = []
+    for k, (kind, blob, plain) in enumerate(_stock_streams(pa)):
+        (tmp_path / f"stock_{k}.bin").write_bytes(blob)
+        (tmp_path / f"plain_{k}.bin").write_bytes(plain)
+        man.append(f"{kind} stock_{k}.bin plain_{k}.bin")
+    (tmp_path / "stock.txt").write_text("\n".join(man) + "\n")
     r = subprocess.run([BIN, "arrow", str(inp), str(tmp_path)], capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
+    n_lz4 = sum(1 for m in man if m.startswith("lz4f"))
+    assert f"stock streams decoded: {len(man) - n_lz4}" in r.stdout
+    assert f"stock streams decoded: {n_lz4}" in r.stdout
     for tag, name in (("zstd", "zstd"), ("lz4f", "lz4")):
         comp = (tmp_path / f"arrow_{tag}.bin").read_bytes()
         assert len(comp) < len(data)
