@@ -73,9 +73,11 @@ KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
            # decompress = inflate_lanes_kernel (lane per segment) + inflate_kernel in
            # defer-only mode; timed together
            "deflate": ("deflate_compress_kernel", "inflate_lanes_kernel"),
-           # decompress = zstd_lanes_kernel (lane per segment) + zstd_decompress_kernel in
-           # defer-only mode; timed together
-           "zstd": ("zstd_compress_kernel", "zstd_lanes_kernel"),
+           # compress = zstd_parse_kernel + zstd_entropy_kernel; decompress =
+           # zstd_lanes_kernel (predefined-table frames) + zstd_decompress_kernel (literals,
+           # tables) + zstd_handoff_kernel (sequences, lane per segment); each timed together
+           "zstd": ("zstd_parse_kernel+zstd_entropy_kernel",
+                    "zstd_decompress_kernel+zstd_handoff_kernel"),
            # compress = deflate_dyn_parse_kernel + deflate_dyn_emit_kernel (one event pair
            # brackets both); decompress = inflate_lanes_kernel deferring every dynamic block
            # to inflate_kernel
@@ -179,8 +181,10 @@ def kernel_lines(codec_name, r, traffic_json, leg="headline"):
     traffic = None
     try:
         with open(traffic_json) as f:
-            # per-launch HBM bytes of this leg's kernel, from its own PMC passes
-            traffic = json.load(f).get(f"{leg}/{dominant[0]}")
+            # per-launch HBM bytes of this leg's kernel(s), from its own PMC passes
+            tj = json.load(f)
+            parts = [tj.get(f"{leg}/{k}") for k in dominant[0].split("+")]
+            traffic = sum(parts) if all(p is not None for p in parts) else None
     except (OSError, ValueError):
         pass
     roof = {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 2),
@@ -525,9 +529,10 @@ def main():
     if zs is not None:
         res["zstd"] = leg_summary(
             "zstd", zs, world, args.steps, args.traffic_json,
-            "BASELINE configs[4] codec: Zstd frame per 64 KiB segment (raw literals, "
-            "predefined FSE sequences), compress + decompress, 1 GiB Arrow record-batch "
-            "buffer per GPU" + (", RCCL size all-gather" if world > 1 else ""))
+            "BASELINE configs[4] codec: level-1-class Zstd frame per 64 KiB segment "
+            "(repeat-offset parse, Huffman literals, per-table FSE / RLE / predefined "
+            "sequence codes), compress + decompress, 1 GiB Arrow record-batch buffer per GPU"
+            + (", RCCL size all-gather" if world > 1 else ""))
     if df is not None:
         res["deflate"] = leg_summary(
             "deflate", df, world, args.steps, args.traffic_json,

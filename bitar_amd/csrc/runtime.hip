@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/bitar_hip.h"
+#include "zstd_hand.hip.h"
 
 namespace bitar_hip {
 __global__ void lz4_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
@@ -37,6 +38,9 @@ __global__ void zstd_entropy_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                        const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                        uint32_t*, uint32_t*, uint32_t, uint8_t*);
+__global__ void zstd_hlit_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
+                                 const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
+                                 const uint8_t*, uint32_t*);
 template <uint32_t L>
 __global__ void zstd_handoff_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                     const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
@@ -486,12 +490,15 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
     // the wave decoder hands the sequence sections of its frames' last blocks to the lane
     // executor through a stream-ordered scratch (zstd_decompress.hip kHand*: 6 KiB per
     // segment)
-    constexpr uint64_t kHandStride = 4ull * (16 + 3 * 512);
     void* hscr = nullptr;
-    HIP_TRY(hipMallocAsync(&hscr, (uint64_t)nseg * kHandStride, s), "scratch allocation");
+    HIP_TRY(hipMallocAsync(&hscr, (uint64_t)nseg * bitar_hip::zhand::kStride, s),
+            "scratch allocation");
     hipLaunchKernelGGL(bitar_hip::zstd_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs,
                        slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
                        L ? 1u : 0u, static_cast<uint8_t*>(hscr));
+    hipLaunchKernelGGL(bitar_hip::zstd_hlit_kernel, dim3((nseg + 15) / 16), dim3(64), 0, s,
+                       srcs, slab, stride, d_sizes, nseg, seg, out, d_produced,
+                       static_cast<const uint8_t*>(hscr), err_word(ctx, s));
     hipLaunchKernelGGL(bitar_hip::zstd_handoff_kernel<16>, dim3((nseg + 15) / 16), dim3(64), 0, s,
                        srcs, slab, stride, d_sizes, nseg, seg, out, d_produced,
                        static_cast<const uint8_t*>(hscr), err_word(ctx, s));

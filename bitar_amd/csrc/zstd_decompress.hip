@@ -12,6 +12,7 @@
 // segment's output slot and copied from there by the sequence executor: output writes never
 // overtake the literal reads (op <= cap - remaining literals).
 #include "stream_ring.hip.h"
+#include "zstd_hand.hip.h"
 
 #include <type_traits>
 
@@ -664,12 +665,8 @@ __device__ __forceinline__ void exec_chunk(State& s, uint8_t* win, uint8_t* ring
   s.op += co;
 }
 
-// Hand-off to the lane-per-segment sequence executor (zstd_lanes.hip zstd_handoff_kernel):
-// per segment kHandStride bytes of scratch = a record of kHandRec words, then the LL, OF and
-// ML decode cells (kHandCells words each, the LDS cell format sym | nbits << 8 | base << 16)
-constexpr uint32_t kHandRec = 16, kHandCells = 512, kHandMinSeq = 16;
-constexpr uint64_t kHandStride = 4ull * (kHandRec + 3 * kHandCells);
-constexpr uint32_t kHanded = 0xFFFFFFFDu;  // produced[i] while the executor owns segment i
+// Hand-off to the lane kernels (zstd_hand.hip.h)
+using zhand::kHanded;
 
 struct Frame {
   uint32_t rep0, rep1, rep2;
@@ -718,6 +715,7 @@ __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs
   // where the literals come from: the stream (raw), one byte (RLE), or the slot tail
   uint32_t lit_stream = 0, lit_byte = 0;
   GMEM uint8_t* lit_tail = s.dst + (s.cap - regen);
+  if (hand && lane == 0) hand[zhand::kLitPend] = 0u;  // set below if the lanes decode them
   if (lt == 0) {
     if (q + regen > end) return 0;
     lit_stream = q;
@@ -739,24 +737,52 @@ __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs
     } else if (!fr.huf_log) {
       return 0;
     }
-    if (nstreams == 1) {
-      if (!huf_stream_fast(s, win, t, fr.huf_log, cs, cl, lit_tail, regen)) return 0;
-    } else {
+    // the streams: one, or four behind a jump table
+    uint32_t st = cs, s1 = cl, s2 = 0, s3 = 0, s4 = 0, qq = regen;
+    if (nstreams != 1) {
       if (cl < 6) return 0;
       const uint32_t j = load_le(s, win, cs, 4);
-      const uint32_t s1 = j & 0xFFFFu, s2 = j >> 16, s3 = load_le(s, win, cs + 4, 2);
+      s1 = j & 0xFFFFu;
+      s2 = j >> 16;
+      s3 = load_le(s, win, cs + 4, 2);
       if (6ull + s1 + s2 + s3 > cl) return 0;
-      const uint32_t s4 = cl - 6 - s1 - s2 - s3;
-      const uint32_t qq = (regen + 3) / 4;
+      s4 = cl - 6 - s1 - s2 - s3;
+      qq = (regen + 3) / 4;
       if (3 * qq > regen) return 0;
-      const uint32_t st = cs + 6;
-      if (!huf_stream_fast(s, win, t, fr.huf_log, st, s1, lit_tail, qq)) return 0;
-      if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1, s2, lit_tail + qq, qq)) return 0;
-      if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1 + s2, s3, lit_tail + 2 * qq, qq)) return 0;
-      if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1 + s2 + s3, s4, lit_tail + 3 * qq,
-                      regen - 3 * qq)) return 0;
+      st = cs + 6;
     }
-    global_fence_wave();  // the executor reads back what the streams wrote
+    // a last block with enough sequences goes to the lane kernels, literals included: peek
+    // at its sequence count (the same test as the hand-off below)
+    bool lanes_lits = false;
+    if (hand && last_block && q + csz < end) {
+      const uint32_t qs = q + csz;
+      uint32_t ns = load_le(s, win, qs, 1);
+      if (ns >= 128 && ns < 255 && qs + 2 <= end) ns = ((ns - 128) << 8) + load_le(s, win, qs + 1, 1);
+      else if (ns == 255 && qs + 3 <= end) ns = load_le(s, win, qs + 1, 2) + 0x7F00u;
+      else if (ns >= 128) ns = 0;
+      lanes_lits = ns >= zhand::kMinSeq;
+    }
+    if (lanes_lits) {
+      lds_order();
+      const uint32_t ne = 1u << fr.huf_log;
+      for (uint32_t u = lane; u < ne / 2; u += kWave)
+        hand[zhand::kHufAt + u] = (uint32_t)t.huf[2 * u] | ((uint32_t)t.huf[2 * u + 1] << 16);
+      const uint32_t rv = lane == 0 ? 1u : lane == 1 ? fr.huf_log | (nstreams << 8)
+                          : lane == 2 ? st : lane == 3 ? s1 : lane == 4 ? s2 : lane == 5 ? s3
+                          : lane == 6 ? s4 : qq;
+      if (lane < 8) hand[zhand::kLitPend + lane] = rv;
+    } else {
+      if (nstreams == 1) {
+        if (!huf_stream_fast(s, win, t, fr.huf_log, st, s1, lit_tail, regen)) return 0;
+      } else {
+        if (!huf_stream_fast(s, win, t, fr.huf_log, st, s1, lit_tail, qq)) return 0;
+        if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1, s2, lit_tail + qq, qq)) return 0;
+        if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1 + s2, s3, lit_tail + 2 * qq, qq)) return 0;
+        if (!huf_stream_fast(s, win, t, fr.huf_log, st + s1 + s2 + s3, s4, lit_tail + 3 * qq,
+                        regen - 3 * qq)) return 0;
+      }
+      global_fence_wave();  // the executor reads back what the streams wrote
+    }
     q += csz;
   }
   uint32_t lp = 0;  // literals consumed
@@ -835,7 +861,7 @@ __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs
     }
     if (q >= end) return 0;
     ZP_END(3, tm);
-    if (hand && last_block && nseq >= kHandMinSeq) {
+    if (hand && last_block && nseq >= zhand::kMinSeq) {
       // everything before this block is output; the executor continues from s.op
       flush(s, ring, s.op, true);
       global_fence_wave();
@@ -843,7 +869,7 @@ __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs
       for (uint32_t k = 0; k < 3; ++k) {
         const uint32_t nc = 1u << fr.al[k];
         lds_order();
-        for (uint32_t u = lane; u < nc; u += kWave) hand[kHandRec + k * kHandCells + u] = t.fse[k][u];
+        for (uint32_t u = lane; u < nc; u += kWave) hand[zhand::kCellsAt + k * zhand::kCells + u] = t.fse[k][u];
       }
       const uint32_t rv = lane == 0 ? q : lane == 1 ? end : lane == 2 ? nseq
                           : lane == 3 ? fr.al[0] | (fr.al[1] << 8) | (fr.al[2] << 16) | (lt << 24)
@@ -1172,7 +1198,7 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     fr.pre[0] = fr.pre[1] = fr.pre[2] = false;
     fr.huf_log = 0;
     bool bad = false, last = false, handed = false;
-    GMEM uint32_t* hand = hscr && !cks ? global_ptr(reinterpret_cast<uint32_t*>(hscr + (uint64_t)i * kHandStride))
+    GMEM uint32_t* hand = hscr && !cks ? global_ptr(reinterpret_cast<uint32_t*>(hscr + (uint64_t)i * zhand::kStride))
                                        : nullptr;
     while (!last) {
       if (p + 3 > cs) { bad = true; break; }
@@ -1209,6 +1235,11 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     }
     if (bad) break;
     if (handed) {  // the executor finishes the frame (and its final checks)
+#ifdef ZPROF
+      ZP_ADD(0, ZP_T() - t_all);
+      lds_order();
+      if (lane_id() < 16) atomicAdd(&g_zprof[lane_id()], zp_lds[lane_id()]);
+#endif
       if (lane_id() == 0) produced[i] = kHanded;
       return;
     }

@@ -24,6 +24,7 @@
 // where lanes would copy up to 64 KiB each, are instead copied by the whole wave, one
 // lane's block after another, with coalesced 16-B accesses.
 #include "lane_copy.hip.h"
+#include "zstd_hand.hip.h"
 
 namespace bitar_hip {
 
@@ -382,10 +383,128 @@ __global__ __launch_bounds__(64) void zstd_lanes_kernel(
 // (L2-resident, 6 KiB per segment), with the wave kernel's acceptance checks, then the final
 // frame checks.  kHand* mirror zstd_decompress.hip.
 namespace zsh {
-constexpr uint32_t kHandRec = 16, kHandCells = 512;
-constexpr uint64_t kHandStride = 4ull * (kHandRec + 3 * kHandCells);
-constexpr uint32_t kHanded = 0xFFFFFFFDu;
+constexpr uint32_t kHandRec = zhand::kRec, kHandCells = zhand::kCells;
+constexpr uint64_t kHandStride = zhand::kStride;
+constexpr uint32_t kHanded = zhand::kHanded;
+
+// Backward bit reader over stream bytes [q, end) of one lane's frame (bits below q read as
+// zero) as a queue of four 32-bit words: the window is W0:W1 (64 bits), the refill drops W0
+// and loads the next word below W3, so a load has three refills to land.
+struct QBits {
+  uint32_t w0, w1, w2, w3;
+  uint32_t used;    // bits consumed from the top of W0:W1
+  int32_t at;       // frame offset of the lowest byte of W3
+  __device__ __forceinline__ static uint32_t word(const GMEM uint8_t* s, int32_t a, uint32_t q) {
+    const int32_t lo = (int32_t)q - 4;
+    uint32_t v;
+    __builtin_memcpy(&v, s + (a < lo ? lo : a), 4);
+    const int32_t below = (int32_t)q - a;
+    return below <= 0 ? v : below >= 4 ? 0u : v & (~0u << (8 * (uint32_t)below));
+  }
+  __device__ __forceinline__ void init(const GMEM uint8_t* s, uint32_t q, uint32_t end) {
+    at = (int32_t)end - 16;
+    w0 = word(s, at + 12, q);
+    w1 = word(s, at + 8, q);
+    w2 = word(s, at + 4, q);
+    w3 = word(s, at, q);
+    used = 0;
+  }
+  __device__ __forceinline__ void refill(const GMEM uint8_t* s, uint32_t q) {
+    if (used >= 32) {
+      w0 = w1;
+      w1 = w2;
+      w2 = w3;
+      at -= 4;
+      w3 = word(s, at, q);
+      used -= 32;
+    }
+  }
+  __device__ __forceinline__ uint32_t peek(uint32_t n) const {  // n <= 32, used + n <= 64
+    const uint64_t c = ((uint64_t)w0 << 32) | w1;
+    return (uint32_t)(c >> (64 - used - n)) & ((1u << n) - 1u);
+  }
+  // bits still unread below the window top: 8 (top - q) - used, top = at + 16
+  __device__ __forceinline__ int32_t remaining(uint32_t q) const {
+    return 8 * (at + 16 - (int32_t)q) - (int32_t)used;
+  }
+};
 }  // namespace zsh
+
+// The Huffman literal streams of handed-off blocks (kLitPend): 16 segments per wave, one lane
+// per stream (lane 4 l + j = stream j of segment l), the segments' decode tables in LDS; each
+// lane decodes its stream backward (one table lookup per symbol, 8 symbols per 8-byte store)
+// into the tail of the segment's output slot, where zstd_handoff_kernel reads the literals.
+// Acceptance: the stream is consumed exactly (the wave decoder's huf_stream rule).
+__global__ __launch_bounds__(64) void zstd_hlit_kernel(
+    const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
+    uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
+    uint8_t* __restrict__ out, uint32_t* __restrict__ produced,
+    const uint8_t* __restrict__ hscr, uint32_t* __restrict__ err) {
+  using namespace zhand;
+  constexpr uint32_t S = 16;
+  __shared__ uint32_t tab[S][kHufWords];  // 2^11 u16 entries per segment
+  const uint32_t lane = lane_id();
+  for (uint32_t l = 0; l < S; ++l) {
+    const uint32_t il = blockIdx.x * S + l;
+    if (il >= nseg || produced[il] != kHanded) continue;
+    const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
+    if (h[kLitPend] != 1u) continue;
+    const uint32_t nw = (1u << (h[kHufLog] & 0xFFu)) / 2;
+    for (uint32_t u = lane; u < nw; u += kWave) tab[l][u] = h[kHufAt + u];
+  }
+  lds_order();
+  const uint32_t l = lane >> 2, j = lane & 3u;
+  const uint32_t i = blockIdx.x * S + l;
+  if (i >= nseg || produced[i] != kHanded) return;
+  const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
+  if (h[kLitPend] != 1u) return;
+  const uint32_t hl = h[kHufLog], log = hl & 0xFFu, ns = hl >> 8;
+  if (j >= ns) return;
+  const uint32_t regen = h[kRegen], qq = h[kQQ];
+  const uint32_t s1 = h[kS1], s2 = h[kS2], s3 = h[kS3], s4 = h[kS4];
+  const uint32_t start = h[kStreams] + (j >= 1 ? s1 : 0u) + (j >= 2 ? s2 : 0u) + (j >= 3 ? s3 : 0u);
+  const uint32_t len = j == 0 ? s1 : j == 1 ? s2 : j == 2 ? s3 : s4;
+  const uint32_t n = ns == 1 ? regen : j < 3 ? qq : regen - 3 * qq;
+  const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
+  GMEM uint8_t* dst = global_ptr(out + (uint64_t)i * seg + (seg - regen) + j * qq);
+  const uint16_t* t = reinterpret_cast<const uint16_t*>(tab[l]);
+  bool ok = len > 0;
+  uint32_t lastb = 0;
+  if (ok) {
+    lastb = src[start + len - 1];
+    ok = lastb != 0;
+  }
+  if (ok) {
+    zsh::QBits b;
+    b.init(src, start, start + len);
+    b.used = 8 - (31u - (uint32_t)__builtin_clz(lastb));  // the end mark and the zeros above it
+    const uint32_t mask = (1u << log) - 1u;
+    uint64_t acc = 0;
+    uint32_t k = 0;
+    for (; k + 8 <= n; k += 8) {
+#pragma unroll
+      for (uint32_t r = 0; r < 8; ++r) {
+        b.refill(src, start);
+        const uint32_t e = t[b.peek(log) & mask];
+        b.used += e >> 8;
+        acc = r == 0 ? (uint64_t)(e & 0xFFu) : acc | ((uint64_t)(e & 0xFFu) << (8 * r));
+      }
+      lanes::st8(dst + k, acc);
+    }
+    for (; k < n; ++k) {
+      b.refill(src, start);
+      const uint32_t e = t[b.peek(log) & mask];
+      b.used += e >> 8;
+      dst[k] = (uint8_t)(e & 0xFFu);
+    }
+    ok = b.remaining(start) == 0;
+  }
+  if (!ok) {
+    produced[i] = 0xFFFFFFFFu;
+    atomicOr(err, 1u);
+  }
+}
+
 
 template <uint32_t L>
 __global__ __launch_bounds__(64) void zstd_handoff_kernel(
@@ -509,10 +628,14 @@ __global__ __launch_bounds__(64) void zstd_handoff_kernel(
         ok = false;
         break;
       }
+#ifndef BITAR_ZH_NOLIT
       lits(ll);
+#endif
       op += ll;
       lp += ll;
+#ifndef BITAR_ZH_NOMATCH
       copy_match(dst + op, off, ml, op + ml + 32 <= limit());
+#endif
       op += ml;
     }
     if (ok && b.remaining(q) != 0) ok = false;
