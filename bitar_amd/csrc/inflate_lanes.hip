@@ -240,6 +240,12 @@ __global__ __launch_bounds__(64) void inflate_lanes_kernel(
   }
 }
 
+template __global__ void inflate_lanes_kernel<4>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                                 const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                                 uint32_t*);
+template __global__ void inflate_lanes_kernel<8>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                                 const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                                 uint32_t*);
 template __global__ void inflate_lanes_kernel<16>(const uint8_t* const*, const uint8_t*, uint64_t,
                                                   const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                                   uint32_t*);

@@ -404,16 +404,21 @@ extern "C" int bitar_hip_debug_set_zstd_lanes(int lanes) {
   return (int)old;
 }
 
-// segments per wave of inflate_lanes_kernel: BITAR_HIP_INFLATE_LANES = 32 / 16, 0 = off
+// segments per wave of inflate_lanes_kernel: BITAR_HIP_INFLATE_LANES = 4 / 8 / 16 / 32, 0 = off
+static uint32_t inflate_lanes_from(long x) {
+  return x <= 0 ? 0u : x >= 32 ? 32u : x >= 16 ? 16u : x >= 8 ? 8u : 4u;
+}
 static std::atomic<uint32_t> g_inflate_lanes{[] {
   const char* e = std::getenv("BITAR_HIP_INFLATE_LANES");
-  const long x = e ? std::strtol(e, nullptr, 10) : 16;
-  return x <= 0 ? 0u : x >= 32 ? 32u : 16u;
+  // 4: 4516 waves per GiB hide more of each lane's load latency than 16 (1129 waves, about
+  // one per SIMD): 1-GiB decode kind 1 17.3 -> 15.5 ms, kind 5 14.6 -> 12.7, kind 6 9.8 ->
+  // 8.9; stored-only (random) data 9.2 -> 10.4
+  return inflate_lanes_from(e ? std::strtol(e, nullptr, 10) : 4);
 }()};
 static uint32_t inflate_lanes() { return g_inflate_lanes.load(std::memory_order_relaxed); }
 extern "C" int bitar_hip_debug_set_inflate_lanes(int lanes) {
   const uint32_t old = inflate_lanes();
-  g_inflate_lanes.store(lanes <= 0 ? 0u : lanes >= 32 ? 32u : 16u);
+  g_inflate_lanes.store(inflate_lanes_from(lanes));
   return (int)old;
 }
 
@@ -458,12 +463,14 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
     const uint32_t L = inflate_lanes();
     if (L) {
       const dim3 g((nseg + L - 1) / L);
-      if (L == 32)
-        hipLaunchKernelGGL(bitar_hip::inflate_lanes_kernel<32>, g, dim3(64), 0, s, srcs, slab,
-                           stride, d_sizes, nseg, seg, out, d_produced);
-      else
-        hipLaunchKernelGGL(bitar_hip::inflate_lanes_kernel<16>, g, dim3(64), 0, s, srcs, slab,
-                           stride, d_sizes, nseg, seg, out, d_produced);
+#define BITAR_INFL_LANES(N)                                                                  \
+  hipLaunchKernelGGL(bitar_hip::inflate_lanes_kernel<N>, g, dim3(64), 0, s, srcs, slab, stride, \
+                     d_sizes, nseg, seg, out, d_produced)
+      if (L == 32) BITAR_INFL_LANES(32);
+      else if (L == 16) BITAR_INFL_LANES(16);
+      else if (L == 8) BITAR_INFL_LANES(8);
+      else BITAR_INFL_LANES(4);
+#undef BITAR_INFL_LANES
     }
     hipLaunchKernelGGL(bitar_hip::inflate_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
                        stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s), L ? 1u : 0u);
