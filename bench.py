@@ -98,9 +98,10 @@ def reduce_max_sum(vals_max, vals_sum, world):
         return list(vals_max), list(vals_sum)
     import torch
     import torch.distributed as dist
-    dev = torch.cuda.current_device()
-    a = torch.tensor(list(vals_max), dtype=torch.float64, device=f"cuda:{dev}")
-    b = torch.tensor(list(vals_sum), dtype=torch.float64, device=f"cuda:{dev}")
+    # RCCL reduces device tensors; gloo (the one-GPU rehearsal) host tensors
+    dev = f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu"
+    a = torch.tensor(list(vals_max), dtype=torch.float64, device=dev)
+    b = torch.tensor(list(vals_sum), dtype=torch.float64, device=dev)
     dist.all_reduce(a, op=dist.ReduceOp.MAX)
     dist.all_reduce(b, op=dist.ReduceOp.SUM)
     return a.tolist(), b.tolist()
@@ -440,9 +441,14 @@ def main():
     import bitar_amd
 
     world, rank, local = launch.rank_env()
+    backend = launch.dist_backend()
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        gpu = launch.rank_device(local, torch.cuda.device_count())
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{gpu}"))
+        else:  # one-GPU rehearsal of the N-rank path (bitar_amd.launch.dist_backend)
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -501,7 +507,10 @@ def main():
                    "codec": CODEC_NAMES[args.codec],
                    "input_kind": args.kind,
                    "parallelism": (f"{world} ranks, round-robin batches of 256 segments, "
-                                   "RCCL all-gather of sizes") if world > 1 else "1 GPU"},
+                                   + ("RCCL all-gather of sizes" if backend == "nccl" else
+                                      f"{backend} all-gather of sizes (ranks sharing "
+                                      f"{torch.cuda.device_count()} GPU(s): rehearsal)"))
+                                  if world > 1 else "1 GPU"},
         "compression_ratio": round(U / r["csize_total"], 4),
         "compress_gibs": round(r["local"]["nbytes"] / r["t_comp"] / GIB, 3),
         "decompress_gibs": round(r["local"]["nbytes"] / r["t_dec"] / GIB, 3),

@@ -25,6 +25,21 @@ def rank_env():
     return world, rank, local
 
 
+def dist_backend() -> str:
+    """The process group's backend: RCCL ("nccl") between GPUs.  BITAR_DIST_BACKEND=gloo is
+    the one-GPU rehearsal of the N-rank path: the collectives run over gloo on host copies
+    and the ranks share the visible GPUs (rank_device)."""
+    return os.environ.get("BITAR_DIST_BACKEND", "nccl")
+
+
+def rank_device(local: int, ndev: int) -> int:
+    """The GPU of local rank `local`: one GPU per rank (RCCL refuses two ranks on one
+    device); under the gloo rehearsal, ranks beyond the visible GPUs share them."""
+    if dist_backend() == "gloo" and ndev > 0:
+        return local % ndev
+    return local
+
+
 def is_rank_process() -> bool:
     return "WORLD_SIZE" in os.environ and "RANK" in os.environ
 

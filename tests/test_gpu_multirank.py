@@ -1,0 +1,35 @@
+"""The N-rank bench path on real hardware, rehearsed on one GPU: `bench.py --gpus 2` spawns
+two rank processes (bitar_amd.launch), each drives the HIP engine on the box's GPU, the
+size all-gather runs over gloo on host copies (BITAR_DIST_BACKEND=gloo; RCCL refuses two
+ranks on one device), and rank 0 prints the one JSON line.  The 8-GPU RCCL run is the
+driver's; this covers the launcher, per-rank device work, barriers, max-over-ranks timing
+and the sharded legs (headline, configs[3] record batch, Zstd, DEFLATE)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def test_bench_two_ranks_share_one_gpu():
+    env = dict(os.environ, BITAR_DIST_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--bytes", str(64 << 20), "--record-bytes", str(256 << 20),
+           "--only", "recordbatch,zstd,deflate"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["roundtrip_ok"] and r["value"] > 0
+    assert r["config"]["segments_per_gpu"] == 1024  # 128 MiB job, batches of 256 segments
+    for leg in ("recordbatch", "zstd", "deflate"):
+        assert r[leg]["roundtrip_ok"], leg
