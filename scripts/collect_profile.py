@@ -21,9 +21,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # the x2 correction is for 16-B-per-lane streaming reads; the lane-per-segment decoders
-# (zstd_lanes_kernel, inflate_lanes_kernel) read 8 B per lane, so their FETCH_SIZE is taken
+# (zstd_lanes_kernel, inflate_lanes_kernel, zstd_hlit_kernel, zstd_handoff_kernel) read 4-8 B
+# per lane, so their FETCH_SIZE is taken
 # as reported
-FETCH_FACTOR = {"zstd_lanes_kernel": 1.0, "inflate_lanes_kernel": 1.0}
+FETCH_FACTOR = {"zstd_lanes_kernel": 1.0, "inflate_lanes_kernel": 1.0, "zstd_hlit_kernel": 1.0,
+                "zstd_handoff_kernel": 1.0}
 
 
 def per_kernel(path):
