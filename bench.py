@@ -260,6 +260,18 @@ def host_threads():
         return os.cpu_count() or 1
 
 
+def cpu_quota():
+    """CPUs' worth of time this process's cgroup may use (cgroup v2 cpu.max), None if
+    unlimited or unknown: the GPU box shares its host CPUs, so this can be far below the
+    visible core count."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def stock_decode(eng, args):
     """GPU decode of streams the stock libraries produced on the host from the same input
     (compressed and uploaded outside the timed region; the decode is timed with HIP events
@@ -421,6 +433,8 @@ def cpu_baseline(args):
                                   "level 1, 59460-B segments"},
         "configs0": cfg0,
         "os_cpu_count": os.cpu_count(),
+        # the threads above run inside this CPU-time quota (cgroup cpu.max) when it is set
+        "cpu_quota_cores": cpu_quota(),
     }
 
 
