@@ -38,6 +38,7 @@ __global__ void zstd_entropy_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                        const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                        uint32_t*, uint32_t*, uint32_t, uint8_t*);
+template <uint32_t S>
 __global__ void zstd_hlit_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                  const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
                                  const uint8_t*, uint32_t*);
@@ -422,6 +423,22 @@ extern "C" int bitar_hip_debug_set_inflate_lanes(int lanes) {
   return (int)old;
 }
 
+// segments per wave of zstd_hlit_kernel / zstd_handoff_kernel (4 / 8 / 16): tuning knobs
+// BITAR_HIP_HLIT_SEGS, BITAR_HIP_HANDOFF_LANES, read once
+static uint32_t pow2_knob(const char* name, uint32_t dflt) {
+  const char* e = std::getenv(name);
+  const long x = e ? std::strtol(e, nullptr, 10) : (long)dflt;
+  return x >= 16 ? 16u : x >= 8 ? 8u : 4u;
+}
+static uint32_t hlit_segs() {
+  static const uint32_t v = pow2_knob("BITAR_HIP_HLIT_SEGS", 16);
+  return v;
+}
+static uint32_t handoff_lanes() {
+  static const uint32_t v = pow2_knob("BITAR_HIP_HANDOFF_LANES", 16);
+  return v;
+}
+
 static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            const void* const* d_srcs, const void* d_slab, uint64_t stride,
                            const uint32_t* d_sizes, uint32_t nseg, uint32_t seg, void* d_out,
@@ -503,12 +520,19 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
     hipLaunchKernelGGL(bitar_hip::zstd_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs,
                        slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
                        L ? 1u : 0u, static_cast<uint8_t*>(hscr));
-    hipLaunchKernelGGL(bitar_hip::zstd_hlit_kernel, dim3((nseg + 15) / 16), dim3(64), 0, s,
-                       srcs, slab, stride, d_sizes, nseg, seg, out, d_produced,
-                       static_cast<const uint8_t*>(hscr), err_word(ctx, s));
-    hipLaunchKernelGGL(bitar_hip::zstd_handoff_kernel<16>, dim3((nseg + 15) / 16), dim3(64), 0, s,
-                       srcs, slab, stride, d_sizes, nseg, seg, out, d_produced,
-                       static_cast<const uint8_t*>(hscr), err_word(ctx, s));
+    const uint8_t* hs = static_cast<const uint8_t*>(hscr);
+    uint32_t* ew = err_word(ctx, s);
+#define BITAR_ZSTD_TAIL(K, N)                                                                \
+  hipLaunchKernelGGL(bitar_hip::K<N>, dim3((nseg + N - 1) / N), dim3(64), 0, s, srcs, slab, \
+                     stride, d_sizes, nseg, seg, out, d_produced, hs, ew)
+    const uint32_t hs_n = hlit_segs(), ho_n = handoff_lanes();
+    if (hs_n == 4) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 4);
+    else if (hs_n == 8) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 8);
+    else BITAR_ZSTD_TAIL(zstd_hlit_kernel, 16);
+    if (ho_n == 4) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 4);
+    else if (ho_n == 8) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 8);
+    else BITAR_ZSTD_TAIL(zstd_handoff_kernel, 16);
+#undef BITAR_ZSTD_TAIL
     const hipError_t le = hipGetLastError();
     HIP_TRY(hipFreeAsync(hscr, s), "scratch release");
     HIP_TRY(le, "decompress launch");

@@ -387,47 +387,13 @@ constexpr uint32_t kHandRec = zhand::kRec, kHandCells = zhand::kCells;
 constexpr uint64_t kHandStride = zhand::kStride;
 constexpr uint32_t kHanded = zhand::kHanded;
 
-// Backward bit reader over stream bytes [q, end) of one lane's frame (bits below q read as
-// zero) as a queue of four 32-bit words: the window is W0:W1 (64 bits), the refill drops W0
-// and loads the next word below W3, so a load has three refills to land.
-struct QBits {
-  uint32_t w0, w1, w2, w3;
-  uint32_t used;    // bits consumed from the top of W0:W1
-  int32_t at;       // frame offset of the lowest byte of W3
-  __device__ __forceinline__ static uint32_t word(const GMEM uint8_t* s, int32_t a, uint32_t q) {
-    const int32_t lo = (int32_t)q - 4;
-    uint32_t v;
-    __builtin_memcpy(&v, s + (a < lo ? lo : a), 4);
-    const int32_t below = (int32_t)q - a;
-    return below <= 0 ? v : below >= 4 ? 0u : v & (~0u << (8 * (uint32_t)below));
-  }
-  __device__ __forceinline__ void init(const GMEM uint8_t* s, uint32_t q, uint32_t end) {
-    at = (int32_t)end - 16;
-    w0 = word(s, at + 12, q);
-    w1 = word(s, at + 8, q);
-    w2 = word(s, at + 4, q);
-    w3 = word(s, at, q);
-    used = 0;
-  }
-  __device__ __forceinline__ void refill(const GMEM uint8_t* s, uint32_t q) {
-    if (used >= 32) {
-      w0 = w1;
-      w1 = w2;
-      w2 = w3;
-      at -= 4;
-      w3 = word(s, at, q);
-      used -= 32;
-    }
-  }
-  __device__ __forceinline__ uint32_t peek(uint32_t n) const {  // n <= 32, used + n <= 64
-    const uint64_t c = ((uint64_t)w0 << 32) | w1;
-    return (uint32_t)(c >> (64 - used - n)) & ((1u << n) - 1u);
-  }
-  // bits still unread below the window top: 8 (top - q) - used, top = at + 16
-  __device__ __forceinline__ int32_t remaining(uint32_t q) const {
-    return 8 * (at + 16 - (int32_t)q) - (int32_t)used;
-  }
-};
+// 4 stream bytes at offset a, as loaded: no select on the value, so the load's wait lands
+// where the word is first used (below q it reads [q - 4, q) instead; peek masks those bits)
+__device__ __forceinline__ uint32_t word_raw(const GMEM uint8_t* s, int32_t a, int32_t lo) {
+  uint32_t v;
+  __builtin_memcpy(&v, s + (a < lo ? lo : a), 4);
+  return v;
+}
 }  // namespace zsh
 
 // The Huffman literal streams of handed-off blocks (kLitPend): 16 segments per wave, one lane
@@ -435,13 +401,13 @@ struct QBits {
 // lane decodes its stream backward (one table lookup per symbol, 8 symbols per 8-byte store)
 // into the tail of the segment's output slot, where zstd_handoff_kernel reads the literals.
 // Acceptance: the stream is consumed exactly (the wave decoder's huf_stream rule).
+template <uint32_t S>
 __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced,
     const uint8_t* __restrict__ hscr, uint32_t* __restrict__ err) {
   using namespace zhand;
-  constexpr uint32_t S = 16;
   __shared__ uint32_t tab[S][kHufWords];  // 2^11 u16 entries per segment
   const uint32_t lane = lane_id();
   for (uint32_t l = 0; l < S; ++l) {
@@ -455,7 +421,7 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
   lds_order();
   const uint32_t l = lane >> 2, j = lane & 3u;
   const uint32_t i = blockIdx.x * S + l;
-  if (i >= nseg || produced[i] != kHanded) return;
+  if (l >= S || i >= nseg || produced[i] != kHanded) return;
   const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
   if (h[kLitPend] != 1u) return;
   const uint32_t hl = h[kHufLog], log = hl & 0xFFu, ns = hl >> 8;
@@ -475,29 +441,59 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     ok = lastb != 0;
   }
   if (ok) {
-    zsh::QBits b;
-    b.init(src, start, start + len);
-    b.used = 8 - (31u - (uint32_t)__builtin_clz(lastb));  // the end mark and the zeros above it
+    // Backward bit reader whose eight words live in FIXED registers W0..W7: phase p decodes
+    // from the window W[p]:W[p+1] (W[p] the higher-addressed word) until it has used 32 bits,
+    // then reloads W[p] with the word eight below it, which the window reaches seven phases
+    // later.  A rotating queue would move each new word on the very next refill and so wait
+    // for its load (and, vmcnt being in order, for every store before it) there; the one
+    // full wait left is at the loop head, once per eight words.
+    // Bits below the stream start q read as zero (masked at the peek, from the position).
+    const int32_t q = (int32_t)start, lo = q >= 4 ? q - 4 : 0;
+    int32_t top = (int32_t)(start + len);  // stream offset just above the window
+#ifndef BITAR_HLIT_NW
+#define BITAR_HLIT_NW 8
+#endif
+    constexpr uint32_t NW = BITAR_HLIT_NW;
+    uint32_t W[NW];
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) W[w] = zsh::word_raw(src, top - 4 * (int32_t)(w + 1), lo);
+    uint32_t used = 8 - (31u - (uint32_t)__builtin_clz(lastb));  // the end mark and zeros above it
     const uint32_t mask = (1u << log) - 1u;
     uint64_t acc = 0;
-    uint32_t k = 0;
-    for (; k + 8 <= n; k += 8) {
-#pragma unroll
-      for (uint32_t r = 0; r < 8; ++r) {
-        b.refill(src, start);
-        const uint32_t e = t[b.peek(log) & mask];
-        b.used += e >> 8;
-        acc = r == 0 ? (uint64_t)(e & 0xFFu) : acc | ((uint64_t)(e & 0xFFu) << (8 * r));
+    uint32_t k = 0, ac = 0;
+    auto phase = [&](uint32_t hi, uint32_t lo32, uint32_t& slot) __attribute__((always_inline)) {
+      const uint64_t c = ((uint64_t)hi << 32) | lo32;
+      while (used < 32 && k < n) {
+        uint32_t v = (uint32_t)(c >> (64 - used - log)) & mask;
+        const int32_t rem = 8 * (top - q) - (int32_t)used;  // stream bits not yet consumed
+        if (rem < (int32_t)log) v &= rem <= 0 ? 0u : ~0u << (log - (uint32_t)rem);
+        const uint32_t e = t[v];
+        used += e >> 8;
+        acc |= (uint64_t)(e & 0xFFu) << (8 * ac);
+        ++k;
+        if (++ac == 8) {
+          lanes::st8(dst + k - 8, acc);
+          acc = 0;
+          ac = 0;
+        }
       }
-      lanes::st8(dst + k, acc);
+      // (unconditional: a conditional load is a phi the compiler settles with vmcnt(0); when
+      // the phase ended on k == n instead, the loop ends and the word is not read)
+      slot = zsh::word_raw(src, top - 4 * (int32_t)(NW + 1), lo);
+      if (used >= 32) {
+        top -= 4;
+        used -= 32;
+      }
+    };
+    while (k < n) {
+#pragma unroll
+      for (uint32_t p = 0; p < NW; ++p) {
+        phase(W[p], W[(p + 1) % NW], W[p]);
+        if (k >= n) break;
+      }
     }
-    for (; k < n; ++k) {
-      b.refill(src, start);
-      const uint32_t e = t[b.peek(log) & mask];
-      b.used += e >> 8;
-      dst[k] = (uint8_t)(e & 0xFFu);
-    }
-    ok = b.remaining(start) == 0;
+    for (uint32_t r = 0; r < ac; ++r) dst[k - ac + r] = (uint8_t)(acc >> (8 * r));
+    ok = 8 * (top - q) - (int32_t)used == 0;
   }
   if (!ok) {
     produced[i] = 0xFFFFFFFFu;
@@ -670,6 +666,21 @@ __global__ __launch_bounds__(64) void zstd_handoff_kernel(
 template __global__ void zstd_handoff_kernel<16>(const uint8_t* const*, const uint8_t*, uint64_t,
                                                  const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                                  uint32_t*, const uint8_t*, uint32_t*);
+template __global__ void zstd_handoff_kernel<4>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                                 const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                                 uint32_t*, const uint8_t*, uint32_t*);
+template __global__ void zstd_handoff_kernel<8>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                                 const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                                 uint32_t*, const uint8_t*, uint32_t*);
+template __global__ void zstd_hlit_kernel<4>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                            const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                            uint32_t*, const uint8_t*, uint32_t*);
+template __global__ void zstd_hlit_kernel<8>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                            const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                            uint32_t*, const uint8_t*, uint32_t*);
+template __global__ void zstd_hlit_kernel<16>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                             const uint32_t*, uint32_t, uint32_t, uint8_t*,
+                                             uint32_t*, const uint8_t*, uint32_t*);
 
 template __global__ void zstd_lanes_kernel<64>(const uint8_t* const*, const uint8_t*, uint64_t,
                                                const uint32_t*, uint32_t, uint32_t, uint8_t*,
