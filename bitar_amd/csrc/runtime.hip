@@ -47,6 +47,13 @@ __global__ void zstd_handoff_kernel(const uint8_t* const*, const uint8_t*, uint6
                                     const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
                                     const uint8_t*, uint32_t*);
 template <uint32_t L>
+__global__ void zstd_seqdec_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
+                                   const uint32_t*, uint32_t, uint32_t, uint32_t*, uint8_t*,
+                                   uint64_t*, uint32_t, uint32_t*);
+__global__ void zstd_exec_kernel(const uint8_t* const*, const uint8_t*, uint64_t, uint32_t,
+                                 uint32_t, uint8_t*, uint32_t*, const uint8_t*,
+                                 const uint64_t*, uint32_t);
+template <uint32_t L>
 __global__ void zstd_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                   const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
 __global__ void deflate_dyn_parse_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
@@ -434,6 +441,19 @@ static uint32_t hlit_segs() {
   static const uint32_t v = pow2_knob("BITAR_HIP_HLIT_SEGS", 16);
   return v;
 }
+// two-phase sequence execution (zstd_seq.hip) for segments <= 64 KiB: BITAR_HIP_ZSTD_SEQ=0
+// leaves every handed-off segment to the lane executor (tests cover both)
+static std::atomic<uint32_t> g_zstd_seq{[] {
+  const char* e = std::getenv("BITAR_HIP_ZSTD_SEQ");
+  return e ? (uint32_t)(std::strtol(e, nullptr, 10) != 0) : 1u;
+}()};
+extern "C" int bitar_hip_debug_set_zstd_seq(int on) {
+  return (int)g_zstd_seq.exchange(on ? 1u : 0u);
+}
+static uint32_t seqdec_segs() {
+  static const uint32_t v = pow2_knob("BITAR_HIP_SEQDEC_SEGS", 16);
+  return v;
+}
 static uint32_t handoff_lanes() {
   static const uint32_t v = pow2_knob("BITAR_HIP_HANDOFF_LANES", 16);
   return v;
@@ -529,11 +549,31 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
     if (hs_n == 4) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 4);
     else if (hs_n == 8) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 8);
     else BITAR_ZSTD_TAIL(zstd_hlit_kernel, 16);
+    // segments <= 64 KiB: FSE chains -> records (a lane per segment), records -> output (a
+    // wave per segment); segments with more than rcap sequences stay with the lane executor
+    void* recs = nullptr;
+    if (g_zstd_seq.load(std::memory_order_relaxed) && seg <= 65536) {
+      const uint32_t rcap = seg / 3 + 1;  // every valid frame (matches are >= 3 bytes)
+      HIP_TRY(hipMallocAsync(&recs, (uint64_t)nseg * rcap * 8, s), "scratch allocation");
+      auto* rp = static_cast<uint64_t*>(recs);
+      const uint32_t sd = seqdec_segs();
+#define BITAR_SEQDEC(N)                                                                      \
+  hipLaunchKernelGGL(bitar_hip::zstd_seqdec_kernel<N>, dim3((nseg + N - 1) / N), dim3(64), 0, s, \
+                     srcs, slab, stride, d_sizes, nseg, seg, d_produced,                      \
+                     static_cast<uint8_t*>(hscr), rp, rcap, ew)
+      if (sd == 4) BITAR_SEQDEC(4);
+      else if (sd == 8) BITAR_SEQDEC(8);
+      else BITAR_SEQDEC(16);
+#undef BITAR_SEQDEC
+      hipLaunchKernelGGL(bitar_hip::zstd_exec_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
+                         stride, nseg, seg, out, d_produced, hs, rp, rcap);
+    }
     if (ho_n == 4) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 4);
     else if (ho_n == 8) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 8);
     else BITAR_ZSTD_TAIL(zstd_handoff_kernel, 16);
 #undef BITAR_ZSTD_TAIL
     const hipError_t le = hipGetLastError();
+    if (recs) HIP_TRY(hipFreeAsync(recs, s), "scratch release");
     HIP_TRY(hipFreeAsync(hscr, s), "scratch release");
     HIP_TRY(le, "decompress launch");
   }

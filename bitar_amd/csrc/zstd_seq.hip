@@ -1,0 +1,419 @@
+// zstd_seq.hip -- two-phase execution of the sequence sections that the wave Zstd decoder
+// (zstd_decompress.hip) hands over (zstd_hand.hip.h), for segments of at most 64 KiB.
+//
+// Phase A, zstd_seqdec_kernel: ONE LANE PER SEGMENT runs the serial part -- the backward FSE
+// bitstream, whose states chain from sequence to sequence -- and nothing else: every decoded
+// sequence becomes one 8-byte record {literal length, match length, offset} (repeat offsets
+// resolved), with all of the wave decoder's acceptance checks (oracle/bitar_zstd.c
+// zs_sequences; the final frame checks too).  The three decode tables of a segment live in
+// LDS as 16-bit cells (symbol | next-state number << 6; the state's bit count and baseline
+// are recomputed from the number), 2.5 KiB per segment: 16 segments per wave, four waves per
+// CU, so the 16384 chains of a GiB are all resident in one round and no cell lookup leaves
+// the CU (the lane executor reads its 4-byte cells from L2 / the Infinity Cache).
+//
+// Phase B, zstd_exec_kernel: ONE WAVE PER SEGMENT executes the records 64 at a time.  The
+// batch's output is produced 64 bytes per step, one byte per lane: the literal-run and match
+// starts that fall in the step are scattered to their lanes through LDS, a prefix max gives
+// every lane the run it lies in; a literal lane loads its byte, a match lane reads its source
+// from the LDS history ring (or HBM when farther back), or -- source inside the same step --
+// from another lane by pointer jumping; the step is stored into the ring, which is flushed to
+// HBM in 16-B blocks (stream_ring.hip.h).  No per-lane wildcopies: every output byte is
+// written once, by a coalesced store.
+//
+// Records: u64 = ll | ml << 17 | off << 34 (each <= 65536 for a segment <= 64 KiB).
+#include "lane_copy.hip.h"
+#include "stream_ring.hip.h"
+#include "zstd_hand.hip.h"
+
+namespace bitar_hip {
+
+namespace zsq {
+
+using namespace zhand;
+
+constexpr uint32_t kRecs = 0xFFFFFFFCu;  // produced[i]: phase A done, records ready
+constexpr uint32_t kTab = 1280;          // cells per segment: LL 512 | OF 256 | ML 512
+constexpr uint32_t kOfAt = 512, kMlAt = 768;
+
+// Literal-length / match-length code -> baseline and extra-bit count (RFC 8878
+// 3.1.1.3.2.1.1), computed: the codes in the middle of both tables share one shape.
+__host__ __device__ constexpr uint32_t mid_t(uint32_t m) {
+  return m < 4 ? m : (2u + (m & 1u)) << ((m >> 1) - 1u);
+}
+__host__ __device__ constexpr uint32_t mid_bits(uint32_t m) { return m < 4 ? 1u : m >> 1; }
+__host__ __device__ constexpr uint32_t ll_bits(uint32_t c) {
+  return c < 16 ? 0u : c < 25 ? mid_bits(c - 16) : c - 19;
+}
+__host__ __device__ constexpr uint32_t ll_base(uint32_t c) {
+  return c < 16 ? c : c < 25 ? 16u + 2u * mid_t(c - 16) : 1u << (c - 19);
+}
+__host__ __device__ constexpr uint32_t ml_bits(uint32_t c) {
+  return c < 32 ? 0u : c < 43 ? mid_bits(c - 32) : c - 36;
+}
+__host__ __device__ constexpr uint32_t ml_base(uint32_t c) {
+  return c < 32 ? c + 3 : c < 43 ? 35u + 2u * mid_t(c - 32) : (1u << (c - 36)) + 3u;
+}
+
+// the RFC tables, to check the arithmetic at compile time
+constexpr uint32_t kLLB[36] = {0,  1,  2,  3,  4,  5,  6,   7,   8,   9,    10,   11,
+                               12, 13, 14, 15, 16, 18, 20,  22,  24,  28,   32,   40,
+                               48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384,
+                               32768, 65536};
+constexpr uint32_t kLLX[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  0,  0,  1,  1,
+                               1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+constexpr uint32_t kMLB[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13,   14,   15,   16,
+                               17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27,   28,   29,   30,
+                               31, 32, 33, 34, 35, 37, 39, 41, 43, 47, 51,   59,   67,   83,
+                               99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771,
+                               65539};
+constexpr uint32_t kMLX[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                               0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1,
+                               2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+constexpr bool codes_ok() {
+  for (uint32_t c = 0; c < 36; ++c)
+    if (ll_base(c) != kLLB[c] || ll_bits(c) != kLLX[c]) return false;
+  for (uint32_t c = 0; c < 53; ++c)
+    if (ml_base(c) != kMLB[c] || ml_bits(c) != kMLX[c]) return false;
+  return true;
+}
+static_assert(codes_ok(), "literal / match length code arithmetic");
+
+// The same, branch-free for the decode loop: every shift amount masked to 5 bits, so each
+// arm is well defined and the compiler selects instead of branching on the exec mask.
+// (a ?: chain whose arms are not all trivial becomes exec-mask branches; `sel` is a select)
+__device__ __forceinline__ uint32_t sel(bool c, uint32_t a, uint32_t b) {
+  const uint32_t m = 0u - (uint32_t)c;
+  return (a & m) | (b & ~m);
+}
+__device__ __forceinline__ uint32_t mid_t_d(uint32_t m) {
+  return sel(m < 4, m, (2u + (m & 1u)) << (((m >> 1) - 1u) & 31u));
+}
+__device__ __forceinline__ uint32_t mid_bits_d(uint32_t m) { return sel(m < 4, 1u, m >> 1); }
+__device__ __forceinline__ void ll_code(uint32_t c, uint32_t& base, uint32_t& bits) {
+  const uint32_t m = c - 16, h = (c - 19) & 31u;
+  base = sel(c < 16, c, sel(c < 25, 16u + 2u * mid_t_d(m), 1u << h));
+  bits = sel(c < 16, 0u, sel(c < 25, mid_bits_d(m), h));
+}
+__device__ __forceinline__ void ml_code(uint32_t c, uint32_t& base, uint32_t& bits) {
+  const uint32_t m = c - 32, h = (c - 36) & 31u;
+  base = sel(c < 32, c + 3, sel(c < 43, 35u + 2u * mid_t_d(m), (1u << h) + 3u));
+  bits = sel(c < 32, 0u, sel(c < 43, mid_bits_d(m), h));
+}
+
+// 4-byte scratch cell (sym | state bits << 8 | baseline << 16) -> 16-bit LDS cell
+// (sym | next-state number << 6): number = (baseline + 2^al) >> bits, in [1, 1024)
+__device__ __forceinline__ uint32_t cell16(uint32_t c, uint32_t al) {
+  const uint32_t nb = (c >> 8) & 0xFFu, base = c >> 16;
+  return (c & 63u) | (((base + (1u << al)) >> nb) << 6);
+}
+
+// a cell's state bit count and next-state baseline (FSE_buildDTable's rule)
+struct Step {
+  uint32_t nb, base;
+};
+__device__ __forceinline__ Step step_of(uint32_t cell, uint32_t al) {
+  const uint32_t ns = cell >> 6;
+  const uint32_t nb = al - (31u - (uint32_t)__builtin_clz(ns));
+  return {nb, (ns << nb) - (1u << al)};
+}
+
+}  // namespace zsq
+
+// ---- phase A -----------------------------------------------------------------------------
+// L segments per wave (lane l < L owns segment blockIdx.x * L + l).  A segment is taken when
+// the wave decoder handed it over (produced == kHanded) and it has at most `rcap` sequences;
+// on success produced = kRecs and the record count / final output size are in the scratch
+// record (kNseq stays, kOpEnd = final size), on a failed check produced = SEGMENT_ERROR and
+// the stream's error word is set.  Others stay kHanded for zstd_handoff_kernel.
+template <uint32_t L>
+__global__ __launch_bounds__(64) void zstd_seqdec_kernel(
+    const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
+    uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
+    uint32_t* __restrict__ produced, uint8_t* __restrict__ hscr, uint64_t* __restrict__ recs,
+    uint32_t rcap, uint32_t* __restrict__ err) {
+  using namespace zsq;
+  using lanes::ld8;
+  __shared__ __attribute__((aligned(16))) uint16_t cel[L * kTab];
+  const uint32_t lane = lane_id();
+  // stage the decode tables of the wave's segments, 4 cells per lane per step
+  for (uint32_t l = 0; l < L; ++l) {
+    const uint32_t il = blockIdx.x * L + l;
+    if (il >= nseg || produced[il] != kHanded) continue;
+    const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
+    if (h[kNseq] > rcap) continue;
+    const uint32_t als = h[kAls];
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) {
+      const uint32_t al = (als >> (8 * k)) & 0xFFu;
+      const uint32_t n4 = al >= 2 ? (1u << al) / 4 : 1u;
+      const GMEM uint4* t = reinterpret_cast<const GMEM uint4*>(h + kCellsAt + k * kCells);
+      uint16_t* d = cel + l * kTab + (k == 0 ? 0u : k == 1 ? kOfAt : kMlAt);
+      for (uint32_t u = lane; u < n4; u += kWave) {
+        const uint4 c = t[u];
+        const uint32_t lo = cell16(c.x, al) | (cell16(c.y, al) << 16);
+        const uint32_t hi = cell16(c.z, al) | (cell16(c.w, al) << 16);
+        *reinterpret_cast<uint2*>(d + 4 * u) = make_uint2(lo, hi);
+      }
+    }
+  }
+  lds_order();
+  const uint32_t i = blockIdx.x * L + lane;
+  if (lane >= L || i >= nseg || produced[i] != kHanded) return;
+  GMEM uint32_t* h = global_ptr(reinterpret_cast<uint32_t*>(hscr + (uint64_t)i * kStride));
+  const uint32_t nseq = h[kNseq];
+  if (nseq > rcap) return;
+  const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
+  GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap);
+  const uint32_t cs = csizes[i];
+  const uint32_t q = h[kQ], end = h[kEnd], w3 = h[kAls], regen = h[kRegen];
+  uint32_t op = h[kOp];
+  uint32_t r0 = h[kRep0], r1 = h[kRep1], r2 = h[kRep2];
+  const uint32_t fsz = h[kFsz], fcs = h[kFcs];
+  const uint32_t al0 = w3 & 0xFFu, al1 = (w3 >> 8) & 0xFFu, al2 = (w3 >> 16) & 0xFFu;
+  const uint16_t* tll = cel + lane * kTab;
+  const uint16_t* tof = tll + kOfAt;
+  const uint16_t* tml = tll + kMlAt;
+  const uint32_t cap = seg;
+  // Backward bit reader: C = the 8 stream bytes at [ptr, ptr + 8), `used` bits consumed from
+  // its top; N1, N2 = the 16 bytes below, loaded two reloads ahead.  Two reloads per
+  // sequence, both unconditional and branch-free, so a load's wait lands at its first use a
+  // whole sequence later (a load under a condition is a phi the compiler settles with
+  // vmcnt(0) on the spot -- and vmcnt is in order, so that also waits for the record stores).
+  // Bytes below q are not masked: a stream that reads them is rejected by the final count
+  // whatever they hold, and a valid one never takes bits from them.
+  const int32_t lo = (int32_t)q - 8;  // q >= 12 inside the frame
+  auto at = [&](int32_t a) __attribute__((always_inline)) { return ld8(src + (a < lo ? lo : a)); };
+  int32_t ptr = (int32_t)end - 8;
+  uint64_t C = at(ptr), N1 = at(ptr - 8), N2 = at(ptr - 16);
+  uint32_t used = 0;
+  auto reload = [&]() __attribute__((always_inline)) {
+    uint32_t sb = used >> 3;
+    sb = sb > 8 ? 8u : sb;  // (only a malformed stream consumes more between two reloads)
+    const uint32_t sh = 8 * sb;
+    const uint64_t c_hi = sh == 64 ? 0ull : C << sh, n1_hi = sh == 64 ? 0ull : N1 << sh;
+    const uint64_t c_lo = sh == 0 ? 0ull : N1 >> (64 - sh), n1_lo = sh == 0 ? 0ull : N2 >> (64 - sh);
+    C = c_hi | c_lo;
+    N1 = n1_hi | n1_lo;
+    used -= sh;
+    ptr -= (int32_t)sb;
+    N2 = at(ptr - 16);
+  };
+  auto read = [&](uint32_t n) __attribute__((always_inline)) {
+    const uint32_t sh = (64 - used - n) & 63u;
+    const uint32_t v = (uint32_t)(C >> sh) & ((1u << n) - 1u);
+    used += n;
+    return v;
+  };
+  const uint32_t lastb = (uint32_t)(C >> 56);
+  bool ok = lastb != 0;
+  uint32_t lp = 0;
+  if (ok) {
+    used = 8 - (31u - (uint32_t)__builtin_clz(lastb));
+    uint32_t sll = read(al0), sof = read(al1), sml = read(al2);
+    uint32_t cll = tll[sll], cof = tof[sof], cml = tml[sml];
+    int32_t rem = 0;  // stream bits left after the last sequence
+    // Groups of kG sequences: the group's records stay in registers and are stored at its end
+    // (the compiler waits for every outstanding store at the next load use -- it treats loads
+    // and stores as completing out of order -- so one store burst per group, not per
+    // sequence).  Sequences past nseq in the last group are decoded from whatever bits follow
+    // and discarded (state indices stay inside their tables: FSE keeps base + 2^nb <= size).
+    constexpr uint32_t kG = 8;
+    for (uint32_t k0 = 0; k0 < nseq; k0 += kG) {
+      uint64_t rb[kG];
+#pragma unroll
+      for (uint32_t j = 0; j < kG; ++j) {
+        const uint32_t k = k0 + j;
+        const bool valid = k < nseq;
+        reload();
+        const uint32_t ofc = cof & 63u;
+        const uint32_t ofv = (1u << ofc) + read(ofc);
+        uint32_t mlb, mlx;
+        ml_code(cml & 63u, mlb, mlx);
+        const uint32_t ml = mlb + read(mlx);
+        reload();  // <= 16 extra + 26 state bits follow
+        uint32_t llb, llx;
+        ll_code(cll & 63u, llb, llx);
+        const uint32_t ll = llb + read(llx);
+        // next states (none after the last sequence: no bits read)
+        const bool more = k + 1 < nseq;
+        const Step a = step_of(cll, al0), c = step_of(cml, al2), o = step_of(cof, al1);
+        sll = a.base + read(more ? a.nb : 0u);
+        sml = c.base + read(more ? c.nb : 0u);
+        sof = o.base + read(more ? o.nb : 0u);
+        cll = tll[sll];
+        cof = tof[sof];
+        cml = tml[sml];
+        rem = sel(k + 1 == nseq, (uint32_t)(8 * (ptr - (int32_t)q) + 64 - (int32_t)used), (uint32_t)rem);
+        // repeat offsets in select form (no exec-mask branches)
+        const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
+        const uint32_t off =
+            sel(ofv > 3, ofv - 3, sel(idx == 1, r0, sel(idx == 2, r1, sel(idx == 3, r2, r0 - 1))));
+        const bool shift2 = ofv > 3 || idx >= 3, shift1 = ofv > 3 || idx >= 2;
+        const uint32_t c0 = r0, c1 = r1, c2 = r2;
+        r2 = sel(shift2, c1, c2);
+        r1 = sel(shift1, c0, c1);
+        r0 = off;
+        rb[j] = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)off << 34);
+        // (bitwise: a short-circuit || is a branch)
+        const bool bad = (lp + ll > regen) | (op + ml + (regen - lp) > cap) | (off == 0) |
+                         (off > op + ll);
+        ok = ok & !(valid & bad);
+        op += sel(valid, ll + ml, 0u);
+        lp += sel(valid, ll, 0u);
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kG; ++j)
+        if (k0 + j < nseq) rec[k0 + j] = rb[j];
+      if (!ok) break;
+    }
+    if (ok && rem != 0) ok = false;
+  }
+  if (ok && (uint64_t)op + (regen - lp) > cap) ok = false;
+  if (ok) {
+    op += regen - lp;
+    ok = end == cs && (!fsz || fcs == op);
+  }
+  if (ok) {
+    h[kOpEnd] = op;
+    produced[i] = kRecs;
+  } else {
+    produced[i] = 0xFFFFFFFFu;
+    atomicOr(err, 1u);
+  }
+}
+
+// ---- phase B -----------------------------------------------------------------------------
+// One wave per segment with produced == kRecs: out[kOp, kOpEnd) from the records, the
+// literals (raw: the frame; RLE: one byte; Huffman: the slot tail, decoded there by
+// zstd_hlit_kernel) and the history.  The literal tail is read ahead of every store: phase A
+// checked op + unread literals <= capacity before each sequence.
+__global__ __launch_bounds__(64) void zstd_exec_kernel(
+    const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
+    uint64_t slot_stride, uint32_t nseg, uint32_t seg, uint8_t* __restrict__ out,
+    uint32_t* __restrict__ produced, const uint8_t* __restrict__ hscr,
+    const uint64_t* __restrict__ recs, uint32_t rcap) {
+  using namespace zsq;
+  using namespace sr;
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+  __shared__ uint32_t ev[kWave];
+  const uint32_t i = blockIdx.x;
+  if (i >= nseg || uniform(produced[i]) != kRecs) return;
+  const uint32_t lane = lane_id();
+  const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
+  const uint32_t nseq = uniform(h[kNseq]), w3 = uniform(h[kAls]), litv = uniform(h[kLitV]);
+  const uint32_t regen = uniform(h[kRegen]), op0 = uniform(h[kOp]), opend = uniform(h[kOpEnd]);
+  const uint32_t lt = w3 >> 24;
+  const uint32_t cap = seg;
+  State s;
+  s.dst = global_ptr(out + (uint64_t)i * seg);
+  s.cap = cap;
+  s.op = op0;
+  s.flushed = op0;
+  s.fenced = op0;  // out[0, op0) was written by an earlier launch
+  const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
+  // literal index j -> byte: lsrc[j] (raw / Huffman) or the RLE byte
+  const GMEM uint8_t* lsrc = lt == 0 ? src + litv : s.dst + (cap - regen);
+  const uint32_t lbyte = litv & 0xFFu;
+  const uintptr_t base = (uintptr_t)s.dst;
+  const GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap);
+  uint32_t lp = 0;
+  // one 64-byte step at output [xa, xa + 64) ∩ [.., xa + act): e = the run each lane lies in
+  // (key << 24 | payload: odd key = literals, payload = output pos - literal index; even key
+  // = match, payload = offset)
+  auto chunk = [&](uint32_t xa, uint32_t nact, uint32_t e) __attribute__((always_inline)) {
+    const uint32_t x = xa + lane;
+    const bool act = lane < nact;
+    const bool ism = ((e >> 24) & 1u) == 0;
+    const uint32_t pay = e & 0xFFFFFFu;
+    const uint32_t from = x - pay;  // literal index, or match source position
+    // far history (before the ring's reach, or written by the wave decoder): HBM, after a
+    // fence over what this wave flushed
+    const bool far = act && ism && from < xa && (from < op0 || from + kNearOff < x);
+    if (ballot(far && from >= s.fenced)) {
+      flush(s, ring, xa, true);
+      global_fence_wave();
+      s.fenced = s.flushed;
+    }
+    uint32_t v = 0, ptr = lane;
+    bool pend = false;
+    if (act) {
+      if (!ism) {
+        v = lt == 1 ? lbyte : (uint32_t)lsrc[from];
+      } else if (from >= xa) {
+        ptr = from - xa;
+        pend = true;
+      } else if (far) {
+        v = s.dst[from];
+      } else {
+        v = ring[(base + from) & kRingMask];
+      }
+    }
+    // sources inside this step: pointer jumping (each round halves the chains)
+    while (ballot(pend)) {
+      const uint32_t w = v | (pend ? 0x100u : 0u) | (ptr << 9);
+      const uint32_t t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ptr << 2), (int)w);
+      if (pend) {
+        if (t & 0x100u) {
+          ptr = t >> 9;
+        } else {
+          v = t & 0xFFu;
+          pend = false;
+        }
+      }
+    }
+    lds_order();
+    if (act) ring[(base + x) & kRingMask] = (uint8_t)v;
+    lds_order();
+  };
+  for (uint32_t kb = 0; kb < nseq; kb += kWave) {
+    const uint32_t n = nseq - kb < kWave ? nseq - kb : kWave;
+    const uint64_t r = lane < n ? rec[kb + lane] : 0ull;
+    const uint32_t ll = (uint32_t)r & 0x1FFFFu, ml = (uint32_t)(r >> 17) & 0x1FFFFu,
+                   off = (uint32_t)(r >> 34);
+    const uint32_t inc = wave_incl_sum(ll + ml), ex = inc - (ll + ml);
+    const uint32_t linc = wave_incl_sum(ll), lex = linc - ll;
+    const uint32_t T = readlane(inc, kWave - 1), LT = readlane(linc, kWave - 1);
+    const uint32_t e_lit = ((2u * lane + 1u) << 24) | ((s.op + ex) - (lp + lex));
+    const uint32_t e_mat = ((2u * lane + 2u) << 24) | off;
+    uint32_t carry = 0;
+    for (uint32_t cb = 0; cb < T; cb += kWave) {
+      const uint32_t xa = s.op + cb;
+      if (xa + kWave - s.flushed > kFlushAt) flush(s, ring, xa, false);
+      lds_order();
+      ev[lane] = 0u;
+      lds_order();
+      const uint32_t p1 = ex - cb, p2 = ex + ll - cb;
+      if (lane < n && ll && p1 < kWave) ev[p1] = e_lit;
+      if (lane < n && p2 < kWave) ev[p2] = e_mat;
+      lds_order();
+      uint32_t e = ev[lane];
+      e = wave_incl_max(e > carry ? e : carry);
+      carry = readlane(e, kWave - 1);
+      chunk(xa, T - cb < kWave ? T - cb : kWave, e);
+    }
+    s.op += T;
+    lp += LT;
+  }
+  // the literals after the last sequence
+  const uint32_t rest = regen - lp;
+  for (uint32_t cb = 0; cb < rest; cb += kWave) {
+    const uint32_t xa = s.op + cb;
+    if (xa + kWave - s.flushed > kFlushAt) flush(s, ring, xa, false);
+    chunk(xa, rest - cb < kWave ? rest - cb : kWave, (1u << 24) | (s.op - lp));
+  }
+  s.op += rest;
+  flush(s, ring, s.op, true);
+  if (lane == 0) produced[i] = opend;
+}
+
+template __global__ void zstd_seqdec_kernel<16>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                                const uint32_t*, uint32_t, uint32_t, uint32_t*,
+                                                uint8_t*, uint64_t*, uint32_t, uint32_t*);
+template __global__ void zstd_seqdec_kernel<4>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                               const uint32_t*, uint32_t, uint32_t, uint32_t*,
+                                               uint8_t*, uint64_t*, uint32_t, uint32_t*);
+template __global__ void zstd_seqdec_kernel<8>(const uint8_t* const*, const uint8_t*, uint64_t,
+                                               const uint32_t*, uint32_t, uint32_t, uint32_t*,
+                                               uint8_t*, uint64_t*, uint32_t, uint32_t*);
+
+}  // namespace bitar_hip
