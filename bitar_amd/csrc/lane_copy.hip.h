@@ -19,6 +19,7 @@ __device__ __forceinline__ uint64_t ld8(const GMEM uint8_t* p) {
   return v;
 }
 __device__ __forceinline__ void st8(GMEM uint8_t* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
+__device__ __forceinline__ void st16(GMEM uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
 // little-endian value of the n <= 4 bytes at p (byte loads: never reads past p + n)
 __device__ __forceinline__ uint32_t ldn(const GMEM uint8_t* p, uint32_t n) {
   uint32_t v = 0;

@@ -52,7 +52,7 @@ __global__ void zstd_seqdec_kernel(const uint8_t* const*, const uint8_t*, uint64
                                    uint64_t*, uint32_t, uint32_t*);
 __global__ void zstd_exec_kernel(const uint8_t* const*, const uint8_t*, uint64_t, uint32_t,
                                  uint32_t, uint8_t*, uint32_t*, const uint8_t*,
-                                 const uint64_t*, uint32_t);
+                                 const uint64_t*, uint32_t, uint32_t*);
 template <uint32_t L>
 __global__ void zstd_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                   const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
@@ -566,7 +566,7 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
       else BITAR_SEQDEC(16);
 #undef BITAR_SEQDEC
       hipLaunchKernelGGL(bitar_hip::zstd_exec_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
-                         stride, nseg, seg, out, d_produced, hs, rp, rcap);
+                         stride, nseg, seg, out, d_produced, hs, rp, rcap, ew);
     }
     if (ho_n == 4) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 4);
     else if (ho_n == 8) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 8);

@@ -33,7 +33,6 @@ enum : uint32_t {
   kStreams,    // frame offset of the first stream
   kS1, kS2, kS3, kS4,  // stream lengths
   kQQ,         // literals per stream (the last one: regen - 3 kQQ)
-  kOpEnd,      // zstd_seqdec_kernel: the frame's decoded size (zstd_seq.hip)
 };
 
 }  // namespace zhand

@@ -100,6 +100,12 @@ __device__ __forceinline__ void ml_code(uint32_t c, uint32_t& base, uint32_t& bi
   bits = sel(c < 32, 0u, sel(c < 43, mid_bits_d(m), h));
 }
 
+// lane k of each quad, to all four (DPP quad_perm broadcast)
+template <int K>
+__device__ __forceinline__ uint32_t qbcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xF, 0xF, false);
+}
+
 // 4-byte scratch cell (sym | state bits << 8 | baseline << 16) -> 16-bit LDS cell
 // (sym | next-state number << 6): number = (baseline + 2^al) >> bits, in [1, 1024)
 __device__ __forceinline__ uint32_t cell16(uint32_t c, uint32_t al) {
@@ -122,9 +128,8 @@ __device__ __forceinline__ Step step_of(uint32_t cell, uint32_t al) {
 // ---- phase A -----------------------------------------------------------------------------
 // L segments per wave (lane l < L owns segment blockIdx.x * L + l).  A segment is taken when
 // the wave decoder handed it over (produced == kHanded) and it has at most `rcap` sequences;
-// on success produced = kRecs and the record count / final output size are in the scratch
-// record (kNseq stays, kOpEnd = final size), on a failed check produced = SEGMENT_ERROR and
-// the stream's error word is set.  Others stay kHanded for zstd_handoff_kernel.
+// on success (the bitstream consumed exactly) produced = kRecs, else SEGMENT_ERROR and the
+// stream's error word; the sequence rules are checked by zstd_exec_kernel.  Others stay kHanded for zstd_handoff_kernel.
 template <uint32_t L>
 __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
@@ -157,141 +162,143 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
     }
   }
   lds_order();
-  const uint32_t i = blockIdx.x * L + lane;
-  if (lane >= L || i >= nseg || produced[i] != kHanded) return;
+  // Four lanes per segment (lane 4 l + j): j = 0 the literal-length table, 1 match lengths,
+  // 2 offsets, 3 a copy of lane 0.  Each lane looks up its own table, works out its code's
+  // baseline and extra bits and its state's bit count, the quad exchanges the widths (DPP
+  // quad broadcasts) so every lane knows where its fields lie in the bitstream, each lane
+  // extracts its two fields, and the quad exchanges the three values; the bit reader,
+  // repeat offsets and records are replicated over the quad.  One wave instruction thus
+  // advances all three FSE chains of 16 segments.
+  const uint32_t l = lane >> 2, j = lane & 3u;
+  const uint32_t i = blockIdx.x * L + l;
+  if (l >= L || i >= nseg || produced[i] != kHanded) return;  // quad-uniform
   GMEM uint32_t* h = global_ptr(reinterpret_cast<uint32_t*>(hscr + (uint64_t)i * kStride));
   const uint32_t nseq = h[kNseq];
   if (nseq > rcap) return;
   const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
   GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap);
   const uint32_t cs = csizes[i];
-  const uint32_t q = h[kQ], end = h[kEnd], w3 = h[kAls], regen = h[kRegen];
-  uint32_t op = h[kOp];
+  const uint32_t q = h[kQ], end = h[kEnd], w3 = h[kAls];
   uint32_t r0 = h[kRep0], r1 = h[kRep1], r2 = h[kRep2];
-  const uint32_t fsz = h[kFsz], fcs = h[kFcs];
-  const uint32_t al0 = w3 & 0xFFu, al1 = (w3 >> 8) & 0xFFu, al2 = (w3 >> 16) & 0xFFu;
-  const uint16_t* tll = cel + lane * kTab;
-  const uint16_t* tof = tll + kOfAt;
-  const uint16_t* tml = tll + kMlAt;
-  const uint32_t cap = seg;
-  // Backward bit reader: C = the 8 stream bytes at [ptr, ptr + 8), `used` bits consumed from
-  // its top; N1, N2 = the 16 bytes below, loaded two reloads ahead.  Two reloads per
-  // sequence, both unconditional and branch-free, so a load's wait lands at its first use a
-  // whole sequence later (a load under a condition is a phi the compiler settles with
-  // vmcnt(0) on the spot -- and vmcnt is in order, so that also waits for the record stores).
-  // Bytes below q are not masked: a stream that reads them is rejected by the final count
-  // whatever they hold, and a valid one never takes bits from them.
+  const uint32_t al0 = w3 & 0xFFu, al1 = (w3 >> 8) & 0xFFu;
+  const uint32_t t = j == 1 ? 2u : j == 2 ? 1u : 0u;  // table in the frame's LL, OF, ML order
+  const uint32_t al = (w3 >> (8 * t)) & 0xFFu;
+  const uint16_t* tab = cel + l * kTab + (t == 0 ? 0u : t == 1 ? kOfAt : kMlAt);
+  // code -> baseline / extra bits: ll_code / ml_code as one formula with per-table constants
+  // (an offset code c is the formula's top range: extra bits c, baseline 2^c)
+  const uint32_t c_lo = t == 0 ? 16u : t == 2 ? 32u : 0u, c_mid = t == 0 ? 25u : t == 2 ? 43u : 0u;
+  const uint32_t c_add = t == 2 ? 3u : 0u, c_mb = t == 0 ? 16u : t == 2 ? 35u : 0u;
+  const uint32_t c_hs = t == 0 ? 19u : t == 2 ? 36u : 0u;
+  // Backward bit reader (replicated over the quad): C = the 8 stream bytes at [ptr, ptr+8),
+  // `used` bits consumed from its top; N1, N2 = the 16 bytes below.  Two reloads per
+  // sequence, unconditional and branch-free (a load under a condition is a phi the compiler
+  // settles with vmcnt(0) on the spot).  Between two reloads at most 47 bits are consumed,
+  // so a reload shifts by 0..6 bytes.  Bytes below q are not masked: a stream that reads
+  // them is rejected by the final count whatever they hold, a valid one never uses them.
   const int32_t lo = (int32_t)q - 8;  // q >= 12 inside the frame
   auto at = [&](int32_t a) __attribute__((always_inline)) { return ld8(src + (a < lo ? lo : a)); };
   int32_t ptr = (int32_t)end - 8;
   uint64_t C = at(ptr), N1 = at(ptr - 8), N2 = at(ptr - 16);
   uint32_t used = 0;
   auto reload = [&]() __attribute__((always_inline)) {
-    uint32_t sb = used >> 3;
-    sb = sb > 8 ? 8u : sb;  // (only a malformed stream consumes more between two reloads)
-    const uint32_t sh = 8 * sb;
-    const uint64_t c_hi = sh == 64 ? 0ull : C << sh, n1_hi = sh == 64 ? 0ull : N1 << sh;
-    const uint64_t c_lo = sh == 0 ? 0ull : N1 >> (64 - sh), n1_lo = sh == 0 ? 0ull : N2 >> (64 - sh);
-    C = c_hi | c_lo;
-    N1 = n1_hi | n1_lo;
-    used -= sh;
-    ptr -= (int32_t)sb;
+    const uint32_t sh = used & ~7u;
+    C = (C << sh) | ((N1 >> (63u - sh)) >> 1);  // (two shifts: sh = 0 shifts N1 out)
+    N1 = (N1 << sh) | ((N2 >> (63u - sh)) >> 1);
+    used &= 7u;
+    ptr -= (int32_t)(sh >> 3);
     N2 = at(ptr - 16);
   };
-  auto read = [&](uint32_t n) __attribute__((always_inline)) {
-    const uint32_t sh = (64 - used - n) & 63u;
-    const uint32_t v = (uint32_t)(C >> sh) & ((1u << n) - 1u);
-    used += n;
-    return v;
+  auto peek = [&](uint32_t p, uint32_t n) __attribute__((always_inline)) {
+    return (uint32_t)(C >> ((64u - p - n) & 63u)) & ((1u << n) - 1u);
   };
   const uint32_t lastb = (uint32_t)(C >> 56);
-  bool ok = lastb != 0;
-  uint32_t lp = 0;
+  bool ok = lastb != 0 && end == cs;
   if (ok) {
     used = 8 - (31u - (uint32_t)__builtin_clz(lastb));
-    uint32_t sll = read(al0), sof = read(al1), sml = read(al2);
-    uint32_t cll = tll[sll], cof = tof[sof], cml = tml[sml];
-    int32_t rem = 0;  // stream bits left after the last sequence
-    // Groups of kG sequences: the group's records stay in registers and are stored at its end
-    // (the compiler waits for every outstanding store at the next load use -- it treats loads
-    // and stores as completing out of order -- so one store burst per group, not per
-    // sequence).  Sequences past nseq in the last group are decoded from whatever bits follow
-    // and discarded (state indices stay inside their tables: FSE keeps base + 2^nb <= size).
+    // initial states, in the order LL, OF, ML
+    uint32_t cell = tab[peek(used + (t == 0 ? 0u : t == 1 ? al0 : al0 + al1), al)];
+    used += (w3 & 0xFFu) + ((w3 >> 8) & 0xFFu) + ((w3 >> 16) & 0xFFu);
+    auto step = [&](bool more) __attribute__((always_inline)) {
+      reload();
+      const uint32_t sym = cell & 63u, ns = cell >> 6;
+      const uint32_t m = sym - c_lo, hh = (sym - c_hs) & 31u;
+      const uint32_t base = sel(sym < c_lo, sym + c_add,
+                                sel(sym < c_mid, c_mb + 2u * mid_t_d(m), (1u << hh) + c_add));
+      const uint32_t x = sel(sym < c_lo, 0u, sel(sym < c_mid, mid_bits_d(m), hh));
+      const uint32_t nb0 = al - (31u - (uint32_t)__builtin_clz(ns));
+      const uint32_t nbase = (ns << nb0) - (1u << al);
+      const uint32_t nb = more ? nb0 : 0u;  // no state update after the last sequence
+      const uint32_t w = x | (nb << 8);
+      const uint32_t wl = qbcast<0>(w), wm = qbcast<1>(w), wo = qbcast<2>(w);
+      const uint32_t xl = wl & 0xFFu, xm = wm & 0xFFu, xo = wo & 0xFFu;
+      const uint32_t nbl = wl >> 8, nbm = wm >> 8, nbo = wo >> 8;
+      // bits: offset extra, match extra | literal extra, LL state, ML state, OF state
+      const uint32_t e1 = peek(used + sel(t == 2, xo, 0u), x);
+      used += xo + xm;
+      reload();
+      const uint32_t e2 = peek(used, x);
+      const uint32_t sof = xl + sel(t == 0, 0u, sel(t == 2, nbl, nbl + nbm));
+      const uint32_t sbits = peek(used + sof, nb);
+      used += xl + nbl + nbm + nbo;
+      const uint32_t val = base + sel(t == 0, e2, e1);
+      cell = tab[nbase + sbits];
+      const uint32_t ll = qbcast<0>(val), ml = qbcast<1>(val), ofv = qbcast<2>(val);
+      // repeat offsets in select form (no exec-mask branches)
+      const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
+      const uint32_t off =
+          sel(ofv > 3, ofv - 3, sel(idx == 1, r0, sel(idx == 2, r1, sel(idx == 3, r2, r0 - 1))));
+      const bool shift2 = ofv > 3 || idx >= 3, shift1 = ofv > 3 || idx >= 2;
+      const uint32_t c0 = r0, c1 = r1, c2 = r2;
+      r2 = sel(shift2, c1, c2);
+      r1 = sel(shift1, c0, c1);
+      r0 = off;
+      // (an offset past 2^30 - 1 is out of range anyway: saturated, zstd_exec_kernel rejects)
+      const uint32_t os = off < 0x3FFFFFFFu ? off : 0x3FFFFFFFu;
+      return (uint64_t)ll | ((uint64_t)(ml - 3) << 17) | ((uint64_t)os << 34);
+    };
+    // Groups of kG sequences: the records stay in registers and lane 0 of the quad stores
+    // them at the group's end (the compiler waits for every outstanding store at the next
+    // load use -- it does not let loads overtake stores -- so one store burst per group)
     constexpr uint32_t kG = 8;
-    for (uint32_t k0 = 0; k0 < nseq; k0 += kG) {
+    uint32_t k = 0;
+    for (; k + kG <= nseq; k += kG) {
       uint64_t rb[kG];
 #pragma unroll
-      for (uint32_t j = 0; j < kG; ++j) {
-        const uint32_t k = k0 + j;
-        const bool valid = k < nseq;
-        reload();
-        const uint32_t ofc = cof & 63u;
-        const uint32_t ofv = (1u << ofc) + read(ofc);
-        uint32_t mlb, mlx;
-        ml_code(cml & 63u, mlb, mlx);
-        const uint32_t ml = mlb + read(mlx);
-        reload();  // <= 16 extra + 26 state bits follow
-        uint32_t llb, llx;
-        ll_code(cll & 63u, llb, llx);
-        const uint32_t ll = llb + read(llx);
-        // next states (none after the last sequence: no bits read)
-        const bool more = k + 1 < nseq;
-        const Step a = step_of(cll, al0), c = step_of(cml, al2), o = step_of(cof, al1);
-        sll = a.base + read(more ? a.nb : 0u);
-        sml = c.base + read(more ? c.nb : 0u);
-        sof = o.base + read(more ? o.nb : 0u);
-        cll = tll[sll];
-        cof = tof[sof];
-        cml = tml[sml];
-        rem = sel(k + 1 == nseq, (uint32_t)(8 * (ptr - (int32_t)q) + 64 - (int32_t)used), (uint32_t)rem);
-        // repeat offsets in select form (no exec-mask branches)
-        const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
-        const uint32_t off =
-            sel(ofv > 3, ofv - 3, sel(idx == 1, r0, sel(idx == 2, r1, sel(idx == 3, r2, r0 - 1))));
-        const bool shift2 = ofv > 3 || idx >= 3, shift1 = ofv > 3 || idx >= 2;
-        const uint32_t c0 = r0, c1 = r1, c2 = r2;
-        r2 = sel(shift2, c1, c2);
-        r1 = sel(shift1, c0, c1);
-        r0 = off;
-        rb[j] = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)off << 34);
-        // (bitwise: a short-circuit || is a branch)
-        const bool bad = (lp + ll > regen) | (op + ml + (regen - lp) > cap) | (off == 0) |
-                         (off > op + ll);
-        ok = ok & !(valid & bad);
-        op += sel(valid, ll + ml, 0u);
-        lp += sel(valid, ll, 0u);
-      }
+      for (uint32_t g = 0; g < kG; ++g) rb[g] = step(k + g + 1 < nseq);
+      if (j == 0) {
 #pragma unroll
-      for (uint32_t j = 0; j < kG; ++j)
-        if (k0 + j < nseq) rec[k0 + j] = rb[j];
-      if (!ok) break;
+        for (uint32_t g = 0; g < kG; ++g) rec[k + g] = rb[g];
+      }
     }
-    if (ok && rem != 0) ok = false;
+    for (; k < nseq; ++k) {
+      const uint64_t r = step(k + 1 < nseq);
+      if (j == 0) rec[k] = r;
+    }
+    ok = 8 * (ptr - (int32_t)q) + 64 - (int32_t)used == 0;  // the stream consumed exactly
   }
-  if (ok && (uint64_t)op + (regen - lp) > cap) ok = false;
-  if (ok) {
-    op += regen - lp;
-    ok = end == cs && (!fsz || fcs == op);
-  }
-  if (ok) {
-    h[kOpEnd] = op;
-    produced[i] = kRecs;
-  } else {
-    produced[i] = 0xFFFFFFFFu;
-    atomicOr(err, 1u);
+  if (j == 0) {
+    if (ok) {
+      produced[i] = kRecs;
+    } else {
+      produced[i] = 0xFFFFFFFFu;
+      atomicOr(err, 1u);
+    }
   }
 }
 
 // ---- phase B -----------------------------------------------------------------------------
-// One wave per segment with produced == kRecs: out[kOp, kOpEnd) from the records, the
-// literals (raw: the frame; RLE: one byte; Huffman: the slot tail, decoded there by
-// zstd_hlit_kernel) and the history.  The literal tail is read ahead of every store: phase A
-// checked op + unread literals <= capacity before each sequence.
+// One wave per segment with produced == kRecs: out[kOp, ..) from the records, the literals
+// (raw: the frame; RLE: one byte; Huffman: the slot tail, decoded there by zstd_hlit_kernel)
+// and the history.  Each batch of 64 records is checked before it runs -- the wave
+// decoder's per-sequence rules (literals left, output room for the match and the unread
+// literals, 1 <= offset <= output so far) from the batch's prefix sums -- and the frame's
+// content size at the end; a failure sets SEGMENT_ERROR and the error word.  The literal
+// tail is read ahead of every store: room for the unread literals was checked.
 __global__ __launch_bounds__(64) void zstd_exec_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, uint32_t nseg, uint32_t seg, uint8_t* __restrict__ out,
     uint32_t* __restrict__ produced, const uint8_t* __restrict__ hscr,
-    const uint64_t* __restrict__ recs, uint32_t rcap) {
+    const uint64_t* __restrict__ recs, uint32_t rcap, uint32_t* __restrict__ err) {
   using namespace zsq;
   using namespace sr;
   __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
@@ -301,7 +308,8 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   const uint32_t lane = lane_id();
   const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
   const uint32_t nseq = uniform(h[kNseq]), w3 = uniform(h[kAls]), litv = uniform(h[kLitV]);
-  const uint32_t regen = uniform(h[kRegen]), op0 = uniform(h[kOp]), opend = uniform(h[kOpEnd]);
+  const uint32_t regen = uniform(h[kRegen]), op0 = uniform(h[kOp]);
+  const uint32_t fsz = uniform(h[kFsz]), fcs = uniform(h[kFcs]);
   const uint32_t lt = w3 >> 24;
   const uint32_t cap = seg;
   State s;
@@ -317,6 +325,7 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   const uintptr_t base = (uintptr_t)s.dst;
   const GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap);
   uint32_t lp = 0;
+  bool ok = true;
   // one 64-byte step at output [xa, xa + 64) ∩ [.., xa + act): e = the run each lane lies in
   // (key << 24 | payload: odd key = literals, payload = output pos - literal index; even key
   // = match, payload = offset)
@@ -368,11 +377,20 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   for (uint32_t kb = 0; kb < nseq; kb += kWave) {
     const uint32_t n = nseq - kb < kWave ? nseq - kb : kWave;
     const uint64_t r = lane < n ? rec[kb + lane] : 0ull;
-    const uint32_t ll = (uint32_t)r & 0x1FFFFu, ml = (uint32_t)(r >> 17) & 0x1FFFFu,
+    const uint32_t ll = (uint32_t)r & 0x1FFFFu, ml = lane < n ? ((uint32_t)(r >> 17) & 0x1FFFFu) + 3 : 0u,
                    off = (uint32_t)(r >> 34);
     const uint32_t inc = wave_incl_sum(ll + ml), ex = inc - (ll + ml);
     const uint32_t linc = wave_incl_sum(ll), lex = linc - ll;
     const uint32_t T = readlane(inc, kWave - 1), LT = readlane(linc, kWave - 1);
+    {
+      const uint32_t lpk = lp + lex, opk = s.op + ex;  // before sequence k
+      const bool bad = (lpk + ll > regen) | (opk + ml + (regen - lpk) > cap) | (off == 0) |
+                       (off > opk + ll);
+      if (ballot(lane < n && bad)) {
+        ok = false;
+        break;
+      }
+    }
     const uint32_t e_lit = ((2u * lane + 1u) << 24) | ((s.op + ex) - (lp + lex));
     const uint32_t e_mat = ((2u * lane + 2u) << 24) | off;
     uint32_t carry = 0;
@@ -395,7 +413,7 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
     lp += LT;
   }
   // the literals after the last sequence
-  const uint32_t rest = regen - lp;
+  const uint32_t rest = ok ? regen - lp : 0u;
   for (uint32_t cb = 0; cb < rest; cb += kWave) {
     const uint32_t xa = s.op + cb;
     if (xa + kWave - s.flushed > kFlushAt) flush(s, ring, xa, false);
@@ -403,7 +421,15 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   }
   s.op += rest;
   flush(s, ring, s.op, true);
-  if (lane == 0) produced[i] = opend;
+  ok = ok && (!fsz || fcs == s.op);
+  if (lane == 0) {
+    if (ok) {
+      produced[i] = s.op;
+    } else {
+      produced[i] = 0xFFFFFFFFu;
+      atomicOr(err, 1u);
+    }
+  }
 }
 
 template __global__ void zstd_seqdec_kernel<16>(const uint8_t* const*, const uint8_t*, uint64_t,
