@@ -408,7 +408,12 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced,
     const uint8_t* __restrict__ hscr, uint32_t* __restrict__ err) {
   using namespace zhand;
-  __shared__ uint32_t tab[S][kHufWords];  // 2^11 u16 entries per segment
+  // Per segment: the 2^11-entry table as symbol bytes plus each symbol's code length, 2.25
+  // KiB instead of 4 KiB of (symbol | length) entries, so 16 segments take 36 KiB and four
+  // workgroups share a CU: every stream of a GiB is resident in one round (two lookups per
+  // symbol, the second a tiny table)
+  __shared__ uint16_t tab[S][kHufWords];  // two symbol bytes per entry pair
+  __shared__ uint8_t len8[S][256];
   const uint32_t lane = lane_id();
   for (uint32_t l = 0; l < S; ++l) {
     const uint32_t il = blockIdx.x * S + l;
@@ -416,7 +421,12 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
     if (h[kLitPend] != 1u) continue;
     const uint32_t nw = (1u << (h[kHufLog] & 0xFFu)) / 2;
-    for (uint32_t u = lane; u < nw; u += kWave) tab[l][u] = h[kHufAt + u];
+    for (uint32_t u = lane; u < nw; u += kWave) {
+      const uint32_t w = h[kHufAt + u];
+      tab[l][u] = (uint16_t)((w & 0xFFu) | ((w >> 8) & 0xFF00u));
+      len8[l][w & 0xFFu] = (uint8_t)(w >> 8);  // (every entry of a symbol: the same length)
+      len8[l][(w >> 16) & 0xFFu] = (uint8_t)(w >> 24);
+    }
   }
   lds_order();
   const uint32_t l = lane >> 2, j = lane & 3u;
@@ -433,7 +443,8 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
   const uint32_t n = ns == 1 ? regen : j < 3 ? qq : regen - 3 * qq;
   const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
   GMEM uint8_t* dst = global_ptr(out + (uint64_t)i * seg + (seg - regen) + j * qq);
-  const uint16_t* t = reinterpret_cast<const uint16_t*>(tab[l]);
+  const uint8_t* t = reinterpret_cast<const uint8_t*>(tab[l]);
+  const uint8_t* tl = len8[l];
   bool ok = len > 0;
   uint32_t lastb = 0;
   if (ok) {
@@ -467,9 +478,9 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
         uint32_t v = (uint32_t)(c >> (64 - used - log)) & mask;
         const int32_t rem = 8 * (top - q) - (int32_t)used;  // stream bits not yet consumed
         if (rem < (int32_t)log) v &= rem <= 0 ? 0u : ~0u << (log - (uint32_t)rem);
-        const uint32_t e = t[v];
-        used += e >> 8;
-        acc |= (uint64_t)(e & 0xFFu) << (8 * ac);
+        const uint32_t sym = t[v];
+        used += tl[sym];
+        acc |= (uint64_t)sym << (8 * ac);
         ++k;
         if (++ac == 8) {
           lanes::st8(dst + k - 8, acc);

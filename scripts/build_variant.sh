@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/../bitar_amd"
 name=$1; defs=$2
 mkdir -p build_$name lib/variants
-for f in runtime lz4_decompress inflate compress util_kernels zstd_decompress zstd_compress zstd_lanes inflate_lanes deflate_dyn checksum lz4_chain; do
+for f in runtime lz4_decompress inflate compress util_kernels zstd_decompress zstd_compress zstd_lanes inflate_lanes deflate_dyn checksum lz4_chain zstd_seq; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics $defs -c csrc/$f.hip -o build_$name/$f.o &
 done
 wait
