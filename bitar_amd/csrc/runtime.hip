@@ -34,7 +34,11 @@ __global__ void inflate_lanes_kernel(const uint8_t* const*, const uint8_t*, uint
 __global__ void zstd_parse_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint2*);
 __global__ void zstd_entropy_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
                                     const uint2*, uint8_t*, uint64_t, uint8_t* const*, uint32_t*,
-                                    uint32_t*);
+                                    uint32_t*, uint8_t*, uint64_t);
+__global__ void zstd_walk_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t, uint8_t*, uint64_t);
+__global__ void zstd_emit_kernel(const uint8_t*, uint64_t, uint32_t, const uint8_t*, uint64_t,
+                                 uint8_t*, uint64_t, uint8_t* const*, uint32_t*, const uint8_t*,
+                                 uint64_t);
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                        const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                        uint32_t*, uint32_t*, uint32_t, uint8_t*);
@@ -343,15 +347,24 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
     // stream-ordered scratch: per segment the literal area + records (zstd_compress.hip),
     // then {nlit, nseq} per segment
     const uint64_t scr_stride = ((uint64_t)seg + 15u & ~15ull) + 8ull * (seg / 4u + 2u) + 255u & ~255ull;
+    // + the chain-walk scratch (zstd_compress.hip walk_stride: a 3400-byte header with the
+    // tables, then one u32 per sequence)
+    const uint64_t w_stride = (3400ull + 4ull * (seg / 4u + 2u) + 255u) & ~255ull;
     void* scratch = nullptr;
-    HIP_TRY(hipMallocAsync(&scratch, nseg * scr_stride + nseg * 8u, s), "scratch allocation");
+    HIP_TRY(hipMallocAsync(&scratch, nseg * scr_stride + nseg * 8u + nseg * w_stride, s),
+            "scratch allocation");
     auto* scr = static_cast<uint8_t*>(scratch);
     auto* meta = reinterpret_cast<uint2*>(scr + nseg * scr_stride);
+    auto* wscr = scr + nseg * scr_stride + nseg * 8u;
     hipLaunchKernelGGL(bitar_hip::zstd_parse_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in, n,
                        seg, scr, scr_stride, meta);
     hipLaunchKernelGGL(bitar_hip::zstd_entropy_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
                        n, seg, scr, scr_stride, meta, slab, slot_stride, dsts, d_sizes,
-                       err_word(ctx, s));
+                       err_word(ctx, s), wscr, w_stride);
+    hipLaunchKernelGGL(bitar_hip::zstd_walk_kernel, dim3((uint32_t)((nseg + 15) / 16)), dim3(64),
+                       0, s, scr, scr_stride, seg, (uint32_t)nseg, wscr, w_stride);
+    hipLaunchKernelGGL(bitar_hip::zstd_emit_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in, n,
+                       seg, scr, scr_stride, slab, slot_stride, dsts, d_sizes, wscr, w_stride);
     const hipError_t le = hipGetLastError();
     HIP_TRY(hipFreeAsync(scratch, s), "scratch release");
     HIP_TRY(le, "compress launch");

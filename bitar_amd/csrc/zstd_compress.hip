@@ -113,6 +113,16 @@ __host__ __device__ constexpr uint64_t scratch_stride(uint32_t seg) {
   return (lit_cap(seg) + 8ull * (seg / 4u + 2u) + 255u) & ~255ull;
 }
 
+// walk scratch (pass 2 -> zstd_walk_kernel -> zstd_emit_kernel), per segment: a 16-word record
+// (kW*), the FSE state tables (u16, kTabDummy + 1) and transforms (3 x 64 u32), then one u32
+// per sequence: its three chains' state bits (OF, then ML, then LL) | their count << 26
+enum : uint32_t { kWHanded = 0, kWP0, kWBlk, kWN, kWNseq, kWAls, kWSt0, kWSt1, kWSt2 };
+constexpr uint32_t kWTabs = 64, kWTr = kWTabs + 2 * 1284, kWWords = kWTr + 3 * 64 * 4;
+static_assert(kWWords == 3400, "runtime.hip sizes the walk scratch with this header");
+__host__ __device__ constexpr uint64_t walk_stride(uint32_t seg) {
+  return ((uint64_t)kWWords + 4ull * (seg / 4u + 2u) + 255u) & ~255ull;
+}
+
 // ---- pass 1: the parse, literals + sequence records ---------------------------------------
 struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the literal area
   GMEM uint2* seqs;
@@ -545,7 +555,8 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     uint8_t* __restrict__ scratch, uint64_t sstride, const uint2* __restrict__ meta,
     uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
-    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err, uint8_t* __restrict__ wscr,
+    uint64_t wstride) {
   using namespace cmp;
   using namespace zse;
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
@@ -841,89 +852,26 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     ZSE_PHASE(5)
     o.put_lds(L.desc, L.u[1]);
     const uint32_t al_ll = L.u[2], al_of = L.u[3], al_ml = L.u[4];
-    // the bitstream, last sequence first (oracle bo_zstd_compress_block).  Per 64 sequences
-    // (highest first): every lane stores its sequence's three symbol transforms; lanes 0..2
-    // walk the OF / ML / LL state chains, sequence 63 down to 0, writing the state bits back
-    // over the transforms; then every lane places its field (states, then LL, ML, OF extra
-    // bits) by a prefix sum.
-    const uint32_t p0 = o.op;
-    uint32_t bits = 0, zeroed = p0;
-    uint32_t st = 0;  // lane c < 3: the state of chain c (OF, ML, LL)
-    const uint32_t top = nseq - 1;
-    const uint32_t cl = lane < 3 ? lane : 3u;
-    const uint32_t tb = cl == 0 ? kTabOF : cl == 1 ? kTabML : cl == 2 ? kTabLL : kTabDummy;
-    const uint32_t m_of = cl == 0 ? ~0u : 0u, m_ml = cl == 1 ? ~0u : 0u, m_ll = cl == 2 ? ~0u : 0u;
-    uint2 prec = seqs[(top >> 6) * kWave + lane < nseq ? (top >> 6) * kWave + lane : top];
-    for (int32_t c = (int32_t)(top >> 6); c >= 0 && !o.overflow; --c) {
-      const uint32_t j = (uint32_t)c * kWave + lane;
-      const bool act = j < nseq;
-      const uint2 rec = prec;
-      if (c > 0) prec = seqs[(uint32_t)(c - 1) * kWave + lane];  // prefetch the next step
-      const uint32_t ll = rec.x & 0x1FFFFu, ov = rec.x >> 17, mlb = rec.y - 3u;
-      const uint32_t llc = ll_code(ll), mlc = ml_code(rec.y), ofc = hb32(ov);
-      lds_order();
-      const uint32_t eOF = L.tr[1][ofc], eML = L.tr[2][mlc], eLL = L.tr[0][llc];
-      // the chain lane's transform of sequence k: readlanes (no LDS round trip on the
-      // state chain, whose only memory access is the state table)
-      auto tr_of = [&](uint32_t k) __attribute__((always_inline)) {  // (no branches)
-        return (readlane(eOF, k) & m_of) | (readlane(eML, k) & m_ml) | (readlane(eLL, k) & m_ll);
-      };
-      // per sequence lane: each chain's state bits | their count << 24 (written by
-      // writelane: no LDS store on the chain)
-      uint32_t w0 = 0, w1 = 0, w2 = 0;
-      int32_t k = 63;
-      if (c == (int32_t)(top >> 6)) {  // the last sequence initialises the three states
-        k = (int32_t)(top & 63u);
-        const uint32_t e = tr_of((uint32_t)k);
-        const uint32_t d = tr_d(e);
-        const uint32_t nbo = (d + (1u << 15)) >> 16;
-        const uint32_t val = (nbo << 16) - d;
-        lds_order();
-        st = L.tabs[tb + (uint32_t)((int32_t)(val >> nbo) + tr_f(e))];  // no state bits
-        --k;
-      }
-#ifdef BITAR_ZSTD_NOWALK
-      k = -1;
-#endif
-      for (; k >= 0; --k) {
-        const uint32_t e = tr_of((uint32_t)k);
-        const uint32_t nb = (st + tr_d(e)) >> 16;
-        const uint32_t out = (st & ((1u << nb) - 1u)) | (nb << 24);
-        lds_order();
-        st = L.tabs[tb + (uint32_t)((int32_t)(st >> nb) + tr_f(e))];
-        w0 = writelane(w0, readlane(out, 0), (uint32_t)k);
-        w1 = writelane(w1, readlane(out, 1), (uint32_t)k);
-        w2 = writelane(w2, readlane(out, 2), (uint32_t)k);
-      }
-      const uint32_t nof = w0 >> 24, nml = w1 >> 24, nll = w2 >> 24;
-      const uint64_t stb = (uint64_t)(w0 & 0xFFFFFFu) | ((uint64_t)(w1 & 0xFFFFFFu) << nof) |
-                           ((uint64_t)(w2 & 0xFFFFFFu) << (nof + nml));
-      const uint32_t stn = nof + nml + nll;
-      const uint32_t llb = sT.ll_bits[llc], mlbits = sT.ml_bits[mlc];
-      // part 0: state bits + literal-length extra (<= 26 + 16); part 1: match-length extra,
-      // then offset extra (<= 16 + 16)
-      const uint64_t f0 = stb | ((uint64_t)(ll & ((1u << llb) - 1u)) << stn);
-      const uint64_t f1 = (uint64_t)(mlb & ((1u << mlbits) - 1u)) |
-                          ((uint64_t)(ov & ((1u << ofc) - 1u)) << mlbits);
-#ifndef BITAR_ZSTD_NOPUT
-      o.put_bits(act ? f0 : 0u, act ? stn + llb : 0u, act ? f1 : 0u, act ? mlbits + ofc : 0u,
-                 p0, bits, zeroed);
-#else
-      if (lane == 0) L.u[8] += (uint32_t)f0 + (uint32_t)f1;
-#endif
-    }
+    // The sequence bitstream goes to two more launches (the state chains walked on four
+    // lanes per segment by zstd_walk_kernel, the fields placed by zstd_emit_kernel): hand
+    // the tables and where the bitstream starts over, with everything before it in HBM.
     if (!o.overflow) {
-      // final states (ML, OF, LL: the decoder reads LL first) and the end mark
-      const uint32_t sOF = readlane(st, 0), sML = readlane(st, 1), sLL = readlane(st, 2);
-      const uint64_t fin = (uint64_t)(sML & ((1u << al_ml) - 1u)) |
-                           ((uint64_t)(sOF & ((1u << al_of) - 1u)) << al_ml) |
-                           ((uint64_t)(sLL & ((1u << al_ll) - 1u)) << (al_ml + al_of)) |
-                           (1ull << (al_ml + al_of + al_ll));
-      const uint32_t fn = al_ml + al_of + al_ll + 1;
-      o.put_bits(lane == 0 ? fin : 0u, lane == 0 ? fn : 0u, 0, 0, p0, bits, zeroed);
-      o.op = p0 + ((bits + 7) >> 3);
+      GMEM uint32_t* w = global_ptr(reinterpret_cast<uint32_t*>(wscr + (uint64_t)i_seg * wstride));
+      o.flush(o.op, true);
+      lds_order();
+      for (uint32_t k = lane; k < (kTabDummy + 1 + 1) / 2; k += kWave)
+        w[kWTabs / 4 + k] = reinterpret_cast<const uint32_t*>(L.tabs)[k];
+      for (uint32_t k = lane; k < 3 * 64; k += kWave) w[kWTr / 4 + k] = (&L.tr[0][0])[k];
+      const uint32_t rv = lane == kWHanded ? 1u : lane == kWP0 ? o.op : lane == kWBlk ? blk
+                          : lane == kWN ? n : lane == kWNseq ? nseq
+                          : al_ll | (al_of << 8) | (al_ml << 16);
+      if (lane <= kWAls) w[lane] = rv;
+      return;
     }
   }
+  // nothing handed over (no sequences, or the slot overflowed): the record says so
+  if (lane == 0)
+    reinterpret_cast<GMEM uint32_t*>(global_ptr(wscr + (uint64_t)i_seg * wstride))[kWHanded] = 0u;
 
   // ---- the block: compressed, or raw when that is not smaller ----
   const bool stored = o.overflow || o.op - (blk + 3) >= n;
@@ -944,6 +892,201 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
   if (lane < 3) o.dst[blk + lane] = (uint8_t)(hdr >> (8 * lane));
   if (lane == 0) sizes[i_seg] = o.op;
   (void)err;
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t zsq_qbcast(uint32_t v) {  // lane K of each quad, to all four
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xF, 0xF, false);
+}
+
+// ---- pass 3: the FSE state chains, four lanes per segment ----------------------------------
+// Lane 4 l + j of the wave walks chain j (0 offsets, 1 match lengths, 2 literal lengths; 3
+// repeats 0) of segment blockIdx.x * 16 + l, last sequence first, with the segment's state
+// table and transforms in LDS: the three chains of a segment are independent, so each is a
+// lane's own loop (the wave kernel walked them one sequence at a time with readlanes).  Per
+// sequence the quad packs the three chains' state bits into one word (OF, then ML, then LL,
+// count << 26) -- the `stb` / `stn` of the old walk -- stored 8 at a time; the final states
+// go to the segment's record.  Same arithmetic as the walk it replaces (oracle
+// bo_zstd_compress_block), so the bitstream is unchanged bit for bit.
+constexpr uint32_t kWalkSegs = 16;
+__global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict__ scratch,
+                                                        uint64_t sstride, uint32_t seg,
+                                                        uint32_t nseg, uint8_t* __restrict__ wscr,
+                                                        uint64_t wstride) {
+  using namespace cmp;
+  using namespace zse;
+  __shared__ __attribute__((aligned(16))) uint16_t tabs[kWalkSegs][1284];
+  __shared__ uint32_t trs[kWalkSegs][3][64];
+  const uint32_t lane = lane_id();
+  for (uint32_t k = lane; k < sizeof(Tabs); k += kWave)
+    reinterpret_cast<uint8_t*>(&sT)[k] = reinterpret_cast<const uint8_t*>(&kT)[k];
+  for (uint32_t l = 0; l < kWalkSegs; ++l) {
+    const uint32_t il = blockIdx.x * kWalkSegs + l;
+    if (il >= nseg) break;
+    const GMEM uint32_t* w = global_ptr(reinterpret_cast<const uint32_t*>(wscr + (uint64_t)il * wstride));
+    if (w[kWHanded] != 1u) continue;
+    for (uint32_t k = lane; k < 1284 / 2; k += kWave)
+      reinterpret_cast<uint32_t*>(tabs[l])[k] = w[kWTabs / 4 + k];
+    for (uint32_t k = lane; k < 3 * 64; k += kWave) (&trs[l][0][0])[k] = w[kWTr / 4 + k];
+  }
+  lds_order();
+  const uint32_t l = lane >> 2, j = lane & 3u;
+  const uint32_t i = blockIdx.x * kWalkSegs + l;
+  if (i >= nseg) return;  // quad-uniform
+  GMEM uint32_t* w = global_ptr(reinterpret_cast<uint32_t*>(wscr + (uint64_t)i * wstride));
+  if (w[kWHanded] != 1u) return;
+  const uint32_t nseq = w[kWNseq];
+  const GMEM uint2* seqs = reinterpret_cast<const GMEM uint2*>(
+      global_ptr(scratch + (uint64_t)i * sstride + lit_cap(seg)));
+  GMEM uint32_t* words = w + kWWords / 4;
+  const uint32_t c = j == 3 ? 0u : j;  // chain
+  const uint16_t* tb = tabs[l] + (c == 0 ? kTabOF : c == 1 ? kTabML : kTabLL);
+  const uint32_t* tr = trs[l][c == 0 ? 1 : c == 1 ? 2 : 0];
+  auto code = [&](uint2 rec) __attribute__((always_inline)) {
+    const uint32_t ll = rec.x & 0x1FFFFu, ov = rec.x >> 17;
+    return c == 0 ? hb32(ov) : c == 1 ? ml_code(rec.y) : ll_code(ll);
+  };
+  // the last sequence initialises the states (no state bits)
+  const uint32_t top = nseq - 1;
+  uint32_t st;
+  {
+    const uint32_t e = tr[code(seqs[top])];
+    const uint32_t d = tr_d(e);
+    const uint32_t nbo = (d + (1u << 15)) >> 16;
+    const uint32_t val = (nbo << 16) - d;
+    st = tb[(int32_t)(val >> nbo) + tr_f(e)];
+  }
+  // one chain step: this chain's state bits | count << 16 (only the state table read is on
+  // the loop-carried chain); pack: the quad's word
+  auto walk = [&](uint32_t e) __attribute__((always_inline)) {
+    const uint32_t nb = (st + tr_d(e)) >> 16;
+    const uint32_t out = (st & ((1u << nb) - 1u)) | (nb << 16);
+    st = tb[(int32_t)(st >> nb) + tr_f(e)];
+    return out;
+  };
+  auto pack = [&](uint32_t out) __attribute__((always_inline)) {
+    const uint32_t oo = zsq_qbcast<0>(out), om = zsq_qbcast<1>(out), ol = zsq_qbcast<2>(out);
+    const uint32_t nof = oo >> 16, nml = om >> 16, nll = ol >> 16;
+    return (oo & 0xFFFFu) | ((om & 0xFFFFu) << nof) | ((ol & 0xFFFFu) << (nof + nml)) |
+           ((nof + nml + nll) << 26);
+  };
+  if (j == 0) words[top] = 0u;
+  int32_t k = (int32_t)top - 1;
+  constexpr int32_t kG = 8;
+  // groups of 8: the records' transforms looked up together (independent of the states), then
+  // the chain, then the words, stored together
+  uint2 r[kG];
+#pragma unroll
+  for (int32_t g = 0; g < kG; ++g) r[g] = seqs[k - g >= 0 ? k - g : 0];
+  for (; k >= kG - 1; k -= kG) {
+    uint32_t e[kG], o[kG];
+#pragma unroll
+    for (int32_t g = 0; g < kG; ++g) e[g] = tr[code(r[g])];
+#pragma unroll
+    for (int32_t g = 0; g < kG; ++g) r[g] = seqs[k - kG - g >= 0 ? k - kG - g : 0];  // next group
+#pragma unroll
+    for (int32_t g = 0; g < kG; ++g) o[g] = walk(e[g]);
+#pragma unroll
+    for (int32_t g = 0; g < kG; ++g) o[g] = pack(o[g]);
+    if (j == 0) {
+#pragma unroll
+      for (int32_t g = 0; g < kG; ++g) words[k - g] = o[g];
+    }
+  }
+  for (; k >= 0; --k) {
+    const uint32_t o = pack(walk(tr[code(seqs[k])]));
+    if (j == 0) words[k] = o;
+  }
+  if (j < 3) w[kWSt0 + j] = st;
+}
+
+// ---- pass 4: the sequence bitstream ---------------------------------------------------------
+// One wave per handed-over segment: the fields of 64 sequences per step (highest first), the
+// final states and end mark, then the block header (or the raw block when the compressed one
+// is not smaller) -- the tail of zstd_entropy_kernel, with the state bits from pass 3.
+__global__ __launch_bounds__(64) void zstd_emit_kernel(
+    const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
+    const uint8_t* __restrict__ scratch, uint64_t sstride, uint8_t* __restrict__ slab,
+    uint64_t slot_stride, uint8_t* const* __restrict__ dsts, uint32_t* __restrict__ sizes,
+    const uint8_t* __restrict__ wscr, uint64_t wstride) {
+  using namespace cmp;
+  using namespace zse;
+  __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
+  const uint32_t i_seg = blockIdx.x;
+  const uint64_t seg_off = (uint64_t)i_seg * seg;
+  if (seg_off >= n_total) return;
+  const GMEM uint32_t* w = global_ptr(reinterpret_cast<const uint32_t*>(wscr + (uint64_t)i_seg * wstride));
+  if (uniform(w[kWHanded]) != 1u) return;
+  const uint32_t lane = lane_id();
+  for (uint32_t k = lane; k < sizeof(Tabs); k += kWave)
+    reinterpret_cast<uint8_t*>(&sT)[k] = reinterpret_cast<const uint8_t*>(&kT)[k];
+  lds_order();
+  const uint32_t p0 = uniform(w[kWP0]), blk = uniform(w[kWBlk]), n = uniform(w[kWN]);
+  const uint32_t nseq = uniform(w[kWNseq]), als = uniform(w[kWAls]);
+  const uint32_t al_ll = als & 0xFFu, al_of = (als >> 8) & 0xFFu, al_ml = als >> 16;
+  const GMEM uint8_t* src = global_ptr(input + seg_off);
+  const GMEM uint2* seqs = reinterpret_cast<const GMEM uint2*>(
+      global_ptr(scratch + (uint64_t)i_seg * sstride + lit_cap(seg)));
+  const GMEM uint32_t* words = w + kWWords / 4;
+  EntOut o;
+  o.ring = obuf;
+  o.dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
+  o.cap = slot_stride;
+  o.op = p0;
+  o.flushed = p0;  // the frame up to p0 is in the slot (zstd_entropy_kernel)
+  o.overflow = false;
+  uint32_t bits = 0, zeroed = p0;
+  const uint32_t top = nseq - 1;
+  uint2 prec = seqs[(top >> 6) * kWave + lane < nseq ? (top >> 6) * kWave + lane : top];
+  uint32_t pw = words[(top >> 6) * kWave + lane < nseq ? (top >> 6) * kWave + lane : top];
+  for (int32_t c = (int32_t)(top >> 6); c >= 0 && !o.overflow; --c) {
+    const uint32_t j = (uint32_t)c * kWave + lane;
+    const bool act = j < nseq;
+    const uint2 rec = prec;
+    const uint32_t wd = pw;
+    if (c > 0) {  // prefetch the next step
+      prec = seqs[(uint32_t)(c - 1) * kWave + lane];
+      pw = words[(uint32_t)(c - 1) * kWave + lane];
+    }
+    const uint32_t ll = rec.x & 0x1FFFFu, ov = rec.x >> 17, mlb = rec.y - 3u;
+    const uint32_t llc = ll_code(ll), mlc = ml_code(rec.y), ofc = hb32(ov);
+    const uint64_t stb = wd & 0x3FFFFFFu;
+    const uint32_t stn = wd >> 26;
+    const uint32_t llb = sT.ll_bits[llc], mlbits = sT.ml_bits[mlc];
+    // part 0: state bits + literal-length extra (<= 26 + 16); part 1: match-length extra,
+    // then offset extra (<= 16 + 16)
+    const uint64_t f0 = stb | ((uint64_t)(ll & ((1u << llb) - 1u)) << stn);
+    const uint64_t f1 = (uint64_t)(mlb & ((1u << mlbits) - 1u)) |
+                        ((uint64_t)(ov & ((1u << ofc) - 1u)) << mlbits);
+    o.put_bits(act ? f0 : 0u, act ? stn + llb : 0u, act ? f1 : 0u, act ? mlbits + ofc : 0u,
+               p0, bits, zeroed);
+  }
+  if (!o.overflow) {
+    // final states (ML, OF, LL: the decoder reads LL first) and the end mark
+    const uint32_t sOF = uniform(w[kWSt0]), sML = uniform(w[kWSt1]), sLL = uniform(w[kWSt2]);
+    const uint64_t fin = (uint64_t)(sML & ((1u << al_ml) - 1u)) |
+                         ((uint64_t)(sOF & ((1u << al_of) - 1u)) << al_ml) |
+                         ((uint64_t)(sLL & ((1u << al_ll) - 1u)) << (al_ml + al_of)) |
+                         (1ull << (al_ml + al_of + al_ll));
+    const uint32_t fn = al_ml + al_of + al_ll + 1;
+    o.put_bits(lane == 0 ? fin : 0u, lane == 0 ? fn : 0u, 0, 0, p0, bits, zeroed);
+    o.op = p0 + ((bits + 7) >> 3);
+  }
+  // the block: compressed, or raw when that is not smaller
+  const bool stored = o.overflow || o.op - (blk + 3) >= n;
+  uint32_t hdr;
+  if (stored) {
+    global_fence_wave();  // earlier stores to this range land first
+    wave_copy_global(o.dst + blk + 3, src, n);
+    o.op = blk + 3 + n;
+    hdr = 1u | (n << 3);
+  } else {
+    hdr = 1u | (2u << 1) | ((o.op - (blk + 3)) << 3);
+    o.flush(o.op, true);
+  }
+  global_fence_wave();
+  if (lane < 3) o.dst[blk + lane] = (uint8_t)(hdr >> (8 * lane));
+  if (lane == 0) sizes[i_seg] = o.op;
 }
 
 }  // namespace bitar_hip
