@@ -348,8 +348,8 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
     // then {nlit, nseq} per segment
     const uint64_t scr_stride = ((uint64_t)seg + 15u & ~15ull) + 8ull * (seg / 4u + 2u) + 255u & ~255ull;
     // + the chain-walk scratch (zstd_compress.hip walk_stride: a 3400-byte header with the
-    // tables, then one u32 per sequence)
-    const uint64_t w_stride = (3400ull + 4ull * (seg / 4u + 2u) + 255u) & ~255ull;
+    // tables, then 10 bytes per sequence)
+    const uint64_t w_stride = (3400ull + 10ull * (seg / 4u + 2u) + 255u) & ~255ull;
     void* scratch = nullptr;
     HIP_TRY(hipMallocAsync(&scratch, nseg * scr_stride + nseg * 8u + nseg * w_stride, s),
             "scratch allocation");

@@ -114,13 +114,15 @@ __host__ __device__ constexpr uint64_t scratch_stride(uint32_t seg) {
 }
 
 // walk scratch (pass 2 -> zstd_walk_kernel -> zstd_emit_kernel), per segment: a 16-word record
-// (kW*), the FSE state tables (u16, kTabDummy + 1) and transforms (3 x 64 u32), then one u32
-// per sequence: its three chains' state bits (OF, then ML, then LL) | their count << 26
+// (kW*), the FSE state tables (u16, kTabDummy + 1) and transforms (3 x 64 u32); then per
+// sequence its three codes (u32: LL | OF << 6 | ML << 11, written by pass 2) and each
+// chain's state bits | their count << 12 (u16, chains OF, ML, LL one array each)
 enum : uint32_t { kWHanded = 0, kWP0, kWBlk, kWN, kWNseq, kWAls, kWSt0, kWSt1, kWSt2 };
 constexpr uint32_t kWTabs = 64, kWTr = kWTabs + 2 * 1284, kWWords = kWTr + 3 * 64 * 4;
 static_assert(kWWords == 3400, "runtime.hip sizes the walk scratch with this header");
+__host__ __device__ constexpr uint32_t walk_cap(uint32_t seg) { return seg / 4u + 2u; }  // >= nseq
 __host__ __device__ constexpr uint64_t walk_stride(uint32_t seg) {
-  return ((uint64_t)kWWords + 4ull * (seg / 4u + 2u) + 255u) & ~255ull;
+  return ((uint64_t)kWWords + 10ull * walk_cap(seg) + 255u) & ~255ull;
 }
 
 // ---- pass 1: the parse, literals + sequence records ---------------------------------------
@@ -796,6 +798,8 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     for (uint32_t k = lane; k < 3 * 64; k += kWave) (&L.sh[0][0])[k] = 0;
     lds_order();
     uint32_t c0r = 1, c1r = 4, c2r = 8;  // the history before the step (uniform)
+    GMEM uint32_t* wcodes = reinterpret_cast<GMEM uint32_t*>(
+        global_ptr(wscr + (uint64_t)i_seg * wstride + kWWords));
     uint2 nrec = lane < nseq ? seqs[lane] : make_uint2(0, 3);
     for (uint32_t c0 = 0; c0 < nseq; c0 += kWave) {
       const uint32_t j = c0 + lane;
@@ -827,10 +831,12 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       c1r = readlane(r1a, cnt - 1);
       c2r = readlane(r2a, cnt - 1);
       if (act) {
-        atomicAdd(&L.sh[0][ll_code(ll)], 1u);
-        atomicAdd(&L.sh[1][hb32(ov)], 1u);
-        atomicAdd(&L.sh[2][ml_code(ml)], 1u);
+        const uint32_t llc = ll_code(ll), ofc = hb32(ov), mlc = ml_code(ml);
+        atomicAdd(&L.sh[0][llc], 1u);
+        atomicAdd(&L.sh[1][ofc], 1u);
+        atomicAdd(&L.sh[2][mlc], 1u);
         seqs[j] = make_uint2(ll | (ov << 17), ml);
+        wcodes[j] = llc | (ofc << 6) | (mlc << 11);  // for zstd_walk_kernel
       }
     }
     lds_order();
@@ -936,66 +942,57 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
   GMEM uint32_t* w = global_ptr(reinterpret_cast<uint32_t*>(wscr + (uint64_t)i * wstride));
   if (w[kWHanded] != 1u) return;
   const uint32_t nseq = w[kWNseq];
-  const GMEM uint2* seqs = reinterpret_cast<const GMEM uint2*>(
-      global_ptr(scratch + (uint64_t)i * sstride + lit_cap(seg)));
-  GMEM uint32_t* words = w + kWWords / 4;
+  const uint32_t cap = walk_cap(seg);
+  const GMEM uint32_t* codes = w + kWWords / 4;
+  GMEM uint16_t* outs = reinterpret_cast<GMEM uint16_t*>(w + kWWords / 4 + cap) + (j < 3 ? j : 0u) * cap;
   const uint32_t c = j == 3 ? 0u : j;  // chain
   const uint16_t* tb = tabs[l] + (c == 0 ? kTabOF : c == 1 ? kTabML : kTabLL);
   const uint32_t* tr = trs[l][c == 0 ? 1 : c == 1 ? 2 : 0];
-  auto code = [&](uint2 rec) __attribute__((always_inline)) {
-    const uint32_t ll = rec.x & 0x1FFFFu, ov = rec.x >> 17;
-    return c == 0 ? hb32(ov) : c == 1 ? ml_code(rec.y) : ll_code(ll);
-  };
+  // this chain's code in the code word (LL 6 bits, OF 5, ML 6)
+  const uint32_t csh = c == 0 ? 6u : c == 1 ? 11u : 0u, cmask = c == 0 ? 31u : 63u;
+  auto code = [&](uint32_t cw) __attribute__((always_inline)) { return (cw >> csh) & cmask; };
   // the last sequence initialises the states (no state bits)
   const uint32_t top = nseq - 1;
   uint32_t st;
   {
-    const uint32_t e = tr[code(seqs[top])];
+    const uint32_t e = tr[code(codes[top])];
     const uint32_t d = tr_d(e);
     const uint32_t nbo = (d + (1u << 15)) >> 16;
     const uint32_t val = (nbo << 16) - d;
     st = tb[(int32_t)(val >> nbo) + tr_f(e)];
   }
-  // one chain step: this chain's state bits | count << 16 (only the state table read is on
-  // the loop-carried chain); pack: the quad's word
+  // one chain step: this chain's state bits | count << 12 (only the state table read is on
+  // the loop-carried chain)
   auto walk = [&](uint32_t e) __attribute__((always_inline)) {
     const uint32_t nb = (st + tr_d(e)) >> 16;
-    const uint32_t out = (st & ((1u << nb) - 1u)) | (nb << 16);
+    const uint32_t out = (st & ((1u << nb) - 1u)) | (nb << 12);
     st = tb[(int32_t)(st >> nb) + tr_f(e)];
     return out;
   };
-  auto pack = [&](uint32_t out) __attribute__((always_inline)) {
-    const uint32_t oo = zsq_qbcast<0>(out), om = zsq_qbcast<1>(out), ol = zsq_qbcast<2>(out);
-    const uint32_t nof = oo >> 16, nml = om >> 16, nll = ol >> 16;
-    return (oo & 0xFFFFu) | ((om & 0xFFFFu) << nof) | ((ol & 0xFFFFu) << (nof + nml)) |
-           ((nof + nml + nll) << 26);
-  };
-  if (j == 0) words[top] = 0u;
+  if (j < 3) outs[top] = 0;
   int32_t k = (int32_t)top - 1;
   constexpr int32_t kG = 8;
-  // groups of 8: the records' transforms looked up together (independent of the states), then
-  // the chain, then the words, stored together
-  uint2 r[kG];
+  // groups of 8: the transforms looked up together (independent of the states), then the
+  // chain; the lane's 8 outputs stored together
+  uint32_t r[kG];
 #pragma unroll
-  for (int32_t g = 0; g < kG; ++g) r[g] = seqs[k - g >= 0 ? k - g : 0];
+  for (int32_t g = 0; g < kG; ++g) r[g] = codes[k - g >= 0 ? k - g : 0];
   for (; k >= kG - 1; k -= kG) {
     uint32_t e[kG], o[kG];
 #pragma unroll
     for (int32_t g = 0; g < kG; ++g) e[g] = tr[code(r[g])];
 #pragma unroll
-    for (int32_t g = 0; g < kG; ++g) r[g] = seqs[k - kG - g >= 0 ? k - kG - g : 0];  // next group
+    for (int32_t g = 0; g < kG; ++g) r[g] = codes[k - kG - g >= 0 ? k - kG - g : 0];  // next group
 #pragma unroll
     for (int32_t g = 0; g < kG; ++g) o[g] = walk(e[g]);
+    if (j < 3) {
 #pragma unroll
-    for (int32_t g = 0; g < kG; ++g) o[g] = pack(o[g]);
-    if (j == 0) {
-#pragma unroll
-      for (int32_t g = 0; g < kG; ++g) words[k - g] = o[g];
+      for (int32_t g = 0; g < kG; ++g) outs[k - g] = (uint16_t)o[g];
     }
   }
   for (; k >= 0; --k) {
-    const uint32_t o = pack(walk(tr[code(seqs[k])]));
-    if (j == 0) words[k] = o;
+    const uint32_t o = walk(tr[code(codes[k])]);
+    if (j < 3) outs[k] = (uint16_t)o;
   }
   if (j < 3) w[kWSt0 + j] = st;
 }
@@ -1027,7 +1024,8 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
   const GMEM uint8_t* src = global_ptr(input + seg_off);
   const GMEM uint2* seqs = reinterpret_cast<const GMEM uint2*>(
       global_ptr(scratch + (uint64_t)i_seg * sstride + lit_cap(seg)));
-  const GMEM uint32_t* words = w + kWWords / 4;
+  const uint32_t cap = walk_cap(seg);
+  const GMEM uint16_t* outs = reinterpret_cast<const GMEM uint16_t*>(w + kWWords / 4 + cap);
   EntOut o;
   o.ring = obuf;
   o.dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
@@ -1038,7 +1036,13 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
   uint32_t bits = 0, zeroed = p0;
   const uint32_t top = nseq - 1;
   uint2 prec = seqs[(top >> 6) * kWave + lane < nseq ? (top >> 6) * kWave + lane : top];
-  uint32_t pw = words[(top >> 6) * kWave + lane < nseq ? (top >> 6) * kWave + lane : top];
+  auto word = [&](uint32_t j) __attribute__((always_inline)) {  // OF | ML | LL bits, counts
+    const uint32_t oo = outs[j], om = outs[cap + j], ol = outs[2 * cap + j];
+    const uint32_t nof = oo >> 12, nml = om >> 12, nll = ol >> 12;
+    return (oo & 0xFFFu) | ((om & 0xFFFu) << nof) | ((ol & 0xFFFu) << (nof + nml)) |
+           ((nof + nml + nll) << 26);
+  };
+  uint32_t pw = word((top >> 6) * kWave + lane < nseq ? (top >> 6) * kWave + lane : top);
   for (int32_t c = (int32_t)(top >> 6); c >= 0 && !o.overflow; --c) {
     const uint32_t j = (uint32_t)c * kWave + lane;
     const bool act = j < nseq;
@@ -1046,7 +1050,7 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
     const uint32_t wd = pw;
     if (c > 0) {  // prefetch the next step
       prec = seqs[(uint32_t)(c - 1) * kWave + lane];
-      pw = words[(uint32_t)(c - 1) * kWave + lane];
+      pw = word((uint32_t)(c - 1) * kWave + lane);
     }
     const uint32_t ll = rec.x & 0x1FFFFu, ov = rec.x >> 17, mlb = rec.y - 3u;
     const uint32_t llc = ll_code(ll), mlc = ml_code(rec.y), ofc = hb32(ov);
