@@ -73,12 +73,13 @@ KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
            # decompress = inflate_lanes_kernel (lane per segment) + inflate_kernel in
            # defer-only mode; timed together
            "deflate": ("deflate_compress_kernel", "inflate_lanes_kernel"),
-           # compress = zstd_parse_kernel + zstd_entropy_kernel; decompress =
+           # compress = zstd_parse_kernel + zstd_entropy_kernel + zstd_walk_kernel (FSE state
+           # chains, a lane per chain) + zstd_emit_kernel (sequence bitstream); decompress =
            # zstd_lanes_kernel (predefined-table frames) + zstd_decompress_kernel (headers,
            # tables) + zstd_hlit_kernel (Huffman literals) + zstd_seqdec_kernel (FSE chains ->
            # records, lane per segment) + zstd_exec_kernel (records -> output, wave per
            # segment); each timed together
-           "zstd": ("zstd_parse_kernel+zstd_entropy_kernel",
+           "zstd": ("zstd_parse_kernel+zstd_entropy_kernel+zstd_walk_kernel+zstd_emit_kernel",
                     "zstd_decompress_kernel+zstd_hlit_kernel+zstd_seqdec_kernel+zstd_exec_kernel"),
            # compress = deflate_dyn_parse_kernel + deflate_dyn_emit_kernel (one event pair
            # brackets both); decompress = inflate_lanes_kernel deferring every dynamic block

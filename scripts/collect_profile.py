@@ -22,10 +22,12 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # the x2 correction is for 16-B-per-lane streaming reads; the lane-per-segment decoders
 # (zstd_lanes_kernel, inflate_lanes_kernel, zstd_hlit_kernel, zstd_handoff_kernel,
-# zstd_seqdec_kernel) and the record executor (8-B records, 1-B literals) read 1-8 B per lane,
+# zstd_seqdec_kernel, zstd_walk_kernel) and the record executor / bitstream emitter (8-B records,
+# 1-B literals, 2-4-B state words) read 1-8 B per lane,
 # so their FETCH_SIZE is taken as reported
 FETCH_FACTOR = {"zstd_lanes_kernel": 1.0, "inflate_lanes_kernel": 1.0, "zstd_hlit_kernel": 1.0,
-                "zstd_handoff_kernel": 1.0, "zstd_seqdec_kernel": 1.0, "zstd_exec_kernel": 1.0}
+                "zstd_handoff_kernel": 1.0, "zstd_seqdec_kernel": 1.0, "zstd_exec_kernel": 1.0,
+                "zstd_walk_kernel": 1.0, "zstd_emit_kernel": 1.0}
 
 
 def per_kernel(path):
