@@ -677,8 +677,8 @@ struct Frame {
 };
 
 // one compressed block at stream [p, p + len)
-// 0: malformed, 1: decoded, 2: handed off (the sequences of the frame's last block go to the
-// lane executor: hand != null, last block, no checksum, >= kHandMinSeq sequences)
+// 0: malformed, 1: decoded, 2: handed off (the frame's last block goes to the lane kernels:
+// hand != null, i.e. no checksum, and last block)
 __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr, uint32_t p,
                       uint32_t len, GMEM uint32_t* hand, bool last_block, uint32_t fsz,
                       uint32_t fcs) {
@@ -760,7 +760,8 @@ __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs
       if (ns >= 128 && ns < 255 && qs + 2 <= end) ns = ((ns - 128) << 8) + load_le(s, win, qs + 1, 1);
       else if (ns == 255 && qs + 3 <= end) ns = load_le(s, win, qs + 1, 2) + 0x7F00u;
       else if (ns >= 128) ns = 0;
-      lanes_lits = ns >= zhand::kMinSeq;
+      (void)ns;
+      lanes_lits = true;  // every last block is handed over, with or without sequences
     }
     if (lanes_lits) {
       lds_order();
@@ -861,7 +862,7 @@ __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs
     }
     if (q >= end) return 0;
     ZP_END(3, tm);
-    if (hand && last_block && nseq >= zhand::kMinSeq) {
+    if (hand && last_block) {
       // everything before this block is output; the executor continues from s.op
       flush(s, ring, s.op, true);
       global_fence_wave();
@@ -1064,6 +1065,18 @@ __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs
     ZP_END(4, tq);
   } else if (q != end) {
     return 0;
+  } else if (hand && last_block) {
+    // no sequences: the literals go over too (their Huffman streams may be with
+    // zstd_hlit_kernel already: a block of 64 Ki literals and no match -- libzstd writes
+    // such blocks for incompressible columns -- would be one wave's serial decode)
+    flush(s, ring, s.op, true);
+    global_fence_wave();
+    const uint32_t rv = lane <= 1 ? q : lane == 2 ? 0u : lane == 3 ? (lt << 24)
+                        : lane == 4 ? (lt == 0 ? lit_stream : lit_byte)
+                        : lane == 5 ? regen : lane == 6 ? s.op : lane == 7 ? fr.rep0
+                        : lane == 8 ? fr.rep1 : lane == 9 ? fr.rep2 : lane == 10 ? fsz : fcs;
+    if (lane < 12) hand[lane] = rv;
+    return 2;
   }
   if ((uint64_t)s.op + (regen - lp) > s.cap) return 0;
   copy_lits(regen - lp);

@@ -12,7 +12,7 @@ namespace bitar_hip {
 
 namespace zhand {
 
-constexpr uint32_t kRec = 32, kCells = 512, kHufWords = 1024, kMinSeq = 16;
+constexpr uint32_t kRec = 32, kCells = 512, kHufWords = 1024;
 constexpr uint32_t kCellsAt = kRec, kHufAt = kRec + 3 * kCells;
 constexpr uint64_t kStride = 4ull * (kRec + 3 * kCells + kHufWords);
 constexpr uint32_t kHanded = 0xFFFFFFFDu;  // produced[i] while the lane kernels own segment i

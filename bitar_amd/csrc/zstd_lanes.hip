@@ -600,8 +600,12 @@ __global__ __launch_bounds__(64) void zstd_handoff_kernel(
   b.C = PBits::at(src, b.ptr, q);
   b.N = PBits::at(src, b.ptr - 8, q);
   const uint32_t lastb = (uint32_t)(b.C >> 56);
-  if (lastb == 0) ok = false;
-  if (ok) {
+  if (nseq == 0) {
+    ok = q == end;  // no sequences: no bitstream
+  } else if (lastb == 0) {
+    ok = false;
+  }
+  if (ok && nseq) {
     b.used = 8 - (31u - (uint32_t)__builtin_clz(lastb));
     uint32_t sll = b.read(al0), sof = b.read(al1), sml = b.read(al2);
     uint32_t cll = tll[sll], cof = tof[sof], cml = tml[sml];

@@ -212,8 +212,10 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
     return (uint32_t)(C >> ((64u - p - n) & 63u)) & ((1u << n) - 1u);
   };
   const uint32_t lastb = (uint32_t)(C >> 56);
-  bool ok = lastb != 0 && end == cs;
-  if (ok) {
+  bool ok = (lastb != 0 || nseq == 0) && end == cs;
+  if (nseq == 0) {
+    ok = ok && q == end;  // no sequences: no bitstream
+  } else if (ok) {
     used = 8 - (31u - (uint32_t)__builtin_clz(lastb));
     // initial states, in the order LL, OF, ML
     uint32_t cell = tab[peek(used + (t == 0 ? 0u : t == 1 ? al0 : al0 + al1), al)];
