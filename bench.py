@@ -158,6 +158,13 @@ def run_job(eng, codec_name, kind, job_bytes, seg, nstreams, steps, warmup, worl
     # per-launch durations (each event pair brackets exactly one kernel launch)
     comp_ms = [c0.elapsed_time(c1) for ce, _ in ev for c0, c1 in ce.values()]
     dec_ms = [d0.elapsed_time(d1) for _, de in ev for d0, d1 in de.values()]
+
+    def span(evs):  # first start to last end of one step's concurrent launches (ms)
+        ref = next(iter(evs.values()))[0]
+        return (max(ref.elapsed_time(e1) for _, e1 in evs.values()) -
+                min(ref.elapsed_time(e0) for e0, _ in evs.values()))
+    comp_span = [span(ce) for ce, _ in ev]
+    dec_span = [span(de) for _, de in ev]
     local = {"nbytes": job.layout.local_bytes, "nseg": job.layout.local_nseg,
              "parts": len(job.layout.parts)}
     total_c = int(job.index[-1].item())
@@ -165,6 +172,8 @@ def run_job(eng, codec_name, kind, job_bytes, seg, nstreams, steps, warmup, worl
     (elapsed, bad), (csum,) = reduce_max_sum([elapsed, 0.0 if ok else 1.0], [float(csize)], world)
     return {"elapsed": elapsed, "ok": bad == 0.0, "csize_local": csize, "csize_total": total_c,
             "t_comp": sum(comp_ms) / len(comp_ms) / 1e3, "t_dec": sum(dec_ms) / len(dec_ms) / 1e3,
+            "t_comp_span": sum(comp_span) / len(comp_span) / 1e3,
+            "t_dec_span": sum(dec_span) / len(dec_span) / 1e3,
             "local": local, "job_bytes": job_bytes}
 
 
@@ -181,13 +190,20 @@ def kernel_lines(codec_name, r, traffic_json, leg="headline"):
     kc, kd = KERNELS[codec_name]
     t_comp, t_dec = r["t_comp"], r["t_dec"]
     dominant = (kc, comp_bytes, t_comp) if t_comp >= t_dec else (kd, dec_bytes, t_dec)
+    if parts > 1:
+        # the parts' launches run at once on their queue-pair streams: one launch's duration
+        # is not its share of the GPU.  The roofline is the step's launches together: all
+        # parts' bytes over first start to last end.
+        tc, td = r["t_comp_span"], r["t_dec_span"]
+        dominant = ((f"{kc} x{parts} concurrent", comp_bytes * parts, tc) if tc >= td else
+                    (f"{kd} x{parts} concurrent", dec_bytes * parts, td))
     achieved = dominant[1] / dominant[2] / 1e9
     traffic = None
     try:
         with open(traffic_json) as f:
             # per-launch HBM bytes of this leg's kernel(s), from its own PMC passes
             tj = json.load(f)
-            parts = [tj.get(f"{leg}/{k}") for k in dominant[0].split("+")]
+            parts = [tj.get(f"{leg}/{k}") for k in dominant[0].split(" ")[0].split("+")]
             traffic = sum(parts) if all(p is not None for p in parts) else None
     except (OSError, ValueError):
         pass
