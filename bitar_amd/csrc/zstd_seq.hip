@@ -303,8 +303,11 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
     const uint64_t* __restrict__ recs, uint32_t rcap, uint32_t* __restrict__ err) {
   using namespace zsq;
   using namespace sr;
-  __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
-  __shared__ uint32_t ev[kWave];
+  // (a trash byte / word per lane after the ring and the event array: lanes with nothing to
+  // store write there instead of branching -- exec-mask changes are scalar instructions, and
+  // the scalar unit, shared by the CU's waves, bounds this kernel)
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kRing + kWave];
+  __shared__ uint32_t ev[2 * kWave];
   const uint32_t i = blockIdx.x;
   if (i >= nseg || uniform(produced[i]) != kRecs) return;
   const uint32_t lane = lane_id();
@@ -324,6 +327,8 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   // literal index j -> byte: lsrc[j] (raw / Huffman) or the RLE byte
   const GMEM uint8_t* lsrc = lt == 0 ? src + litv : s.dst + (cap - regen);
   const uint32_t lbyte = litv & 0xFFu;
+  // (a literal-less segment's lsrc may lie past the buffer: index 0 of the output instead)
+  const GMEM uint8_t* lsafe = regen ? lsrc : s.dst;
   const uintptr_t base = (uintptr_t)s.dst;
   const GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap);
   uint32_t lp = 0;
@@ -345,40 +350,35 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
       global_fence_wave();
       s.fenced = s.flushed;
     }
-    uint32_t v = 0, ptr = lane;
-    bool pend = false;
-    if (act) {
-      if (!ism) {
-        v = lt == 1 ? lbyte : (uint32_t)lsrc[from];
-      } else if (from >= xa) {
-        ptr = from - xa;
-        pend = true;
-      } else if (far) {
-        v = s.dst[from];
-      } else {
-        v = ring[(base + from) & kRingMask];
-      }
+    // every lane loads both candidates (branch-free): its literal byte (index 0 for the
+    // others) and its ring byte
+    const bool lit = act && !ism;
+    const uint32_t vl = lt == 1 ? lbyte : (uint32_t)lsafe[lit ? from : 0u];
+    lds_order();
+    const uint32_t vr = ring[(base + from) & kRingMask];
+    uint32_t v = lit ? vl : vr;
+    if (ballot(far)) {  // (rare)
+      if (far) v = s.dst[from];
     }
+    bool pend = act && ism && from >= xa;
+    uint32_t ptr = pend ? from - xa : lane;
     // sources inside this step: pointer jumping (each round halves the chains)
     while (ballot(pend)) {
       const uint32_t w = v | (pend ? 0x100u : 0u) | (ptr << 9);
       const uint32_t t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ptr << 2), (int)w);
-      if (pend) {
-        if (t & 0x100u) {
-          ptr = t >> 9;
-        } else {
-          v = t & 0xFFu;
-          pend = false;
-        }
-      }
+      const bool still = pend && (t & 0x100u);
+      v = pend && !still ? t & 0xFFu : v;
+      ptr = still ? t >> 9 : ptr;
+      pend = still;
     }
     lds_order();
-    if (act) ring[(base + x) & kRingMask] = (uint8_t)v;
+    ring[act ? (uint32_t)((base + x) & kRingMask) : kRing + lane] = (uint8_t)v;
     lds_order();
   };
   for (uint32_t kb = 0; kb < nseq; kb += kWave) {
     const uint32_t n = nseq - kb < kWave ? nseq - kb : kWave;
-    const uint64_t r = lane < n ? rec[kb + lane] : 0ull;
+    const uint64_t r0 = rec[kb + (lane < n ? lane : n - 1)];
+    const uint64_t r = lane < n ? r0 : 0ull;
     const uint32_t ll = (uint32_t)r & 0x1FFFFu, ml = lane < n ? ((uint32_t)(r >> 17) & 0x1FFFFu) + 3 : 0u,
                    off = (uint32_t)(r >> 34);
     const uint32_t inc = wave_incl_sum(ll + ml), ex = inc - (ll + ml);
@@ -403,8 +403,8 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
       ev[lane] = 0u;
       lds_order();
       const uint32_t p1 = ex - cb, p2 = ex + ll - cb;
-      if (lane < n && ll && p1 < kWave) ev[p1] = e_lit;
-      if (lane < n && p2 < kWave) ev[p2] = e_mat;
+      ev[lane < n && ll && p1 < kWave ? p1 : kWave + lane] = e_lit;
+      ev[lane < n && p2 < kWave ? p2 : kWave + lane] = e_mat;
       lds_order();
       uint32_t e = ev[lane];
       e = wave_incl_max(e > carry ? e : carry);
