@@ -19,6 +19,12 @@
 
 #include <type_traits>
 
+// token-walk form (tuning knob, scripts/build_variant.sh): 4 = walk_tokens4 (default),
+// 1 = walk_tokens, the round-1 form (kind 1 decode 2.89 -> 2.67 ms/GiB, kind 2 5.05 -> 4.49)
+#ifndef BITAR_LZ4D_WALK
+#define BITAR_LZ4D_WALK 4
+#endif
+
 namespace bitar_hip {
 
 
@@ -134,6 +140,57 @@ __device__ __forceinline__ uint32_t walk_tokens(uint32_t pw, uint32_t pr, uint32
   return out;
 }
 
+// Walk form 4 (the default).  Lane 63 is a sentinel that never qualifies, so "the next token
+// lies past the parsed lanes" needs no compare of its own: pw = next lane clamped to 63
+// (bits 0..5) | output length (bits 6..13, 255: not eligible) | unclamped next lane (bits
+// 24..30: the stream advance when the walk ends after this sequence).  The room is kept as
+// a remainder (one s_sub_u32 both subtracts and tests: its borrow is "does not fit"), the
+// word read is itself the next lane select (v_readlane takes the low 6 bits of its
+// lane-select SGPR; >= 4 instructions separate each VALU write of e / e2 from its use as a
+// lane select), and the loop is unrolled twice: 3 SALU + 3 VALU per sequence (form 1: 8 + 3;
+// the batch is bound by the CU's shared scalar unit as much as by the VALU).  `adv` = the
+// stream bytes consumed.
+__device__ __forceinline__ uint32_t walk_tokens4(uint32_t pw, uint32_t pr, uint32_t lim,
+                                                 uint32_t& adv, uint32_t& vrec) {
+  uint32_t out, e, e2, r, ol, rem, m0_saved;
+  __asm__ volatile(
+      "s_mov_b32 %[m0s], m0\n"
+      "s_mov_b32 %[e], 0\n"
+      "s_mov_b32 %[e2], 0\n"
+      "s_mov_b32 %[rem], %[lim]\n"
+      "s_mov_b32 m0, 0\n"
+      "L_w4_%=:\n"
+      "v_readlane_b32 %[e2], %[pw], %[e]\n"
+      "v_readlane_b32 %[r], %[pr], %[e]\n"
+      "s_bfe_u32 %[ol], %[e2], 0x80006\n"
+      "s_sub_u32 %[rem], %[rem], %[ol]\n"
+      "s_cbranch_scc1 L_da_%=\n"
+      "v_writelane_b32 %[vr], %[r], m0\n"
+      "s_add_u32 m0, m0, %[ol]\n"
+      "v_readlane_b32 %[e], %[pw], %[e2]\n"
+      "v_readlane_b32 %[r], %[pr], %[e2]\n"
+      "s_bfe_u32 %[ol], %[e], 0x80006\n"
+      "s_sub_u32 %[rem], %[rem], %[ol]\n"
+      "s_cbranch_scc1 L_db_%=\n"
+      "v_writelane_b32 %[vr], %[r], m0\n"
+      "s_add_u32 m0, m0, %[ol]\n"
+      "s_branch L_w4_%=\n"
+      "L_da_%=:\n"
+      "s_lshr_b32 %[e], %[e], 24\n"
+      "s_branch L_out_%=\n"
+      "L_db_%=:\n"
+      "s_lshr_b32 %[e], %[e2], 24\n"
+      "L_out_%=:\n"
+      "s_mov_b32 %[out], m0\n"
+      "s_mov_b32 m0, %[m0s]\n"
+      : [e] "=&s"(e), [e2] "=&s"(e2), [out] "=&s"(out), [r] "=&s"(r), [ol] "=&s"(ol),
+        [rem] "=&s"(rem), [m0s] "=&s"(m0_saved), [vr] "+v"(vrec)
+      : [pw] "v"(pw), [pr] "v"(pr), [lim] "s"(lim)
+      : "scc");
+  adv = e;
+  return out;
+}
+
 }  // namespace lz4d
 
 // Two instantiations, launched back to back by the runtime:
@@ -236,13 +293,20 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       // bits) -- the output start goes into bits 24..29 after the walk; offsets >= 4096 (FAR
       // batches) get their high bits from the token lane below.
       const uint32_t nxt = lane + 3 + (lx ? 1u : 0u) + (mx ? 1u : 0u) + cL;
-      const uint32_t pw = nxt | ((csimple ? colen : 255u) << 7);
       const uint32_t pr = (coff & 4095u) | ((cL & 63u) << 12) | (lane << 18);
       // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
       const uint32_t room = s.cap - s.op;
       const uint32_t lim = room < kBatchOut ? room : kBatchOut;
       uint32_t k, vrec = 0;
+#if BITAR_LZ4D_WALK == 4
+      const bool celig = csimple && lane < kWave - 1;  // lane 63: the walk's sentinel
+      const uint32_t pw = (nxt < kWave - 1 ? nxt : kWave - 1) | ((celig ? colen : 255u) << 6) |
+                          (nxt << 24);
+      const uint32_t out = walk_tokens4(pw, pr, lim, k, vrec);
+#else
+      const uint32_t pw = nxt | ((csimple ? colen : 255u) << 7);
       const uint32_t out = walk_tokens(pw, pr, lim, k, vrec);
+#endif
       if (out == 0) {
         // the first token qualifies only for a FAR batch: worth trying one
         if (!FAR) want_far = (ballot(cfar) & 1ull) != 0;

@@ -239,6 +239,44 @@ __device__ __forceinline__ uint32_t chain_fast(uint64_t& m, uint64_t extm, uint3
   return l;
 }
 
+// Form 2 (BITAR_CMP_CHAIN == 2, the default; kind-2 LZ4 compress 6.25 -> 6.03 ms/GiB): lanes that need the cooperative extension carry a length
+// of 128 (lenw, one v_cndmask per window), so the per-match "is it an extension lane" test
+// folds into the chain-end compare and runs once per window: 7 SALU + 1 VALU per match.
+// The lane's chain bit is set here (the caller sets it again after the extension).
+#ifndef BITAR_CMP_CHAIN
+#define BITAR_CMP_CHAIN 2
+#endif
+constexpr uint32_t kExtLen = 128;
+__device__ __forceinline__ uint32_t chain_fast2(uint64_t& m, uint32_t lenw, uint64_t& chain,
+                                                uint32_t& e) {
+  uint32_t l, ml;
+  uint64_t t;
+  __asm__ volatile(
+      "L_c2_%=:\n"
+      "s_ff1_i32_b64 %[l], %[m]\n"
+      "v_readlane_b32 %[ml], %[len], %[l]\n"
+      "s_bitset1_b64 %[ch], %[l]\n"
+      "s_add_u32 %[e], %[l], %[ml]\n"
+      "s_cmp_gt_u32 %[e], 63\n"
+      "s_cbranch_scc1 L_end_%=\n"
+      "s_lshl_b64 %[t], -1, %[e]\n"
+      "s_and_b64 %[m], %[m], %[t]\n"
+      "s_cbranch_scc1 L_c2_%=\n"
+      "s_mov_b32 %[l], 64\n"
+      "s_branch L_out_%=\n"
+      "L_end_%=:\n"
+      "s_cmp_lt_u32 %[e], 128\n"
+      "s_cbranch_scc0 L_out_%=\n"
+      "s_mov_b64 %[m], 0\n"
+      "s_mov_b32 %[l], 64\n"
+      "L_out_%=:\n"
+      : [l] "=&s"(l), [ml] "=&s"(ml), [t] "=&s"(t), [m] "+s"(m), [ch] "+s"(chain),
+        [e] "+s"(e)
+      : [len] "v"(lenw)
+      : "scc");
+  return l;
+}
+
 // The window-scan parse over one segment; hands each window to E::window and the tail to
 // E::sequence.
 // Returns where the tail literals start (the emitter's pending_from).
@@ -347,9 +385,17 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       uint32_t mlen_v = len;
       uint64_t m = valid;
       uint32_t e = 0;
+#if BITAR_CMP_CHAIN == 2
+      uint32_t lenw;
+      __asm__("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(lenw) : "v"(len), "v"(kExtLen), "s"(extm));
+#endif
       while (m) {  // the greedy chain: the next match is the first valid lane past the end
         // matches that need no extension: the hand-scheduled scalar loop
+#if BITAR_CMP_CHAIN == 2
+        const uint32_t l = chain_fast2(m, lenw, chain, e);
+#else
         const uint32_t l = chain_fast(m, extm, len, chain, e);
+#endif
         if (l >= kWave) break;
         uint32_t mlen = readlane(len, l);
         {  // lane l's match reached kPreExt bytes: extend it cooperatively
