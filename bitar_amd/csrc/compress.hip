@@ -111,7 +111,7 @@ struct Lz4Out : ByteOut {
     // followed by one length byte if the run is >= 15 bytes.
     const uint64_t above = lane == 63 ? 0ull : W.chain & (~0ull << (lane + 1));
     const uint32_t s = lowbit(above);
-    const bool lit = (!cl) & (above != 0) & (q >= lit_start);
+    const bool lit = !cl && above && q >= lit_start;
     const uint32_t lit_nlx = W.x + s - lit_start >= 15 ? 1u : 0u;
     const uint32_t o = op + incl - e;  // chain lanes: sequence start
     // every lane stores every byte kind; lanes without one store into their trash byte
@@ -124,15 +124,7 @@ struct Lz4Out : ByteOut {
     ring[cl ? at(h) : tr] = (uint8_t)W.off;
     ring[cl ? at(h + 1) : tr] = (uint8_t)(W.off >> 8);
     ring[cl && nmx ? at(h + 2) : tr] = (uint8_t)(ml - 15);
-#if BITAR_CMP_SELECT
-    // the literal lane's address computed on every lane (pinned by the empty asm): the
-    // compiler otherwise wraps it in an exec-mask if
-    uint32_t la = at(op + incl + 1 + lit_nlx + (q - lit_start));
-    __asm__("" : "+v"(la));
-    ring[lit ? la : tr] = (uint8_t)W.byte;
-#else
     ring[lit ? at(op + incl + 1 + lit_nlx + (q - lit_start)) : tr] = (uint8_t)W.byte;
-#endif
     // literals of the first sequence that precede the window (anchor < x): from the ring
     if (anchor < W.x) {
       const uint32_t l0 = lowbit(W.chain);

@@ -24,9 +24,6 @@
 #ifndef BITAR_LZ4D_WALK
 #define BITAR_LZ4D_WALK 4
 #endif
-#ifndef BITAR_LZ4D_SELECT
-#define BITAR_LZ4D_SELECT 0
-#endif
 
 namespace bitar_hip {
 
@@ -285,14 +282,9 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       // a real offset (within the ring, or any distance in a FAR batch: far sources are read
       // back from HBM below), not before the segment start (conservatively, as if this token
       // opened the batch)
-#if BITAR_LZ4D_SELECT
       // bitwise on the compares: short-circuit forms compile to an exec-mask branch
       const bool cfar = ((!lx) | (b1 < 255u)) & ((!mx) | (b2 < 255u)) & (colen <= 64u) &
                         (coff != 0) & (coff <= s.op + cL);
-#else
-      const bool cfar = (!lx || b1 < 255u) && (!mx || b2 < 255u) && colen <= 64u && coff != 0 &&
-                        coff <= s.op + cL;
-#endif
       const bool csimple = cfar && (FAR || coff <= kNearOff);
       // walk record: next token lane (7 bits, <= 127 for an eligible token, see
       // kMaxEligibleNext; the walk stops at a lane >= 64, which was not parsed, after
@@ -349,16 +341,12 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const int32_t srel = (int32_t)(ostart + jL + mm) - (int32_t)joff;  // vs op
       const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
       const uint32_t lit_addr = wrel + seqlane + 1 + (jL >= 15u ? 1u : 0u) + r;
-#if BITAR_LZ4D_SELECT
       // every form computed before the selects (the empty asm pins them), so the compiler
       // does not turn the selects into an exec-mask if / else
       uint32_t lit_a = lit_addr, hist_a = hist, alias_a = (uint32_t)srel | 0x80000000u;
       __asm__("" : "+v"(lit_a), "+v"(hist_a), "+v"(alias_a));
       uint32_t st = srel >= 0 ? alias_a : hist_a;
       st = is_lit ? lit_a : st;
-#else
-      uint32_t st = is_lit ? lit_addr : srel >= 0 ? ((uint32_t)srel | 0x80000000u) : hist;
-#endif
       if (big && srel < -(int32_t)kNearOff && !is_lit)
         st = (s.op + (uint32_t)srel) | 0x40000000u;  // far: the output position
       // pointer doubling until no lane of the batch aliases another (chains strictly descend)
@@ -383,11 +371,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       }
       ring[(base + s.op + lane) & kRingMask] = (uint8_t)g;
       lds_order();
-#if BITAR_LZ4D_SELECT
       s.ip += __builtin_amdgcn_readfirstlane(k);  // (k is an SGPR: keeps the add scalar)
-#else
-      s.ip += k;
-#endif
       s.op += out;
       return out;
     };

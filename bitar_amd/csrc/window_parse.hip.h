@@ -246,9 +246,6 @@ __device__ __forceinline__ uint32_t chain_fast(uint64_t& m, uint64_t extm, uint3
 #ifndef BITAR_CMP_CHAIN
 #define BITAR_CMP_CHAIN 2
 #endif
-#ifndef BITAR_CMP_SELECT
-#define BITAR_CMP_SELECT 0
-#endif
 constexpr uint32_t kExtLen = 128;
 __device__ __forceinline__ uint32_t chain_fast2(uint64_t& m, uint32_t lenw, uint64_t& chain,
                                                 uint32_t& e) {
