@@ -24,6 +24,9 @@
 #ifndef BITAR_LZ4D_WALK
 #define BITAR_LZ4D_WALK 4
 #endif
+#ifndef BITAR_LZ4D_LOOP
+#define BITAR_LZ4D_LOOP 0
+#endif
 
 namespace bitar_hip {
 
@@ -350,7 +353,11 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       if (big && srel < -(int32_t)kNearOff && !is_lit)
         st = (s.op + (uint32_t)srel) | 0x40000000u;  // far: the output position
       // pointer doubling until no lane of the batch aliases another (chains strictly descend)
+#if BITAR_LZ4D_LOOP
+      const uint64_t live = ballot(lane < out);  // lanes of the batch (a VALU compare, not 5 SALU)
+#else
       const uint64_t live = out >= 64 ? ~0ull : (1ull << out) - 1;  // lanes of the batch
+#endif
       while (ballot((int32_t)st < 0) & live) {
         const uint32_t other = bpermute_lane(st, st & 63u);
         st = (st & 0x80000000u) ? other : st;
@@ -375,6 +382,24 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       s.op += out;
       return out;
     };
+#if BITAR_LZ4D_LOOP
+    if constexpr (!FARK) {
+      // one loop condition computed at the end of each batch (the for / continue / break
+      // form compiles to ~12 SALU of uniform-bool bookkeeping per batch)
+      want_far = false;
+      if (s.ip + kBatchIn <= s.csize) {
+        uint32_t t;
+        do {
+          const uint32_t o = batch(std::false_type{});
+          // "a batch was made and the next one fits the stream": one compare (the select
+          // in asm, so the compiler keeps it a single scalar branch)
+          const uint32_t rest = s.csize - s.ip;
+          __asm__("s_cmp_lg_u32 %1, 0\n s_cselect_b32 %0, %2, 0" : "=s"(t) : "s"(o), "s"(rest)
+                  : "scc");
+        } while (t >= kBatchIn);
+      }
+    } else
+#endif
     for (;;) {
       if (s.ip + kBatchIn > s.csize) break;
       if constexpr (FARK) {
