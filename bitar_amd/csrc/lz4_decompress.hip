@@ -24,9 +24,6 @@
 #ifndef BITAR_LZ4D_WALK
 #define BITAR_LZ4D_WALK 4
 #endif
-#ifndef BITAR_LZ4D_LOOP
-#define BITAR_LZ4D_LOOP 0
-#endif
 
 namespace bitar_hip {
 
@@ -353,11 +350,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       if (big && srel < -(int32_t)kNearOff && !is_lit)
         st = (s.op + (uint32_t)srel) | 0x40000000u;  // far: the output position
       // pointer doubling until no lane of the batch aliases another (chains strictly descend)
-#if BITAR_LZ4D_LOOP
       const uint64_t live = ballot(lane < out);  // lanes of the batch (a VALU compare, not 5 SALU)
-#else
-      const uint64_t live = out >= 64 ? ~0ull : (1ull << out) - 1;  // lanes of the batch
-#endif
       while (ballot((int32_t)st < 0) & live) {
         const uint32_t other = bpermute_lane(st, st & 63u);
         st = (st & 0x80000000u) ? other : st;
@@ -382,7 +375,6 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       s.op += out;
       return out;
     };
-#if BITAR_LZ4D_LOOP
     if constexpr (!FARK) {
       // one loop condition computed at the end of each batch (the for / continue / break
       // form compiles to ~12 SALU of uniform-bool bookkeeping per batch)
@@ -399,7 +391,6 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         } while (t >= kBatchIn);
       }
     } else
-#endif
     for (;;) {
       if (s.ip + kBatchIn > s.csize) break;
       if constexpr (FARK) {
