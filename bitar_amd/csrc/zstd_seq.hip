@@ -360,16 +360,19 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
     if (ballot(far)) {  // (rare)
       if (far) v = s.dst[from];
     }
-    bool pend = act && ism && from >= xa;
-    uint32_t ptr = pend ? from - xa : lane;
+    // the pending flag kept as data (0x100 / 0), not as a loop-carried lane mask: a bool
+    // updated in a divergent loop costs ~8 scalar mask merges per round
+    const bool pend0 = act && ism && from >= xa;
+    uint32_t pv = pend0 ? 0x100u : 0u;
+    uint32_t ptr = pend0 ? from - xa : lane;
     // sources inside this step: pointer jumping (each round halves the chains)
-    while (ballot(pend)) {
-      const uint32_t w = v | (pend ? 0x100u : 0u) | (ptr << 9);
+    while (ballot(pv != 0)) {
+      const uint32_t w = v | pv | (ptr << 9);
       const uint32_t t = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ptr << 2), (int)w);
-      const bool still = pend && (t & 0x100u);
-      v = pend && !still ? t & 0xFFu : v;
+      const uint32_t still = pv & t;
+      v = (pv ^ still) ? t & 0xFFu : v;  // resolved this round
       ptr = still ? t >> 9 : ptr;
-      pend = still;
+      pv = still;
     }
     lds_order();
     ring[act ? (uint32_t)((base + x) & kRingMask) : kRing + lane] = (uint8_t)v;
