@@ -50,3 +50,35 @@ def test_recordbatch_8gib_four_streams():
         job.free()
     finally:
         e.close()
+
+
+def test_zstd_column_8gib_configs4():
+    """BASELINE configs[4] at its full 8 GiB job size on one GPU: level-1-class Zstd frames
+    per 64 KiB chunk of an int64 column buffer (kind 5, the Parquet-column shape), dealt in
+    round-robin batches over two queue-pair streams, byte-exact round trip, the job-wide frame
+    index, and sampled chunks bit-exact against the oracle's encoder."""
+    import bitar_amd
+    from bitar_amd.job import ShardedJob
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    e = bitar_amd.Engine(0, num_streams=2)
+    try:
+        seg = 65536
+        job = ShardedJob(e, bitar_amd.CODEC_ZSTD, 8 << 30, seg, world=1, rank=0, nstreams=2)
+        assert job.layout.local_nseg == 131072
+        job.generate(5, 11)
+        job.step()
+        job.sync()
+        assert job.verify()
+        sizes = down(job.sizes).astype(np.uint32)
+        assert int(job.index[-1].item()) == int(sizes.astype(np.int64).sum())
+        assert sizes.astype(np.int64).sum() < (8 << 30) // 3  # a column compresses > 3x
+        for g in (0, 255, 256, 65535, 65536, 131071):
+            plain = down(job.data[g * seg:(g + 1) * seg])
+            r, comp = O.zstd_compress(plain.tobytes())
+            assert r == 0 and len(comp) == sizes[g], g
+            got = down(job.slab[g * job.stride:g * job.stride + int(sizes[g])]).tobytes()
+            assert got == comp, g
+        job.free()
+    finally:
+        e.close()
