@@ -203,8 +203,9 @@ def kernel_lines(codec_name, r, traffic_json, leg="headline"):
         with open(traffic_json) as f:
             # per-launch HBM bytes of this leg's kernel(s), from its own PMC passes
             tj = json.load(f)
-            parts = [tj.get(f"{leg}/{k}") for k in dominant[0].split(" ")[0].split("+")]
-            traffic = sum(parts) if all(p is not None for p in parts) else None
+            per = [tj.get(f"{leg}/{k}") for k in dominant[0].split(" ")[0].split("+")]
+            # (concurrent parts: the roofline covers all of the step's launches of the kernel)
+            traffic = sum(per) * parts if all(p is not None for p in per) else None
     except (OSError, ValueError):
         pass
     roof = {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 2),

@@ -30,10 +30,12 @@ FETCH_FACTOR = {"zstd_lanes_kernel": 1.0, "inflate_lanes_kernel": 1.0, "zstd_hli
                 "zstd_walk_kernel": 1.0, "zstd_emit_kernel": 1.0}
 
 
-def per_kernel(path):
+def per_kernel(path, grid=None):
     agg = {}
     with open(path) as f:
         for r in csv.DictReader(f):
+            if grid is not None and int(r["Grid_Size"]) != grid:
+                continue
             name = r["Kernel_Name"].split("(")[0]
             if name.startswith("void "):  # templated kernels: "void ns::k<16u>"
                 name = name[5:]
@@ -44,11 +46,15 @@ def per_kernel(path):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
-LEGS = ("headline", "zstd", "deflate", "deflate_dyn")
+LEGS = ("headline", "zstd", "deflate", "deflate_dyn", "recordbatch")
+# legs whose kernels also run in the headline job of the same pass: only their own launches
+# (by grid size) are averaged -- the record-batch job's parts are 8 GiB / 4 streams = 32768
+# segments of 64 KiB, one 64-lane workgroup each
+LEG_GRID = {"recordbatch": 32768 * 64}
 # the kernels each leg is about (every pass also runs the headline's LZ4 kernels)
 LEG_KERNELS = {"headline": ("lz4_",), "zstd": ("zstd_",),
                "deflate": ("deflate_compress", "inflate"),
-               "deflate_dyn": ("deflate_dyn_", "inflate")}
+               "deflate_dyn": ("deflate_dyn_", "inflate"), "recordbatch": ("lz4_",)}
 
 
 def main():
@@ -63,8 +69,9 @@ def main():
         if not os.path.exists(prof):
             continue
         shutil.copy(prof, os.path.join(rdir, f"kernel_stats_{leg}.csv"))
-        fetch = per_kernel(os.path.join(out, f"pmc_{tag}_{leg}_FETCH_SIZE", "pmc_counter_collection.csv"))
-        write = per_kernel(os.path.join(out, f"pmc_{tag}_{leg}_WRITE_SIZE", "pmc_counter_collection.csv"))
+        g = LEG_GRID.get(leg)
+        fetch = per_kernel(os.path.join(out, f"pmc_{tag}_{leg}_FETCH_SIZE", "pmc_counter_collection.csv"), g)
+        write = per_kernel(os.path.join(out, f"pmc_{tag}_{leg}_WRITE_SIZE", "pmc_counter_collection.csv"), g)
         for k in sorted(set(fetch) | set(write)):
             if not k.startswith(LEG_KERNELS[leg]):
                 continue

@@ -12,7 +12,7 @@ if [ -n "$PROFILE" ]; then
   # one kernel-trace pass and one pass per PMC counter for each leg on its own (--only), so a
   # kernel's averages never mix launches of different legs (the record-batch leg also runs
   # lz4_compress_kernel, the stock-decode leg lz4_decompress_kernel, ...)
-  for leg in ${PROF_LEGS:-headline zstd deflate deflate_dyn}; do
+  for leg in ${PROF_LEGS:-headline zstd deflate deflate_dyn recordbatch}; do
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$leg -o trace --output-format csv -- \
       python3 bench.py --only $leg ${BENCH_ARGS} > gpurun_out/prof_${TAG}_$leg.log 2>&1 || { echo prof $leg failed; tail -30 gpurun_out/prof_${TAG}_$leg.log; exit 1; }
     for ctr in FETCH_SIZE WRITE_SIZE; do
