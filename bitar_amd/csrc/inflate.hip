@@ -385,26 +385,85 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
     }
     // (2) scalar walk over the real symbols
     const uint32_t lim = room < 64 ? room : 64;
-    uint32_t k = 0, out = 0, sel = 0, ostart = 0;
-    bool stop = false, taken_all = true;  // taken_all: stopped only because the batch is full
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-      while (!stop && k < kWave * (j + 1)) {
-        const uint32_t e = readlane(rec[j], k & 63u);
-        const uint32_t ol = (e >> 9) & 127u;
-        if (out + ol > lim) {
-          stop = true;
-          taken_all = ol != 127u && lim == 64u;
-          break;
-        }
-        if (lane - out < ol) { sel = e; ostart = out; }
-        out += ol;
-        k = e & 511u;
-      }
+    // Written out (scalar issue binds the walk): the output position in m0, the room as a
+    // remainder whose s_sub_u32 borrow is "does not fit", each symbol's record dropped into
+    // the lane of its first output byte by v_writelane (a prefix max below hands every
+    // output byte its record); the candidate index k (< 256: lane k & 63 of rec[k >> 6]) is
+    // range-checked per vector, v_readlane taking the low 6 bits of its lane select.
+    uint32_t k, out, olx, vrec = 0;
+    {
+      uint32_t e, ol, rem, m0_saved;
+      __asm__ volatile(
+          "s_mov_b32 %[m0s], m0\n"
+          "s_mov_b32 %[k], 0\n"
+          "s_mov_b32 %[rem], %[lim]\n"
+          "s_mov_b32 %[olx], 0\n"
+          "s_mov_b32 m0, 0\n"
+          "L_i0_%=:\n"
+          "s_cmp_ge_u32 %[k], 64\n"
+          "s_cbranch_scc1 L_i1_%=\n"
+          "v_readlane_b32 %[e], %[r0], %[k]\n"
+          "s_bfe_u32 %[ol], %[e], 0x70009\n"
+          "s_sub_u32 %[rem], %[rem], %[ol]\n"
+          "s_cbranch_scc1 L_stop_%=\n"
+          "v_writelane_b32 %[vr], %[e], m0\n"
+          "s_add_u32 m0, m0, %[ol]\n"
+          "s_and_b32 %[k], %[e], 511\n"
+          "s_branch L_i0_%=\n"
+          "L_i1_%=:\n"
+          "s_cmp_ge_u32 %[k], 128\n"
+          "s_cbranch_scc1 L_i2_%=\n"
+          "v_readlane_b32 %[e], %[r1], %[k]\n"
+          "s_bfe_u32 %[ol], %[e], 0x70009\n"
+          "s_sub_u32 %[rem], %[rem], %[ol]\n"
+          "s_cbranch_scc1 L_stop_%=\n"
+          "v_writelane_b32 %[vr], %[e], m0\n"
+          "s_add_u32 m0, m0, %[ol]\n"
+          "s_and_b32 %[k], %[e], 511\n"
+          "s_branch L_i1_%=\n"
+          "L_i2_%=:\n"
+          "s_cmp_ge_u32 %[k], 192\n"
+          "s_cbranch_scc1 L_i3_%=\n"
+          "v_readlane_b32 %[e], %[r2], %[k]\n"
+          "s_bfe_u32 %[ol], %[e], 0x70009\n"
+          "s_sub_u32 %[rem], %[rem], %[ol]\n"
+          "s_cbranch_scc1 L_stop_%=\n"
+          "v_writelane_b32 %[vr], %[e], m0\n"
+          "s_add_u32 m0, m0, %[ol]\n"
+          "s_and_b32 %[k], %[e], 511\n"
+          "s_branch L_i2_%=\n"
+          "L_i3_%=:\n"
+          "s_cmp_ge_u32 %[k], 256\n"
+          "s_cbranch_scc1 L_out_%=\n"
+          "v_readlane_b32 %[e], %[r3], %[k]\n"
+          "s_bfe_u32 %[ol], %[e], 0x70009\n"
+          "s_sub_u32 %[rem], %[rem], %[ol]\n"
+          "s_cbranch_scc1 L_stop_%=\n"
+          "v_writelane_b32 %[vr], %[e], m0\n"
+          "s_add_u32 m0, m0, %[ol]\n"
+          "s_and_b32 %[k], %[e], 511\n"
+          "s_branch L_i3_%=\n"
+          "L_stop_%=:\n"
+          "s_or_b32 %[olx], %[ol], 0x100\n"
+          "L_out_%=:\n"
+          "s_mov_b32 %[out], m0\n"
+          "s_mov_b32 m0, %[m0s]\n"
+          : [k] "=&s"(k), [out] "=&s"(out), [olx] "=&s"(olx), [e] "=&s"(e), [ol] "=&s"(ol),
+            [rem] "=&s"(rem), [m0s] "=&s"(m0_saved), [vr] "+v"(vrec)
+          : [r0] "v"(rec[0]), [r1] "v"(rec[1]), [r2] "v"(rec[2]), [r3] "v"(rec[3]),
+            [lim] "s"(lim)
+          : "scc");
     }
+    // stopped on a symbol (olx = 0x100 | its olen) rather than by running out of candidates:
+    // the batch continues only when that symbol was cut by a full batch
+    const uint32_t olxu = __builtin_amdgcn_readfirstlane(olx);
+    const bool taken_all = olxu == 0 || (olxu != 0x17Fu && lim == 64u);
     if (out == 0) break;
+    // every output byte takes the payload of the latest symbol starting at or before it
+    const uint32_t key = wave_incl_max(vrec ? (lane << 24) | (vrec >> 16) : 0u);
+    const uint32_t ostart = key >> 24;
+    const uint32_t payload = key & 0xFFFFu;
     // (3) sources: the literal / ring history / an earlier lane of this batch
-    const uint32_t payload = sel >> 16;
     const bool lit = (payload & 0x8000u) == 0;
     const uint32_t dist = payload & 0x1FFFu;
     const uint32_t r = lane - ostart;
