@@ -390,7 +390,7 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
     // the lane of its first output byte by v_writelane (a prefix max below hands every
     // output byte its record); the candidate index k (< 256: lane k & 63 of rec[k >> 6]) is
     // range-checked per vector, v_readlane taking the low 6 bits of its lane select.
-    uint32_t k, out, olx, vrec = 0;
+    uint32_t k, out, olx, ns, vrec = 0;
     {
       uint32_t e, ol, rem, m0_saved;
       __asm__ volatile(
@@ -398,6 +398,7 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
           "s_mov_b32 %[k], 0\n"
           "s_mov_b32 %[rem], %[lim]\n"
           "s_mov_b32 %[olx], 0\n"
+          "s_mov_b32 %[ns], 0\n"
           "s_mov_b32 m0, 0\n"
           "L_i0_%=:\n"
           "s_cmp_ge_u32 %[k], 64\n"
@@ -407,6 +408,7 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
           "s_sub_u32 %[rem], %[rem], %[ol]\n"
           "s_cbranch_scc1 L_stop_%=\n"
           "v_writelane_b32 %[vr], %[e], m0\n"
+          "s_add_u32 %[ns], %[ns], 1\n"
           "s_add_u32 m0, m0, %[ol]\n"
           "s_and_b32 %[k], %[e], 511\n"
           "s_branch L_i0_%=\n"
@@ -418,6 +420,7 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
           "s_sub_u32 %[rem], %[rem], %[ol]\n"
           "s_cbranch_scc1 L_stop_%=\n"
           "v_writelane_b32 %[vr], %[e], m0\n"
+          "s_add_u32 %[ns], %[ns], 1\n"
           "s_add_u32 m0, m0, %[ol]\n"
           "s_and_b32 %[k], %[e], 511\n"
           "s_branch L_i1_%=\n"
@@ -429,6 +432,7 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
           "s_sub_u32 %[rem], %[rem], %[ol]\n"
           "s_cbranch_scc1 L_stop_%=\n"
           "v_writelane_b32 %[vr], %[e], m0\n"
+          "s_add_u32 %[ns], %[ns], 1\n"
           "s_add_u32 m0, m0, %[ol]\n"
           "s_and_b32 %[k], %[e], 511\n"
           "s_branch L_i2_%=\n"
@@ -440,6 +444,7 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
           "s_sub_u32 %[rem], %[rem], %[ol]\n"
           "s_cbranch_scc1 L_stop_%=\n"
           "v_writelane_b32 %[vr], %[e], m0\n"
+          "s_add_u32 %[ns], %[ns], 1\n"
           "s_add_u32 m0, m0, %[ol]\n"
           "s_and_b32 %[k], %[e], 511\n"
           "s_branch L_i3_%=\n"
@@ -448,7 +453,8 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
           "L_out_%=:\n"
           "s_mov_b32 %[out], m0\n"
           "s_mov_b32 m0, %[m0s]\n"
-          : [k] "=&s"(k), [out] "=&s"(out), [olx] "=&s"(olx), [e] "=&s"(e), [ol] "=&s"(ol),
+          : [k] "=&s"(k), [out] "=&s"(out), [olx] "=&s"(olx), [ns] "=&s"(ns), [e] "=&s"(e),
+            [ol] "=&s"(ol),
             [rem] "=&s"(rem), [m0s] "=&s"(m0_saved), [vr] "+v"(vrec)
           : [r0] "v"(rec[0]), [r1] "v"(rec[1]), [r2] "v"(rec[2]), [r3] "v"(rec[3]),
             [lim] "s"(lim)
@@ -460,7 +466,10 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
     const bool taken_all = olxu == 0 || (olxu != 0x17Fu && lim == 64u);
     if (out == 0) break;
     // every output byte takes the payload of the latest symbol starting at or before it
-    const uint32_t key = wave_incl_max(vrec ? (lane << 24) | (vrec >> 16) : 0u);
+    // (one symbol -- a batch cut short by a far match or a long code: its record for all)
+    const uint32_t key = __builtin_amdgcn_readfirstlane(ns) == 1u
+                             ? readlane(vrec, 0) >> 16
+                             : wave_incl_max(vrec ? (lane << 24) | (vrec >> 16) : 0u);
     const uint32_t ostart = key >> 24;
     const uint32_t payload = key & 0xFFFFu;
     // (3) sources: the literal / ring history / an earlier lane of this batch
