@@ -19,6 +19,19 @@ CODEC_DEFLATE_DYNAMIC = 4  # HuffmanEncoding::DYNAMIC (decoded as CODEC_DEFLATE)
 SEGMENT_ERROR = 0xFFFFFFFF
 CHECKSUM_CRC32, CHECKSUM_ADLER32, CHECKSUM_CRC32_ADLER32 = 1, 2, 3
 MAX_SEG_SIZE = 65536
+# bitar_hip_config.flags (initial decoder options of a context)
+FLAG_INFLATE_WAVE_ONLY, FLAG_ZSTD_WAVE_ONLY, FLAG_ZSTD_LANE_EXEC, FLAG_COUNT_PATHS = 1, 2, 4, 8
+# bitar_hip_path_counter indices
+PATHS = ("inflate_wave", "inflate_wave_reject", "inflate_batch_segs", "inflate_batches",
+         "zstd_wave", "zstd_handed", "zstd_seqdec", "zstd_seqdec_reject", "zstd_exec",
+         "zstd_exec_reject", "lz4_far")
+PATH_COUNT = 16
+
+
+class DecoderOptions(ctypes.Structure):
+    """bitar_hip_decoder_options (include/bitar_hip.h)"""
+    _fields_ = [("inflate_lanes", ctypes.c_uint32), ("zstd_lanes", ctypes.c_uint32),
+                ("zstd_seq", ctypes.c_uint32), ("count_paths", ctypes.c_uint32)]
 
 # negated arrow::StatusCode (reference src/include/util.h:157-205)
 STATUS_NAMES = {0: "OK", -1: "OutOfMemory", -4: "Invalid", -5: "IOError", -6: "CapacityError",
@@ -75,6 +88,9 @@ def lib():
         "bitar_hip_checksum": (i32, [vp, vp, u32, vp, u64, u32, vp, u32, vp]),
         "bitar_hip_copy_batch": (i32, [vp, vp, vp, vp, vp, u32]),
         "bitar_hip_lz4_chain": (i32, [vp, vp, vp, u32, vp, u32, vp, u64, vp]),
+        "bitar_hip_get_decoder_options": (i32, [vp, ctypes.POINTER(DecoderOptions)]),
+        "bitar_hip_set_decoder_options": (i32, [vp, ctypes.POINTER(DecoderOptions)]),
+        "bitar_hip_path_counters": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -93,7 +109,8 @@ ABI_SYMBOLS = ("bitar_hip_abi_version", "bitar_hip_last_error", "bitar_hip_devic
                "bitar_hip_decompress", "bitar_hip_decompress_slab",
                "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_pack_lz4f", "bitar_hip_fill",
                "bitar_hip_fill_at", "bitar_hip_checksum", "bitar_hip_copy_batch",
-               "bitar_hip_lz4_chain")
+               "bitar_hip_lz4_chain", "bitar_hip_get_decoder_options",
+               "bitar_hip_set_decoder_options", "bitar_hip_path_counters")
 
 
 def check(rc):
@@ -128,7 +145,7 @@ class Engine:
     torch copies and our kernels stay ordered).  Buffers are torch uint8 tensors in HBM.
     """
 
-    def __init__(self, device=0, num_streams=1):
+    def __init__(self, device=0, num_streams=1, flags=0):
         import torch  # plumbing only
         self.torch = torch
         self.device = device
@@ -136,7 +153,7 @@ class Engine:
         class Cfg(ctypes.Structure):
             _fields_ = [("num_streams", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
 
-        cfg = Cfg(num_streams, 0)
+        cfg = Cfg(num_streams, flags)
         ctx = ctypes.c_void_p()
         check(lib().bitar_hip_open(device, ctypes.byref(cfg), ctypes.byref(ctx)))
         self.ctx = ctx
@@ -158,6 +175,26 @@ class Engine:
         if isinstance(stream, int):
             return ctypes.c_void_p(stream)
         return ctypes.c_void_p(stream.cuda_stream)
+
+    def decoder_options(self):
+        o = DecoderOptions()
+        check(lib().bitar_hip_get_decoder_options(self.ctx, ctypes.byref(o)))
+        return {f: getattr(o, f) for f, _ in DecoderOptions._fields_}
+
+    def set_decoder_options(self, **kw):
+        """change this context's decoders (inflate_lanes / zstd_lanes / zstd_seq /
+        count_paths); returns the previous options"""
+        old = self.decoder_options()
+        new = dict(old, **kw)
+        check(lib().bitar_hip_set_decoder_options(
+            self.ctx, ctypes.byref(DecoderOptions(*(new[f] for f, _ in DecoderOptions._fields_)))))
+        return old
+
+    def path_counters(self):
+        """{path: segments} since the last call (waits for the device, then resets)"""
+        v = (ctypes.c_uint64 * PATH_COUNT)()
+        check(lib().bitar_hip_path_counters(self.ctx, v, PATH_COUNT))
+        return {name: int(v[k]) for k, name in enumerate(PATHS)}
 
     def queue_pair_stream(self, qp):
         s = ctypes.c_void_p()

@@ -494,6 +494,7 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
     s.op += out;
     P += k;
     moved = true;
+    ++s.nbatch;
     if (!taken_all) break;  // stopped on a symbol the batch does not take
   }
   if (moved) seek(s, win, b, P);
@@ -539,7 +540,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
-    uint32_t defer_only) {
+    uint32_t defer_only, unsigned long long* __restrict__ stats) {
   using namespace infl;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
   __shared__ __attribute__((aligned(16))) Tables t;
@@ -562,6 +563,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(
   s.fenced = 0;
   s.wb = ~0ull;
   s.wlen = 0;
+  s.nbatch = 0;
 
   Bits b;
   bits_reset(b, 0);
@@ -689,6 +691,14 @@ __global__ __launch_bounds__(64) void inflate_kernel(
   } else if (lane == 0) {
     produced[i] = 0xFFFFFFFFu;
     atomicOr(err, 1u);
+  }
+  if (stats && lane == 0) {  // path counters (bitar_hip_path_counters)
+    atomicAdd(stats + BITAR_HIP_PATH_INFLATE_WAVE, 1ull);
+    if (!ok) atomicAdd(stats + BITAR_HIP_PATH_INFLATE_WAVE_REJECT, 1ull);
+    if (s.nbatch) {
+      atomicAdd(stats + BITAR_HIP_PATH_INFLATE_BATCH_SEGS, 1ull);
+      atomicAdd(stats + BITAR_HIP_PATH_INFLATE_BATCHES, (unsigned long long)s.nbatch);
+    }
   }
 }
 

@@ -208,7 +208,8 @@ template <bool FARK>
 __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
-    uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err) {
+    uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
+    unsigned long long* __restrict__ stats) {
   using namespace lz4d;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
   uint8_t* win = lds;
@@ -431,7 +432,10 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     match_copy(s, ring, off, m);
   }
   if (!FARK && want_far) {
-    if (lane_id() == 0) produced[i] = kDefer;
+    if (lane_id() == 0) {
+      produced[i] = kDefer;
+      if (stats) atomicAdd(stats + BITAR_HIP_PATH_LZ4_FAR, 1ull);
+    }
   } else if (ok) {
     flush(s, ring, s.op, true);
     if (lane_id() == 0) produced[i] = s.op;
@@ -443,9 +447,11 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
 
 template __global__ void lz4_decompress_kernel<false>(const uint8_t* const*, const uint8_t*,
                                                      uint64_t, const uint32_t*, uint32_t,
-                                                     uint32_t, uint8_t*, uint32_t*, uint32_t*);
+                                                     uint32_t, uint8_t*, uint32_t*, uint32_t*,
+                                                     unsigned long long*);
 template __global__ void lz4_decompress_kernel<true>(const uint8_t* const*, const uint8_t*,
                                                     uint64_t, const uint32_t*, uint32_t, uint32_t,
-                                                    uint8_t*, uint32_t*, uint32_t*);
+                                                    uint8_t*, uint32_t*, uint32_t*,
+                                                    unsigned long long*);
 
 }  // namespace bitar_hip

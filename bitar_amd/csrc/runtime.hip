@@ -22,12 +22,12 @@ __global__ void lz4_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*
 template <bool FARK>
 __global__ void lz4_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                       const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
-                                      uint32_t*);
+                                      uint32_t*, unsigned long long*);
 __global__ void deflate_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
                                         uint8_t* const*, uint32_t*, uint32_t*);
 __global__ void inflate_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
-                               uint32_t*, uint32_t);
+                               uint32_t*, uint32_t, unsigned long long*);
 template <uint32_t L>
 __global__ void inflate_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                      const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
@@ -41,7 +41,8 @@ __global__ void zstd_emit_kernel(const uint8_t*, uint64_t, uint32_t, const uint8
                                  uint64_t);
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                        const uint32_t*, uint32_t, uint32_t, uint8_t*,
-                                       uint32_t*, uint32_t*, uint32_t, uint8_t*);
+                                       uint32_t*, uint32_t*, uint32_t, uint8_t*,
+                                       unsigned long long*);
 template <uint32_t S>
 __global__ void zstd_hlit_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                  const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
@@ -53,10 +54,10 @@ __global__ void zstd_handoff_kernel(const uint8_t* const*, const uint8_t*, uint6
 template <uint32_t L>
 __global__ void zstd_seqdec_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                    const uint32_t*, uint32_t, uint32_t, uint32_t*, uint8_t*,
-                                   uint64_t*, uint32_t, uint32_t*);
+                                   uint64_t*, uint32_t, uint32_t*, unsigned long long*);
 __global__ void zstd_exec_kernel(const uint8_t* const*, const uint8_t*, uint64_t, uint32_t,
                                  uint32_t, uint8_t*, uint32_t*, const uint8_t*,
-                                 const uint64_t*, uint32_t, uint32_t*);
+                                 const uint64_t*, uint32_t, uint32_t*, unsigned long long*);
 template <uint32_t L>
 __global__ void zstd_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                   const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
@@ -90,6 +91,9 @@ struct bitar_hip_ctx {
   int device = -1;
   std::vector<hipStream_t> streams;
   uint32_t* d_err = nullptr;  // kErrWords words
+  unsigned long long* d_stats = nullptr;  // BITAR_HIP_PATH_COUNT path counters
+  // decoder options (bitar_hip_decoder_options), per context
+  std::atomic<uint32_t> inflate_lanes{4}, zstd_lanes{16}, zstd_seq{1}, count_paths{0};
   std::mutex mu;              // guards `words`
   std::vector<std::pair<hipStream_t, uint32_t>> words;  // stream -> error word index
 };
@@ -129,6 +133,24 @@ hipStream_t pick_stream(bitar_hip_ctx*, void* stream) {
 constexpr uint32_t kMaxSeg = BITAR_HIP_MAX_SEG_SIZE;
 constexpr uint32_t kMaxZstdFrame = 1u << 30;
 
+// Calls whose kernels need per-segment scratch (dynamic DEFLATE and Zstd compress, Zstd
+// decode) run in chunks of at most kChunkSegs segments (2 GiB of 64 KiB segments: every
+// chunk still fills the chip many times over) over ONE scratch allocation sized for a chunk,
+// so a call's scratch is bounded whatever its size.  Chunks are balanced (a 18059-segment
+// call is one chunk, a 65536-segment call two of 32768).
+constexpr uint64_t kChunkSegs = 32768;
+struct Chunks {
+  uint64_t size;
+  explicit Chunks(uint64_t nseg) {
+    const uint64_t k = (nseg + kChunkSegs - 1) / kChunkSegs;
+    size = k ? (nseg + k - 1) / k : 1;
+  }
+};
+// The device pool's cached stream-ordered memory above this is returned to the driver at
+// the next synchronisation (a chunk of Zstd compress scratch is ~12 GB; steady-state calls
+// stay below this and never touch the driver).
+constexpr uint64_t kPoolKeepBytes = 24ull << 30;
+
 // index of the error word of `stream`; words run out only after 1000+ distinct foreign
 // streams, after which they share the NULL stream's word (still correct, merely coarser)
 uint32_t word_index(bitar_hip_ctx* ctx, hipStream_t stream) {
@@ -156,6 +178,8 @@ int sync_error(uint32_t err) {
 }
 
 }  // namespace
+
+static void init_options(bitar_hip_ctx* ctx, uint32_t flags);
 
 extern "C" {
 
@@ -211,13 +235,16 @@ int bitar_hip_open(int device, const bitar_hip_config* cfg, bitar_hip_ctx** out)
   {
     hipMemPool_t pool;
     if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-      uint64_t keep = ~0ull;
+      uint64_t keep = kPoolKeepBytes;
       (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     }
     (void)hipGetLastError();
   }
+  init_options(ctx, cfg ? cfg->flags : 0u);
   hipError_t e = hipMalloc(&ctx->d_err, kErrWords * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(ctx->d_err, 0, kErrWords * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&ctx->d_stats, BITAR_HIP_PATH_COUNT * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(ctx->d_stats, 0, BITAR_HIP_PATH_COUNT * sizeof(unsigned long long));
   if (e != hipSuccess) {
     bitar_hip_close(ctx);
     return hip_fail(e, "error word");
@@ -234,6 +261,7 @@ int bitar_hip_close(bitar_hip_ctx* ctx) {
       (void)hipStreamDestroy(s);
     }
     if (ctx->d_err) (void)hipFree(ctx->d_err);
+    if (ctx->d_stats) (void)hipFree(ctx->d_stats);
   }
   delete ctx;
   return 0;
@@ -328,16 +356,25 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
                        in, n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
   else if (codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC) {
     // pass 1 (parse -> records + histograms) and pass 2 (codes + emit) through a
-    // stream-ordered scratch per segment (deflate_dyn.hip)
-    // per segment: 2 KiB plan + 16 KiB of window masks + match records (<= one slot)
+    // stream-ordered scratch per segment (deflate_dyn.hip): 2 KiB plan + 16 KiB of window
+    // masks + match records (<= one slot).  Large calls run in chunks of <= kChunkSegs
+    // segments over one scratch allocation, so scratch is bounded whatever the call's size.
     const uint64_t scr_stride = bitar_hip_slot_size(BITAR_HIP_CODEC_DEFLATE, seg) + 2048u + 16384u;
+    const Chunks ch(nseg);
     void* scratch = nullptr;
-    HIP_TRY(hipMallocAsync(&scratch, nseg * scr_stride, s), "scratch allocation");
-    hipLaunchKernelGGL(bitar_hip::deflate_dyn_parse_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
-                       in, n, seg, static_cast<uint8_t*>(scratch), scr_stride, err_word(ctx, s));
-    hipLaunchKernelGGL(bitar_hip::deflate_dyn_emit_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
-                       in, n, seg, static_cast<const uint8_t*>(scratch), scr_stride, slab,
-                       slot_stride, dsts, d_sizes, err_word(ctx, s));
+    HIP_TRY(hipMallocAsync(&scratch, ch.size * scr_stride, s), "scratch allocation");
+    auto* scr = static_cast<uint8_t*>(scratch);
+    for (uint64_t c0 = 0; c0 < nseg; c0 += ch.size) {
+      const uint64_t cn = nseg - c0 < ch.size ? nseg - c0 : ch.size;
+      const uint64_t cb = c0 * seg, nb = n - cb < cn * seg ? n - cb : cn * seg;
+      uint8_t* cslab = slab ? slab + c0 * slot_stride : nullptr;
+      uint8_t* const* cdsts = dsts ? dsts + c0 : nullptr;
+      hipLaunchKernelGGL(bitar_hip::deflate_dyn_parse_kernel, dim3((uint32_t)cn), dim3(64), 0, s,
+                         in + cb, nb, seg, scr, scr_stride, err_word(ctx, s));
+      hipLaunchKernelGGL(bitar_hip::deflate_dyn_emit_kernel, dim3((uint32_t)cn), dim3(64), 0, s,
+                         in + cb, nb, seg, static_cast<const uint8_t*>(scr), scr_stride, cslab,
+                         slot_stride, cdsts, d_sizes + c0, err_word(ctx, s));
+    }
     const hipError_t le = hipGetLastError();
     HIP_TRY(hipFreeAsync(scratch, s), "scratch release");
     HIP_TRY(le, "compress launch");
@@ -350,21 +387,30 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
     // + the chain-walk scratch (zstd_compress.hip walk_stride: a 3400-byte header with the
     // tables, then 10 bytes per sequence)
     const uint64_t w_stride = (3400ull + 10ull * (seg / 4u + 2u) + 255u) & ~255ull;
+    const Chunks ch(nseg);
     void* scratch = nullptr;
-    HIP_TRY(hipMallocAsync(&scratch, nseg * scr_stride + nseg * 8u + nseg * w_stride, s),
+    HIP_TRY(hipMallocAsync(&scratch, ch.size * (scr_stride + 8u + w_stride), s),
             "scratch allocation");
     auto* scr = static_cast<uint8_t*>(scratch);
-    auto* meta = reinterpret_cast<uint2*>(scr + nseg * scr_stride);
-    auto* wscr = scr + nseg * scr_stride + nseg * 8u;
-    hipLaunchKernelGGL(bitar_hip::zstd_parse_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in, n,
-                       seg, scr, scr_stride, meta);
-    hipLaunchKernelGGL(bitar_hip::zstd_entropy_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
-                       n, seg, scr, scr_stride, meta, slab, slot_stride, dsts, d_sizes,
-                       err_word(ctx, s), wscr, w_stride);
-    hipLaunchKernelGGL(bitar_hip::zstd_walk_kernel, dim3((uint32_t)((nseg + 15) / 16)), dim3(64),
-                       0, s, scr, scr_stride, seg, (uint32_t)nseg, wscr, w_stride);
-    hipLaunchKernelGGL(bitar_hip::zstd_emit_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in, n,
-                       seg, scr, scr_stride, slab, slot_stride, dsts, d_sizes, wscr, w_stride);
+    auto* meta = reinterpret_cast<uint2*>(scr + ch.size * scr_stride);
+    auto* wscr = scr + ch.size * scr_stride + ch.size * 8u;
+    for (uint64_t c0 = 0; c0 < nseg; c0 += ch.size) {
+      const uint64_t cn = nseg - c0 < ch.size ? nseg - c0 : ch.size;
+      const uint64_t cb = c0 * seg, nb = n - cb < cn * seg ? n - cb : cn * seg;
+      uint8_t* cslab = slab ? slab + c0 * slot_stride : nullptr;
+      uint8_t* const* cdsts = dsts ? dsts + c0 : nullptr;
+      const uint8_t* cin = in + cb;
+      hipLaunchKernelGGL(bitar_hip::zstd_parse_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin,
+                         nb, seg, scr, scr_stride, meta);
+      hipLaunchKernelGGL(bitar_hip::zstd_entropy_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin,
+                         nb, seg, scr, scr_stride, meta, cslab, slot_stride, cdsts, d_sizes + c0,
+                         err_word(ctx, s), wscr, w_stride);
+      hipLaunchKernelGGL(bitar_hip::zstd_walk_kernel, dim3((uint32_t)((cn + 15) / 16)), dim3(64),
+                         0, s, scr, scr_stride, seg, (uint32_t)cn, wscr, w_stride);
+      hipLaunchKernelGGL(bitar_hip::zstd_emit_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin, nb,
+                         seg, scr, scr_stride, cslab, slot_stride, cdsts, d_sizes + c0, wscr,
+                         w_stride);
+    }
     const hipError_t le = hipGetLastError();
     HIP_TRY(hipFreeAsync(scratch, s), "scratch release");
     HIP_TRY(le, "compress launch");
@@ -409,59 +455,76 @@ int bitar_hip_pointer_info(const void* ptr, int* kind, int* device) {
   return 0;
 }
 
-// segments per wave of zstd_lanes_kernel: BITAR_HIP_ZSTD_LANES = 64 / 32 / 16 / 8, 0 = off
-// (tests switch it with bitar_hip_debug_set_zstd_lanes to cover both decoders)
-static uint32_t lanes_from(long x) {
+// Decoder options: per context (bitar_hip_decoder_options).  The environment variables
+// BITAR_HIP_INFLATE_LANES / BITAR_HIP_ZSTD_LANES / BITAR_HIP_ZSTD_SEQ (tuning runs) set the
+// defaults a context starts from; cfg->flags override them at open.
+static uint32_t zstd_lanes_from(long x) {
   return x <= 0 ? 0u : x >= 64 ? 64u : x >= 32 ? 32u : x >= 16 ? 16u : 8u;
 }
-static std::atomic<uint32_t> g_zstd_lanes{[] {
-  const char* e = std::getenv("BITAR_HIP_ZSTD_LANES");
-  return lanes_from(e ? std::strtol(e, nullptr, 10) : 16);
-}()};
-static uint32_t zstd_lanes() { return g_zstd_lanes.load(std::memory_order_relaxed); }
-extern "C" int bitar_hip_debug_set_zstd_lanes(int lanes) {
-  const uint32_t old = zstd_lanes();
-  g_zstd_lanes.store(lanes_from(lanes));
-  return (int)old;
-}
-
-// segments per wave of inflate_lanes_kernel: BITAR_HIP_INFLATE_LANES = 4 / 8 / 16 / 32, 0 = off
 static uint32_t inflate_lanes_from(long x) {
   return x <= 0 ? 0u : x >= 32 ? 32u : x >= 16 ? 16u : x >= 8 ? 8u : 4u;
 }
-static std::atomic<uint32_t> g_inflate_lanes{[] {
-  const char* e = std::getenv("BITAR_HIP_INFLATE_LANES");
-  // 4: 4516 waves per GiB hide more of each lane's load latency than 16 (1129 waves, about
-  // one per SIMD): 1-GiB decode kind 1 17.3 -> 15.5 ms, kind 5 14.6 -> 12.7, kind 6 9.8 ->
-  // 8.9; stored-only (random) data 9.2 -> 10.4
-  return inflate_lanes_from(e ? std::strtol(e, nullptr, 10) : 4);
-}()};
-static uint32_t inflate_lanes() { return g_inflate_lanes.load(std::memory_order_relaxed); }
-extern "C" int bitar_hip_debug_set_inflate_lanes(int lanes) {
-  const uint32_t old = inflate_lanes();
-  g_inflate_lanes.store(inflate_lanes_from(lanes));
-  return (int)old;
+static long env_long(const char* name, long dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::strtol(e, nullptr, 10) : dflt;
 }
 
-// segments per wave of zstd_hlit_kernel / zstd_handoff_kernel (4 / 8 / 16): tuning knobs
-// BITAR_HIP_HLIT_SEGS, BITAR_HIP_HANDOFF_LANES, read once
+static void init_options(bitar_hip_ctx* ctx, uint32_t flags) {
+  // 4 segments per wave: 4516 waves per GiB hide more of each lane's load latency than 16
+  // (1129 waves, about one per SIMD): 1-GiB decode kind 1 17.3 -> 15.5 ms, kind 5 14.6 ->
+  // 12.7, kind 6 9.8 -> 8.9; stored-only (random) data 9.2 -> 10.4
+  ctx->inflate_lanes = flags & BITAR_HIP_FLAG_INFLATE_WAVE_ONLY
+                           ? 0u : inflate_lanes_from(env_long("BITAR_HIP_INFLATE_LANES", 4));
+  ctx->zstd_lanes = flags & BITAR_HIP_FLAG_ZSTD_WAVE_ONLY
+                        ? 0u : zstd_lanes_from(env_long("BITAR_HIP_ZSTD_LANES", 16));
+  ctx->zstd_seq = flags & BITAR_HIP_FLAG_ZSTD_LANE_EXEC ? 0u : env_long("BITAR_HIP_ZSTD_SEQ", 1) != 0;
+  ctx->count_paths = (flags & BITAR_HIP_FLAG_COUNT_PATHS) ? 1u : 0u;
+}
+
+// the counters' device pointer for a launch, null (= not counted) unless count_paths is on
+static unsigned long long* stats_of(bitar_hip_ctx* ctx) {
+  return ctx->count_paths.load(std::memory_order_relaxed) ? ctx->d_stats : nullptr;
+}
+
+extern "C" int bitar_hip_get_decoder_options(bitar_hip_ctx* ctx, bitar_hip_decoder_options* opt) {
+  if (!ctx || !opt) return fail(BITAR_HIP_INVALID, "null argument");
+  opt->inflate_lanes = ctx->inflate_lanes.load();
+  opt->zstd_lanes = ctx->zstd_lanes.load();
+  opt->zstd_seq = ctx->zstd_seq.load();
+  opt->count_paths = ctx->count_paths.load();
+  return 0;
+}
+
+extern "C" int bitar_hip_set_decoder_options(bitar_hip_ctx* ctx,
+                                             const bitar_hip_decoder_options* opt) {
+  if (!ctx || !opt) return fail(BITAR_HIP_INVALID, "null argument");
+  ctx->inflate_lanes = inflate_lanes_from((long)opt->inflate_lanes);
+  ctx->zstd_lanes = zstd_lanes_from((long)opt->zstd_lanes);
+  ctx->zstd_seq = opt->zstd_seq ? 1u : 0u;
+  ctx->count_paths = opt->count_paths ? 1u : 0u;
+  return 0;
+}
+
+extern "C" int bitar_hip_path_counters(bitar_hip_ctx* ctx, uint64_t* out, uint32_t n) {
+  if (int r = enter(ctx)) return r;
+  if (!out && n) return fail(BITAR_HIP_INVALID, "null out");
+  HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  unsigned long long v[BITAR_HIP_PATH_COUNT];
+  HIP_TRY(hipMemcpy(v, ctx->d_stats, sizeof(v), hipMemcpyDeviceToHost), "read path counters");
+  HIP_TRY(hipMemset(ctx->d_stats, 0, sizeof(v)), "reset path counters");
+  for (uint32_t k = 0; k < n && k < BITAR_HIP_PATH_COUNT; ++k) out[k] = v[k];
+  return 0;
+}
+
+// segments per wave of zstd_hlit_kernel / zstd_handoff_kernel / zstd_seqdec_kernel (4 / 8 /
+// 16): tuning knobs BITAR_HIP_HLIT_SEGS, BITAR_HIP_HANDOFF_LANES, BITAR_HIP_SEQDEC_SEGS, read once
 static uint32_t pow2_knob(const char* name, uint32_t dflt) {
-  const char* e = std::getenv(name);
-  const long x = e ? std::strtol(e, nullptr, 10) : (long)dflt;
+  const long x = env_long(name, (long)dflt);
   return x >= 16 ? 16u : x >= 8 ? 8u : 4u;
 }
 static uint32_t hlit_segs() {
   static const uint32_t v = pow2_knob("BITAR_HIP_HLIT_SEGS", 16);
   return v;
-}
-// two-phase sequence execution (zstd_seq.hip) for segments <= 64 KiB: BITAR_HIP_ZSTD_SEQ=0
-// leaves every handed-off segment to the lane executor (tests cover both)
-static std::atomic<uint32_t> g_zstd_seq{[] {
-  const char* e = std::getenv("BITAR_HIP_ZSTD_SEQ");
-  return e ? (uint32_t)(std::strtol(e, nullptr, 10) != 0) : 1u;
-}()};
-extern "C" int bitar_hip_debug_set_zstd_seq(int on) {
-  return (int)g_zstd_seq.exchange(on ? 1u : 0u);
 }
 static uint32_t seqdec_segs() {
   static const uint32_t v = pow2_knob("BITAR_HIP_SEQDEC_SEGS", 16);
@@ -495,6 +558,7 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
     return fail(BITAR_HIP_INVALID, "null buffer");
   if (nseg > 0x7FFFFFFFu) return fail(BITAR_HIP_INVALID, "too many segments");
   hipStream_t s = pick_stream(ctx, stream);
+  unsigned long long* const stats = stats_of(ctx);
   const auto* srcs = reinterpret_cast<const uint8_t* const*>(d_srcs);
   const auto* slab = static_cast<const uint8_t*>(d_slab);
   auto* out = static_cast<uint8_t*>(d_out);
@@ -503,14 +567,16 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
     // near-history kernel over every segment, then the far-history kernel over the segments
     // it deferred (lz4_decompress.hip)
     hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<false>, dim3(nseg), dim3(64), 0, s, srcs,
-                       slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s));
+                       slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
+                       stats);
     hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<true>, dim3(nseg), dim3(64), 0, s, srcs,
-                       slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s));
+                       slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
+                       stats);
   }
   else if (codec == BITAR_HIP_CODEC_DEFLATE) {
     // lane-per-segment decoder for stored / fixed-Huffman streams first; the wave decoder
     // then takes the segments it deferred (inflate_lanes.hip)
-    const uint32_t L = inflate_lanes();
+    const uint32_t L = ctx->inflate_lanes.load(std::memory_order_relaxed);
     if (L) {
       const dim3 g((nseg + L - 1) / L);
 #define BITAR_INFL_LANES(N)                                                                  \
@@ -523,12 +589,13 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
 #undef BITAR_INFL_LANES
     }
     hipLaunchKernelGGL(bitar_hip::inflate_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
-                       stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s), L ? 1u : 0u);
+                       stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s), L ? 1u : 0u,
+                       stats);
   }
   else {
     // lane-per-segment decoder first; the wave-per-segment decoder then takes the segments it
     // deferred (zstd_lanes.hip)
-    const uint32_t L = zstd_lanes();
+    const uint32_t L = ctx->zstd_lanes.load(std::memory_order_relaxed);
     if (L) {
       const dim3 g((nseg + L - 1) / L);
       if (L == 64)
@@ -544,49 +611,61 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
         hipLaunchKernelGGL(bitar_hip::zstd_lanes_kernel<8>, g, dim3(64), 0, s, srcs, slab,
                            stride, d_sizes, nseg, seg, out, d_produced);
     }
-    // the wave decoder hands the sequence sections of its frames' last blocks to the lane
-    // executor through a stream-ordered scratch (zstd_decompress.hip kHand*: 6 KiB per
-    // segment)
+    // The wave decoder hands the sequence sections of its frames' last blocks over through a
+    // stream-ordered scratch (zstd_hand.hip.h: kStride bytes per segment); segments <= 64 KiB
+    // then run FSE chains -> records (zstd_seqdec_kernel, rcap 8-byte records per segment)
+    // -> output (zstd_exec_kernel), the rest the lane executor.  Both scratch buffers are
+    // allocated before any kernel is queued, once, for a chunk of <= kChunkSegs segments.
+    const Chunks ch(nseg);
+    const bool seq = ctx->zstd_seq.load(std::memory_order_relaxed) && seg <= 65536;
+    const uint32_t rcap = seg / 3 + 1;  // every valid frame (matches are >= 3 bytes)
     void* hscr = nullptr;
-    HIP_TRY(hipMallocAsync(&hscr, (uint64_t)nseg * bitar_hip::zhand::kStride, s),
-            "scratch allocation");
-    hipLaunchKernelGGL(bitar_hip::zstd_decompress_kernel, dim3(nseg), dim3(64), 0, s, srcs,
-                       slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
-                       L ? 1u : 0u, static_cast<uint8_t*>(hscr));
-    const uint8_t* hs = static_cast<const uint8_t*>(hscr);
-    uint32_t* ew = err_word(ctx, s);
-#define BITAR_ZSTD_TAIL(K, N)                                                                \
-  hipLaunchKernelGGL(bitar_hip::K<N>, dim3((nseg + N - 1) / N), dim3(64), 0, s, srcs, slab, \
-                     stride, d_sizes, nseg, seg, out, d_produced, hs, ew)
-    const uint32_t hs_n = hlit_segs(), ho_n = handoff_lanes();
-    if (hs_n == 4) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 4);
-    else if (hs_n == 8) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 8);
-    else BITAR_ZSTD_TAIL(zstd_hlit_kernel, 16);
-    // segments <= 64 KiB: FSE chains -> records (a lane per segment), records -> output (a
-    // wave per segment); segments with more than rcap sequences stay with the lane executor
     void* recs = nullptr;
-    if (g_zstd_seq.load(std::memory_order_relaxed) && seg <= 65536) {
-      const uint32_t rcap = seg / 3 + 1;  // every valid frame (matches are >= 3 bytes)
-      HIP_TRY(hipMallocAsync(&recs, (uint64_t)nseg * rcap * 8, s), "scratch allocation");
-      auto* rp = static_cast<uint64_t*>(recs);
-      const uint32_t sd = seqdec_segs();
-#define BITAR_SEQDEC(N)                                                                      \
-  hipLaunchKernelGGL(bitar_hip::zstd_seqdec_kernel<N>, dim3((nseg + N - 1) / N), dim3(64), 0, s, \
-                     srcs, slab, stride, d_sizes, nseg, seg, d_produced,                      \
-                     static_cast<uint8_t*>(hscr), rp, rcap, ew)
-      if (sd == 4) BITAR_SEQDEC(4);
-      else if (sd == 8) BITAR_SEQDEC(8);
-      else BITAR_SEQDEC(16);
-#undef BITAR_SEQDEC
-      hipLaunchKernelGGL(bitar_hip::zstd_exec_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
-                         stride, nseg, seg, out, d_produced, hs, rp, rcap, ew);
+    HIP_TRY(hipMallocAsync(&hscr, ch.size * bitar_hip::zhand::kStride, s), "scratch allocation");
+    if (seq) {
+      const hipError_t e = hipMallocAsync(&recs, ch.size * rcap * 8, s);
+      if (e != hipSuccess) {
+        (void)hipFreeAsync(hscr, s);
+        return hip_fail(e, "scratch allocation");
+      }
     }
-    if (ho_n == 4) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 4);
-    else if (ho_n == 8) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 8);
-    else BITAR_ZSTD_TAIL(zstd_handoff_kernel, 16);
+    uint8_t* hs = static_cast<uint8_t*>(hscr);
+    auto* rp = static_cast<uint64_t*>(recs);
+    uint32_t* ew = err_word(ctx, s);
+    const uint32_t hs_n = hlit_segs(), ho_n = handoff_lanes(), sd = seqdec_segs();
+    for (uint64_t c0 = 0; c0 < nseg; c0 += ch.size) {
+      const uint32_t cn = (uint32_t)(nseg - c0 < ch.size ? nseg - c0 : ch.size);
+      const uint8_t* const* csrcs = srcs ? srcs + c0 : nullptr;
+      const uint8_t* cslab = slab ? slab + c0 * stride : nullptr;
+      const uint32_t* csz = d_sizes + c0;
+      uint8_t* cout = out + c0 * seg;
+      uint32_t* cprod = d_produced + c0;
+      hipLaunchKernelGGL(bitar_hip::zstd_decompress_kernel, dim3(cn), dim3(64), 0, s, csrcs,
+                         cslab, stride, csz, cn, seg, cout, cprod, ew, L ? 1u : 0u, hs, stats);
+#define BITAR_ZSTD_TAIL(K, N)                                                                 \
+  hipLaunchKernelGGL(bitar_hip::K<N>, dim3((cn + N - 1) / N), dim3(64), 0, s, csrcs, cslab, stride, \
+                     csz, cn, seg, cout, cprod, hs, ew)
+      if (hs_n == 4) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 4);
+      else if (hs_n == 8) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 8);
+      else BITAR_ZSTD_TAIL(zstd_hlit_kernel, 16);
+      if (seq) {
+#define BITAR_SEQDEC(N)                                                                       \
+  hipLaunchKernelGGL(bitar_hip::zstd_seqdec_kernel<N>, dim3((cn + N - 1) / N), dim3(64), 0, s,  \
+                     csrcs, cslab, stride, csz, cn, seg, cprod, hs, rp, rcap, ew, stats)
+        if (sd == 4) BITAR_SEQDEC(4);
+        else if (sd == 8) BITAR_SEQDEC(8);
+        else BITAR_SEQDEC(16);
+#undef BITAR_SEQDEC
+        hipLaunchKernelGGL(bitar_hip::zstd_exec_kernel, dim3(cn), dim3(64), 0, s, csrcs, cslab,
+                           stride, cn, seg, cout, cprod, hs, rp, rcap, ew, stats);
+      }
+      if (ho_n == 4) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 4);
+      else if (ho_n == 8) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 8);
+      else BITAR_ZSTD_TAIL(zstd_handoff_kernel, 16);
 #undef BITAR_ZSTD_TAIL
+    }
     const hipError_t le = hipGetLastError();
-    if (recs) HIP_TRY(hipFreeAsync(recs, s), "scratch release");
+    if (recs) (void)hipFreeAsync(recs, s);
     HIP_TRY(hipFreeAsync(hscr, s), "scratch release");
     HIP_TRY(le, "decompress launch");
   }

@@ -11,6 +11,7 @@
 //   long literal runs bypass the ring and stream HBM -> HBM (wave_copy_global).
 #pragma once
 #include "wave.hip.h"
+#include "../../include/bitar_hip.h"  // BITAR_HIP_PATH_* counter indices
 
 namespace bitar_hip {
 
@@ -40,6 +41,7 @@ struct State {
   uint32_t fenced;     // out[0, fenced) visible to this wave's loads
   uint64_t wb;         // absolute address of win[0] (16-aligned)
   uint32_t wlen;       // bytes of the stream covered by win: [wb, wb + wlen) ∩ segment
+  uint32_t nbatch;     // batches run (inflate_kernel's path counter)
 };
 
 // Stage the stream bytes starting at absolute address `abs` (rounded down to 16 B) into

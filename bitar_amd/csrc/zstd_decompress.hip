@@ -1154,7 +1154,7 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
-    uint32_t defer_only, uint8_t* __restrict__ hscr) {
+    uint32_t defer_only, uint8_t* __restrict__ hscr, unsigned long long* __restrict__ stats) {
   using namespace zsd;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
   __shared__ __attribute__((aligned(16))) Tabs t;
@@ -1253,7 +1253,13 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
       lds_order();
       if (lane_id() < 16) atomicAdd(&g_zprof[lane_id()], zp_lds[lane_id()]);
 #endif
-      if (lane_id() == 0) produced[i] = kHanded;
+      if (lane_id() == 0) {
+        produced[i] = kHanded;
+        if (stats) {
+          atomicAdd(stats + BITAR_HIP_PATH_ZSTD_WAVE, 1ull);
+          atomicAdd(stats + BITAR_HIP_PATH_ZSTD_HANDED, 1ull);
+        }
+      }
       return;
     }
     flush(s, ring, s.op, true);
@@ -1278,6 +1284,7 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     produced[i] = 0xFFFFFFFFu;
     atomicOr(err, 1u);
   }
+  if (stats && lane_id() == 0) atomicAdd(stats + BITAR_HIP_PATH_ZSTD_WAVE, 1ull);
 }
 
 }  // namespace bitar_hip

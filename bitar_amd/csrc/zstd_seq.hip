@@ -135,7 +135,7 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint32_t* __restrict__ produced, uint8_t* __restrict__ hscr, uint64_t* __restrict__ recs,
-    uint32_t rcap, uint32_t* __restrict__ err) {
+    uint32_t rcap, uint32_t* __restrict__ err, unsigned long long* __restrict__ stats) {
   using namespace zsq;
   using lanes::ld8;
   __shared__ __attribute__((aligned(16))) uint16_t cel[L * kTab];
@@ -285,6 +285,10 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
       produced[i] = 0xFFFFFFFFu;
       atomicOr(err, 1u);
     }
+    if (stats) {
+      atomicAdd(stats + BITAR_HIP_PATH_ZSTD_SEQDEC, 1ull);
+      if (!ok) atomicAdd(stats + BITAR_HIP_PATH_ZSTD_SEQDEC_REJECT, 1ull);
+    }
   }
 }
 
@@ -300,7 +304,8 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, uint32_t nseg, uint32_t seg, uint8_t* __restrict__ out,
     uint32_t* __restrict__ produced, const uint8_t* __restrict__ hscr,
-    const uint64_t* __restrict__ recs, uint32_t rcap, uint32_t* __restrict__ err) {
+    const uint64_t* __restrict__ recs, uint32_t rcap, uint32_t* __restrict__ err,
+    unsigned long long* __restrict__ stats) {
   using namespace zsq;
   using namespace sr;
   // (a trash byte / word per lane after the ring and the event array: lanes with nothing to
@@ -434,17 +439,21 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
       produced[i] = 0xFFFFFFFFu;
       atomicOr(err, 1u);
     }
+    if (stats) {
+      atomicAdd(stats + BITAR_HIP_PATH_ZSTD_EXEC, 1ull);
+      if (!ok) atomicAdd(stats + BITAR_HIP_PATH_ZSTD_EXEC_REJECT, 1ull);
+    }
   }
 }
 
 template __global__ void zstd_seqdec_kernel<16>(const uint8_t* const*, const uint8_t*, uint64_t,
                                                 const uint32_t*, uint32_t, uint32_t, uint32_t*,
-                                                uint8_t*, uint64_t*, uint32_t, uint32_t*);
+                                                uint8_t*, uint64_t*, uint32_t, uint32_t*, unsigned long long*);
 template __global__ void zstd_seqdec_kernel<4>(const uint8_t* const*, const uint8_t*, uint64_t,
                                                const uint32_t*, uint32_t, uint32_t, uint32_t*,
-                                               uint8_t*, uint64_t*, uint32_t, uint32_t*);
+                                               uint8_t*, uint64_t*, uint32_t, uint32_t*, unsigned long long*);
 template __global__ void zstd_seqdec_kernel<8>(const uint8_t* const*, const uint8_t*, uint64_t,
                                                const uint32_t*, uint32_t, uint32_t, uint32_t*,
-                                               uint8_t*, uint64_t*, uint32_t, uint32_t*);
+                                               uint8_t*, uint64_t*, uint32_t, uint32_t*, unsigned long long*);
 
 }  // namespace bitar_hip

@@ -61,8 +61,15 @@ typedef struct bitar_hip_ctx bitar_hip_ctx;
 
 typedef struct {
   uint32_t num_streams; /* queue pairs: one HIP stream each (driver.cc:100-157 lcore map) */
-  uint32_t flags;       /* reserved, 0 */
+  uint32_t flags;       /* BITAR_HIP_FLAG_* (0: the default decoders, no path counters) */
 } bitar_hip_config;
+
+/* bitar_hip_config.flags: the context's initial decoder options (bitar_hip_decoder_options);
+ * every context keeps its own, so engines with different settings run side by side. */
+#define BITAR_HIP_FLAG_INFLATE_WAVE_ONLY 0x1u /* no lane inflater in front of inflate_kernel */
+#define BITAR_HIP_FLAG_ZSTD_WAVE_ONLY 0x2u    /* no lane Zstd decoder in front of the wave one */
+#define BITAR_HIP_FLAG_ZSTD_LANE_EXEC 0x4u    /* handed-off sequence sections: lane executor */
+#define BITAR_HIP_FLAG_COUNT_PATHS 0x8u       /* count decoder path entries (see below) */
 
 /* Number of visible gfx950 devices.  Replaces rte_compressdev_devices_get() in
  * CompressDriver::ListAvailableDeviceIds (reference src/driver.cc:173-190). */
@@ -213,6 +220,43 @@ enum bitar_hip_checksum_kind {
 int bitar_hip_checksum(bitar_hip_ctx* ctx, void* stream, uint32_t kind, const void* d_data,
                        uint64_t n, uint32_t seg, const uint32_t* d_lens, uint32_t nseg,
                        uint64_t* d_sums);
+
+/* Decoder selection of one context.  The decoders are interchangeable (every one accepts and
+ * rejects exactly what the oracle does); the options pick which kernels run, for tests and
+ * tuning.  No reference counterpart: the BlueField engine has one decoder. */
+typedef struct {
+  uint32_t inflate_lanes; /* segments per wave of inflate_lanes_kernel: 4, 8, 16 or 32;
+                             0 = inflate_kernel (one wave per segment) alone */
+  uint32_t zstd_lanes;    /* segments per wave of zstd_lanes_kernel: 8, 16, 32 or 64; 0 = off */
+  uint32_t zstd_seq;      /* 1 = handed-off sequence sections run zstd_seqdec_kernel +
+                             zstd_exec_kernel; 0 = the lane executor (zstd_handoff_kernel) */
+  uint32_t count_paths;   /* 1 = count path entries (bitar_hip_path_counters) */
+} bitar_hip_decoder_options;
+
+int bitar_hip_get_decoder_options(bitar_hip_ctx* ctx, bitar_hip_decoder_options* opt);
+/* Takes effect for calls made after it returns (calls already queued keep their kernels). */
+int bitar_hip_set_decoder_options(bitar_hip_ctx* ctx, const bitar_hip_decoder_options* opt);
+
+/* Path counters (counted while count_paths is on): how many segments reached each stage of
+ * the decoders, so tests can show that their inputs exercised the path they target. */
+enum bitar_hip_path_counter {
+  BITAR_HIP_PATH_INFLATE_WAVE = 0,       /* segments decoded by inflate_kernel */
+  BITAR_HIP_PATH_INFLATE_WAVE_REJECT = 1,/*   ... of which rejected */
+  BITAR_HIP_PATH_INFLATE_BATCH_SEGS = 2, /*   ... that ran >= 1 multi-symbol batch */
+  BITAR_HIP_PATH_INFLATE_BATCHES = 3,    /* batches run by inflate_kernel */
+  BITAR_HIP_PATH_ZSTD_WAVE = 4,          /* segments decoded by zstd_decompress_kernel */
+  BITAR_HIP_PATH_ZSTD_HANDED = 5,        /*   ... that handed their last block over */
+  BITAR_HIP_PATH_ZSTD_SEQDEC = 6,        /* handed segments taken by zstd_seqdec_kernel */
+  BITAR_HIP_PATH_ZSTD_SEQDEC_REJECT = 7, /*   ... rejected there */
+  BITAR_HIP_PATH_ZSTD_EXEC = 8,          /* segments executed by zstd_exec_kernel */
+  BITAR_HIP_PATH_ZSTD_EXEC_REJECT = 9,   /*   ... rejected there */
+  BITAR_HIP_PATH_LZ4_FAR = 10,           /* segments deferred to the far-history LZ4 kernel */
+  BITAR_HIP_PATH_COUNT = 16
+};
+
+/* Wait for the device, copy min(n, BITAR_HIP_PATH_COUNT) counters to out (host memory) and
+ * reset them. */
+int bitar_hip_path_counters(bitar_hip_ctx* ctx, uint64_t* out, uint32_t n);
 
 /* Where `ptr` lives: *kind = 0 pageable host, 1 pinned host, 2 device memory (then *device
  * is its ordinal).  Replaces rte_mem_virt2iova() residency assumptions (memory.cc:388). */

@@ -22,8 +22,8 @@ def main():
     L = bitar_amd.lib()
     f = L.bitar_hip_debug_zstd_prof
     f.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    L.bitar_hip_debug_set_zstd_lanes(0)  # the wave decoder alone
     eng = bitar_amd.Engine(0)
+    eng.set_decoder_options(zstd_lanes=0)  # the wave decoder alone
     n, seg = 64 << 20, 65536
     nseg = n // seg
     for kind in [int(k) for k in (args[0] if args else "1,2,6").split(",")]:

@@ -20,15 +20,13 @@ torch = pytest.importorskip("torch")
 
 
 @pytest.fixture(autouse=True, params=[4, 16, 0], ids=["lanes4", "lanes16", "wave"])
-def inflate_decoder(request):
+def inflate_decoder(request, eng):
     """Every test runs with the lane-per-segment inflater in front (inflate_lanes.hip; it
     defers dynamic-Huffman and failing streams to the wave kernel) and with the
-    wave-per-segment inflater alone."""
-    import bitar_amd
-    L = bitar_amd.lib()
-    old = L.bitar_hip_debug_set_inflate_lanes(request.param)
+    wave-per-segment inflater alone (decoder options of the test's context)."""
+    old = eng.set_decoder_options(inflate_lanes=request.param)
     yield request.param
-    L.bitar_hip_debug_set_inflate_lanes(old)
+    eng.set_decoder_options(**old)
 
 
 def test_inflate_all_golden(eng):

@@ -22,20 +22,16 @@ torch = pytest.importorskip("torch")
 
 @pytest.fixture(autouse=True, params=[(16, 1), (64, 0), (0, 1)],
                 ids=["lanes16-seq", "lanes64-handoff", "wave-seq"])
-def zstd_decoder(request):
+def zstd_decoder(request, eng):
     """Every test runs with the lane-per-segment decoder in front (zstd_lanes.hip, 16 or 64
     segments per wave; it defers what it does not take to the wave kernel) and with the
     wave-per-segment decoder alone; the sequence sections the wave kernel hands over run
     through the two-phase record path (zstd_seq.hip, "seq") or the lane executor
     (zstd_handoff_kernel, "handoff")."""
-    import bitar_amd
-    L = bitar_amd.lib()
     lanes, seq = request.param
-    old = L.bitar_hip_debug_set_zstd_lanes(lanes)
-    old_seq = L.bitar_hip_debug_set_zstd_seq(seq)
+    old = eng.set_decoder_options(zstd_lanes=lanes, zstd_seq=seq)
     yield request.param
-    L.bitar_hip_debug_set_zstd_lanes(old)
-    L.bitar_hip_debug_set_zstd_seq(old_seq)
+    eng.set_decoder_options(**old)
 
 
 def _libzstd():
