@@ -302,7 +302,7 @@ def stock_decode(eng, args):
     sys.path.insert(0, os.path.join(HERE, "tests"))
     import stock_lib as S  # stock third-party codecs (baseline infrastructure)
     n = args.bytes
-    th = max(1, min(64, host_threads()))
+    th = baseline_threads()
     legs = (("lz4", S.LZ4, 1, 65536, args.kind, "liblz4 1.9.3 LZ4_compress_default"),
             ("deflate", S.DEFLATE, 1, 59460, args.kind,
              "zlib 1.2.11 raw DEFLATE level 1 (dynamic Huffman), the reference's codec "
@@ -375,21 +375,35 @@ def ipc_sample(nbytes):
     return buf[:nbytes].copy()
 
 
+def baseline_threads():
+    """Threads for the all-core CPU baseline: the CPUs this process may run on, capped by its
+    cgroup CPU-time quota (the GPU box shows 256 CPUs but grants 16 cores' worth): more
+    threads than the quota only thrash."""
+    n = host_threads()
+    q = cpu_quota()
+    if q:
+        n = min(n, max(1, int(-(-q // 1))))
+    return n
+
+
 def cpu_baseline(args):
-    """The stock libraries on this host's cores over a bounded sample of the same workload:
-    liblz4 (north-star codec, 64 KiB segments) and zlib level-1 raw DEFLATE (the reference's
-    codec at 59460-B segments), 1 core and every core of this process's CPU set, best of
-    kNumTests = 3 (apps/demo_app.h:45); plus BASELINE configs[0] on 1 core."""
+    """The CPU baseline of BASELINE.md §2 on this host's cores, over a bounded sample of the
+    same workload, best of kNumTests = 3 (apps/demo_app.h:45): stock liblz4 (the north-star
+    codec, 64 KiB segments), zlib level-1 raw DEFLATE (the reference's codec, 59460-B
+    segments) and libzstd level 1 (configs[4]'s codec, 64 KiB segments, kind-2 input), each
+    on 1 core and on every core the process may use (`cores`); plus BASELINE configs[0] on 1
+    core, and the oracle's C restatement of our LZ4 path ("port") beside them."""
     import numpy as np
     sys.path.insert(0, os.path.join(HERE, "tests"))
-    import oracle_lib as O  # the generator of the same input (baseline leg only)
+    import oracle_lib as O  # the generator of the same input + the port (baseline leg only)
     import stock_lib as S
-    nall = host_threads()
+    nall = baseline_threads()
     n = args.cpu_sample
     data = O.fill(args.kind, 0, n)
+    data2 = None
 
-    def timed(sc, seg, level, sample, threads, reps=3):
-        d = data[:sample]
+    def timed(sc, seg, level, sample, threads, reps=3, src=None):
+        d = (data if src is None else src)[:sample]
         slab, stride, sizes = S.compress(sc, d, seg, level, threads)  # warm-up (+ pages)
         out = S.decompress(sc, slab, stride, sizes, sample, seg, threads)
         assert np.array_equal(out, d)
@@ -409,25 +423,54 @@ def cpu_baseline(args):
 
     lz4_all = timed(S.LZ4, 65536, 1, n, nall)
     lz4_one = timed(S.LZ4, 65536, 1, min(n, 64 << 20), 1)
-    # zlib-1 compresses ~0.1 GiB/s per core: smaller samples keep this leg ~10 s
+    # zlib-1 compresses ~0.15 GiB/s per core: smaller samples keep this leg ~10 s
     z_all = timed(S.DEFLATE, 59460, 1, min(n, max(16 << 20, nall * (8 << 20))), nall)
     z_one = timed(S.DEFLATE, 59460, 1, 16 << 20, 1)
+    # libzstd level 1 on the configs[4] input (the kind-2 Arrow record batch)
+    zs_n = min(n, max(64 << 20, nall * (16 << 20)))
+    data2 = O.fill(2, 1000, zs_n)
+    zs_all = timed(S.ZSTD, 65536, 1, zs_n, nall, src=data2)
+    zs_one = timed(S.ZSTD, 65536, 1, min(zs_n, 32 << 20), 1, src=data2)
+    # the port: the oracle's C restatement of this path (window-scan parse + LZ4 emitter,
+    # LZ4 block decode), bit-exact with the GPU kernels
+    pn = min(n, 16 << 20)
+    stride = O.lz4_bound(65536) + 256 & ~255
+
+    def port(threads):
+        best_c = best_d = 1e30
+        for _ in range(2):
+            t0 = time.perf_counter()
+            r, slab, sizes = O.compress_segments(O.CODEC_LZ4, data[:pn], 65536, stride, threads)
+            t1 = time.perf_counter()
+            assert r == 0
+            blobs = [slab[i * stride:i * stride + sizes[i]] for i in range(sizes.size)]
+            t2 = time.perf_counter()
+            r, out, _ = O.decompress_segments(O.CODEC_LZ4, blobs, 65536, pn, threads)
+            t3 = time.perf_counter()
+            assert r == 0 and np.array_equal(out, data[:pn])
+            best_c, best_d = min(best_c, t1 - t0), min(best_d, t3 - t2)
+        return {"roundtrip_gibs": round(pn / GIB / (best_c + best_d), 4),
+                "compress_gibs": round(pn / GIB / best_c, 4),
+                "decompress_gibs": round(pn / GIB / best_d, 4),
+                "ratio": round(pn / float(sizes.astype(np.int64).sum()), 4),
+                "sample_bytes": pn, "threads": threads}
+
     cfg0 = None
     ipc = ipc_sample(1 << 20)
     if ipc is not None:
         c0 = {}
         for name, sc, seg in (("deflate_raw_l1_59460", S.DEFLATE, 59460),
                               ("lz4_64k", S.LZ4, 65536)):
-            slab, stride, sizes = S.compress(sc, ipc, seg, 1, 1)
-            out = S.decompress(sc, slab, stride, sizes, ipc.size, seg, 1)
+            slab, stride0, sizes = S.compress(sc, ipc, seg, 1, 1)
+            out = S.decompress(sc, slab, stride0, sizes, ipc.size, seg, 1)
             assert np.array_equal(out, ipc)
             reps = 20
             t0 = time.perf_counter()
             for _ in range(reps):
-                S.compress(sc, ipc, seg, 1, 1, stride=stride)
+                S.compress(sc, ipc, seg, 1, 1, stride=stride0)
             t1 = time.perf_counter()
             for _ in range(reps):
-                S.decompress(sc, slab, stride, sizes, ipc.size, seg, 1, out=out)
+                S.decompress(sc, slab, stride0, sizes, ipc.size, seg, 1, out=out)
             t2 = time.perf_counter()
             tc, td = (t1 - t0) / reps, (t2 - t1) / reps
             c0[name] = {"compress_gibs": round(ipc.size / GIB / tc, 4),
@@ -441,19 +484,28 @@ def cpu_baseline(args):
         "value": lz4_all["roundtrip_gibs"],
         "unit": "GiB/s",
         "cores": nall,
-        "kind": "port",
+        "kind": "stock",
+        "kind_note": "BASELINE.md §2's CPU baseline is the stock library: the reference has no "
+                     "software LZ4 path and its DEFLATE is a hardware engine, so no 'reference' "
+                     "build exists; 'port' (the oracle's C restatement of this LZ4 path) is "
+                     "timed below",
         "sample": f"{n >> 20} MiB of the same kind-{args.kind} input, 65536-B segments, stock "
                   f"liblz4 1.9.3 (LZ4_compress_default + LZ4_decompress_safe) on {nall} "
-                  f"threads (one per core of this process's CPU set; os.cpu_count() = "
-                  f"{os.cpu_count()}), best of 3 -- the reference has no software LZ4 path, "
-                  f"so the stock library stands in for it",
+                  f"threads = this process's CPU set ({host_threads()} CPUs, os.cpu_count() "
+                  f"{os.cpu_count()}) capped by its cgroup quota ({cpu_quota()} cores), best of 3",
         "lz4": {"all_cores": lz4_all, "one_core": lz4_one},
         "deflate_zlib1": {"all_cores": z_all, "one_core": z_one,
                           "note": "the reference's codec in software: zlib 1.2.11 raw DEFLATE "
                                   "level 1, 59460-B segments"},
+        "zstd_libzstd1": {"all_cores": zs_all, "one_core": zs_one,
+                          "note": "BASELINE configs[4]'s codec: libzstd level 1, 65536-B "
+                                  "segments, kind-2 Arrow record-batch input"},
+        "port": {"all_cores": port(nall), "one_core": port(1),
+                 "note": "oracle/bitar_oracle.c: the CPU restatement of the GPU LZ4 path "
+                         "(bit-exact), 16 MiB sample"},
         "configs0": cfg0,
         "os_cpu_count": os.cpu_count(),
-        # the threads above run inside this CPU-time quota (cgroup cpu.max) when it is set
+        "affinity_cpus": host_threads(),
         "cpu_quota_cores": cpu_quota(),
     }
 
@@ -563,7 +615,8 @@ def main():
                         f"BASELINE configs[3]: {args.record_bytes >> 30} GiB Arrow record-batch "
                         f"job, 64 KiB chunks, round-robin batches of 256 chunks over {world} "
                         f"GPU(s), {args.streams} concurrent queue-pair streams per GPU, LZ4 "
-                        f"compress + RCCL size all-gather + decompress (total work fixed)")
+                        f"compress + {'RCCL size all-gather + ' if world > 1 else ''}decompress "
+                        f"(total work fixed)")
         s["scaling"] = "strong"
         s["streams_per_gpu"] = args.streams
         res["recordbatch"] = s

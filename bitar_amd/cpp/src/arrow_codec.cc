@@ -355,55 +355,77 @@ arrow::Result<int64_t> HipCodec::Decompress(int64_t input_len, const uint8_t* in
 arrow::Result<int64_t> HipCodec::DecompressZstd(const std::vector<Frame>& frames,
                                                 const uint8_t* d_in, int64_t output_buffer_len,
                                                 uint8_t* output) {
-  const uint64_t nseg = frames.size();
-  if (nseg > 0x7FFFFFFFull) return arrow::Status::Invalid("too many segments");
-  uint64_t seg = 0;
+  const uint64_t nfr = frames.size();
+  const uint64_t cap = static_cast<uint64_t>(output_buffer_len);
+  // Declared content sizes come from untrusted headers: their sum must fit the caller's
+  // buffer BEFORE anything is reserved (a frame without one: only as the single frame, sized
+  // by the output buffer).
+  uint64_t declared = 0;
   for (const Frame& f : frames) {
-    if (!f.has_content && nseg > 1)
+    if (!f.has_content && nfr > 1)
       return arrow::Status::NotImplemented("Zstandard frames without content size");
-    const uint64_t c = f.has_content ? f.content : static_cast<uint64_t>(output_buffer_len);
-    seg = std::max(seg, c);
+    const uint64_t c = f.has_content ? f.content : cap;
+    if (c > (1ull << 30)) return arrow::Status::NotImplemented("Zstandard frame larger than 1 GiB");
+    declared += c;
+    if (declared > cap)
+      return arrow::Status::Invalid("declared Zstandard content exceeds the output buffer (",
+                                    output_buffer_len, ")");
   }
-  seg = std::max<uint64_t>((seg + 15) & ~15ull, 16);
-  if (seg > (1ull << 30)) return arrow::Status::NotImplemented("Zstandard frame larger than 1 GiB");
-  std::vector<const uint8_t*> srcs(nseg);
-  std::vector<uint32_t> csz(nseg);
-  for (uint64_t i = 0; i < nseg; ++i) {
-    srcs[i] = d_in + frames[i].offset;
-    csz[i] = static_cast<uint32_t>(frames[i].csize);
-  }
-  ARROW_RETURN_NOT_OK(Reserve(d_srcs_, c_srcs_, nseg * sizeof(void*)));
-  ARROW_RETURN_NOT_OK(Reserve(d_sizes_, c_sizes_, nseg * 4));
-  ARROW_RETURN_NOT_OK(Reserve(d_off_, c_off_, nseg * 4));  // produced sizes
-  ARROW_RETURN_NOT_OK(Reserve(d_out_, c_out_, nseg * seg));
-  ARROW_RETURN_NOT_OK(Copy(d_srcs_, srcs.data(), nseg * sizeof(void*)));
-  ARROW_RETURN_NOT_OK(Copy(d_sizes_, csz.data(), nseg * 4));
-  auto* dout = static_cast<uint8_t*>(d_out_);
-  BITAR_ABI(bitar_hip_decompress(ctx_, nullptr, BITAR_HIP_CODEC_ZSTD,
-                                 reinterpret_cast<const void* const*>(d_srcs_),
-                                 static_cast<const uint32_t*>(d_sizes_),
-                                 static_cast<uint32_t>(nseg), static_cast<uint32_t>(seg), dout,
-                                 nseg * seg, static_cast<uint32_t*>(d_off_)),
-            "bitar_hip_decompress");
-  std::vector<uint32_t> prod(nseg);
-  ARROW_RETURN_NOT_OK(Copy(prod.data(), d_off_, nseg * 4));
-  ARROW_RETURN_NOT_OK(Sync());
+  // Frames are decoded in groups of consecutive frames, one launch each; a group's staging
+  // is (frames) x (its largest frame), kept within the declared total + 64 KiB, so mixed
+  // frame sizes never reserve more than about the output itself (equal-size frames, what
+  // this codec writes: one group).
+  const uint64_t budget = declared + kSeg;
+  auto rnd = [](uint64_t c) { return std::max<uint64_t>((c + 15) & ~15ull, 16); };
   uint64_t total = 0;
-  for (uint64_t i = 0; i < nseg; ++i) {
-    if (frames[i].has_content && prod[i] != frames[i].content)
-      return arrow::Status::IOError("Zstandard frame ", i, " decoded to a wrong size");
-    total += prod[i];
+  for (uint64_t g0 = 0; g0 < nfr;) {
+    uint64_t g1 = g0, seg = 0;
+    while (g1 < nfr) {
+      const uint64_t c = rnd(frames[g1].has_content ? frames[g1].content : cap);
+      const uint64_t s2 = std::max(seg, c);
+      if (g1 > g0 && ((g1 - g0 + 1) * s2 > budget || g1 - g0 + 1 > 0x7FFFFFFFull)) break;
+      seg = s2;
+      ++g1;
+    }
+    const uint64_t nseg = g1 - g0;
+    std::vector<const uint8_t*> srcs(nseg);
+    std::vector<uint32_t> csz(nseg);
+    for (uint64_t i = 0; i < nseg; ++i) {
+      const Frame& f = frames[g0 + i];
+      if (f.csize > 0xFFFFFFFFull) return arrow::Status::Invalid("Zstandard frame over 4 GiB");
+      srcs[i] = d_in + f.offset;
+      csz[i] = static_cast<uint32_t>(f.csize);
+    }
+    ARROW_RETURN_NOT_OK(Reserve(d_srcs_, c_srcs_, nseg * sizeof(void*)));
+    ARROW_RETURN_NOT_OK(Reserve(d_sizes_, c_sizes_, nseg * 4));
+    ARROW_RETURN_NOT_OK(Reserve(d_off_, c_off_, nseg * 4));  // produced sizes
+    ARROW_RETURN_NOT_OK(Reserve(d_out_, c_out_, nseg * seg));
+    ARROW_RETURN_NOT_OK(Copy(d_srcs_, srcs.data(), nseg * sizeof(void*)));
+    ARROW_RETURN_NOT_OK(Copy(d_sizes_, csz.data(), nseg * 4));
+    auto* dout = static_cast<uint8_t*>(d_out_);
+    BITAR_ABI(bitar_hip_decompress(ctx_, nullptr, BITAR_HIP_CODEC_ZSTD,
+                                   reinterpret_cast<const void* const*>(d_srcs_),
+                                   static_cast<const uint32_t*>(d_sizes_),
+                                   static_cast<uint32_t>(nseg), static_cast<uint32_t>(seg), dout,
+                                   nseg * seg, static_cast<uint32_t*>(d_off_)),
+              "bitar_hip_decompress");
+    std::vector<uint32_t> prod(nseg);
+    ARROW_RETURN_NOT_OK(Copy(prod.data(), d_off_, nseg * 4));
+    ARROW_RETURN_NOT_OK(Sync());
+    for (uint64_t i = 0; i < nseg; ++i) {
+      const Frame& f = frames[g0 + i];
+      if (f.has_content && prod[i] != f.content)
+        return arrow::Status::IOError("Zstandard frame ", g0 + i, " decoded to a wrong size");
+      if (total + prod[i] > cap)
+        return arrow::Status::Invalid("decompressed size exceeds the output buffer (",
+                                      output_buffer_len, ")");
+      // frame i's output sits at i * seg: gather them back to back
+      ARROW_RETURN_NOT_OK(Copy(output + total, dout + i * seg, prod[i]));
+      total += prod[i];
+    }
+    ARROW_RETURN_NOT_OK(Sync());
+    g0 = g1;
   }
-  if (total > static_cast<uint64_t>(output_buffer_len))
-    return arrow::Status::Invalid("decompressed size ", total, " exceeds the output buffer (",
-                                  output_buffer_len, ")");
-  // frame i's output sits at i * seg: gather them back to back
-  uint64_t at = 0;
-  for (uint64_t i = 0; i < nseg; ++i) {
-    ARROW_RETURN_NOT_OK(Copy(output + at, dout + i * seg, prod[i]));
-    at += prod[i];
-  }
-  ARROW_RETURN_NOT_OK(Sync());
   return static_cast<int64_t>(total);
 }
 
@@ -471,15 +493,18 @@ arrow::Result<int64_t> HipCodec::DecompressLz4f(const std::vector<Frame>& frames
         return arrow::Status::Invalid("LZ4 stream exceeds the output buffer");
       ARROW_ASSIGN_OR_RAISE(got, Lz4Independent(f, d_in, dout + total));
     } else {
+      // the kernel takes 32-bit offsets: relative to the frame, whose size must fit
+      if (f.csize > 0xFFFFFFFFull)
+        return arrow::Status::NotImplemented("linked-block LZ4 frame over 4 GiB");
       std::vector<uint32_t> tab(2 * f.blocks.size());
       for (size_t b = 0; b < f.blocks.size(); ++b) {
-        tab[2 * b] = static_cast<uint32_t>(f.blocks[b].offset);
+        tab[2 * b] = static_cast<uint32_t>(f.blocks[b].offset - f.offset);
         tab[2 * b + 1] = f.blocks[b].csize | (f.blocks[b].raw ? 0x80000000u : 0u);
       }
       ARROW_RETURN_NOT_OK(Reserve(d_srcs_, c_srcs_, tab.size() * 4));
       ARROW_RETURN_NOT_OK(Reserve(d_off_, c_off_, 4));
       ARROW_RETURN_NOT_OK(Copy(d_srcs_, tab.data(), tab.size() * 4));
-      BITAR_ABI(bitar_hip_lz4_chain(ctx_, nullptr, d_in, static_cast<uint32_t>(n),
+      BITAR_ABI(bitar_hip_lz4_chain(ctx_, nullptr, d_in + f.offset, static_cast<uint32_t>(f.csize),
                                     static_cast<const uint32_t*>(d_srcs_),
                                     static_cast<uint32_t>(f.blocks.size()), dout + total,
                                     c_out_ - total, static_cast<uint32_t*>(d_off_)),

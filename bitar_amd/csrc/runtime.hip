@@ -703,8 +703,10 @@ int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream) {
     HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
     return sync_error(err);
   }
-  // NULL: all work on the device (default, queue-pair and foreign streams); every word
-  HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  // NULL: the default stream and this context's queue pairs (not other contexts' or other
+  // libraries' streams); every word of the context is read and cleared
+  HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+  for (hipStream_t q : ctx->streams) HIP_TRY(hipStreamSynchronize(q), "hipStreamSynchronize");
   std::vector<uint32_t> words(kErrWords);
   HIP_TRY(hipMemcpy(words.data(), ctx->d_err, kErrWords * sizeof(uint32_t),
                     hipMemcpyDeviceToHost), "read error words");

@@ -146,7 +146,8 @@ int bitar_hip_decompress_slab(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
 /* Wait for `stream` and return BITAR_HIP_IO_ERROR if a segment op launched on THAT stream
  * failed since its last sync (each stream has its own sticky device-side error word, read
  * and cleared in stream order, so concurrent queue pairs never see each other's failures).
- * NULL waits for the whole device and reports/clears every stream's word.  Replaces the
+ * NULL waits for the default stream and the context's queue pairs, and reports/clears
+ * every stream's word.  Replaces the
  * completion polling of DequeueBurst + GetErrorCount (reference src/device.cc:84-110,
  * 490-535). */
 int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream);
