@@ -96,11 +96,12 @@ def codec_id(name):
 
 
 def reduce_max_sum(vals_max, vals_sum, world):
-    """MAX over ranks of vals_max, SUM over ranks of vals_sum (float64 lists)."""
-    if world == 1:
-        return list(vals_max), list(vals_sum)
+    """MAX over ranks of vals_max, SUM over ranks of vals_sum (float64 lists); a collective
+    whenever a process group is up (also a one-rank RCCL group)."""
     import torch
     import torch.distributed as dist
+    if not dist.is_initialized():
+        return list(vals_max), list(vals_sum)
     # RCCL reduces device tensors; gloo (the one-GPU rehearsal) host tensors
     dev = f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu"
     a = torch.tensor(list(vals_max), dtype=torch.float64, device=dev)
@@ -140,14 +141,14 @@ def run_job(eng, codec_name, kind, job_bytes, seg, nstreams, steps, warmup, worl
         step(False)
     job.sync()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         step(True)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -510,6 +511,46 @@ def cpu_baseline(args):
     }
 
 
+def frontend_legs(args, headline_ms):
+    """The drop-in C++ API measured by bitar_amd/cpp/build/frontend_bench (a child process):
+    CompressDevice::Compress + Decompress + Recycle on an HBM arrow::Buffer of the headline's
+    size and input (reference apps/demo_app.cc:332-357), and the same round trip with
+    host-resident (pinned) data, whose staging copies cross PCIe, beside the raw link rates."""
+    import subprocess
+    exe = os.path.join(HERE, "bitar_amd", "cpp", "build", "frontend_bench")
+    if not os.path.exists(exe):
+        return {"skipped": "bitar_amd/cpp/build/frontend_bench is not built"}, None
+    cmd = [exe, "--bytes", str(args.bytes), "--seg", str(args.seg), "--kind", str(args.kind),
+           "--steps", str(args.steps), "--warmup", str(args.warmup)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"failed": f"rc {p.returncode}: {p.stderr[-500:]}"}, None
+    r = json.loads(lines[0])
+    h = r["hbm"]
+    fe = {"workload": r["workload"] + " (HBM-resident input and output)",
+          "value": h["roundtrip_gibs"], "unit": "GiB/s", "ms_per_roundtrip": h["ms_per_roundtrip"],
+          "compress_call_ms": h["compress_call_ms"], "decompress_call_ms": h["decompress_call_ms"],
+          "recycle_call_ms": h["recycle_call_ms"], "compression_ratio": h["ratio"],
+          "roundtrip_ok": r["roundtrip_ok"],
+          # > 0: time the C++ front-end adds to the C-ABI headline step (host tables, slot
+          # pool, the arrow::Buffer views, one stream sync per call)
+          "overhead_vs_c_abi": round(h["ms_per_roundtrip"] / headline_ms - 1.0, 4)}
+    hd = None
+    if "host" in r:
+        x = r["host"]
+        hd = {"workload": "the same round trip with host-resident data: pinned HipHost "
+                          "arrow::Buffer input (Compress stages it to HBM) and output "
+                          "(Decompress stages it back) -- PCIe-inclusive, never the headline",
+              "roundtrip_gibs": x["roundtrip_gibs"], "ms_per_roundtrip": x["ms_per_roundtrip"],
+              "compress_call_ms": x["compress_call_ms"],
+              "decompress_call_ms": x["decompress_call_ms"],
+              "roundtrip_ok": r["host_roundtrip_ok"],
+              "link_h2d_gibs": r["h2d_gibs"], "link_d2h_gibs": r["d2h_gibs"],
+              "link_h2d_ms": r["h2d_ms"], "link_d2h_ms": r["d2h_ms"]}
+    return fe, hd
+
+
 def want(args, leg):
     if args.only is None:
         return True
@@ -528,7 +569,9 @@ def main():
 
     world, rank, local = launch.rank_env()
     backend = launch.dist_backend()
-    if world > 1:
+    # a process group whenever a launcher started this rank (world 1 too: one-rank RCCL)
+    use_dist = world > 1 or launch.is_rank_process()
+    if use_dist:
         gpu = launch.rank_device(local, torch.cuda.device_count())
         torch.cuda.set_device(gpu)
         if backend == "nccl":
@@ -564,7 +607,7 @@ def main():
         if not args.no_stock and want(args, "stock"):
             stock = stock_decode(eng, args)
     if rank != 0:
-        if world > 1:
+        if use_dist:
             dist.destroy_process_group()
         return
 
@@ -596,7 +639,7 @@ def main():
                                    + ("RCCL all-gather of sizes" if backend == "nccl" else
                                       f"{backend} all-gather of sizes (ranks sharing "
                                       f"{torch.cuda.device_count()} GPU(s): rehearsal)"))
-                                  if world > 1 else "1 GPU"},
+                                  if use_dist else "1 GPU"},
         "compression_ratio": round(U / r["csize_total"], 4),
         "compress_gibs": round(r["local"]["nbytes"] / r["t_comp"] / GIB, 3),
         "decompress_gibs": round(r["local"]["nbytes"] / r["t_dec"] / GIB, 3),
@@ -615,7 +658,7 @@ def main():
                         f"BASELINE configs[3]: {args.record_bytes >> 30} GiB Arrow record-batch "
                         f"job, 64 KiB chunks, round-robin batches of 256 chunks over {world} "
                         f"GPU(s), {args.streams} concurrent queue-pair streams per GPU, LZ4 "
-                        f"compress + {'RCCL size all-gather + ' if world > 1 else ''}decompress "
+                        f"compress + {'RCCL size all-gather + ' if use_dist and backend == 'nccl' else ''}decompress "
                         f"(total work fixed)")
         s["scaling"] = "strong"
         s["streams_per_gpu"] = args.streams
@@ -628,7 +671,7 @@ def main():
             "BASELINE configs[4] codec: level-1-class Zstd frame per 64 KiB segment "
             "(repeat-offset parse, Huffman literals, per-table FSE / RLE / predefined "
             "sequence codes), compress + decompress, 1 GiB Arrow record-batch buffer per GPU"
-            + (", RCCL size all-gather" if world > 1 else ""))
+            + (", RCCL size all-gather" if use_dist and backend == "nccl" else ""))
     if df is not None:
         res["deflate"] = leg_summary(
             "deflate", df, world, args.steps, args.traffic_json,
@@ -642,10 +685,14 @@ def main():
             "decompress, same input and sharding as the headline")
     if stock is not None:
         res["stock_decode"] = stock[0]
+    if world == 1 and args.codec == "lz4" and (args.only is None or want(args, "frontend")):
+        res["frontend"], hd = frontend_legs(args, res["ms_per_step"])
+        if hd is not None:
+            res["h2d_d2h"] = hd
     if not args.no_cpu_baseline and world == 1 and args.codec == "lz4" and args.only is None:
         res["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(res), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

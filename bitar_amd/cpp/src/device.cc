@@ -27,12 +27,14 @@ namespace internal {
 static constexpr std::uint32_t kMinPreallocateSlots = 20;  // reference memory.h:51
 
 // Pool of compressed-output slots (DeviceMemory, reference memory.cc:120-228): a LIFO free
-// stack of slot addresses carved from HBM chunks, an occupied set, growth on demand.
+// stack of slot addresses carved from HBM chunks, an occupied flag per slot (the reference's
+// occupied set, as a flag array: a 16384-segment call takes and returns 16384 slots, and a
+// hash-set node per slot cost ~1 ms of host time per call), growth on demand.
 class DeviceMemory {
  public:
   DeviceMemory(bitar_hip_ctx* ctx, std::uint64_t slot_size) : ctx_(ctx), slot_size_(slot_size) {}
   ~DeviceMemory() {
-    for (void* c : chunks_) (void)bitar_hip_free(ctx_, c);
+    for (auto& c : chunks_) (void)bitar_hip_free(ctx_, c.base);
   }
 
   arrow::Status Preallocate(std::uint32_t n) { return Grow(n); }
@@ -46,9 +48,10 @@ class DeviceMemory {
     }
     out->resize(n);
     for (std::uint32_t i = 0; i < n; ++i) {
-      (*out)[i] = free_.back();
+      std::uint8_t* a = free_.back();
       free_.pop_back();
-      occupied_.insert((*out)[i]);
+      (*out)[i] = a;
+      *Flag(a) = 1;
     }
     return arrow::Status::OK();
   }
@@ -56,19 +59,50 @@ class DeviceMemory {
   // 1 if addr is the start of an occupied slot (returned to the pool), else 0
   std::size_t Put(const std::uint8_t* addr) {
     const std::lock_guard<std::mutex> lock(mutex_);
-    auto it = occupied_.find(addr);
-    if (it == occupied_.end()) return 0;
-    occupied_.erase(it);
-    free_.push_back(const_cast<std::uint8_t*>(addr));
-    return 1;
+    return PutLocked(addr);
+  }
+
+  // every slot of `buffers`, last to first (one lock for the whole call)
+  std::size_t PutBuffers(const BufferVector& buffers) {
+    const std::lock_guard<std::mutex> lock(mutex_);
+    std::size_t count = 0;
+    for (auto it = std::crbegin(buffers); it != std::crend(buffers); ++it)
+      count += PutLocked(reinterpret_cast<const std::uint8_t*>((*it)->address()));
+    return count;
   }
 
   void PutAll(const std::vector<std::uint8_t*>& slots) {
-    for (auto* s : slots) Put(s);
+    const std::lock_guard<std::mutex> lock(mutex_);
+    for (auto* s : slots) PutLocked(s);
   }
 
  private:
   static constexpr std::uint32_t kGrowSlots = 256;
+  struct Chunk {
+    std::uint8_t* base;
+    std::uint64_t n;
+    std::vector<std::uint8_t> occupied;
+  };
+
+  // the occupied flag of the slot starting at addr, nullptr if addr starts no slot
+  std::uint8_t* Flag(const std::uint8_t* addr) {
+    // chunks_ is sorted by base: the last chunk starting at or below addr
+    auto it = std::upper_bound(chunks_.begin(), chunks_.end(), addr,
+                               [](const std::uint8_t* a, const Chunk& c) { return a < c.base; });
+    if (it == chunks_.begin()) return nullptr;
+    Chunk& c = *(it - 1);
+    const std::uint64_t off = static_cast<std::uint64_t>(addr - c.base);
+    if (off % slot_size_ || off / slot_size_ >= c.n) return nullptr;
+    return &c.occupied[off / slot_size_];
+  }
+
+  std::size_t PutLocked(const std::uint8_t* addr) {
+    std::uint8_t* f = Flag(addr);
+    if (!f || !*f) return 0;
+    *f = 0;
+    free_.push_back(const_cast<std::uint8_t*>(addr));
+    return 1;
+  }
 
   arrow::Status Grow(std::uint32_t n) {
     const std::lock_guard<std::mutex> lock(mutex_);
@@ -79,18 +113,32 @@ class DeviceMemory {
       ARROW_LOG(WARNING) << "Allocating output slots in the critical path (" << n << " slots)";
     void* p = nullptr;
     BITAR_ABI(bitar_hip_alloc(ctx_, slot_size_ * n, &p), "slot pool");
-    chunks_.push_back(p);
     auto* base = static_cast<std::uint8_t*>(p);
+    Chunk c{base, n, std::vector<std::uint8_t>(n, 0)};
+    chunks_.insert(std::upper_bound(chunks_.begin(), chunks_.end(), base,
+                                    [](const std::uint8_t* a, const Chunk& x) { return a < x.base; }),
+                   std::move(c));
     for (std::uint32_t i = n; i-- > 0;) free_.push_back(base + slot_size_ * i);
     return arrow::Status::OK();
   }
 
   bitar_hip_ctx* ctx_;
   const std::uint64_t slot_size_;
-  std::vector<void*> chunks_;
+  std::vector<Chunk> chunks_;  // sorted by base
   std::vector<std::uint8_t*> free_;
-  std::unordered_set<const std::uint8_t*> occupied_;
   std::mutex mutex_;
+};
+
+// A compressed output: a non-owning view of one HBM slot (memory.cc:211-228) whose size is
+// set once the kernel's sizes are back -- so the views are built while the kernel runs.
+class SlotBuffer : public arrow::Buffer {
+ public:
+  SlotBuffer(const std::uint8_t* data, std::shared_ptr<arrow::MemoryManager> mm)
+      : arrow::Buffer(data, 0, std::move(mm)) {}
+  void set_size(std::int64_t n) {
+    size_ = n;
+    capacity_ = n;
+  }
 };
 
 // Per-queue-pair stream and staging (QueuePairMemory, reference memory.cc:237-348): pinned
@@ -364,6 +412,13 @@ arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
                             m->d_chain, stride, m->d_sizes);
   }
   if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sizes, m->d_sizes, 4ull * nops, m->stream);
+  auto mm = hip_memory_manager(device_id_);
+  if (rc == 0 && k == 1) {
+    // the output views, built while the kernel runs (their sizes are set after the sync)
+    compressed_buffers.reserve(nseg);
+    for (std::uint32_t i = 0; i < nseg; ++i)
+      compressed_buffers.emplace_back(std::make_unique<internal::SlotBuffer>(slots[i], mm));
+  }
   // the checksum of the uncompressed input of each op (DPDK input_chksum of a compress op)
   const std::uint32_t ck = checksum_kind();
   if (rc == 0 && ck) {
@@ -381,13 +436,12 @@ arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
     if (m->h_sizes[j] == BITAR_HIP_SEGMENT_ERROR || m->h_sizes[j] > cap)
       return release(arrow::Status::IOError("Compress data output is larger than allocated buffer"));
   }
-  auto mm = hip_memory_manager(device_id_);
-  compressed_buffers.reserve(nseg);
   if (k == 1) {
     for (std::uint32_t i = 0; i < nseg; ++i)
-      compressed_buffers.emplace_back(std::make_unique<arrow::Buffer>(slots[i], m->h_sizes[i], mm));
+      static_cast<internal::SlotBuffer*>(compressed_buffers[i].get())->set_size(m->h_sizes[i]);
     return compressed_buffers;
   }
+  compressed_buffers.reserve(nseg);
   // spread op j's stream over its slots: slot i of the op holds bytes [i*L, (i+1)*L); the
   // op's trailing slots may stay empty and are returned as empty buffers, so that Decompress
   // regroups exactly k buffers per op (the reference returns only the non-empty ones,
@@ -451,8 +505,11 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
   // sources: HBM buffers in place; host buffers staged behind the output area
   std::uint64_t host_bytes = 0;
   std::vector<bool> on_dev(nseg);
+  const arrow::MemoryManager* own_mm = hip_memory_manager(device_id_).get();
   for (std::uint32_t i = 0; i < nseg; ++i) {
-    on_dev[i] = internal::OnDevice(*compressed_buffers[i], device_id_);
+    // (our own slot views: their memory manager says so without a query)
+    on_dev[i] = compressed_buffers[i]->memory_manager().get() == own_mm ||
+                internal::OnDevice(*compressed_buffers[i], device_id_);
     if (!on_dev[i]) host_bytes += (static_cast<std::uint64_t>(compressed_buffers[i]->size()) + 15) & ~15ull;
   }
   const auto out_addr = decompressed_buffer->mutable_address();
@@ -559,11 +616,8 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
 
 template <typename Class, typename Enable>
 std::size_t CompressDevice<Class, Enable>::Recycle(const BufferVector& buffers) {
-  std::size_t count = 0;
   if (!device_memory_) return 0;
-  for (auto it = std::crbegin(buffers); it != std::crend(buffers); ++it)
-    count += device_memory_->Put(reinterpret_cast<const std::uint8_t*>((*it)->address()));
-  return count;
+  return device_memory_->PutBuffers(buffers);
 }
 
 template <typename Class, typename Enable>

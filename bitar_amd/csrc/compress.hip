@@ -262,7 +262,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
   using namespace cmp;
-  __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
+  // (+ one trash entry: probe lanes past the segment insert there, see parse)
+  __shared__ __attribute__((aligned(16))) uint16_t table[(1u << kHashLog) + 8];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];  // + trash bytes
   const uint32_t i_seg = blockIdx.x;
@@ -276,8 +277,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   o.op = 0;
   o.flushed = 0;
   o.overflow = false;
-  parse(global_ptr(input + seg_off), n, global_ptr(input + n_total), table, inring, kMaxDist,
-        0xFFFFFFFFu, o);
+  parse<Lz4Out, false, true>(global_ptr(input + seg_off), n, global_ptr(input + n_total), table,
+                             inring, kMaxDist, 0xFFFFFFFFu, o);
   o.flush(o.op, true);
   if (lane_id() == 0) {
     sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : o.op;

@@ -286,7 +286,14 @@ __device__ __forceinline__ uint32_t chain_fast2(uint64_t& m, uint32_t lenw, uint
 // only a hash match does not start a match when one of the next kRepAhead positions holds a
 // repeat match.
 constexpr uint32_t kRepAhead = 3;
-template <class E, bool REP = false>
+// SKIP (the LZ4 parse, oracle BO_PARSE_SKIP): a window lying entirely inside the current match
+// is skipped (no lookups, no inserts); after kSkipS2 consecutive windows that started no
+// match, the next window is a PROBE of stride 2 (4 after kSkipS4): the 64 positions x + s l
+// look up their candidates; with no match among them they are inserted and the scan moves on
+// to x + 64 s, else nothing is inserted and ordinary windows scan the region from x.  On
+// incompressible stretches a window then covers 256 positions (liblz4's growing search step).
+constexpr uint32_t kSkipS2 = 2, kSkipS4 = 6;
+template <class E, bool REP = false, bool SKIP = false>
 __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, const GMEM uint8_t* in_end,
                                       uint16_t* table, uint8_t* inring, uint32_t max_dist,
                                       uint32_t max_mlen, E& em) {
@@ -327,6 +334,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
     // one window of 64 positions at x; vp = the 16 bytes at x + lane, read during the
     // previous window (the ring already holds them then)
     uint4 vp = make_uint4(0, 0, 0, 0);
+    bool started = false;  // the last window started a match or began inside one (SKIP)
     auto window = [&](uint32_t x) __attribute__((always_inline)) {
       const uint32_t p = x + lane;
       const bool act = p <= last_start;
@@ -451,6 +459,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
         m = e < kWave ? valid & (~0ull << e) : 0ull;
       }
       if (chain) pos = x + e;
+      started = chain != 0 || pos_in > x;
       if constexpr (REP) {
         // the history after this window's matches: the 3 most recently used distinct
         // distances (move-to-front) of [h2, h1, h0, the chain's distances in lane order],
@@ -508,18 +517,64 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
     I.lo = 0;
     lds_order();
     vp = I.bytes16(lane);
-    for (uint32_t x = 0; x <= last_start; x += kWave) {
-      if ((x & (kRow - 1)) == kRow / 2) {
-        const uint32_t k = x / kRow;
+    // Row k+1 is written when the scan reaches 1024 k + 512 (a probe may step past that
+    // point by < 256 positions; the ring then still runs >= 497 B ahead of the scan and holds
+    // every candidate: x - 2560 > 1024 k - 3072)
+    uint32_t next_load = kRow / 2;
+    uint32_t vx = 0;  // vp holds the 16 bytes at vx + lane
+    uint32_t misses = 0;
+    for (uint32_t x = 0; x <= last_start;) {
+      if (x >= next_load) {
+        const uint32_t k = next_load / kRow;
         lds_order();
         write_row(k + 1, nxt);
         F = kRow * (k + 2) - s0;
         I.lo = F > kIn ? F - kIn : 0u;
         em.drain();
         nxt = load_row(k + 2);
+        next_load += kRow;
+      }
+      if constexpr (SKIP) {
+        if (pos >= x + kWave) {  // inside the current match
+          misses = 0;
+          x += kWave;
+          continue;
+        }
+        const uint32_t st = misses >= kSkipS4 ? 4u : misses >= kSkipS2 ? 2u : 1u;
+        if (st > 1) {  // probe of stride st
+          lds_order();
+          const uint32_t p = x + st * lane;
+          const bool act = p <= last_start;
+          const uint32_t v = I.dword(p);
+          const uint32_t h = hash4(v);
+          const uint32_t cand = table[h];
+          const uint32_t cv = I.dword(cand);
+          const bool hit = act & (cand < p) & (p - cand <= max_dist) & (cv == v);
+          if (!ballot(hit)) {
+            // no match among them: insert (ascending, the largest position wins the slot)
+            lds_order();
+            table[act ? h : (1u << kHashLog)] = (uint16_t)p;
+            lds_order();
+            bool redo = act && table[h] < p;
+            while (ballot(redo)) {
+              lds_order();
+              if (redo) table[h] = (uint16_t)p;
+              lds_order();
+              redo = redo && table[h] < p;
+            }
+            ++misses;
+            x += st * kWave;
+            continue;
+          }
+          misses = 0;
+        }
       }
       lds_order();
+      if (vx != x) vp = I.bytes16(x + lane);  // (after skipped windows)
       window(x);
+      vx = x + kWave;
+      if constexpr (SKIP) misses = started ? 0u : misses + 1;
+      x += kWave;
     }
   }
   const uint32_t t0 = em.pending_from(anchor, emitted);

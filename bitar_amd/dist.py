@@ -136,12 +136,15 @@ class SizeGather:
         padded = torch.zeros(self.cap, dtype=torch.int32, device=dev)
         padded[:local_sizes.numel()] = local_sizes.to(torch.int32)
         gathered = torch.empty(self.world * self.cap, dtype=torch.int32, device=dev)
-        if self.world > 1 and dev.type == "cuda" and dist.get_backend(group) != "nccl":
+        # the collective runs whenever a process group is up -- at world size 1 too (a
+        # one-rank RCCL group under torch.distributed.run), so that path is exercised on one GPU
+        coll = self.world > 1 or (dist.is_available() and dist.is_initialized())
+        if coll and dev.type == "cuda" and dist.get_backend(group) != "nccl":
             # gloo gathers host tensors (the CPU tests, the one-GPU rehearsal)
             g = torch.empty(self.world * self.cap, dtype=torch.int32)
             dist.all_gather_into_tensor(g, padded.cpu(), group=group)
             gathered.copy_(g)
-        elif self.world > 1:
+        elif coll:
             dist.all_gather_into_tensor(gathered, padded, group=group)
         else:
             gathered.copy_(padded)

@@ -121,18 +121,57 @@ static int repnear(const int* isrep, uint32_t l, uint32_t cnt) {
     if (l + k < cnt && isrep[l + k]) return 1;
   return 0;
 }
+/* flags & BO_PARSE_SKIP (the LZ4 parse): windows the parse has no use for are skipped, as
+ * liblz4 skips positions (LZ4_compress_generic's search step grows with consecutive misses
+ * and positions inside a match are never searched nor inserted):
+ *   - a window lying entirely inside the current match (pos >= x + 64) is skipped: no
+ *     lookups, no inserts;
+ *   - after BO_SKIP_S2 consecutive windows that started no match (a window that began
+ *     inside a match counts as a hit), the next window is a PROBE of stride s = 2 (4 after
+ *     BO_SKIP_S4 misses): the 64 positions x + s*l (<= last_start) look up their candidates
+ *     exactly as a window does; if none of them holds a match, those positions are inserted
+ *     (ascending: the largest wins) and the scan moves on to x + 64 s; if any does, nothing
+ *     is inserted, the miss count restarts, and the region is scanned by ordinary windows
+ *     from x. */
+#define BO_SKIP_S2 2u
+#define BO_SKIP_S4 6u
 void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
                            uint32_t max_mlen, uint32_t flags, bo_emit_fn emit, void* ctx) {
   uint32_t anchor = 0;
   uint32_t hist[3] = {1, 4, 8};
   const int rep = (flags & BO_PARSE_REP) != 0;
+  const int skip = (flags & BO_PARSE_SKIP) != 0;
   if (n >= BO_MFLIMIT + 1) {
     static __thread uint32_t table[1u << BO_HASH_LOG];
     memset(table, 0, sizeof(table));
     const uint32_t last_start = n - BO_MFLIMIT;        /* match start must be <= n-12 */
     const uint32_t match_limit = n - BO_LASTLITERALS;  /* match end must be <= n-5 */
-    uint32_t pos = 0;
+    uint32_t pos = 0, misses = 0;
     for (uint32_t x = 0; x <= last_start; x += BO_WIN) {
+      if (skip) {
+        if (pos >= x + BO_WIN) { /* inside the current match */
+          misses = 0;
+          continue;
+        }
+        const uint32_t s = misses >= BO_SKIP_S4 ? 4u : misses >= BO_SKIP_S2 ? 2u : 1u;
+        if (s > 1) {
+          int hit = 0;
+          for (uint32_t l = 0; l < BO_WIN && x + s * l <= last_start; ++l) {
+            const uint32_t p = x + s * l, c = table[bo_hash(rd32(src + p))];
+            if (c < p && p - c <= max_dist && rd32(src + c) == rd32(src + p)) hit = 1;
+          }
+          if (!hit) {
+            for (uint32_t l = 0; l < BO_WIN && x + s * l <= last_start; ++l)
+              table[bo_hash(rd32(src + x + s * l))] = x + s * l;
+            ++misses;
+            x += (s - 1) * BO_WIN; /* (+ BO_WIN by the loop) */
+            continue;
+          }
+          misses = 0;
+        }
+      }
+      const uint32_t pos_in = pos;
+      int started = 0;
       uint32_t cnt = last_start - x + 1;
       if (cnt > BO_WIN) cnt = BO_WIN;
       uint32_t cand[BO_WIN], h[BO_WIN];
@@ -174,6 +213,7 @@ void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
         emit(ctx, anchor, i - anchor, i - c, len);
         pos = i + len;
         anchor = pos;
+        started = 1;
         if (rep) {
           const uint32_t d = i - c;
           if (d == hist[1]) {
@@ -190,6 +230,7 @@ void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
           }
         }
       }
+      misses = started || pos_in > x ? 0u : misses + 1;
     }
   }
   emit(ctx, anchor, n - anchor, 0, 0); /* last sequence: literals only */
@@ -240,11 +281,20 @@ static void lz4_emit(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t 
 #define BO_MAX_DIST 2560u
 _Static_assert(BO_MAX_DIST == BO_MAX_DIST_ALL, "one distance cap for all codecs");
 
+/* LZ4 parse flags: BO_PARSE_SKIP (the shipped LZ4 kernel); bo_set_lz4_parse_flags lets the
+ * tests measure the ratio the skipping costs */
+static uint32_t g_lz4_parse_flags = BO_PARSE_SKIP;
+uint32_t bo_set_lz4_parse_flags(uint32_t flags) {
+  const uint32_t old = g_lz4_parse_flags;
+  g_lz4_parse_flags = flags;
+  return old;
+}
+
 int bo_lz4_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
                           uint32_t* csize) {
   if (n > 65536u) return BO_ERR_INVALID;
   lz4_emit_ctx c = {src, dst, cap, 0, 0};
-  bo_window_parse(src, n, BO_MAX_DIST, 0xFFFFFFFFu, lz4_emit, &c);
+  bo_window_parse_flags(src, n, BO_MAX_DIST, 0xFFFFFFFFu, g_lz4_parse_flags, lz4_emit, &c);
   if (c.err) return BO_ERR_IO;
   *csize = c.op;
   return BO_OK;

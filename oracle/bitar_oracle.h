@@ -105,6 +105,8 @@ void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t
                      bo_emit_fn emit, void* ctx);
 #define BO_MAX_DIST_ALL 2560u
 #define BO_PARSE_REP 1u
+#define BO_PARSE_SKIP 2u
+uint32_t bo_set_lz4_parse_flags(uint32_t flags);
 void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t max_mlen,
                            uint32_t flags, bo_emit_fn emit, void* ctx);
 
