@@ -335,7 +335,13 @@ def stock_decode(eng, args):
             if i >= args.warmup:
                 evs.append((e0, e1))
         torch.cuda.synchronize()
-        eng.sync()
+        try:
+            eng.sync()
+        except bitar_amd.BitarError as e:
+            p = prod.cpu().numpy().view(np.uint32)
+            bad = np.nonzero(p == 0xFFFFFFFF)[0]
+            raise RuntimeError(f"stock {name} decode: {e}; {bad.size} failed segments, first "
+                               f"{bad[:8].tolist()}") from e
         ok = bool(torch.equal(out[:n], data)) and int(prod.to(torch.int64).sum().item()) == n
         t = sum(a.elapsed_time(b) for a, b in evs) / len(evs) / 1e3
         alg = (n + C) / t / 1e9
