@@ -374,13 +374,14 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
       const uint32_t dsc = ds < 30 ? ds : 0u;
       const uint32_t de = dist_extra(dsc);
       const uint32_t dist = dist_base(dsc) + ((uint32_t)(bits >> (o2 + dl)) & ((1u << de) - 1));
-      const bool m_ok = is_len && e2 != 0 && ds < 30 && mlen <= 64 && dist <= kNearOff &&
-                        dist <= s.op;
+      // any distance (far history -- beyond the ring's reach, stock zlib streams go to
+      // 32 KiB -- is read back from HBM below)
+      const bool m_ok = is_len && e2 != 0 && ds < 30 && mlen <= 64 && dist <= s.op;
       const uint32_t nb = is_lit ? l1 : o2 + dl + de;
       const uint32_t olen = is_lit ? 1u : m_ok ? mlen : 127u;
-      const uint32_t payload = is_lit ? sym : (0x8000u | dist);
+      const uint32_t payload = is_lit ? sym : (0x8000u | (dist - 1u));
       // record: next candidate (9 bits) | olen (7 bits, 127 = stop) | payload (16 bits:
-      // literal byte, or 0x8000 | distance)
+      // literal byte, or 0x8000 | distance - 1)
       rec[j] = ((c + nb) & 511u) | (olen << 9) | (payload << 16);
     }
     // (2) scalar walk over the real symbols
@@ -474,21 +475,37 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
     const uint32_t payload = key & 0xFFFFu;
     // (3) sources: the literal / ring history / an earlier lane of this batch
     const bool lit = (payload & 0x8000u) == 0;
-    const uint32_t dist = payload & 0x1FFFu;
+    const uint32_t dist = (payload & 0x7FFFu) + 1u;
     const uint32_t r = lane - ostart;
     const float qf = floorf(((float)(r & 63u) + 0.5f) * __builtin_amdgcn_rcpf((float)(dist > 1u ? dist : 1u)));
     const uint32_t mm = dist <= r ? (r & 63u) - (uint32_t)qf * dist : r;
     const int32_t srel = (int32_t)(ostart + mm) - (int32_t)dist;  // vs op
     const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
-    // bit31: alias (low bits: source lane); bit30: literal (low byte); else an LDS address
+    // bit31: alias (low bits: source lane); bit30: literal (low byte); bit29: far history
+    // (low 16 bits: the output position, in HBM); else an LDS address
+    const bool far = !lit && srel < -(int32_t)kNearOff;
     uint32_t st = lit ? (0x40000000u | (payload & 255u))
-                      : srel >= 0 ? ((uint32_t)srel | 0x80000000u) : hist;
+                      : srel >= 0 ? ((uint32_t)srel | 0x80000000u)
+                      : far ? (0x20000000u | (s.op + (uint32_t)srel)) : hist;
     while (ballot((st & 0x80000000u) != 0u && lane < out)) {
       const uint32_t other = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((st & 63u) << 2), (int)st);
       st = (st & 0x80000000u) ? other : st;
     }
     lds_order();
-    const uint32_t v = (st & 0x40000000u) ? (st & 255u) : (uint32_t)win[st & 0x3FFFu];
+    uint32_t v = (st & 0x40000000u) ? (st & 255u) : (uint32_t)win[st & 0x3FFFu];
+    {
+      // far history: already flushed (flushes keep out[.., op - 2112) in HBM and far sources
+      // lie >= 3952 B back); fence once this wave's stores may not be visible to its loads
+      const bool gfar = (st & 0x20000000u) != 0u && lane < out;
+      const uint64_t farm = ballot(gfar);
+      if (farm) {
+        if (ballot((st & 0xFFFFu) >= s.fenced) & farm) {
+          global_fence_wave();
+          s.fenced = s.flushed;
+        }
+        if (gfar) v = s.dst[st & 0xFFFFu];
+      }
+    }
     if (lane < out) ring[(base + s.op + lane) & kRingMask] = (uint8_t)v;
     lds_order();
     s.op += out;
