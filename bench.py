@@ -69,22 +69,27 @@ def parse():
     return p.parse_args()
 
 
+# every kernel one compress / decompress call launches (a "+" list: the HIP events bracket
+# them together and the PMC traffic is their sum; a templated kernel counts all its
+# instantiations -- lz4_decompress_kernel<false> then <true> for the deferred segments)
 KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
-           # decompress = inflate_lanes_kernel (lane per segment) + inflate_kernel in
-           # defer-only mode; timed together
-           "deflate": ("deflate_compress_kernel", "inflate_lanes_kernel"),
+           # decompress = inflate_lanes_kernel (lane per segment: stored / fixed blocks) +
+           # inflate_kernel over the segments it deferred
+           "deflate": ("deflate_compress_kernel", "inflate_lanes_kernel+inflate_kernel"),
            # compress = zstd_parse_kernel + zstd_entropy_kernel + zstd_walk_kernel (FSE state
            # chains, a lane per chain) + zstd_emit_kernel (sequence bitstream); decompress =
            # zstd_lanes_kernel (predefined-table frames) + zstd_decompress_kernel (headers,
            # tables) + zstd_hlit_kernel (Huffman literals) + zstd_seqdec_kernel (FSE chains ->
            # records, lane per segment) + zstd_exec_kernel (records -> output, wave per
-           # segment); each timed together
+           # segment) + zstd_handoff_kernel (what seqdec did not take)
            "zstd": ("zstd_parse_kernel+zstd_entropy_kernel+zstd_walk_kernel+zstd_emit_kernel",
-                    "zstd_decompress_kernel+zstd_hlit_kernel+zstd_seqdec_kernel+zstd_exec_kernel"),
+                    "zstd_lanes_kernel+zstd_decompress_kernel+zstd_hlit_kernel+"
+                    "zstd_seqdec_kernel+zstd_exec_kernel+zstd_handoff_kernel"),
            # compress = deflate_dyn_parse_kernel + deflate_dyn_emit_kernel (one event pair
-           # brackets both); decompress = inflate_lanes_kernel deferring every dynamic block
-           # to inflate_kernel
-           "deflate_dyn": ("deflate_dyn_parse_kernel+deflate_dyn_emit_kernel", "inflate_kernel")}
+           # brackets both); decompress = inflate_lanes_kernel (stored blocks: the random
+           # third) + inflate_kernel (every dynamic block)
+           "deflate_dyn": ("deflate_dyn_parse_kernel+deflate_dyn_emit_kernel",
+                           "inflate_lanes_kernel+inflate_kernel")}
 CODEC_NAMES = {"lz4": "lz4-block", "deflate": "deflate-raw-fixed", "zstd": "zstd-frame",
                "deflate_dyn": "deflate-raw-dynamic"}
 

@@ -200,10 +200,17 @@ struct EntLds {
   uint8_t desc[192];       // Huffman tree description; then modes + table descriptions
   uint8_t tmp[256];        // serial bit writer output (weights FSE form, table descriptions)
   int16_t norm[64];
-  uint16_t tabs[kTabDummy + 1];
-  uint32_t tr[3][64];      // per symbol: deltaNbBits | deltaFindState << 20 (12-bit signed)
-  uint8_t sym_at[512];
-  uint16_t nxt[64];
+  union {
+    // per-quarter literal counts ([0] quarters 0 | 1 << 16, [1] 2 | 3 << 16), dead once
+    // the stream sizes are known -- before the first FSE table is built
+    uint32_t hq[2][256];
+    struct {
+      uint16_t tabs[kTabDummy + 1];
+      uint32_t tr[3][64];  // per symbol: deltaNbBits | deltaFindState << 20 (12-bit signed)
+      uint8_t sym_at[512];
+      uint16_t nxt[64];
+    };
+  };
   uint32_t u[16];          // lane-0 results: sizes, modes, accuracy logs
   uint32_t wk[32];         // lane-0 work: weight counts, code ranges
   union {                  // by phase
@@ -593,8 +600,9 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
   const uint32_t blk = o.op;
   o.op += 3;  // block header, written last
 
-  // ---- literal histogram ----
-  for (uint32_t k = lane; k < 256; k += kWave) L.hist[k] = 0;
+  // ---- literal histogram, per stream quarter (one read of the literals: the quarters' code
+  // lengths -- the stream sizes -- follow from these counts once the code is built) ----
+  for (uint32_t k = lane; k < 2 * 256; k += kWave) (&L.hq[0][0])[k] = 0;
   lds_order();
   const uint32_t qs = (nlit + 3) / 4;
   for (uint32_t b0 = 0; b0 < nlit; b0 += 16u * kWave) {
@@ -603,8 +611,18 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     if (at < nlit) v = *reinterpret_cast<const GMEM uint4*>(lits + at);
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (uint32_t j = 0; j < 16; ++j)
-      if (at + j < nlit) atomicAdd(&L.hist[(wv[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint32_t idx = at + j;
+      // (a quarter holds <= 16384 literals: its count fits 16 bits)
+      const uint32_t q = idx < qs ? 0u : idx < 2 * qs ? 1u : idx < 3 * qs ? 2u : 3u;
+      if (idx < nlit)
+        atomicAdd(&L.hq[q >> 1][(wv[j >> 2] >> (8 * (j & 3))) & 0xFFu], (q & 1u) ? 0x10000u : 1u);
+    }
+  }
+  lds_order();
+  for (uint32_t k = lane; k < 256; k += kWave) {
+    const uint32_t a = L.hq[0][k], b = L.hq[1][k];
+    L.hist[k] = (a & 0xFFFFu) + (a >> 16) + (b & 0xFFFFu) + (b >> 16);
   }
   lds_order();
   uint32_t distinct = 0;
@@ -633,24 +651,16 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       const uint32_t l = L.len[s0 + lane];
       L.w[s0 + lane] = (uint8_t)(l ? lmax + 1 - l : 0u);
     }
-    // stream sizes: the code lengths of each quarter's literals (a second read of them)
+    // stream sizes: each quarter's bits = sum over symbols of code length x its count there
     ns = nlit < 256 ? 1u : 4u;
     uint32_t bq[4] = {0, 0, 0, 0};
     lds_order();
-    for (uint32_t b0 = 0; b0 < nlit; b0 += 16u * kWave) {
-      const uint32_t at = b0 + 16u * lane;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (at < nlit) v = *reinterpret_cast<const GMEM uint4*>(lits + at);
-      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (uint32_t j = 0; j < 16; ++j) {
-        const uint32_t idx = at + j;
-        const uint32_t l = idx < nlit ? (uint32_t)L.len[(wv[j >> 2] >> (8 * (j & 3))) & 0xFFu] : 0u;
-        bq[0] += idx < qs ? l : 0u;
-        bq[1] += idx >= qs && idx < 2 * qs ? l : 0u;
-        bq[2] += idx >= 2 * qs && idx < 3 * qs ? l : 0u;
-        bq[3] += idx >= 3 * qs ? l : 0u;
-      }
+    for (uint32_t s0 = 0; s0 < 256; s0 += kWave) {
+      const uint32_t l = L.len[s0 + lane], a = L.hq[0][s0 + lane], b = L.hq[1][s0 + lane];
+      bq[0] += l * (a & 0xFFFFu);
+      bq[1] += l * (a >> 16);
+      bq[2] += l * (b & 0xFFFFu);
+      bq[3] += l * (b >> 16);
     }
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) bq[q] = readlane(wave_incl_sum(bq[q]), 63);

@@ -41,9 +41,21 @@ def per_kernel(path, grid=None):
                 name = name[5:]
             if not name.startswith("bitar_hip::"):
                 continue
-            key = name.split("::")[-1].split("<")[0]
+            # one key per instantiation: lz4_decompress_kernel<false> and <true> are two
+            # launches of one decompress call (the second mostly exits at once), so their
+            # averages are SUMMED per call below, never averaged together
+            key = name.split("::", 1)[-1]
             agg.setdefault(key, []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def per_call(d):
+    """{kernel base name: sum over its instantiations of their per-launch averages}"""
+    out = {}
+    for k, v in d.items():
+        base = k.split("<")[0]
+        out[base] = out.get(base, 0.0) + v
+    return out
 
 
 LEGS = ("headline", "zstd", "deflate", "deflate_dyn", "recordbatch")
@@ -70,8 +82,8 @@ def main():
             continue
         shutil.copy(prof, os.path.join(rdir, f"kernel_stats_{leg}.csv"))
         g = LEG_GRID.get(leg)
-        fetch = per_kernel(os.path.join(out, f"pmc_{tag}_{leg}_FETCH_SIZE", "pmc_counter_collection.csv"), g)
-        write = per_kernel(os.path.join(out, f"pmc_{tag}_{leg}_WRITE_SIZE", "pmc_counter_collection.csv"), g)
+        fetch = per_call(per_kernel(os.path.join(out, f"pmc_{tag}_{leg}_FETCH_SIZE", "pmc_counter_collection.csv"), g))
+        write = per_call(per_kernel(os.path.join(out, f"pmc_{tag}_{leg}_WRITE_SIZE", "pmc_counter_collection.csv"), g))
         for k in sorted(set(fetch) | set(write)):
             if not k.startswith(LEG_KERNELS[leg]):
                 continue
