@@ -314,8 +314,32 @@ __global__ __launch_bounds__(64) void deflate_compress_kernel(
   const uint32_t eob = fixed_code(256, eb);
   o.put_one(eob, eb);
   o.flush_words((uint32_t)((o.bits + 31) >> 5));
+  // stored blocks instead when they are smaller (incompressible input: the fixed code spends
+  // 9 bits on bytes >= 144) -- zlib's rule for Z_FIXED too, and the dynamic encoder's; blocks
+  // of <= 65535 bytes, the last one final (oracle bo_deflate_fixed_block)
+  uint32_t size = (uint32_t)((o.bits + 7) >> 3);
+  const uint32_t nblk = (n + 65534u) / 65535u;
+  const uint32_t stored = nblk * 5u + n;
+  if (!o.overflow && stored < size) {
+    GMEM uint8_t* d = reinterpret_cast<GMEM uint8_t*>(o.dst);
+    const GMEM uint8_t* in = global_ptr(input + seg_off);
+    global_fence_wave();  // the fixed-Huffman stores to this range land first
+    uint32_t p = 0, q = 0;
+    for (uint32_t b = 0; b < nblk; ++b) {
+      const uint32_t len = n - p < 65535u ? n - p : 65535u;
+      const uint32_t lane = lane_id();
+      const uint32_t hv = lane == 0 ? (b + 1 == nblk ? 1u : 0u)
+                          : lane == 1 ? len & 0xFFu : lane == 2 ? len >> 8
+                          : lane == 3 ? ~len & 0xFFu : (~len >> 8) & 0xFFu;
+      if (lane < 5) d[q + lane] = (uint8_t)hv;
+      wave_copy_global(d + q + 5, in + p, len);
+      p += len;
+      q += 5 + len;
+    }
+    size = stored;
+  }
   if (lane_id() == 0) {
-    sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : (uint32_t)((o.bits + 7) >> 3);
+    sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : size;
     if (o.overflow) atomicOr(err, 2u);
   }
 }

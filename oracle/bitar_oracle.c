@@ -556,6 +556,10 @@ static void dfl_emit(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t 
   put_bits(c, off - kDistBase[ds], kDistExtra[ds]);
 }
 
+/* One fixed-Huffman block -- or, when they are smaller in bytes, stored blocks of <= 65535
+ * bytes (zlib's choice under Z_FIXED too, and the dynamic encoder's rule below): stored =
+ * 5 * ceil(n / 65535) + n bytes against the fixed block's (bits + 7) / 8, the smaller wins,
+ * the fixed block on a tie. */
 int bo_deflate_fixed_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
                            uint32_t* csize) {
   dfl_ctx c = {src, dst, cap, 0, 0};
@@ -563,7 +567,27 @@ int bo_deflate_fixed_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_
   bo_window_parse(src, n, BO_MAX_DIST, 258u, dfl_emit, &c);
   dfl_put_lit(&c, 256);
   if (c.err) return BO_ERR_IO;
-  *csize = (uint32_t)((c.bitpos + 7) >> 3);
+  const uint64_t fixed = (c.bitpos + 7) >> 3;
+  const uint64_t nblk = n ? (n + 65534u) / 65535u : 1;
+  const uint64_t stored = nblk * 5 + n;
+  if (stored < fixed) {
+    uint64_t o = 0;
+    uint32_t p = 0;
+    for (uint64_t b = 0; b < nblk; ++b) {
+      const uint32_t len = n - p < 65535u ? n - p : 65535u;
+      dst[o] = (uint8_t)(b + 1 == nblk);
+      dst[o + 1] = (uint8_t)len;
+      dst[o + 2] = (uint8_t)(len >> 8);
+      dst[o + 3] = (uint8_t)~len;
+      dst[o + 4] = (uint8_t)(~len >> 8);
+      memcpy(dst + o + 5, src + p, len);
+      o += 5 + len;
+      p += len;
+    }
+    *csize = (uint32_t)stored;
+    return BO_OK;
+  }
+  *csize = (uint32_t)fixed;
   return BO_OK;
 }
 
