@@ -20,14 +20,14 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# the x2 correction is for 16-B-per-lane streaming reads; the lane-per-segment decoders
-# (zstd_lanes_kernel, inflate_lanes_kernel, zstd_hlit_kernel, zstd_handoff_kernel,
-# zstd_seqdec_kernel, zstd_walk_kernel) and the record executor / bitstream emitter (8-B records,
-# 1-B literals, 2-4-B state words) read 1-8 B per lane,
-# so their FETCH_SIZE is taken as reported
-FETCH_FACTOR = {"zstd_lanes_kernel": 1.0, "inflate_lanes_kernel": 1.0, "zstd_hlit_kernel": 1.0,
-                "zstd_handoff_kernel": 1.0, "zstd_seqdec_kernel": 1.0, "zstd_exec_kernel": 1.0,
-                "zstd_walk_kernel": 1.0, "zstd_emit_kernel": 1.0}
+# FETCH_SIZE x2 for every kernel: calibrated on known byte counts in each access pattern
+# these kernels use (scripts/calib/pmc_calib.hip -> profiles/r03/calibration.json): 16-B and
+# 1-B coalesced reads and 8-B lane-owned read streams at 16 K concurrent streams all report
+# exactly half their bytes (the counter tallies 128-B requests as 64 B).  Lane streams at
+# 131 K / 2 M concurrent streams report 2.5x / 6.4x their bytes: real L2 over-fetch, kept.
+# WRITE_SIZE is exact for 16-B and 1-B coalesced stores; 8-B lane-owned store streams
+# report 1.7-9.5x their bytes (partial-line write-backs): real write amplification, kept.
+FETCH_FACTOR = {}
 
 
 def per_kernel(path, grid=None):
