@@ -49,7 +49,8 @@ def parse():
     p.add_argument("--bytes", type=int, default=1 << 30, help="headline bytes per rank")
     p.add_argument("--seg", type=int, default=65536)
     p.add_argument("--kind", type=int, default=1, help="0 random, 1 mixed, 2 arrow")
-    p.add_argument("--codec", default="lz4", choices=["lz4", "deflate", "zstd", "deflate_dyn"])
+    p.add_argument("--codec", default="lz4",
+                   choices=["lz4", "deflate", "zstd", "deflate_dyn", "lz4_wide"])
     p.add_argument("--streams", type=int, default=4,
                    help="queue-pair streams per GPU in the configs[3] record-batch leg")
     p.add_argument("--record-bytes", type=int, default=8 << 30,
@@ -61,6 +62,8 @@ def parse():
     p.add_argument("--no-zstd", action="store_true")
     p.add_argument("--no-deflate", action="store_true")
     p.add_argument("--no-recordbatch", action="store_true")
+    p.add_argument("--no-lz4-wide", action="store_true",
+                   help="skip the wide-parse LZ4 leg (the ratio operating point)")
     p.add_argument("--no-stock", action="store_true",
                    help="skip the stock-stream GPU decode legs")
     p.add_argument("--only", default=None,
@@ -73,6 +76,9 @@ def parse():
 # them together and the PMC traffic is their sum; a templated kernel counts all its
 # instantiations -- lz4_decompress_kernel<false> then <true> for the deferred segments)
 KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
+           # the wide parse (16 KiB history): same kernels, other template instance; offsets
+           # past the decoder's LDS ring take lz4_decompress_kernel<true> (far history)
+           "lz4_wide": ("lz4_compress_kernel", "lz4_decompress_kernel"),
            # decompress = inflate_lanes_kernel (lane per segment: stored / fixed blocks) +
            # inflate_kernel over the segments it deferred
            "deflate": ("deflate_compress_kernel", "inflate_lanes_kernel+inflate_kernel"),
@@ -91,13 +97,14 @@ KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
            "deflate_dyn": ("deflate_dyn_parse_kernel+deflate_dyn_emit_kernel",
                            "inflate_lanes_kernel+inflate_kernel")}
 CODEC_NAMES = {"lz4": "lz4-block", "deflate": "deflate-raw-fixed", "zstd": "zstd-frame",
-               "deflate_dyn": "deflate-raw-dynamic"}
+               "deflate_dyn": "deflate-raw-dynamic", "lz4_wide": "lz4-block (wide parse)"}
 
 
 def codec_id(name):
     import bitar_amd
     return {"lz4": bitar_amd.CODEC_LZ4, "deflate": bitar_amd.CODEC_DEFLATE,
-            "zstd": bitar_amd.CODEC_ZSTD, "deflate_dyn": bitar_amd.CODEC_DEFLATE_DYNAMIC}[name]
+            "zstd": bitar_amd.CODEC_ZSTD, "deflate_dyn": bitar_amd.CODEC_DEFLATE_DYNAMIC,
+            "lz4_wide": bitar_amd.CODEC_LZ4_WIDE}[name]
 
 
 def reduce_max_sum(vals_max, vals_sum, world):
@@ -611,6 +618,11 @@ def main():
         # the reference's default frame: dynamic Huffman (config.h:151)
         dd = run_job(eng, "deflate_dyn", args.kind, world * n, 59460, 1, args.steps,
                      args.warmup, world, rank, seed=2000)
+    lw = None
+    if args.codec == "lz4" and not args.no_lz4_wide and want(args, "lz4_wide"):
+        # the ratio operating point: the same job through the wide LZ4 parse
+        lw = run_job(eng, "lz4_wide", args.kind, world * n, seg, 1, args.steps, args.warmup,
+                     world, rank, seed=0)
     sec = stock = None
     if world == 1 and args.codec == "lz4":
         if not args.no_secondary and want(args, "secondary"):
@@ -694,6 +706,14 @@ def main():
             "the reference's DEFAULT frame: raw DEFLATE with dynamic Huffman codes "
             "(HuffmanEncoding::DYNAMIC, config.h:151) per 59460-B segment, compress + "
             "decompress, same input and sharding as the headline")
+    if lw is not None:
+        res["lz4_wide"] = leg_summary(
+            "lz4_wide", lw, world, args.steps, args.traffic_json,
+            "the ratio operating point: the headline job through the wide LZ4 parse "
+            "(BITAR_HIP_CODEC_LZ4_WIDE: 16 KiB history window, 4096-entry table; ordinary "
+            "LZ4 blocks), compress + decompress")
+        if stock is not None:
+            res["lz4_wide"]["liblz4_default_ratio"] = stock[1]["lz4"]
     if stock is not None:
         res["stock_decode"] = stock[0]
     if world == 1 and args.codec == "lz4" and (args.only is None or want(args, "frontend")):

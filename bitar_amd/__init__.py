@@ -16,6 +16,7 @@ CODEC_LZ4 = 1
 CODEC_DEFLATE = 2
 CODEC_ZSTD = 3
 CODEC_DEFLATE_DYNAMIC = 4  # HuffmanEncoding::DYNAMIC (decoded as CODEC_DEFLATE)
+CODEC_LZ4_WIDE = 5  # LZ4 blocks from the wide parse (16 KiB history): the ratio operating point
 SEGMENT_ERROR = 0xFFFFFFFF
 CHECKSUM_CRC32, CHECKSUM_ADLER32, CHECKSUM_CRC32_ADLER32 = 1, 2, 3
 MAX_SEG_SIZE = 65536

@@ -257,14 +257,18 @@ struct DflOut {
 
 }  // namespace cmp
 
+// RING / HLOG: the parse's input ring and hash table -- 4 KiB / 1024 entries (distance cap
+// 2560: BITAR_HIP_CODEC_LZ4, 21 waves per CU), or 16 KiB / 4096 entries (cap 14848:
+// BITAR_HIP_CODEC_LZ4_WIDE, the ratio operating point; 27.3 KiB of LDS, 5 waves per CU)
+template <uint32_t RING, uint32_t HLOG>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
   using namespace cmp;
   // (+ one trash entry: probe lanes past the segment insert there, see parse)
-  __shared__ __attribute__((aligned(16))) uint16_t table[(1u << kHashLog) + 8];
-  __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
+  __shared__ __attribute__((aligned(16))) uint16_t table[(1u << HLOG) + 8];
+  __shared__ __attribute__((aligned(16))) uint8_t inring[RING + kInPad];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];  // + trash bytes
   const uint32_t i_seg = blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
@@ -277,14 +281,20 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   o.op = 0;
   o.flushed = 0;
   o.overflow = false;
-  parse<Lz4Out, false, true>(global_ptr(input + seg_off), n, global_ptr(input + n_total), table,
-                             inring, kMaxDist, 0xFFFFFFFFu, o);
+  parse<Lz4Out, false, true, RING, HLOG>(global_ptr(input + seg_off), n,
+                                         global_ptr(input + n_total), table, inring,
+                                         RING - 1536u, 0xFFFFFFFFu, o);
   o.flush(o.op, true);
   if (lane_id() == 0) {
     sizes[i_seg] = o.overflow ? 0xFFFFFFFFu : o.op;
     if (o.overflow) atomicOr(err, 2u);
   }
 }
+
+template __global__ void lz4_compress_kernel<cmp::kIn, cmp::kHashLog>(
+    const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint8_t* const*, uint32_t*, uint32_t*);
+template __global__ void lz4_compress_kernel<16384, 12>(
+    const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint8_t* const*, uint32_t*, uint32_t*);
 
 __global__ __launch_bounds__(64) void deflate_compress_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,

@@ -17,6 +17,7 @@
 #include "zstd_hand.hip.h"
 
 namespace bitar_hip {
+template <uint32_t RING, uint32_t HLOG>
 __global__ void lz4_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
                                     uint8_t* const*, uint32_t*, uint32_t*);
 template <bool FARK>
@@ -282,7 +283,7 @@ int bitar_hip_device(bitar_hip_ctx* ctx, int* device) {
 
 uint64_t bitar_hip_slot_size(uint32_t codec, uint32_t seg) {
   uint64_t bound;
-  if (codec == BITAR_HIP_CODEC_LZ4)
+  if (codec == BITAR_HIP_CODEC_LZ4 || codec == BITAR_HIP_CODEC_LZ4_WIDE)
     bound = (uint64_t)seg + seg / 255u + 16u;           // LZ4_compressBound
   else if (codec == BITAR_HIP_CODEC_DEFLATE || codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC)
     bound = ((uint64_t)seg * 9 + 7) / 8 + 16u;          // fixed Huffman, 9 bits/literal
@@ -333,7 +334,8 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
                          void* const* d_dsts, uint32_t* d_sizes) {
   if (int r = enter(ctx)) return r;
   if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE &&
-      codec != BITAR_HIP_CODEC_ZSTD && codec != BITAR_HIP_CODEC_DEFLATE_DYNAMIC)
+      codec != BITAR_HIP_CODEC_ZSTD && codec != BITAR_HIP_CODEC_DEFLATE_DYNAMIC &&
+      codec != BITAR_HIP_CODEC_LZ4_WIDE)
     return fail(BITAR_HIP_NOT_IMPLEMENTED, "unknown codec");
   if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
   if (n == 0) return 0;  // empty input -> no segments (reference device.cc:161-164)
@@ -349,8 +351,12 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
   auto* slab = static_cast<uint8_t*>(d_slab);
   auto* dsts = reinterpret_cast<uint8_t* const*>(d_dsts);
   if (codec == BITAR_HIP_CODEC_LZ4)
-    hipLaunchKernelGGL(bitar_hip::lz4_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s, in,
-                       n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
+    hipLaunchKernelGGL((bitar_hip::lz4_compress_kernel<4096, 10>), dim3((uint32_t)nseg), dim3(64),
+                       0, s, in, n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
+  else if (codec == BITAR_HIP_CODEC_LZ4_WIDE)
+    hipLaunchKernelGGL((bitar_hip::lz4_compress_kernel<16384, 12>), dim3((uint32_t)nseg),
+                       dim3(64), 0, s, in, n, seg, slab, slot_stride, dsts, d_sizes,
+                       err_word(ctx, s));
   else if (codec == BITAR_HIP_CODEC_DEFLATE)
     hipLaunchKernelGGL(bitar_hip::deflate_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
                        in, n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
@@ -541,6 +547,7 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            uint64_t capacity, uint32_t* d_produced) {
   if (int r = enter(ctx)) return r;
   if (codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC) codec = BITAR_HIP_CODEC_DEFLATE;  // same decoder
+  if (codec == BITAR_HIP_CODEC_LZ4_WIDE) codec = BITAR_HIP_CODEC_LZ4;              // same format
   if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE &&
       codec != BITAR_HIP_CODEC_ZSTD)
     return fail(BITAR_HIP_NOT_IMPLEMENTED, "unknown codec");

@@ -57,7 +57,8 @@ constexpr uint32_t kInPad = 64;  // mirror of ring[0, 64) after its end: probes 
 constexpr uint32_t kRow = 1024;                   // prefetch row: one 16-B block per lane
 constexpr uint32_t kPreExt = 32;                  // parallel per-lane match extension limit
 
-__device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
+template <uint32_t HLOG = kHashLog>
+__device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - HLOG); }
 
 // 16 bytes at p (any alignment); aligned blocks at or past `end` are not loaded (zeros)
 __device__ __forceinline__ uint4 ld16u(const GMEM uint8_t* p, const GMEM uint8_t* end) {
@@ -120,19 +121,20 @@ struct InRing {
   uint8_t* ring;
   uint32_t in_lo;  // low 32 bits of the segment's input address
   uint32_t lo;     // positions >= lo are in the ring (< the filled end)
+  uint32_t mask;   // ring size - 1 (kIn - 1, or the wide LZ4 parse's 16 KiB ring)
 
   __device__ __forceinline__ uint32_t byte(uint32_t q) const {
-    return ring[(in_lo + q) & kInMask];
+    return ring[(in_lo + q) & mask];
   }
   // 4 / 16 bytes at position q (little-endian); the pad lets the dword reads run past the
   // ring's end without wrapping
   __device__ __forceinline__ uint32_t dword(uint32_t q) const {
-    const uint32_t a = (in_lo + q) & kInMask;
+    const uint32_t a = (in_lo + q) & mask;
     const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring) + (a >> 2);
     return funnel(r32[0], r32[1], a & 3u);
   }
   __device__ __forceinline__ uint4 bytes16(uint32_t q) const {
-    const uint32_t a = (in_lo + q) & kInMask;
+    const uint32_t a = (in_lo + q) & mask;
     const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring) + (a >> 2);
     const uint32_t sh = a & 3u;
     const uint32_t w0 = r32[0], w1 = r32[1], w2 = r32[2], w3 = r32[3], w4 = r32[4];
@@ -293,10 +295,14 @@ constexpr uint32_t kRepAhead = 3;
 // to x + 64 s, else nothing is inserted and ordinary windows scan the region from x.  On
 // incompressible stretches a window then covers 256 positions (liblz4's growing search step).
 constexpr uint32_t kSkipS2 = 2, kSkipS4 = 6;
-template <class E, bool REP = false, bool SKIP = false>
+// RING / HLOG: the input ring's size and the hash table's log2 size (the defaults: 4 KiB and
+// 1024 entries; the wide LZ4 parse: 16 KiB and 4096, max_dist = RING - 1536 either way).
+template <class E, bool REP = false, bool SKIP = false, uint32_t RING = kIn,
+          uint32_t HLOG = kHashLog>
 __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, const GMEM uint8_t* in_end,
                                       uint16_t* table, uint8_t* inring, uint32_t max_dist,
                                       uint32_t max_mlen, E& em) {
+  static_assert(RING >= kIn && (RING & (RING - 1)) == 0, "ring: a power of two >= 4 KiB");
   const uint32_t lane = lane_id();
   uint32_t anchor = 0, emitted = 0;
   uint32_t h0 = 1, h1 = 4, h2 = 8;  // REP: the distance history (uniform)
@@ -304,9 +310,10 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
   I.ring = inring;
   I.in_lo = (uint32_t)(uintptr_t)in;
   I.lo = 0xFFFFFFFFu;  // nothing staged: literal bytes come from HBM
+  I.mask = RING - 1;
   if (n >= kMfLimit + 1) {
     // empty slot = candidate position 0 (the oracle's zeroed table)
-    for (uint32_t k = lane; k < (1u << kHashLog) / 8; k += kWave)
+    for (uint32_t k = lane; k < (1u << HLOG) / 8; k += kWave)
       reinterpret_cast<uint4*>(table)[k] = make_uint4(0, 0, 0, 0);
     const uint32_t last_start = n - kMfLimit;
     const uint32_t match_limit = n - kLastLiterals;
@@ -325,12 +332,12 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       return v;
     };
     auto write_row = [&](uint32_t r, const uint4& v) __attribute__((always_inline)) {
-      const uint32_t blk = (rbase + (kRow / 16) * r + lane) & (kInMask >> 4);
+      const uint32_t blk = (rbase + (kRow / 16) * r + lane) & ((RING - 1) >> 4);
       ring16[blk] = v;
-      if (blk < kInPad / 16) ring16[kIn / 16 + blk] = v;  // the pad mirrors the ring's head
+      if (blk < kInPad / 16) ring16[RING / 16 + blk] = v;  // the pad mirrors the ring's head
     };
     uint32_t pos = 0;
-    uint32_t F = 0;  // the ring holds positions [F - kIn, F)
+    uint32_t F = 0;  // the ring holds positions [F - RING, F)
     // one window of 64 positions at x; vp = the 16 bytes at x + lane, read during the
     // previous window (the ring already holds them then)
     uint4 vp = make_uint4(0, 0, 0, 0);
@@ -339,7 +346,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       const uint32_t p = x + lane;
       const bool act = p <= last_start;
       const uint4 v = vp;
-      const uint32_t h = hash4(v.x);
+      const uint32_t h = hash4<HLOG>(v.x);
       // Table and ring accesses are issued on all lanes (no exec-mask branches: the scalar
       // unit is the bottleneck).  Lanes past last_start exist only in the final window;
       // their table writes are never looked up again.
@@ -529,7 +536,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
         lds_order();
         write_row(k + 1, nxt);
         F = kRow * (k + 2) - s0;
-        I.lo = F > kIn ? F - kIn : 0u;
+        I.lo = F > RING ? F - RING : 0u;
         em.drain();
         nxt = load_row(k + 2);
         next_load += kRow;
@@ -546,14 +553,14 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
           const uint32_t p = x + st * lane;
           const bool act = p <= last_start;
           const uint32_t v = I.dword(p);
-          const uint32_t h = hash4(v);
+          const uint32_t h = hash4<HLOG>(v);
           const uint32_t cand = table[h];
           const uint32_t cv = I.dword(cand);
           const bool hit = act & (cand < p) & (p - cand <= max_dist) & (cv == v);
           if (!ballot(hit)) {
             // no match among them: insert (ascending, the largest position wins the slot)
             lds_order();
-            table[act ? h : (1u << kHashLog)] = (uint16_t)p;
+            table[act ? h : (1u << HLOG)] = (uint16_t)p;
             lds_order();
             bool redo = act && table[h] < p;
             while (ballot(redo)) {

@@ -42,10 +42,16 @@ enum bitar_hip_codec {
   BITAR_HIP_CODEC_LZ4 = 1,
   BITAR_HIP_CODEC_DEFLATE = 2,         /* fixed-Huffman blocks (HuffmanEncoding::FIXED) */
   BITAR_HIP_CODEC_ZSTD = 3,
-  BITAR_HIP_CODEC_DEFLATE_DYNAMIC = 4  /* dynamic Huffman (HuffmanEncoding::DYNAMIC, the
+  BITAR_HIP_CODEC_DEFLATE_DYNAMIC = 4, /* dynamic Huffman (HuffmanEncoding::DYNAMIC, the
                                           reference default, config.h:151); decoded like
                                           DEFLATE.  Compress runs two kernels through a
                                           stream-ordered scratch allocation. */
+  BITAR_HIP_CODEC_LZ4_WIDE = 5         /* LZ4 blocks from the wide parse: 16 KiB history (match
+                                          distance <= 14848), 4096-entry table -- the ratio
+                                          operating point, within a few % of liblz4's ratio
+                                          at a lower speed; the streams are ordinary LZ4 blocks
+                                          (decoded like LZ4).  The front-end selects it with a
+                                          window_size above 12 (config.h:111-114). */
 };
 
 /* Per-segment marker written into sizes[] / produced[] when that segment's op failed

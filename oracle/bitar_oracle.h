@@ -49,7 +49,8 @@ enum {
 
 /* DEFLATE = fixed-Huffman blocks (HuffmanEncoding::FIXED); DEFLATE_DYN = dynamic Huffman
  * (HuffmanEncoding::DYNAMIC, the reference default, config.h:151) */
-enum { BO_CODEC_LZ4 = 1, BO_CODEC_DEFLATE = 2, BO_CODEC_ZSTD = 3, BO_CODEC_DEFLATE_DYN = 4 };
+enum { BO_CODEC_LZ4 = 1, BO_CODEC_DEFLATE = 2, BO_CODEC_ZSTD = 3, BO_CODEC_DEFLATE_DYN = 4,
+       BO_CODEC_LZ4_WIDE = 5 };
 
 /* Configuration::UpdateCompressedSegSize (src/config.cc:59-73). */
 uint32_t bo_compressed_seg_size(uint32_t decompressed_seg_size);
@@ -64,6 +65,9 @@ int bo_lz4_decompress_block(const uint8_t* src, uint32_t csize, uint8_t* dst, ui
  * runs; DESIGN.md "LZ4 compress").  n <= 65536.  cap must be >= bo_lz4_bound(n). */
 int bo_lz4_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
                           uint32_t* csize);
+/* the wide LZ4 parse (16 KiB history, 4096-entry table): BITAR_HIP_CODEC_LZ4_WIDE */
+int bo_lz4_wide_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
+                               uint32_t* csize);
 
 /* ---- raw DEFLATE (RFC 1951) ----------------------------------------------------- */
 uint32_t bo_deflate_bound(uint32_t n);
@@ -106,6 +110,7 @@ void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t
 #define BO_MAX_DIST_ALL 2560u
 #define BO_PARSE_REP 1u
 #define BO_PARSE_SKIP 2u
+#define BO_PARSE_HLOG(h) ((uint32_t)(h) << 8) /* hash table log2 size (0: 10) */
 uint32_t bo_set_lz4_parse_flags(uint32_t flags);
 void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t max_mlen,
                            uint32_t flags, bo_emit_fn emit, void* ctx);

@@ -16,6 +16,7 @@ CODEC_LZ4 = 1
 CODEC_DEFLATE = 2
 CODEC_ZSTD = 3
 CODEC_DEFLATE_DYN = 4
+CODEC_LZ4_WIDE = 5  # the wide LZ4 parse (16 KiB history, 4096-entry table)
 
 BO_OK = 0
 BO_ERR_INVALID = -4
@@ -44,7 +45,7 @@ def lib():
         L.bo_zstd_bound.argtypes = [ctypes.c_uint32]
         for name in ("bo_lz4_decompress_block", "bo_lz4_compress_block", "bo_inflate_raw",
                      "bo_deflate_fixed_block", "bo_zstd_decompress", "bo_zstd_compress_block",
-                     "bo_deflate_dynamic_block"):
+                     "bo_deflate_dynamic_block", "bo_lz4_wide_compress_block"):
             f = getattr(L, name)
             f.restype = ctypes.c_int
             f.argtypes = [u8p, ctypes.c_uint32, u8p, ctypes.c_uint32,
@@ -105,6 +106,12 @@ def lz4_decompress(src, cap):
 def lz4_compress(src):
     n = len(src)
     return _block(lib().bo_lz4_compress_block, src, lz4_bound(n))
+
+
+def lz4_wide_compress(src):
+    """the wide LZ4 parse (BITAR_HIP_CODEC_LZ4_WIDE)"""
+    n = len(src)
+    return _block(lib().bo_lz4_wide_compress_block, src, lz4_bound(n))
 
 
 def inflate(src, cap):

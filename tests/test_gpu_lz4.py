@@ -162,3 +162,55 @@ def test_full_size_roundtrip_1gib(eng, kind):
         assert got == comp, f"segment {i}"
     del data, slab, out
     torch.cuda.empty_cache()
+
+
+# ---- the wide LZ4 parse (BITAR_HIP_CODEC_LZ4_WIDE: the ratio operating point) -------------
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 5, 6])
+@pytest.mark.parametrize("seg", [65536, 59460, 2048, 13])
+def test_wide_compress_bit_exact_vs_oracle(eng, kind, seg):
+    """lz4_compress_kernel<16384, 12> writes the oracle's bo_lz4_wide_compress_block stream
+    byte for byte; our decoder (its far-history kernel: distances up to 14848) and liblz4's
+    semantics (the oracle decoder) round-trip it."""
+    import bitar_amd
+    n = 5 * seg + seg // 3 + 1 if seg > 100 else 1000
+    data = O.fill(kind, 78, n)
+    slab, stride, sizes = eng.compress(bitar_amd.CODEC_LZ4_WIDE, up(data)[:n], seg)
+    eng.sync()
+    r, oslab, osizes = O.compress_segments(O.CODEC_LZ4_WIDE, data, seg, stride)
+    assert r == 0
+    gsizes = down(sizes).astype(np.uint32)
+    assert np.array_equal(gsizes, osizes)
+    gslab = down(slab)
+    for i in range(gsizes.size):
+        a = gslab[i * stride:i * stride + gsizes[i]]
+        b = oslab[i * stride:i * stride + osizes[i]]
+        assert np.array_equal(a, b), f"segment {i}"
+    out, prod = eng.decompress(bitar_amd.CODEC_LZ4_WIDE, slab, stride, sizes, seg)
+    eng.sync()
+    assert np.array_equal(down(out)[:n], data)
+
+
+def test_wide_full_size_roundtrip_and_ratio(eng):
+    """1 GiB of the headline input through the wide parse: round trip, sampled segments equal
+    the oracle's, and the ratio gains over the fast parse."""
+    import bitar_amd
+    n, seg = 1 << 30, 65536
+    data = eng.empty(n)
+    eng.fill(1, 0, data)
+    ratios = {}
+    for codec in (bitar_amd.CODEC_LZ4, bitar_amd.CODEC_LZ4_WIDE):
+        slab, stride, sizes = eng.compress(codec, data, seg)
+        eng.sync()
+        out, prod = eng.decompress(codec, slab, stride, sizes, seg)
+        eng.sync()
+        assert torch.equal(out[:n], data)
+        ratios[codec] = n / float(sizes.to(torch.int64).sum().item())
+        if codec == bitar_amd.CODEC_LZ4_WIDE:
+            gs = down(sizes).astype(np.uint32)
+            for i in (0, 5, 16383):
+                plain = down(data[i * seg:(i + 1) * seg]).tobytes()
+                r, comp = O.lz4_wide_compress(plain)
+                assert r == 0 and comp == down(slab[i * stride:i * stride + int(gs[i])]).tobytes()
+        del slab, out
+    assert ratios[bitar_amd.CODEC_LZ4_WIDE] > 1.03 * ratios[bitar_amd.CODEC_LZ4], ratios
+    torch.cuda.empty_cache()

@@ -391,3 +391,20 @@ def test_lz4_skip_parse_ratio_cost():
                 assert r == 0 and out == d[i * seg:(i + 1) * seg].tobytes()
     finally:
         L.bo_set_lz4_parse_flags(old)
+
+
+def test_lz4_wide_parse_ratio_and_streams():
+    """BITAR_HIP_CODEC_LZ4_WIDE (16 KiB history, 4096-entry table) gains ratio on every
+    compressible kind against the fast parse and writes ordinary LZ4 blocks (liblz4 and the
+    oracle decode them; distances reach past the fast parse's 2560)."""
+    n, seg = 2 << 20, 65536
+    stride = (O.lz4_bound(seg) + 255) & ~255
+    for kind in (1, 2, 5, 6):
+        d = O.fill(kind, 9, n)
+        r, slab, sizes = O.compress_segments(O.CODEC_LZ4, d, seg, stride, 4)
+        rw, slabw, sizesw = O.compress_segments(O.CODEC_LZ4_WIDE, d, seg, stride, 4)
+        assert r == 0 and rw == 0
+        assert sizesw.astype(np.int64).sum() < sizes.astype(np.int64).sum(), kind
+        blobs = [slabw[i * stride:i * stride + sizesw[i]] for i in range(sizesw.size)]
+        r, out, prod = O.decompress_segments(O.CODEC_LZ4_WIDE, blobs, seg, n, 4)
+        assert r == 0 and np.array_equal(out, d)
