@@ -714,6 +714,7 @@ def main():
             "LZ4 blocks), compress + decompress")
         if stock is not None:
             res["lz4_wide"]["liblz4_default_ratio"] = stock[1]["lz4"]
+            res["stock_ratio"]["ours_lz4_wide"] = res["lz4_wide"]["compression_ratio"]
     if stock is not None:
         res["stock_decode"] = stock[0]
     if world == 1 and args.codec == "lz4" and (args.only is None or want(args, "frontend")):
