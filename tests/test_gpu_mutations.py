@@ -241,3 +241,45 @@ def test_two_engines_with_different_decoders_concurrently(eng):
     finally:
         a.close()
         b.close()
+
+
+# ---- LZ4: the far-history kernel (lz4_decompress_kernel<true>) ------------------------------
+def test_lz4_far_path_mutations_like_oracle(eng):
+    """Streams whose matches reach past the decoder's LDS ring -- the wide parse's (<= 14848
+    back) and liblz4's (<= 65535) -- are deferred to lz4_decompress_kernel<true>, whose FAR
+    batches read history back from HBM after a wave fence.  Mutated, they must decode as the
+    oracle's bo_lz4_decompress_block decides; the counters show the far kernel ran."""
+    old = eng.set_decoder_options(count_paths=1)
+    try:
+        eng.path_counters()
+        rng = np.random.default_rng(1977)
+        bases = []
+        for kind, n, seed in ((1, 65536, 41), (2, 65536, 42), (5, 65536, 43), (6, 40000, 44)):
+            plain = O.fill(kind, seed, n).tobytes()
+            r, wide = O.lz4_wide_compress(plain)
+            assert r == 0
+            bases.append(wide)
+        try:
+            L = ctypes.CDLL("liblz4.so.1")
+            L.LZ4_compress_default.restype = ctypes.c_int
+            for kind, n, seed in ((1, 65536, 45), (5, 65536, 46)):
+                plain = O.fill(kind, seed, n).tobytes()
+                buf = ctypes.create_string_buffer(n + n // 255 + 16)
+                r = L.LZ4_compress_default(plain, buf, n, len(buf))
+                assert r > 0
+                bases.append(buf.raw[:r])
+        except OSError:
+            pass
+        _check_like_oracle(eng, O.CODEC_LZ4, bases, O.lz4_decompress)
+        c0 = eng.path_counters()
+        assert c0["lz4_far"] > 0, c0
+        cases = []
+        for b in bases:
+            cases += _mutations(b, rng, 40, hot=(len(b) // 2, len(b)))
+        n_ok = _check_like_oracle(eng, O.CODEC_LZ4, cases, O.lz4_decompress)
+        c = eng.path_counters()
+        assert c["lz4_far"] > len(cases) // 4, c
+        assert n_ok < len(cases)
+        print(f"lz4 far mutations: {len(cases)} cases, {n_ok} accepted, counters {c}")
+    finally:
+        eng.set_decoder_options(**old)
