@@ -281,7 +281,10 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   o.op = 0;
   o.flushed = 0;
   o.overflow = false;
-  parse<Lz4Out, false, true, RING, HLOG>(global_ptr(input + seg_off), n,
+#ifndef BITAR_CMP_LZ4_SKIP
+#define BITAR_CMP_LZ4_SKIP 1  // tuning knob: 0 = the plain window scan (not the oracle's LZ4 parse)
+#endif
+  parse<Lz4Out, false, BITAR_CMP_LZ4_SKIP != 0, RING, HLOG>(global_ptr(input + seg_off), n,
                                          global_ptr(input + n_total), table, inring,
                                          RING - 1536u, 0xFFFFFFFFu, o);
   o.flush(o.op, true);

@@ -288,13 +288,16 @@ __device__ __forceinline__ uint32_t chain_fast2(uint64_t& m, uint32_t lenw, uint
 // only a hash match does not start a match when one of the next kRepAhead positions holds a
 // repeat match.
 constexpr uint32_t kRepAhead = 3;
-// SKIP (the LZ4 parse, oracle BO_PARSE_SKIP): a window lying entirely inside the current match
-// is skipped (no lookups, no inserts); after kSkipS2 consecutive windows that started no
-// match, the next window is a PROBE of stride 2 (4 after kSkipS4): the 64 positions x + s l
-// look up their candidates; with no match among them they are inserted and the scan moves on
-// to x + 64 s, else nothing is inserted and ordinary windows scan the region from x.  On
-// incompressible stretches a window then covers 256 positions (liblz4's growing search step).
-constexpr uint32_t kSkipS2 = 2, kSkipS4 = 6;
+// SKIP (the LZ4 parse, oracle BO_PARSE_SKIP): with g = the gate (the parse position, or after
+// a probe hit the end of the probed span, whichever is later), a window lying entirely inside
+// the current match is skipped (no lookups, no inserts); a window starting >= kSkipProbe past g
+// (two windows with no match start) is a PROBE of stride 2 (4 from kSkipWide past g): the 64
+// positions x + s l look up their candidates; with no match among them they are inserted and
+// the scan moves on to x + 64 s, else nothing is inserted, g moves to x + 64 (s - 1) - 127 and
+// ordinary windows scan the region from x.  On incompressible stretches a window then covers
+// 256 positions (liblz4's growing search step).  The common case -- an ordinary window close
+// to the gate -- costs one scalar compare: both special cases lie outside (g - 64, g + 128).
+constexpr uint32_t kSkipProbe = 128, kSkipWide = 640;
 // RING / HLOG: the input ring's size and the hash table's log2 size (the defaults: 4 KiB and
 // 1024 entries; the wide LZ4 parse: 16 KiB and 4096, max_dist = RING - 1536 either way).
 template <class E, bool REP = false, bool SKIP = false, uint32_t RING = kIn,
@@ -341,7 +344,6 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
     // one window of 64 positions at x; vp = the 16 bytes at x + lane, read during the
     // previous window (the ring already holds them then)
     uint4 vp = make_uint4(0, 0, 0, 0);
-    bool started = false;  // the last window started a match or began inside one (SKIP)
     auto window = [&](uint32_t x) __attribute__((always_inline)) {
       const uint32_t p = x + lane;
       const bool act = p <= last_start;
@@ -466,7 +468,6 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
         m = e < kWave ? valid & (~0ull << e) : 0ull;
       }
       if (chain) pos = x + e;
-      started = chain != 0 || pos_in > x;
       if constexpr (REP) {
         // the history after this window's matches: the 3 most recently used distinct
         // distances (move-to-front) of [h2, h1, h0, the chain's distances in lane order],
@@ -528,8 +529,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
     // point by < 256 positions; the ring then still runs >= 497 B ahead of the scan and holds
     // every candidate: x - 2560 > 1024 k - 3072)
     uint32_t next_load = kRow / 2;
-    uint32_t vx = 0;  // vp holds the 16 bytes at vx + lane
-    uint32_t misses = 0;
+    uint32_t g = 0;  // SKIP: the gate, >= pos
     for (uint32_t x = 0; x <= last_start;) {
       if (x >= next_load) {
         const uint32_t k = next_load / kRow;
@@ -542,45 +542,47 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
         next_load += kRow;
       }
       if constexpr (SKIP) {
-        if (pos >= x + kWave) {  // inside the current match
-          misses = 0;
-          x += kWave;
-          continue;
-        }
-        const uint32_t st = misses >= kSkipS4 ? 4u : misses >= kSkipS2 ? 2u : 1u;
-        if (st > 1) {  // probe of stride st
-          lds_order();
-          const uint32_t p = x + st * lane;
-          const bool act = p <= last_start;
-          const uint32_t v = I.dword(p);
-          const uint32_t h = hash4<HLOG>(v);
-          const uint32_t cand = table[h];
-          const uint32_t cv = I.dword(cand);
-          const bool hit = act & (cand < p) & (p - cand <= max_dist) & (cv == v);
-          if (!ballot(hit)) {
-            // no match among them: insert (ascending, the largest position wins the slot)
+        if (x - g + (kWave - 1) >= kSkipProbe + kWave - 1) {  // g >= x + 64, or x >= g + 128
+          if (pos >= x + kWave) {  // inside the current match
+            x += kWave;
             lds_order();
-            table[act ? h : (1u << HLOG)] = (uint16_t)p;
-            lds_order();
-            bool redo = act && table[h] < p;
-            while (ballot(redo)) {
-              lds_order();
-              if (redo) table[h] = (uint16_t)p;
-              lds_order();
-              redo = redo && table[h] < p;
-            }
-            ++misses;
-            x += st * kWave;
+            vp = I.bytes16(x + lane);
             continue;
           }
-          misses = 0;
+          if (x >= g + kSkipProbe) {  // a probe of stride st
+            const uint32_t st = x >= g + kSkipWide ? 4u : 2u;
+            lds_order();
+            const uint32_t p = x + st * lane;
+            const bool act = p <= last_start;
+            const uint32_t v = I.dword(p);
+            const uint32_t h = hash4<HLOG>(v);
+            const uint32_t cand = table[h];
+            const uint32_t cv = I.dword(cand);
+            const bool hit = act & (cand < p) & (p - cand <= max_dist) & (cv == v);
+            if (!ballot(hit)) {
+              // no match among them: insert (ascending, the largest position wins the slot)
+              lds_order();
+              table[act ? h : (1u << HLOG)] = (uint16_t)p;
+              lds_order();
+              bool redo = act && table[h] < p;
+              while (ballot(redo)) {
+                lds_order();
+                if (redo) table[h] = (uint16_t)p;
+                lds_order();
+                redo = redo && table[h] < p;
+              }
+              x += st * kWave;
+              continue;
+            }
+            g = x + kWave * (st - 1) - 127u;  // ordinary windows over the probed span
+          }
+          lds_order();
+          vp = I.bytes16(x + lane);  // (after skipped windows / probes)
         }
       }
       lds_order();
-      if (vx != x) vp = I.bytes16(x + lane);  // (after skipped windows)
       window(x);
-      vx = x + kWave;
-      if constexpr (SKIP) misses = started ? 0u : misses + 1;
+      if constexpr (SKIP) g = g > pos ? g : pos;
       x += kWave;
     }
   }

@@ -123,18 +123,20 @@ static int repnear(const int* isrep, uint32_t l, uint32_t cnt) {
 }
 /* flags & BO_PARSE_SKIP (the LZ4 parse): windows the parse has no use for are skipped, as
  * liblz4 skips positions (LZ4_compress_generic's search step grows with consecutive misses
- * and positions inside a match are never searched nor inserted):
+ * and positions inside a match are never searched nor inserted).  With g = the gate (the
+ * parse position, or -- after a probe hit -- the end of the probed span, whichever is later):
  *   - a window lying entirely inside the current match (pos >= x + 64) is skipped: no
  *     lookups, no inserts;
- *   - after BO_SKIP_S2 consecutive windows that started no match (a window that began
- *     inside a match counts as a hit), the next window is a PROBE of stride s = 2 (4 after
- *     BO_SKIP_S4 misses): the 64 positions x + s*l (<= last_start) look up their candidates
- *     exactly as a window does; if none of them holds a match, those positions are inserted
- *     (ascending: the largest wins) and the scan moves on to x + 64 s; if any does, nothing
- *     is inserted, the miss count restarts, and the region is scanned by ordinary windows
- *     from x. */
-#define BO_SKIP_S2 2u
-#define BO_SKIP_S4 6u
+ *   - a window starting >= 128 positions past g (two windows with no match start) is a PROBE
+ *     of stride s = 2 (s = 4 from 640 past g): the 64 positions x + s*l (<= last_start) look
+ *     up their candidates exactly as a window does; if none of them holds a match, those
+ *     positions are inserted (ascending: the largest wins) and the scan moves on to
+ *     x + 64 s; if any does, nothing is inserted, g moves to x + 64 (s - 1) - 127 (so the
+ *     probed span is scanned by ordinary windows), and ordinary windows go on from x;
+ *   - after every ordinary window g = max(g, pos).
+ * (The GPU tests all three conditions with one scalar compare per window.) */
+#define BO_SKIP_PROBE 128u
+#define BO_SKIP_WIDE 640u
 void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
                            uint32_t max_mlen, uint32_t flags, bo_emit_fn emit, void* ctx) {
   uint32_t anchor = 0;
@@ -148,15 +150,12 @@ void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
     memset(table, 0, sizeof(uint32_t) << hlog);
     const uint32_t last_start = n - BO_MFLIMIT;        /* match start must be <= n-12 */
     const uint32_t match_limit = n - BO_LASTLITERALS;  /* match end must be <= n-5 */
-    uint32_t pos = 0, misses = 0;
+    uint32_t pos = 0, g = 0;
     for (uint32_t x = 0; x <= last_start; x += BO_WIN) {
       if (skip) {
-        if (pos >= x + BO_WIN) { /* inside the current match */
-          misses = 0;
-          continue;
-        }
-        const uint32_t s = misses >= BO_SKIP_S4 ? 4u : misses >= BO_SKIP_S2 ? 2u : 1u;
-        if (s > 1) {
+        if (pos >= x + BO_WIN) continue; /* inside the current match */
+        if (x >= g + BO_SKIP_PROBE) {    /* (g >= pos: see below) */
+          const uint32_t s = x >= g + BO_SKIP_WIDE ? 4u : 2u;
           int hit = 0;
           for (uint32_t l = 0; l < BO_WIN && x + s * l <= last_start; ++l) {
             const uint32_t p = x + s * l, c = table[bo_hash_n(rd32(src + p), hlog)];
@@ -165,15 +164,12 @@ void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
           if (!hit) {
             for (uint32_t l = 0; l < BO_WIN && x + s * l <= last_start; ++l)
               table[bo_hash_n(rd32(src + x + s * l), hlog)] = x + s * l;
-            ++misses;
             x += (s - 1) * BO_WIN; /* (+ BO_WIN by the loop) */
             continue;
           }
-          misses = 0;
+          g = x + BO_WIN * (s - 1) - 127u;
         }
       }
-      const uint32_t pos_in = pos;
-      int started = 0;
       uint32_t cnt = last_start - x + 1;
       if (cnt > BO_WIN) cnt = BO_WIN;
       uint32_t cand[BO_WIN], h[BO_WIN];
@@ -215,7 +211,6 @@ void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
         emit(ctx, anchor, i - anchor, i - c, len);
         pos = i + len;
         anchor = pos;
-        started = 1;
         if (rep) {
           const uint32_t d = i - c;
           if (d == hist[1]) {
@@ -232,7 +227,7 @@ void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
           }
         }
       }
-      misses = started || pos_in > x ? 0u : misses + 1;
+      if (pos > g) g = pos;
     }
   }
   emit(ctx, anchor, n - anchor, 0, 0); /* last sequence: literals only */
