@@ -79,8 +79,8 @@ KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
            # the wide parse (16 KiB history): same kernels, other template instance; offsets
            # past the decoder's LDS ring take lz4_decompress_kernel<true> (far history)
            "lz4_wide": ("lz4_compress_kernel", "lz4_decompress_kernel"),
-           # decompress = inflate_lanes_kernel (lane per segment: stored / fixed blocks) +
-           # inflate_kernel over the segments it deferred
+           # decompress = inflate_kernel (wave per segment; the lane-per-segment
+           # inflate_lanes_kernel runs in front only when a context turns it on)
            "deflate": ("deflate_compress_kernel", "inflate_lanes_kernel+inflate_kernel"),
            # compress = zstd_parse_kernel + zstd_entropy_kernel + zstd_walk_kernel (FSE state
            # chains, a lane per chain) + zstd_emit_kernel (sequence bitstream); decompress =
@@ -92,8 +92,7 @@ KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
                     "zstd_lanes_kernel+zstd_decompress_kernel+zstd_hlit_kernel+"
                     "zstd_seqdec_kernel+zstd_exec_kernel+zstd_handoff_kernel"),
            # compress = deflate_dyn_parse_kernel + deflate_dyn_emit_kernel (one event pair
-           # brackets both); decompress = inflate_lanes_kernel (stored blocks: the random
-           # third) + inflate_kernel (every dynamic block)
+           # brackets both); decompress = inflate_kernel (as for "deflate")
            "deflate_dyn": ("deflate_dyn_parse_kernel+deflate_dyn_emit_kernel",
                            "inflate_lanes_kernel+inflate_kernel")}
 CODEC_NAMES = {"lz4": "lz4-block", "deflate": "deflate-raw-fixed", "zstd": "zstd-frame",

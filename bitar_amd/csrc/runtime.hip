@@ -476,11 +476,14 @@ static long env_long(const char* name, long dflt) {
 }
 
 static void init_options(bitar_hip_ctx* ctx, uint32_t flags) {
-  // 4 segments per wave: 4516 waves per GiB hide more of each lane's load latency than 16
-  // (1129 waves, about one per SIMD): 1-GiB decode kind 1 17.3 -> 15.5 ms, kind 5 14.6 ->
-  // 12.7, kind 6 9.8 -> 8.9; stored-only (random) data 9.2 -> 10.4
+  // The lane inflater in front of the wave inflater is off by default since the wave
+  // inflater's batches take far matches (round 3): 1 GiB fixed-Huffman decode, wave alone vs
+  // 4 lanes per wave in front: kind 1 11.6 / 14.1 ms, kind 2 12.4 / 17.6, kind 5 13.3 / 12.6,
+  // kind 6 11.7 / 8.9 (the lanes win long-match data only; splitting segments between the
+  // two by compression ratio was slower than either: the launches run one after the other).
+  // Dynamic blocks always take the wave inflater.  inflate_lanes = 4 keeps the lane form.
   ctx->inflate_lanes = flags & BITAR_HIP_FLAG_INFLATE_WAVE_ONLY
-                           ? 0u : inflate_lanes_from(env_long("BITAR_HIP_INFLATE_LANES", 4));
+                           ? 0u : inflate_lanes_from(env_long("BITAR_HIP_INFLATE_LANES", 0));
   ctx->zstd_lanes = flags & BITAR_HIP_FLAG_ZSTD_WAVE_ONLY
                         ? 0u : zstd_lanes_from(env_long("BITAR_HIP_ZSTD_LANES", 16));
   ctx->zstd_seq = flags & BITAR_HIP_FLAG_ZSTD_LANE_EXEC ? 0u : env_long("BITAR_HIP_ZSTD_SEQ", 1) != 0;

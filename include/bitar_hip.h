@@ -72,7 +72,9 @@ typedef struct {
 
 /* bitar_hip_config.flags: the context's initial decoder options (bitar_hip_decoder_options);
  * every context keeps its own, so engines with different settings run side by side. */
-#define BITAR_HIP_FLAG_INFLATE_WAVE_ONLY 0x1u /* no lane inflater in front of inflate_kernel */
+#define BITAR_HIP_FLAG_INFLATE_WAVE_ONLY 0x1u /* no lane inflater in front of inflate_kernel
+                                                 (the default since round 3; the flag also
+                                                 overrides BITAR_HIP_INFLATE_LANES) */
 #define BITAR_HIP_FLAG_ZSTD_WAVE_ONLY 0x2u    /* no lane Zstd decoder in front of the wave one */
 #define BITAR_HIP_FLAG_ZSTD_LANE_EXEC 0x4u    /* handed-off sequence sections: lane executor */
 #define BITAR_HIP_FLAG_COUNT_PATHS 0x8u       /* count decoder path entries (see below) */

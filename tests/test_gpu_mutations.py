@@ -215,6 +215,8 @@ def test_two_engines_with_different_decoders_concurrently(eng):
     b = bitar_amd.Engine(0, num_streams=1, flags=bitar_amd.FLAG_COUNT_PATHS
                          | bitar_amd.FLAG_INFLATE_WAVE_ONLY | bitar_amd.FLAG_ZSTD_WAVE_ONLY)
     try:
+        assert a.decoder_options()["inflate_lanes"] == 0  # the default since round 3
+        a.set_decoder_options(inflate_lanes=4)
         assert a.decoder_options()["inflate_lanes"] == 4
         assert b.decoder_options()["inflate_lanes"] == 0 and b.decoder_options()["zstd_lanes"] == 0
         n, seg = 64 * 59460, 59460
