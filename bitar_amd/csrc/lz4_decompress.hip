@@ -19,12 +19,6 @@
 
 #include <type_traits>
 
-// token-walk form (tuning knob, scripts/build_variant.sh): 4 = walk_tokens4 (default),
-// 1 = walk_tokens, the round-1 form (kind 1 decode 2.89 -> 2.67 ms/GiB, kind 2 5.05 -> 4.49)
-#ifndef BITAR_LZ4D_WALK
-#define BITAR_LZ4D_WALK 4
-#endif
-
 namespace bitar_hip {
 
 
@@ -36,15 +30,17 @@ using namespace sr;
 // stream bytes the batch path may touch past ip: 64 candidate tokens, each with up to two
 // length bytes and <= 60 literals, plus its offset
 constexpr uint32_t kBatchIn = 132;
-// output bytes one batch may produce (one per lane)
-constexpr uint32_t kBatchOut = kWave;
-// Largest next-token lane of an ELIGIBLE token (colen <= 64, minmatch 4): lane 63 + token +
-// 2 offset bytes + a literal-length byte + max(60 literals with no match-length byte,
+// output bytes one batch may produce: two per lane, as two halves of 64 (lane t holds
+// output bytes t and 64 + t); one sequence of the batch produces at most kSeqOut of them
+constexpr uint32_t kBatchOut = 2 * kWave;
+constexpr uint32_t kSeqOut = kWave;
+// Largest next-token lane of an ELIGIBLE token (colen <= kSeqOut, minmatch 4): lane 63 +
+// token + 2 offset bytes + a literal-length byte + max(60 literals with no match-length byte,
 // 45 literals + a match-length byte, since an extended match is >= 19 bytes).  The walk
 // record keeps it in 7 bits; widening eligibility must keep this <= 127.
 constexpr uint32_t kMaxEligibleNext =
-    (kWave - 1) + 3 + 1 + ((kBatchOut - 4) > (kBatchOut - 19) + 1 ? (kBatchOut - 4)
-                                                                    : (kBatchOut - 19) + 1);
+    (kWave - 1) + 3 + 1 + ((kSeqOut - 4) > (kSeqOut - 19) + 1 ? (kSeqOut - 4)
+                                                                : (kSeqOut - 19) + 1);
 static_assert(kMaxEligibleNext <= 127, "next-token lane overflows the walk record's 7 bits");
 
 // 256 stream bytes held in ONE register, dword-packed: lane l holds bytes vb+4l .. vb+4l+3
@@ -105,76 +101,93 @@ __device__ __forceinline__ bool ext_len(State& s, uint8_t* win, SVec& sv, uint32
 
 
 // The batch's token walk: from lane 0, follow the chain of candidate tokens while each
-// sequence is eligible and fits in lim output bytes; sequence records (pr of the token
-// lane) are dropped into the lane of the sequence's first output byte.  Returns the output
-// byte count; k = the first unconsumed token lane.  Written out because the scalar chain is
-// the batch's bound (the SQ issues one SALU per SIMD every 4 cycles): 8 SALU + 3 VALU per
-// sequence, output position kept in m0 (the v_writelane lane select).
-__device__ __forceinline__ uint32_t walk_tokens(uint32_t pw, uint32_t pr, uint32_t lim,
-                                                uint32_t& k, uint32_t& vrec) {
-  uint32_t out, e, r, ol, n, m0_saved;
-  // m0 is reserved to the compiler: saved and restored around the loop
-  __asm__ volatile(
-      "s_mov_b32 %[m0s], m0\n"
-      "s_mov_b32 %[k], 0\n"
-      "s_mov_b32 m0, 0\n"
-      "L_walk_%=:\n"
-      "v_readlane_b32 %[e], %[pw], %[k]\n"
-      "v_readlane_b32 %[r], %[pr], %[k]\n"
-      "s_lshr_b32 %[ol], %[e], 7\n"
-      "s_add_u32 %[n], m0, %[ol]\n"
-      "s_cmp_gt_u32 %[n], %[lim]\n"
-      "s_cbranch_scc1 L_done_%=\n"
-      "v_writelane_b32 %[vr], %[r], m0\n"
-      "s_mov_b32 m0, %[n]\n"
-      "s_and_b32 %[k], %[e], 0x7f\n"
-      "s_cmp_lt_u32 %[k], 64\n"
-      "s_cbranch_scc1 L_walk_%=\n"
-      "L_done_%=:\n"
-      "s_mov_b32 %[out], m0\n"
-      "s_mov_b32 m0, %[m0s]\n"
-      : [k] "=&s"(k), [out] "=&s"(out), [e] "=&s"(e), [r] "=&s"(r), [ol] "=&s"(ol),
-        [n] "=&s"(n), [m0s] "=&s"(m0_saved), [vr] "+v"(vrec)
-      : [pw] "v"(pw), [pr] "v"(pr), [lim] "s"(lim)
-      : "scc");
-  return out;
-}
-
-// Walk form 4 (the default).  Lane 63 is a sentinel that never qualifies, so "the next token
-// lies past the parsed lanes" needs no compare of its own: pw = next lane clamped to 63
-// (bits 0..5) | output length (bits 6..13, 255: not eligible) | unclamped next lane (bits
-// 24..30: the stream advance when the walk ends after this sequence).  The room is kept as
-// a remainder (one s_sub_u32 both subtracts and tests: its borrow is "does not fit"), the
-// word read is itself the next lane select (v_readlane takes the low 6 bits of its
-// lane-select SGPR; >= 4 instructions separate each VALU write of e / e2 from its use as a
-// lane select), and the loop is unrolled twice: 3 SALU + 3 VALU per sequence (form 1: 8 + 3;
-// the batch is bound by the CU's shared scalar unit as much as by the VALU).  `adv` = the
-// stream bytes consumed.
-__device__ __forceinline__ uint32_t walk_tokens4(uint32_t pw, uint32_t pr, uint32_t lim,
-                                                 uint32_t& adv, uint32_t& vrec) {
+// sequence is eligible and fits in lim (<= 128) output bytes; each sequence's record (pr of
+// its token lane) is dropped into the lane of its first output byte (v_writelane), in v0
+// for sequences starting in the first half (output bytes 0..63), in v1 for the second
+// (64..127; the lane select is m0 mod 64).  Written out because the scalar chain is the
+// batch's bound (one SALU per SIMD every 4 cycles, shared by the CU).  Lane 63 is a sentinel
+// that never qualifies, so "the next token lies past the parsed lanes" needs no compare of
+// its own: pw = next lane clamped to 63 (bits 0..5) | output length (bits 6..13, 255: not
+// eligible) | unclamped next lane (bits 24..30: the stream advance when the walk ends after
+// this sequence).  The room is kept as a remainder (one s_sub_u32 both subtracts and tests:
+// its borrow is "does not fit"), the word read is itself the next lane select (v_readlane
+// takes the low 6 bits of its lane-select SGPR; >= 4 instructions separate each VALU write of
+// e / e2 from its use as a lane select), each loop is unrolled twice: 3 SALU + 3 VALU per
+// sequence.  Phase A's room ends at byte 64, so its loop never tests the half; the sequence
+// that crosses byte 64 (or starts at it) is placed once by the hand-over code, then phase B
+// runs with the whole room.  `adv` = the stream bytes consumed.
+__device__ __forceinline__ uint32_t walk_tokens2h(uint32_t pw, uint32_t pr, uint32_t lim,
+                                                  uint32_t& adv, uint32_t& v0, uint32_t& v1) {
   uint32_t out, e, e2, r, ol, rem, m0_saved;
   __asm__ volatile(
       "s_mov_b32 %[m0s], m0\n"
       "s_mov_b32 %[e], 0\n"
       "s_mov_b32 %[e2], 0\n"
-      "s_mov_b32 %[rem], %[lim]\n"
+      "s_min_u32 %[rem], %[lim], 64\n"
       "s_mov_b32 m0, 0\n"
-      "L_w4_%=:\n"
+      // phase A: sequences ending at or before byte 64 (or lim)
+      "L_a_%=:\n"
       "v_readlane_b32 %[e2], %[pw], %[e]\n"
       "v_readlane_b32 %[r], %[pr], %[e]\n"
       "s_bfe_u32 %[ol], %[e2], 0x80006\n"
       "s_sub_u32 %[rem], %[rem], %[ol]\n"
-      "s_cbranch_scc1 L_da_%=\n"
-      "v_writelane_b32 %[vr], %[r], m0\n"
+      "s_cbranch_scc1 L_xa_%=\n"
+      "v_writelane_b32 %[v0], %[r], m0\n"
       "s_add_u32 m0, m0, %[ol]\n"
       "v_readlane_b32 %[e], %[pw], %[e2]\n"
       "v_readlane_b32 %[r], %[pr], %[e2]\n"
       "s_bfe_u32 %[ol], %[e], 0x80006\n"
       "s_sub_u32 %[rem], %[rem], %[ol]\n"
-      "s_cbranch_scc1 L_db_%=\n"
-      "v_writelane_b32 %[vr], %[r], m0\n"
+      "s_cbranch_scc1 L_xb_%=\n"
+      "v_writelane_b32 %[v0], %[r], m0\n"
       "s_add_u32 m0, m0, %[ol]\n"
-      "s_branch L_w4_%=\n"
+      "s_branch L_a_%=\n"
+      // hand-over, failing word in e2 (last consumed: e): fits the whole room?
+      "L_xa_%=:\n"
+      "s_sub_u32 %[rem], %[lim], m0\n"
+      "s_sub_u32 %[rem], %[rem], %[ol]\n"
+      "s_cbranch_scc1 L_da_%=\n"
+      "s_cmp_lt_u32 m0, 64\n"
+      "s_cbranch_scc0 L_xa1_%=\n"
+      "v_writelane_b32 %[v0], %[r], m0\n"
+      "s_add_u32 m0, m0, %[ol]\n"
+      "s_branch L_b_%=\n"
+      "L_xa1_%=:\n"
+      "v_writelane_b32 %[v1], %[r], m0\n"
+      "s_add_u32 m0, m0, %[ol]\n"
+      "s_branch L_b_%=\n"
+      // hand-over, failing word in e (last consumed: e2)
+      "L_xb_%=:\n"
+      "s_sub_u32 %[rem], %[lim], m0\n"
+      "s_sub_u32 %[rem], %[rem], %[ol]\n"
+      "s_cbranch_scc1 L_db_%=\n"
+      "s_cmp_lt_u32 m0, 64\n"
+      "s_cbranch_scc0 L_xb1_%=\n"
+      "v_writelane_b32 %[v0], %[r], m0\n"
+      "s_add_u32 m0, m0, %[ol]\n"
+      "s_branch L_b2_%=\n"
+      "L_xb1_%=:\n"
+      "v_writelane_b32 %[v1], %[r], m0\n"
+      "s_add_u32 m0, m0, %[ol]\n"
+      "s_branch L_b2_%=\n"
+      // phase B: every later sequence starts past byte 64
+      "L_b_%=:\n"
+      "v_readlane_b32 %[e], %[pw], %[e2]\n"
+      "v_readlane_b32 %[r], %[pr], %[e2]\n"
+      "s_bfe_u32 %[ol], %[e], 0x80006\n"
+      "s_sub_u32 %[rem], %[rem], %[ol]\n"
+      "s_cbranch_scc1 L_db_%=\n"
+      "v_writelane_b32 %[v1], %[r], m0\n"
+      "s_add_u32 m0, m0, %[ol]\n"
+      "L_b2_%=:\n"
+      "v_readlane_b32 %[e2], %[pw], %[e]\n"
+      "v_readlane_b32 %[r], %[pr], %[e]\n"
+      "s_bfe_u32 %[ol], %[e2], 0x80006\n"
+      "s_sub_u32 %[rem], %[rem], %[ol]\n"
+      "s_cbranch_scc1 L_da_%=\n"
+      "v_writelane_b32 %[v1], %[r], m0\n"
+      "s_add_u32 m0, m0, %[ol]\n"
+      "s_branch L_b_%=\n"
       "L_da_%=:\n"
       "s_lshr_b32 %[e], %[e], 24\n"
       "s_branch L_out_%=\n"
@@ -184,7 +197,7 @@ __device__ __forceinline__ uint32_t walk_tokens4(uint32_t pw, uint32_t pr, uint3
       "s_mov_b32 %[out], m0\n"
       "s_mov_b32 m0, %[m0s]\n"
       : [e] "=&s"(e), [e2] "=&s"(e2), [out] "=&s"(out), [r] "=&s"(r), [ol] "=&s"(ol),
-        [rem] "=&s"(rem), [m0s] "=&s"(m0_saved), [vr] "+v"(vrec)
+        [rem] "=&s"(rem), [m0s] "=&s"(m0_saved), [v0] "+v"(v0), [v1] "+v"(v1)
       : [pw] "v"(pw), [pr] "v"(pr), [lim] "s"(lim)
       : "scc");
   adv = e;
@@ -284,7 +297,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       // back from HBM below), not before the segment start (conservatively, as if this token
       // opened the batch)
       // bitwise on the compares: short-circuit forms compile to an exec-mask branch
-      const bool cfar = ((!lx) | (b1 < 255u)) & ((!mx) | (b2 < 255u)) & (colen <= 64u) &
+      const bool cfar = ((!lx) | (b1 < 255u)) & ((!mx) | (b2 < 255u)) & (colen <= kSeqOut) &
                         (coff != 0) & (coff <= s.op + cL);
       const bool csimple = cfar && (FAR || coff <= kNearOff);
       // walk record: next token lane (7 bits, <= 127 for an eligible token, see
@@ -299,79 +312,90 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
       const uint32_t room = s.cap - s.op;
       const uint32_t lim = room < kBatchOut ? room : kBatchOut;
-      uint32_t k, vrec = 0;
-#if BITAR_LZ4D_WALK == 4
+      uint32_t k, vrec0 = 0, vrec1 = 0;
       const bool celig = csimple && lane < kWave - 1;  // lane 63: the walk's sentinel
       const uint32_t pw = (nxt < kWave - 1 ? nxt : kWave - 1) | ((celig ? colen : 255u) << 6) |
                           (nxt << 24);
-      const uint32_t out = walk_tokens4(pw, pr, lim, k, vrec);
-#else
-      const uint32_t pw = nxt | ((csimple ? colen : 255u) << 7);
-      const uint32_t out = walk_tokens(pw, pr, lim, k, vrec);
-#endif
+      const uint32_t out = walk_tokens2h(pw, pr, lim, k, vrec0, vrec1);
       if (out == 0) {
         // the first token qualifies only for a FAR batch: worth trying one
         if (!FAR) want_far = (ballot(cfar) & 1ull) != 0;
         return 0u;
       }
-      // every output byte takes the record of the latest sequence starting at or before it
-      const uint32_t key = wave_incl_max(vrec ? vrec | (lane << 24) : 0u);
-      // (3) sources: window literal / ring history / HBM history (far) / alias of an earlier
-      // byte of the batch (branch-free: every lane computes every form).  bit31: alias (low 6
-      // bits: the source lane); bit30: far (low 16 bits: the output position); else an LDS
-      // byte address.
-      const uint32_t ostart = key >> 24;
-      const uint32_t seqlane = (key >> 18) & 63u;
-      const uint32_t jL = (key >> 12) & 63u;
-      uint32_t joff = key & 4095u;
       // FAR batches (entered only where a near batch could not start: stock streams with
       // offsets beyond the ring's reach; ours stay <= 2560) read far history from HBM
-      const bool big = FAR;
-      if (big) joff |= bpermute_lane(coff & ~4095u, seqlane);  // offsets >= 4096
-      const uint32_t r = lane - ostart;
-      const bool is_lit = r < jL;
-      const uint32_t m = r - jL;
-      // overlapping copy (offset <= match position): fold the source into the first period
-      // (m mod off, exact in fp32 for m, off < 64); skipped when no byte of the batch needs it
-      uint32_t mm = m;
-      if (ballot(!is_lit && joff <= m && lane < out)) {
-        const float qf = floorf(((float)(m & 63u) + 0.5f) *
-                                __builtin_amdgcn_rcpf((float)(joff > 1u ? joff : 1u)));
-        mm = joff <= m ? (m & 63u) - (uint32_t)qf * joff : m;
-      }
-      const int32_t srel = (int32_t)(ostart + jL + mm) - (int32_t)joff;  // vs op
-      const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
-      const uint32_t lit_addr = wrel + seqlane + 1 + (jL >= 15u ? 1u : 0u) + r;
-      // every form computed before the selects (the empty asm pins them), so the compiler
-      // does not turn the selects into an exec-mask if / else
-      uint32_t lit_a = lit_addr, hist_a = hist, alias_a = (uint32_t)srel | 0x80000000u;
-      __asm__("" : "+v"(lit_a), "+v"(hist_a), "+v"(alias_a));
-      uint32_t st = srel >= 0 ? alias_a : hist_a;
-      st = is_lit ? lit_a : st;
-      if (big && srel < -(int32_t)kNearOff && !is_lit)
-        st = (s.op + (uint32_t)srel) | 0x40000000u;  // far: the output position
-      // pointer doubling until no lane of the batch aliases another (chains strictly descend)
-      const uint64_t live = ballot(lane < out);  // lanes of the batch (a VALU compare, not 5 SALU)
-      while (ballot((int32_t)st < 0) & live) {
-        const uint32_t other = bpermute_lane(st, st & 63u);
-        st = (st & 0x80000000u) ? other : st;
-      }
-      // (4) one gather (LDS, or HBM for far history), one store
-      lds_order();
-      uint32_t g = lds[st & 0x3FFFu];
-      if (big) {
-        const bool gfar = (st >> 30) == 1u && lane < out;
-        const uint64_t farm = ballot(gfar);
-        // history only in HBM: make this wave's flushed stores visible to its loads
-        if (farm && (ballot((st & 0xFFFFu) >= s.fenced) & farm)) {
-          global_fence_wave();
-          s.fenced = s.flushed;
+      constexpr bool big = FAR;
+      if (big) stay_far = false;
+      // (3)+(4) for the output bytes 64h .. 64h+63 (lane t: byte 64h + t); `key` is the
+      // byte's sequence record with its output start in bits 24..30
+      auto half = [&](auto h_tag, uint32_t key) __attribute__((always_inline)) {
+        constexpr uint32_t H = decltype(h_tag)::value;
+        const uint32_t q = lane + H * kWave;  // output byte of this lane (vs op)
+        // sources: window literal / ring history / HBM history (far) / alias of an earlier
+        // byte of this half (branch-free: every lane computes every form).  bit31: alias
+        // (low 6 bits: the source lane); bit30: far (low 16 bits: the output position); else
+        // an LDS byte address.  Bytes of the first half are in the ring already when the
+        // second half reads them.
+        const uint32_t ostart = key >> 24;
+        const uint32_t seqlane = (key >> 18) & 63u;
+        const uint32_t jL = (key >> 12) & 63u;
+        uint32_t joff = key & 4095u;
+        if (big) joff |= bpermute_lane(coff & ~4095u, seqlane);  // offsets >= 4096
+        const uint32_t r = q - ostart;  // < kSeqOut: a sequence is at most 64 bytes
+        const bool is_lit = r < jL;
+        const uint32_t m = r - jL;
+        // overlapping copy (offset <= match position): fold the source into the first period
+        // (m mod off, exact in fp32 for m, off < 64); skipped when no byte needs it
+        uint32_t mm = m;
+        if (ballot(!is_lit && joff <= m && q < out)) {
+          const float qf = floorf(((float)(m & 63u) + 0.5f) *
+                                  __builtin_amdgcn_rcpf((float)(joff > 1u ? joff : 1u)));
+          mm = joff <= m ? (m & 63u) - (uint32_t)qf * joff : m;
         }
-        if (gfar) g = s.dst[st & 0xFFFFu];
-        stay_far = farm != 0;  // keep to FAR batches while they meet far history
+        const int32_t srel = (int32_t)(ostart + jL + mm) - (int32_t)joff;  // vs op
+        const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
+        const uint32_t lit_addr = wrel + seqlane + 1 + (jL >= 15u ? 1u : 0u) + r;
+        // every form computed before the selects (the empty asm pins them), so the compiler
+        // does not turn the selects into an exec-mask if / else
+        uint32_t lit_a = lit_addr, hist_a = hist, alias_a = (uint32_t)srel | 0x80000000u;
+        __asm__("" : "+v"(lit_a), "+v"(hist_a), "+v"(alias_a));
+        uint32_t st = srel >= (int32_t)(H * kWave) ? alias_a : hist_a;
+        st = is_lit ? lit_a : st;
+        if (big && srel < -(int32_t)kNearOff && !is_lit)
+          st = (s.op + (uint32_t)srel) | 0x40000000u;  // far: the output position
+        // pointer doubling until no byte of the half aliases another (chains strictly
+        // descend; the source lane is srel mod 64)
+        const uint64_t live = ballot(q < out);  // (a VALU compare, not 5 SALU)
+        while (ballot((int32_t)st < 0) & live) {
+          const uint32_t other = bpermute_lane(st, st & 63u);
+          st = (st & 0x80000000u) ? other : st;
+        }
+        // one gather (LDS, or HBM for far history), one store
+        lds_order();
+        uint32_t g = lds[st & 0x3FFFu];
+        if (big) {
+          const bool gfar = (st >> 30) == 1u && q < out;
+          const uint64_t farm = ballot(gfar);
+          // history only in HBM: make this wave's flushed stores visible to its loads
+          if (farm && (ballot((st & 0xFFFFu) >= s.fenced) & farm)) {
+            global_fence_wave();
+            s.fenced = s.flushed;
+          }
+          if (gfar) g = s.dst[st & 0xFFFFu];
+          stay_far |= farm != 0;  // keep to FAR batches while they meet far history
+        }
+        ring[(base + s.op + q) & kRingMask] = (uint8_t)g;
+        lds_order();
+      };
+      // every output byte takes the record of the latest sequence starting at or before it
+      const uint32_t key0 = wave_incl_max(vrec0 ? vrec0 | (lane << 24) : 0u);
+      half(std::integral_constant<uint32_t, 0>{}, key0);
+      if (out > kWave) {
+        // second half: its own starts (all past byte 64), else the first half's last record
+        const uint32_t key1 = wave_incl_max(vrec1 ? vrec1 | ((lane + kWave) << 24) : 0u);
+        const uint32_t carry = readlane(key0, kWave - 1);
+        half(std::integral_constant<uint32_t, 1>{}, key1 > carry ? key1 : carry);
       }
-      ring[(base + s.op + lane) & kRingMask] = (uint8_t)g;
-      lds_order();
       s.ip += __builtin_amdgcn_readfirstlane(k);  // (k is an SGPR: keeps the add scalar)
       s.op += out;
       return out;
