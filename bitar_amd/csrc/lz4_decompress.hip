@@ -82,10 +82,6 @@ struct SVec {
   }
 };
 
-__device__ __forceinline__ uint32_t bpermute_lane(uint32_t v, uint32_t src_lane) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
-}
-
 // LZ4 length extension from the register vector; long runs (> 32 bytes of 255s) fall back
 // to the 64-byte ballot scan.
 __device__ __forceinline__ bool ext_len(State& s, uint8_t* win, SVec& sv, uint32_t& len) {
@@ -101,91 +97,91 @@ __device__ __forceinline__ bool ext_len(State& s, uint8_t* win, SVec& sv, uint32
 
 
 // The batch's token walk: from lane 0, follow the chain of candidate tokens while each
-// sequence is eligible and fits in lim (<= 128) output bytes; each sequence's record (pr of
-// its token lane) is dropped into the lane of its first output byte (v_writelane), in v0
-// for sequences starting in the first half (output bytes 0..63), in v1 for the second
-// (64..127; the lane select is m0 mod 64).  Written out because the scalar chain is the
-// batch's bound (one SALU per SIMD every 4 cycles, shared by the CU).  Lane 63 is a sentinel
-// that never qualifies, so "the next token lies past the parsed lanes" needs no compare of
-// its own: pw = next lane clamped to 63 (bits 0..5) | output length (bits 6..13, 255: not
-// eligible) | unclamped next lane (bits 24..30: the stream advance when the walk ends after
-// this sequence).  The room is kept as a remainder (one s_sub_u32 both subtracts and tests:
-// its borrow is "does not fit"), the word read is itself the next lane select (v_readlane
-// takes the low 6 bits of its lane-select SGPR; >= 4 instructions separate each VALU write of
-// e / e2 from its use as a lane select), each loop is unrolled twice: 3 SALU + 3 VALU per
-// sequence.  Phase A's room ends at byte 64, so its loop never tests the half; the sequence
-// that crosses byte 64 (or starts at it) is placed once by the hand-over code, then phase B
-// runs with the whole room.  `adv` = the stream bytes consumed.
-__device__ __forceinline__ uint32_t walk_tokens2h(uint32_t pw, uint32_t pr, uint32_t lim,
-                                                  uint32_t& adv, uint32_t& v0, uint32_t& v1) {
-  uint32_t out, e, e2, r, ol, rem, m0_saved;
+// sequence is eligible and fits in lim (<= 128) output bytes, and mark the lane of each
+// sequence's first output byte with the sequence's token lane (v_writelane), in v0 for
+// sequences starting in the first half (output bytes 0..63), in v1 for the second (64..127;
+// the lane select is m0 mod 64).  Written out because the scalar chain is the batch's bound
+// (one SALU per SIMD every 4 cycles, shared by the CU).  pw = next lane clamped to 63 (bits
+// 0..5) | output length (bits 6..13, 255: not eligible) | kWordTag (bit 20: a written word
+// is never 0) | unclamped next lane (bits 24..30: the stream advance when the walk ends after
+// this sequence).  The word of the sequence before is what is written: its bits 0..5 are
+// this sequence's token lane (the first sequence's "word before" is kWordTag alone: lane 0,
+// advance 0), so the walk reads one word per sequence and the records stay in their token
+// lanes.  Lane 63 is a sentinel that never qualifies, so "the next token lies past the
+// parsed lanes" needs no compare of its own.  The room is kept as a remainder (one s_sub_u32
+// both subtracts and tests: its borrow is "does not fit"), the word read is itself the next
+// lane select (v_readlane takes the low 6 bits of its lane-select SGPR; >= 4 instructions
+// separate each VALU write of e / e2 from its use as a lane select), each loop is unrolled
+// twice: 3 SALU + 2 VALU per sequence.  Phase A's room ends at byte 64, so its loop never
+// tests the half; the sequence that crosses byte 64 (or starts at it) is placed once by the
+// hand-over code, then phase B runs with the whole room.  `adv` = the stream bytes consumed.
+constexpr uint32_t kWordTag = 1u << 20;
+__device__ __forceinline__ uint32_t walk_tokens2h(uint32_t pw, uint32_t lim, uint32_t& adv,
+                                                  uint32_t& v0, uint32_t& v1) {
+  uint32_t out, e, e2, ol, rem, m0_saved;
   __asm__ volatile(
       "s_mov_b32 %[m0s], m0\n"
-      "s_mov_b32 %[e], 0\n"
+      "s_mov_b32 %[e], %[tag]\n"
       "s_mov_b32 %[e2], 0\n"
       "s_min_u32 %[rem], %[lim], 64\n"
       "s_mov_b32 m0, 0\n"
       // phase A: sequences ending at or before byte 64 (or lim)
       "L_a_%=:\n"
       "v_readlane_b32 %[e2], %[pw], %[e]\n"
-      "v_readlane_b32 %[r], %[pr], %[e]\n"
       "s_bfe_u32 %[ol], %[e2], 0x80006\n"
       "s_sub_u32 %[rem], %[rem], %[ol]\n"
       "s_cbranch_scc1 L_xa_%=\n"
-      "v_writelane_b32 %[v0], %[r], m0\n"
+      "v_writelane_b32 %[v0], %[e], m0\n"
       "s_add_u32 m0, m0, %[ol]\n"
       "v_readlane_b32 %[e], %[pw], %[e2]\n"
-      "v_readlane_b32 %[r], %[pr], %[e2]\n"
       "s_bfe_u32 %[ol], %[e], 0x80006\n"
       "s_sub_u32 %[rem], %[rem], %[ol]\n"
       "s_cbranch_scc1 L_xb_%=\n"
-      "v_writelane_b32 %[v0], %[r], m0\n"
+      "v_writelane_b32 %[v0], %[e2], m0\n"
       "s_add_u32 m0, m0, %[ol]\n"
       "s_branch L_a_%=\n"
-      // hand-over, failing word in e2 (last consumed: e): fits the whole room?
+      // hand-over, failing word in e2 (word before: e): fits the whole room?
       "L_xa_%=:\n"
       "s_sub_u32 %[rem], %[lim], m0\n"
       "s_sub_u32 %[rem], %[rem], %[ol]\n"
       "s_cbranch_scc1 L_da_%=\n"
       "s_cmp_lt_u32 m0, 64\n"
       "s_cbranch_scc0 L_xa1_%=\n"
-      "v_writelane_b32 %[v0], %[r], m0\n"
+      "v_writelane_b32 %[v0], %[e], m0\n"
       "s_add_u32 m0, m0, %[ol]\n"
       "s_branch L_b_%=\n"
       "L_xa1_%=:\n"
-      "v_writelane_b32 %[v1], %[r], m0\n"
+      "v_writelane_b32 %[v1], %[e], m0\n"
       "s_add_u32 m0, m0, %[ol]\n"
       "s_branch L_b_%=\n"
-      // hand-over, failing word in e (last consumed: e2)
+      // hand-over, failing word in e (word before: e2)
       "L_xb_%=:\n"
       "s_sub_u32 %[rem], %[lim], m0\n"
       "s_sub_u32 %[rem], %[rem], %[ol]\n"
       "s_cbranch_scc1 L_db_%=\n"
       "s_cmp_lt_u32 m0, 64\n"
       "s_cbranch_scc0 L_xb1_%=\n"
-      "v_writelane_b32 %[v0], %[r], m0\n"
+      "v_writelane_b32 %[v0], %[e2], m0\n"
       "s_add_u32 m0, m0, %[ol]\n"
       "s_branch L_b2_%=\n"
       "L_xb1_%=:\n"
-      "v_writelane_b32 %[v1], %[r], m0\n"
+      "v_writelane_b32 %[v1], %[e2], m0\n"
       "s_add_u32 m0, m0, %[ol]\n"
       "s_branch L_b2_%=\n"
       // phase B: every later sequence starts past byte 64
       "L_b_%=:\n"
       "v_readlane_b32 %[e], %[pw], %[e2]\n"
-      "v_readlane_b32 %[r], %[pr], %[e2]\n"
       "s_bfe_u32 %[ol], %[e], 0x80006\n"
       "s_sub_u32 %[rem], %[rem], %[ol]\n"
       "s_cbranch_scc1 L_db_%=\n"
-      "v_writelane_b32 %[v1], %[r], m0\n"
+      "v_writelane_b32 %[v1], %[e2], m0\n"
       "s_add_u32 m0, m0, %[ol]\n"
       "L_b2_%=:\n"
       "v_readlane_b32 %[e2], %[pw], %[e]\n"
-      "v_readlane_b32 %[r], %[pr], %[e]\n"
       "s_bfe_u32 %[ol], %[e2], 0x80006\n"
       "s_sub_u32 %[rem], %[rem], %[ol]\n"
       "s_cbranch_scc1 L_da_%=\n"
-      "v_writelane_b32 %[v1], %[r], m0\n"
+      "v_writelane_b32 %[v1], %[e], m0\n"
       "s_add_u32 m0, m0, %[ol]\n"
       "s_branch L_b_%=\n"
       "L_da_%=:\n"
@@ -196,9 +192,9 @@ __device__ __forceinline__ uint32_t walk_tokens2h(uint32_t pw, uint32_t pr, uint
       "L_out_%=:\n"
       "s_mov_b32 %[out], m0\n"
       "s_mov_b32 m0, %[m0s]\n"
-      : [e] "=&s"(e), [e2] "=&s"(e2), [out] "=&s"(out), [r] "=&s"(r), [ol] "=&s"(ol),
-        [rem] "=&s"(rem), [m0s] "=&s"(m0_saved), [v0] "+v"(v0), [v1] "+v"(v1)
-      : [pw] "v"(pw), [pr] "v"(pr), [lim] "s"(lim)
+      : [e] "=&s"(e), [e2] "=&s"(e2), [out] "=&s"(out), [ol] "=&s"(ol), [rem] "=&s"(rem),
+        [m0s] "=&s"(m0_saved), [v0] "+v"(v0), [v1] "+v"(v1)
+      : [pw] "v"(pw), [lim] "s"(lim), [tag] "i"(kWordTag)
       : "scc");
   adv = e;
   return out;
@@ -292,31 +288,29 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const uint32_t coff = cb0 | (cb1 << 8);
       const uint32_t cml = 4 + (mx ? 15u + b2 : cm4);
       const uint32_t colen = cL + cml;
-      // eligible: at most one length byte each (< 255), <= 64 output bytes (so <= 60 literals),
+      // eligible: <= 64 output bytes (so <= 60 literals; a length byte of 255, which would
+      // continue the length, makes colen >= 274, so this also means "one length byte each"),
       // a real offset (within the ring, or any distance in a FAR batch: far sources are read
       // back from HBM below), not before the segment start (conservatively, as if this token
       // opened the batch)
       // bitwise on the compares: short-circuit forms compile to an exec-mask branch
-      const bool cfar = ((!lx) | (b1 < 255u)) & ((!mx) | (b2 < 255u)) & (colen <= kSeqOut) &
-                        (coff != 0) & (coff <= s.op + cL);
+      const bool cfar = (colen <= kSeqOut) & (coff - 1u < s.op + cL);
       const bool csimple = cfar && (FAR || coff <= kNearOff);
-      // walk record: next token lane (7 bits, <= 127 for an eligible token, see
+      // walk word: next token lane (7 bits, <= 127 for an eligible token, see
       // kMaxEligibleNext; the walk stops at a lane >= 64, which was not parsed, after
       // consuming the sequence) | output length (255: not eligible, the walk's one compare
       // then stops; an ineligible token's wider nxt only ORs into those already-set bits).
-      // Sequence record: offset mod 4096 (12 bits) | literal count (6 bits) | token lane (6
-      // bits) -- the output start goes into bits 24..29 after the walk; offsets >= 4096 (FAR
-      // batches) get their high bits from the token lane below.
+      // Sequence record (stays in the token lane): offset (16 bits) | literal count.
       const uint32_t nxt = lane + 3 + (lx ? 1u : 0u) + (mx ? 1u : 0u) + cL;
-      const uint32_t pr = (coff & 4095u) | ((cL & 63u) << 12) | (lane << 18);
+      const uint32_t pr = coff | (cL << 16);
       // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
       const uint32_t room = s.cap - s.op;
       const uint32_t lim = room < kBatchOut ? room : kBatchOut;
       uint32_t k, vrec0 = 0, vrec1 = 0;
       const bool celig = csimple && lane < kWave - 1;  // lane 63: the walk's sentinel
       const uint32_t pw = (nxt < kWave - 1 ? nxt : kWave - 1) | ((celig ? colen : 255u) << 6) |
-                          (nxt << 24);
-      const uint32_t out = walk_tokens2h(pw, pr, lim, k, vrec0, vrec1);
+                          kWordTag | (nxt << 24);
+      const uint32_t out = walk_tokens2h(pw, lim, k, vrec0, vrec1);
       if (out == 0) {
         // the first token qualifies only for a FAR batch: worth trying one
         if (!FAR) want_far = (ballot(cfar) & 1ull) != 0;
@@ -327,7 +321,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       constexpr bool big = FAR;
       if (big) stay_far = false;
       // (3)+(4) for the output bytes 64h .. 64h+63 (lane t: byte 64h + t); `key` is the
-      // byte's sequence record with its output start in bits 24..30
+      // byte's sequence: its token lane (bits 0..5) and output start (bits 24..30)
       auto half = [&](auto h_tag, uint32_t key) __attribute__((always_inline)) {
         constexpr uint32_t H = decltype(h_tag)::value;
         const uint32_t q = lane + H * kWave;  // output byte of this lane (vs op)
@@ -337,10 +331,12 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         // an LDS byte address.  Bytes of the first half are in the ring already when the
         // second half reads them.
         const uint32_t ostart = key >> 24;
-        const uint32_t seqlane = (key >> 18) & 63u;
-        const uint32_t jL = (key >> 12) & 63u;
-        uint32_t joff = key & 4095u;
-        if (big) joff |= bpermute_lane(coff & ~4095u, seqlane);  // offsets >= 4096
+        const uint32_t seqlane = key & 63u;
+        // the record from its token lane (ds_bpermute reads address bits 2..7 only)
+        const uint32_t rec =
+            (uint32_t)__builtin_amdgcn_ds_bpermute((int)(key << 2), (int)pr);
+        const uint32_t jL = rec >> 16;
+        const uint32_t joff = rec & 0xFFFFu;
         const uint32_t r = q - ostart;  // < kSeqOut: a sequence is at most 64 bytes
         const bool is_lit = r < jL;
         const uint32_t m = r - jL;
@@ -363,12 +359,25 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         st = is_lit ? lit_a : st;
         if (big && srel < -(int32_t)kNearOff && !is_lit)
           st = (s.op + (uint32_t)srel) | 0x40000000u;  // far: the output position
-        // pointer doubling until no byte of the half aliases another (chains strictly
-        // descend; the source lane is srel mod 64)
-        const uint64_t live = ballot(q < out);  // (a VALU compare, not 5 SALU)
-        while (ballot((int32_t)st < 0) & live) {
-          const uint32_t other = bpermute_lane(st, st & 63u);
-          st = (st & 0x80000000u) ? other : st;
+        // pointer doubling until no byte of the half aliases another: every alias chain
+        // strictly descends (srel <= q - 1, past-the-end bytes included), so <= 6 rounds
+        // (written out: the compiler's form of this loop spends three branches on the
+        // usual zero rounds; ds_bpermute reads its lane from address bits 2..7 only)
+        {
+          uint32_t a, o;
+          __asm__ volatile(
+              "L_dbl_%=:\n"
+              "v_cmp_gt_i32_e32 vcc, 0, %[st]\n"
+              "s_cbranch_vccz L_dbe_%=\n"
+              "v_lshlrev_b32_e32 %[a], 2, %[st]\n"
+              "ds_bpermute_b32 %[o], %[a], %[st]\n"
+              "s_waitcnt lgkmcnt(0)\n"
+              "v_cndmask_b32_e32 %[st], %[st], %[o], vcc\n"
+              "s_branch L_dbl_%=\n"
+              "L_dbe_%=:\n"
+              : [st] "+v"(st), [a] "=&v"(a), [o] "=&v"(o)
+              :
+              : "vcc", "memory");
         }
         // one gather (LDS, or HBM for far history), one store
         lds_order();
@@ -388,11 +397,11 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         lds_order();
       };
       // every output byte takes the record of the latest sequence starting at or before it
-      const uint32_t key0 = wave_incl_max(vrec0 ? vrec0 | (lane << 24) : 0u);
+      const uint32_t key0 = wave_incl_max(vrec0 ? (vrec0 & 63u) | (lane << 24) : 0u);
       half(std::integral_constant<uint32_t, 0>{}, key0);
       if (out > kWave) {
         // second half: its own starts (all past byte 64), else the first half's last record
-        const uint32_t key1 = wave_incl_max(vrec1 ? vrec1 | ((lane + kWave) << 24) : 0u);
+        const uint32_t key1 = wave_incl_max(vrec1 ? (vrec1 & 63u) | ((lane + kWave) << 24) : 0u);
         const uint32_t carry = readlane(key0, kWave - 1);
         half(std::integral_constant<uint32_t, 1>{}, key1 > carry ? key1 : carry);
       }
