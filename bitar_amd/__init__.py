@@ -25,7 +25,10 @@ FLAG_INFLATE_WAVE_ONLY, FLAG_ZSTD_WAVE_ONLY, FLAG_ZSTD_LANE_EXEC, FLAG_COUNT_PAT
 # bitar_hip_path_counter indices
 PATHS = ("inflate_wave", "inflate_wave_reject", "inflate_batch_segs", "inflate_batches",
          "zstd_wave", "zstd_handed", "zstd_seqdec", "zstd_seqdec_reject", "zstd_exec",
-         "zstd_exec_reject", "lz4_far")
+         "zstd_exec_reject", "lz4_far",
+         # LZ4 batch diagnostics (a -DBITAR_LZ4D_PROFILE=1 build only)
+         "lz4_batches", "lz4_batch_bytes", "lz4_general_seqs", "lz4_stop_parse",
+         "lz4_stop_ineligible")
 PATH_COUNT = 16
 
 

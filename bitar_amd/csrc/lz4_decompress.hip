@@ -19,6 +19,12 @@
 
 #include <type_traits>
 
+// diagnostic build: count batches, their bytes, general-path sequences and why walks end
+// (BITAR_HIP_PATH_LZ4_* 11..15; costs a few SALU per batch, so off by default)
+#ifndef BITAR_LZ4D_PROFILE
+#define BITAR_LZ4D_PROFILE 0
+#endif
+
 namespace bitar_hip {
 
 
@@ -247,6 +253,8 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   const uint32_t base = (uint32_t)(uintptr_t)s.dst;  // ring index = absolute address & mask
   const uint32_t src_lo = (uint32_t)(uintptr_t)s.src;
   bool want_far = false, stay_far = false;
+  [[maybe_unused]] uint32_t p_batches = 0, p_bytes = 0, p_general = 0, p_stop_parse = 0,
+                            p_stop_inel = 0;
   while (ok) {
     // ---- batch fast path: up to kBatchOut output bytes of short sequences per step ------
     // 1. every lane l decodes "a token at stream position ip+l" from the LDS window
@@ -315,6 +323,12 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         // the first token qualifies only for a FAR batch: worth trying one
         if (!FAR) want_far = (ballot(cfar) & 1ull) != 0;
         return 0u;
+      }
+      if constexpr (BITAR_LZ4D_PROFILE != 0) {
+        p_batches += 1;
+        p_bytes += out;
+        if (k >= kWave - 1) p_stop_parse += 1;
+        else if ((readlane(pw, k) >> 6 & 255u) == 255u) p_stop_inel += 1;
       }
       // FAR batches (entered only where a near batch could not start: stock streams with
       // offsets beyond the ring's reach; ours stay <= 2560) read far history from HBM
@@ -443,6 +457,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     }
     if (!FARK && want_far) break;  // defer the segment to the FAR kernel
     // ---- general path: one sequence, any shape -----------------------------------------
+    if constexpr (BITAR_LZ4D_PROFILE != 0) p_general += 1;
     if (s.ip >= s.csize) { ok = false; break; }
     const uint32_t token = sv.get(s, win, s.ip);
     s.ip += 1;
@@ -463,6 +478,15 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     m += 4;
     if ((uint64_t)s.op + m > s.cap) { ok = false; break; }
     match_copy(s, ring, off, m);
+  }
+  if constexpr (BITAR_LZ4D_PROFILE != 0) {
+    if (stats && lane_id() == 0) {
+      atomicAdd(stats + BITAR_HIP_PATH_LZ4_BATCHES, (unsigned long long)p_batches);
+      atomicAdd(stats + BITAR_HIP_PATH_LZ4_BATCH_BYTES, (unsigned long long)p_bytes);
+      atomicAdd(stats + BITAR_HIP_PATH_LZ4_GENERAL_SEQS, (unsigned long long)p_general);
+      atomicAdd(stats + BITAR_HIP_PATH_LZ4_STOP_PARSE, (unsigned long long)p_stop_parse);
+      atomicAdd(stats + BITAR_HIP_PATH_LZ4_STOP_INELIGIBLE, (unsigned long long)p_stop_inel);
+    }
   }
   if (!FARK && want_far) {
     if (lane_id() == 0) {

@@ -260,6 +260,15 @@ enum bitar_hip_path_counter {
   BITAR_HIP_PATH_ZSTD_EXEC = 8,          /* segments executed by zstd_exec_kernel */
   BITAR_HIP_PATH_ZSTD_EXEC_REJECT = 9,   /*   ... rejected there */
   BITAR_HIP_PATH_LZ4_FAR = 10,           /* segments deferred to the far-history LZ4 kernel */
+  /* 11..15: LZ4 batch-path diagnostics, filled only by a library built with
+     -DBITAR_LZ4D_PROFILE=1 (scripts/build_variant.sh): batches, their output bytes,
+     sequences decoded by the general path, batches whose walk ended at the parsed lanes'
+     end, batches whose walk ended at an ineligible sequence */
+  BITAR_HIP_PATH_LZ4_BATCHES = 11,
+  BITAR_HIP_PATH_LZ4_BATCH_BYTES = 12,
+  BITAR_HIP_PATH_LZ4_GENERAL_SEQS = 13,
+  BITAR_HIP_PATH_LZ4_STOP_PARSE = 14,
+  BITAR_HIP_PATH_LZ4_STOP_INELIGIBLE = 15,
   BITAR_HIP_PATH_COUNT = 16
 };
 
