@@ -23,7 +23,28 @@ namespace bitar_hip {
 namespace cmp {
 
 // ---- LZ4 emitter ---------------------------------------------------------------------
-struct Lz4Out : ByteOut {
+// m's bit for this lane ? a : b (m an SGPR pair used directly as the lane mask)
+__device__ __forceinline__ uint32_t lane_sel(uint64_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  __asm__("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+  return r;
+}
+// LDS of the LZ4 emitter past its output ring: the spill area (a window writes at most
+// 269 + 64 literals and 17 sequence headers: unwrapped addresses reach kLz4Obuf - 1 + 421), the
+// trash bytes (lane + 0..2), and the literal bases by chain rank (kWave dwords, then one
+// trash dword every other lane writes: a per-lane one measured slower, more LDS)
+// The output ring is 512 B (1 KiB before the round-3 emitter: the smaller LDS footprint
+// measured 2-3 % faster than the same emitter on 1 KiB; the flushes stay per input row).
+#ifndef BITAR_CMP_LZ4_OBUF
+#define BITAR_CMP_LZ4_OBUF 512
+#endif
+constexpr uint32_t kLz4Obuf = BITAR_CMP_LZ4_OBUF;
+constexpr uint32_t kSpill = 448;
+constexpr uint32_t kTrash = kLz4Obuf + kSpill;
+constexpr uint32_t kLz4Lds = kLz4Obuf + kSpill + 80;  // bytes before the literal-base table
+
+struct Lz4Out : ByteOutT<kLz4Obuf> {
+  uint32_t* scr;  // literal bases by chain rank (LDS)
   __device__ __forceinline__ void put_ext(uint32_t v) {  // 255 ... 255, v % 255
     const uint32_t cnt = v / 255u + 1;
     for (uint32_t k = 0; k < cnt; k += kWave) {
@@ -74,26 +95,37 @@ struct Lz4Out : ByteOut {
   // input ring, every match < 274 bytes: at most one length byte each): each match lane
   // writes its header bytes and each literal lane its own byte, all lanes at once, at
   // offsets from a prefix sum of the sequence sizes.
+  //
+  // Addresses are relative to the ring index of op WITHOUT wrapping (at most ~420 bytes per
+  // window land past the ring's end, in the spill area, and are copied back to the ring's
+  // head afterwards), so a sequence's five header bytes take one address and immediate
+  // offsets.  A header byte a sequence does not have (no literal-length / match-length byte)
+  // is written anyway, before the bytes that overwrite its position: the first literal or the
+  // offset, and the next sequence's token.  Lanes with nothing to write use the trash bytes.
+  // A literal lane finds its sequence's literal base in LDS, written there by the sequence's
+  // match lane at its rank among the window's match lanes (v_mbcnt), which is also the
+  // literal lane's own rank.
   __device__ __forceinline__ void window(const GMEM uint8_t* in, const InRing& I, const Window& W,
                                          uint32_t anchor, uint32_t) {
     if (!W.chain || overflow) return;
     const uint32_t lane = lane_id();
     const uint32_t q = W.x + lane;
-    const bool cl = (W.chain >> lane) & 1;
+    const uint64_t chain = W.chain;
     // match ends increase along the chain, so "end of the previous match" is a prefix max
-    const uint32_t end_incl = wave_incl_max(cl ? q + W.mlen : 0u);
+    const uint32_t end_incl = wave_incl_max(lane_sel(chain, q + W.mlen, 0u));
     const uint32_t end_excl = wave_shr1(end_incl);
-    const uint32_t lit_start = max(anchor, cl ? end_excl : end_incl);
+    const uint32_t lit_start = max(anchor, lane_sel(chain, end_excl, end_incl));
     const uint32_t lit_len = q - lit_start;  // chain lanes: their literal run
     const uint32_t ml = W.mlen - kMinMatch;
     const uint32_t nlx = lit_len >= 15 ? 1u : 0u, nmx = ml >= 15 ? 1u : 0u;
-    const uint32_t e = cl ? 1 + nlx + lit_len + 2 + nmx : 0u;
+    const uint32_t hoff = 1 + nlx + lit_len;  // chain lanes: the offset, vs the token
+    const uint32_t e = lane_sel(chain, hoff + 2 + nmx, 0u);
     const uint32_t incl = wave_incl_sum(e);
     const uint32_t total = readlane(incl, 63);
-    if (((ballot(lit_len >= 270) | ballot(ml >= 270)) & W.chain) || anchor < I.lo ||
+    if (((ballot(lit_len >= 270) | ballot(ml >= 270)) & chain) || anchor < I.lo ||
         (uint64_t)op + total > cap) {
       // general path, one sequence at a time
-      uint64_t m = W.chain;
+      uint64_t m = chain;
       uint32_t a = anchor;
       while (m) {
         const uint32_t l = (uint32_t)__builtin_ctzll(m);
@@ -105,34 +137,41 @@ struct Lz4Out : ByteOut {
       return;
     }
     room(total);
-    // A literal lane (not a match start, not inside a match) belongs to the sequence of the
-    // lowest chain lane s above it: that sequence starts at op + incl (no chain lane lies
-    // between), its literal run at lit_start (= this lane's prefix max), and its token is
-    // followed by one length byte if the run is >= 15 bytes.
-    const uint64_t above = lane == 63 ? 0ull : W.chain & (~0ull << (lane + 1));
-    const uint32_t s = lowbit(above);
-    const bool lit = !cl && above && q >= lit_start;
-    const uint32_t lit_nlx = W.x + s - lit_start >= 15 ? 1u : 0u;
-    const uint32_t o = op + incl - e;  // chain lanes: sequence start
-    // every lane stores every byte kind; lanes without one store into their trash byte
-    // past the ring (no exec-mask branches)
-    const uint32_t tr = kObuf + lane;
-    const uint32_t h = o + 1 + nlx + lit_len;
+    const uint32_t base = at(op);  // unwrapped addresses from here: base + [0, total)
+    // chain lanes: token at a, literal-length byte at a + 1, literals, offset at h, h + 1,
+    // match-length byte at h + 2; other lanes write into the trash bytes
+    const uint32_t a = lane_sel(chain, base + incl - e, kTrash + lane);
+    const uint32_t h = a + lane_sel(chain, hoff, 0u);
     lds_order();
-    ring[cl ? at(o) : tr] = (uint8_t)(((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15));
-    ring[cl && nlx ? at(o + 1) : tr] = (uint8_t)(lit_len - 15);
-    ring[cl ? at(h) : tr] = (uint8_t)W.off;
-    ring[cl ? at(h + 1) : tr] = (uint8_t)(W.off >> 8);
-    ring[cl && nmx ? at(h + 2) : tr] = (uint8_t)(ml - 15);
-    ring[lit ? at(op + incl + 1 + lit_nlx + (q - lit_start)) : tr] = (uint8_t)W.byte;
+    ring[h + 2] = (uint8_t)(ml - 15);       // (no such byte: the next token overwrites it)
+    ring[a + 1] = (uint8_t)(lit_len - 15);  // (no such byte: a literal or the offset does)
+    ring[a] = (uint8_t)(((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15));
+    ring[h] = (uint8_t)W.off;
+    ring[h + 1] = (uint8_t)(W.off >> 8);
+    // a literal lane (not a match start, not inside a match) belongs to the sequence of the
+    // lowest chain lane above it, whose rank among the chain lanes equals its own
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)chain, 0u));
+    const uint32_t nch = (uint32_t)__builtin_popcountll(chain);
+    scr[lane_sel(chain, rank, kWave)] = a + 1 + nlx - lit_start;  // (kWave: trash slot)
+    lds_order();
+    const uint64_t litm = ~chain & ballot(rank < nch) & ballot(q >= lit_start);
+    ring[lane_sel(litm, scr[rank] + q, kTrash + lane)] = (uint8_t)W.byte;
     // literals of the first sequence that precede the window (anchor < x): from the ring
     if (anchor < W.x) {
-      const uint32_t l0 = lowbit(W.chain);
-      const uint32_t d0 = op + 1 + (W.x + l0 - anchor >= 15 ? 1u : 0u) - anchor;
+      const uint32_t l0 = lowbit(chain);
+      const uint32_t d0 = base + 1 + (W.x + l0 - anchor >= 15 ? 1u : 0u) - anchor;
       for (uint32_t k = anchor; k < W.x; k += kWave) {
         const uint32_t qq = k + lane;
-        if (qq < W.x) ring[at(d0 + qq)] = (uint8_t)I.byte(qq);
+        if (qq < W.x) ring[d0 + qq] = (uint8_t)I.byte(qq);
       }
+    }
+    // bytes that went past the ring's end belong at its head
+    if (base + total > kLz4Obuf) {
+      lds_order();
+      const uint32_t nd = (base + total - kLz4Obuf + 3) / 4;
+      uint32_t* r32 = reinterpret_cast<uint32_t*>(ring);
+      for (uint32_t k = lane; k < nd; k += kWave) r32[k] = r32[kLz4Obuf / 4 + k];
     }
     lds_order();
     op += total;
@@ -269,13 +308,14 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   // (+ one trash entry: probe lanes past the segment insert there, see parse)
   __shared__ __attribute__((aligned(16))) uint16_t table[(1u << HLOG) + 8];
   __shared__ __attribute__((aligned(16))) uint8_t inring[RING + kInPad];
-  __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];  // + trash bytes
+  __shared__ __attribute__((aligned(16))) uint8_t obuf[kLz4Lds + 4 * (kWave + 4)];
   const uint32_t i_seg = blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
   Lz4Out o;
   o.ring = obuf;
+  o.scr = reinterpret_cast<uint32_t*>(obuf + kLz4Lds);
   o.dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
   o.cap = slot_stride;
   o.op = 0;

@@ -157,15 +157,17 @@ struct Window {
 // ---- byte output staged in an LDS ring, flushed in aligned 16-B blocks ----------------
 constexpr uint32_t kObuf = BITAR_CMP_OBUF, kObufMask = kObuf - 1;
 
-struct ByteOut {
-  uint8_t* ring;      // LDS, kObuf bytes + one trash byte per lane
+template <uint32_t OB = kObuf>
+struct ByteOutT {
+  static constexpr uint32_t kSize = OB, kMask = OB - 1;
+  uint8_t* ring;      // LDS, OB bytes + one trash byte per lane
   GMEM uint8_t* dst;  // slot
   uint64_t cap;
   uint32_t op, flushed;
   bool overflow;
 
   __device__ __forceinline__ uint32_t at(uint32_t k) const {
-    return ((uint32_t)(uintptr_t)dst + k) & kObufMask;
+    return ((uint32_t)(uintptr_t)dst + k) & kMask;
   }
   __device__ __forceinline__ void flush(uint32_t upto, bool final) {
     const uint32_t lane = lane_id();
@@ -196,7 +198,7 @@ struct ByteOut {
   }
   __device__ __forceinline__ bool room(uint32_t n) {
     if ((uint64_t)op + n > cap) { overflow = true; return false; }
-    if (op + n - flushed > kObuf - 64) flush(op, false);
+    if (op + n - flushed > OB - 64) flush(op, false);
     return true;
   }
   // lanes < n write byte `v` at op + lane
@@ -207,6 +209,7 @@ struct ByteOut {
     op += n;
   }
 };
+using ByteOut = ByteOutT<>;
 
 // The greedy chain's common step, written out (the parse is bound by scalar issue: the SQ
 // issues one SALU per SIMD every 4 cycles): from the non-empty lane set m, take the first
