@@ -162,6 +162,20 @@ struct QueuePairMemory {
   std::vector<std::uint64_t> checksums;  // of the last call
   void* d_chain = nullptr;  // chained ops (max_sgl_segs > 1): one stream per op
   std::uint64_t chain_cap = 0;
+  // what d_ptrs[0, ptr_mirror.size()) holds: a steady-state caller gets its slots back in the
+  // same order every call (LIFO pool, Recycle last to first), so the slot-pointer table of a
+  // compress call -- and of the decompress call over those slots -- is usually already on the
+  // device and its copy is skipped
+  std::vector<std::uint64_t> ptr_mirror;
+
+  // d_ptrs[0, n) <- h_ptrs[0, n) on the queue pair's stream, unless d_ptrs already holds them
+  int UploadPtrs(std::uint32_t n) {
+    if (ptr_mirror.size() >= n && std::memcmp(ptr_mirror.data(), h_ptrs, 8ull * n) == 0) return 0;
+    const int rc = bitar_hip_memcpy(ctx, d_ptrs, h_ptrs, 8ull * n, stream);
+    if (rc == 0) ptr_mirror.assign(h_ptrs, h_ptrs + n);
+    else ptr_mirror.clear();
+    return rc;
+  }
 
   ~QueuePairMemory() {
     if (!ctx) return;
@@ -217,6 +231,7 @@ struct QueuePairMemory {
     d_sizes = nullptr;
     d_prod = nullptr;
     table_cap = 0;
+    ptr_mirror.clear();
     void* p = nullptr;
     BITAR_ABI(bitar_hip_host_alloc(ctx, cap * 8, &p), "qp tables");
     h_ptrs = static_cast<std::uint64_t*>(p);
@@ -383,6 +398,7 @@ arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
     return st;
   };
   auto failed = [&](int rc) {
+    m->ptr_mirror.clear();  // (a failed stream: the table's copy may not have landed)
     return release(internal::FromAbi(
         rc, "Failed to compress via queue pair " + std::to_string(queue_pair_id) +
                 " of compress device " + std::to_string(device_id_)));
@@ -402,7 +418,7 @@ arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
   if (k == 1) {
     for (std::uint32_t i = 0; i < nseg; ++i)
       m->h_ptrs[i] = static_cast<std::uint64_t>(reinterpret_cast<uintptr_t>(slots[i]));
-    rc = bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 8ull * nseg, m->stream);
+    rc = m->UploadPtrs(nseg);
     if (rc == 0)
       rc = bitar_hip_compress_scattered(ctx_, m->stream, codec, d_in, n, seg,
                                         reinterpret_cast<void* const*>(m->d_ptrs), slot_size_,
@@ -461,6 +477,7 @@ arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
     m->h_sizes[nops + e] = piece[i];
     ++e;
   }
+  m->ptr_mirror.clear();
   rc = bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 16ull * nseg, m->stream);
   if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->d_sizes, m->h_sizes + nops, 4ull * e, m->stream);
   if (rc == 0)
@@ -538,7 +555,7 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
   std::uint32_t nunits = nseg;  // ops, one produced size / checksum each
   std::uint64_t unit = seg;
   if (k == 1) {
-    BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 8ull * nseg, m->stream), "tables");
+    BITAR_ABI(m->UploadPtrs(nseg), "tables");
     BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_sizes, m->h_sizes, 4ull * nseg, m->stream), "tables");
     rc = bitar_hip_decompress(ctx_, m->stream, codec,
                               reinterpret_cast<const void* const*>(m->d_ptrs), m->d_sizes, nseg,
@@ -568,6 +585,7 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
         at += m->h_sizes[i];
       }
     }
+    m->ptr_mirror.clear();
     BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_ptrs, m->h_ptrs, 8ull * (2ull * nseg + nops), m->stream),
               "tables");
     BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_sizes, m->h_sizes, 4ull * (nseg + nops), m->stream),
@@ -599,6 +617,7 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
   if (rc == 0) rc = bitar_hip_sync(ctx_, m->stream);
   if (rc == 0) m->checksums.assign(m->h_sums, ck ? m->h_sums + nunits : m->h_sums);
   if (rc != 0) {
+    m->ptr_mirror.clear();
     return internal::FromAbi(rc, "Failed to decompress via queue pair " +
                                      std::to_string(queue_pair_id) + " of compress device " +
                                      std::to_string(device_id_));
