@@ -15,6 +15,7 @@
 
 #include "../../include/bitar_hip.h"
 #include "zstd_hand.hip.h"
+#include "zstd_layout.hip.h"
 
 namespace bitar_hip {
 template <uint32_t RING, uint32_t HLOG>
@@ -389,10 +390,10 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
     // pass 1 (parse -> literals + sequence records) and pass 2 (entropy coding) through a
     // stream-ordered scratch: per segment the literal area + records (zstd_compress.hip),
     // then {nlit, nseq} per segment
-    const uint64_t scr_stride = ((uint64_t)seg + 15u & ~15ull) + 8ull * (seg / 4u + 2u) + 255u & ~255ull;
-    // + the chain-walk scratch (zstd_compress.hip walk_stride: a 3400-byte header with the
-    // tables, then 10 bytes per sequence)
-    const uint64_t w_stride = (3400ull + 10ull * (seg / 4u + 2u) + 255u) & ~255ull;
+    const uint64_t scr_stride = bitar_hip::zse::scratch_stride(seg);
+    // + the chain-walk scratch (zstd_layout.hip.h: a 3400-byte header with the tables, then
+    // 10 bytes per sequence and 12 per step of 64 sequences)
+    const uint64_t w_stride = bitar_hip::zse::walk_stride(seg);
     const Chunks ch(nseg);
     void* scratch = nullptr;
     HIP_TRY(hipMallocAsync(&scratch, ch.size * (scr_stride + 8u + w_stride), s),

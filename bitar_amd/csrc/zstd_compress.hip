@@ -18,6 +18,7 @@
 //                        sequence bitstream, each lane placing its bit field by a prefix
 //                        sum into the LDS output ring.
 #include "huffman.hip.h"
+#include "zstd_layout.hip.h"
 #include "window_parse.hip.h"
 
 namespace bitar_hip {
@@ -107,23 +108,7 @@ __device__ __forceinline__ uint32_t ml_code(uint32_t ml) {  // ml >= 3
   return b < 128 ? sT.ml_code[b] : hb32(b) + 36u;
 }
 
-// ---- scratch layout --------------------------------------------------------------------------
-__host__ __device__ constexpr uint64_t lit_cap(uint32_t seg) { return ((uint64_t)seg + 15u) & ~15ull; }
-__host__ __device__ constexpr uint64_t scratch_stride(uint32_t seg) {
-  return (lit_cap(seg) + 8ull * (seg / 4u + 2u) + 255u) & ~255ull;
-}
-
-// walk scratch (pass 2 -> zstd_walk_kernel -> zstd_emit_kernel), per segment: a 16-word record
-// (kW*), the FSE state tables (u16, kTabDummy + 1) and transforms (3 x 64 u32); then per
-// sequence its three codes (u32: LL | OF << 6 | ML << 11, written by pass 2) and each
-// chain's state bits | their count << 12 (u16, chains OF, ML, LL one array each)
-enum : uint32_t { kWHanded = 0, kWP0, kWBlk, kWN, kWNseq, kWAls, kWSt0, kWSt1, kWSt2 };
-constexpr uint32_t kWTabs = 64, kWTr = kWTabs + 2 * 1284, kWWords = kWTr + 3 * 64 * 4;
-static_assert(kWWords == 3400, "runtime.hip sizes the walk scratch with this header");
-__host__ __device__ constexpr uint32_t walk_cap(uint32_t seg) { return seg / 4u + 2u; }  // >= nseq
-__host__ __device__ constexpr uint64_t walk_stride(uint32_t seg) {
-  return ((uint64_t)kWWords + 10ull * walk_cap(seg) + 255u) & ~255ull;
-}
+// ---- scratch layout: zstd_layout.hip.h ------------------------------------------------------
 
 // ---- pass 1: the parse, literals + sequence records ---------------------------------------
 struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the literal area
@@ -187,6 +172,41 @@ struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the lit
     }
   }
 };
+
+// ---- repeat offsets (RFC 8878 3.1.2.5), 64 sequences per step ------------------------------
+// The offset value of each lane's sequence (distance o, literal length ll) from the history
+// {c0, c1, c2} before the step; the history after the step replaces c0..c2 (cnt = the
+// step's sequences).  Scanned lane-parallel: after sequence i, r0 = o_i; r1 = o_{j-1} for the
+// last j <= i that is not a plain repeat of r0 (ll_j > 0 && o_j == o_{j-1}); r2 = r1 before the
+// last k <= i that is neither such a repeat nor a repeat of r1 (prefix maxima + bpermute).
+// Every cross-lane op runs on all 64 lanes (a DPP or bpermute source lane that is off in
+// EXEC reads as 0).  Used by zstd_entropy_kernel (codes, histograms) and again by
+// zstd_emit_kernel (extra bits), so the records are never rewritten.
+__device__ __forceinline__ uint32_t rep_scan(uint32_t ll, uint32_t o, bool act, uint32_t cnt,
+                                             uint32_t& c0r, uint32_t& c1r, uint32_t& c2r) {
+  const uint32_t lane = lane_id();
+  const uint32_t so = wave_shr1(o);
+  const uint32_t oprev = lane == 0 ? c0r : so;                      // r0 before
+  const bool same = !act || (ll != 0 && o == oprev);
+  const uint32_t mj = wave_incl_max(same ? 0u : lane + 1);
+  const uint32_t p1 = bpermute(oprev, mj ? mj - 1 : 0u);
+  const uint32_t r1a = mj ? p1 : c1r;                               // r1 after
+  const uint32_t s1 = wave_shr1(r1a);
+  const uint32_t r1b = lane == 0 ? c1r : s1;                        // r1 before
+  const bool ev = !same && o != r1b;
+  const uint32_t mk = wave_incl_max(ev ? lane + 1 : 0u);
+  const uint32_t p2 = bpermute(r1b, mk ? mk - 1 : 0u);
+  const uint32_t r2a = mk ? p2 : c2r;                               // r2 after
+  const uint32_t s2 = wave_shr1(r2a);
+  const uint32_t r2b = lane == 0 ? c2r : s2;                        // r2 before
+  uint32_t ov;
+  if (ll) ov = o == oprev ? 1u : o == r1b ? 2u : o == r2b ? 3u : o + 3u;
+  else ov = o == r1b ? 1u : o == r2b ? 2u : o == oprev - 1u ? 3u : o + 3u;
+  c0r = readlane(o, cnt - 1);
+  c1r = readlane(r1a, cnt - 1);
+  c2r = readlane(r2a, cnt - 1);
+  return ov;
+}
 
 // ---- pass 2: entropy coding ------------------------------------------------------------------
 // FSE state tables in LDS: literal lengths at 0 (<= 512 states), offsets at 512 (<= 256),
@@ -800,16 +820,15 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     o.put(nh == 1 ? nseq : lane == 0 ? (nseq >> 8) + 128u : nseq & 0xFFu, nh);
   }
   if (nseq && !o.overflow) {
-    // repeat offsets (RFC 8878 3.1.2.5), codes, histograms; the records become {literal
-    // length | offset value << 17, match length}.  The history is scanned lane-parallel,
-    // 64 sequences per step: after sequence i, r0 = o_i; r1 = o_{j-1} for the last j <= i
-    // that is not a plain repeat of r0 (ll_j > 0 && o_j == o_{j-1}); r2 = r1 before the last
-    // k <= i that is neither such a repeat nor a repeat of r1 (prefix maxima + bpermute)
+    // repeat offsets (rep_scan), codes, histograms, 64 sequences per step; the history
+    // before each step goes to the walk scratch (the records stay as the parse wrote them)
     for (uint32_t k = lane; k < 3 * 64; k += kWave) (&L.sh[0][0])[k] = 0;
     lds_order();
     uint32_t c0r = 1, c1r = 4, c2r = 8;  // the history before the step (uniform)
     GMEM uint32_t* wcodes = reinterpret_cast<GMEM uint32_t*>(
         global_ptr(wscr + (uint64_t)i_seg * wstride + kWWords));
+    GMEM uint32_t* whist = reinterpret_cast<GMEM uint32_t*>(
+        global_ptr(wscr + (uint64_t)i_seg * wstride + walk_hist_at(seg)));
     uint2 nrec = lane < nseq ? seqs[lane] : make_uint2(0, 3);
     for (uint32_t c0 = 0; c0 < nseq; c0 += kWave) {
       const uint32_t j = c0 + lane;
@@ -818,34 +837,14 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       if (c0 + kWave + lane < nseq) nrec = seqs[c0 + kWave + lane];  // prefetch the next step
       const uint32_t ll = rec.x & 0x1FFFFu, o = rec.x >> 17, ml = rec.y;
       const uint32_t cnt = nseq - c0 < kWave ? nseq - c0 : kWave;
-      // (every cross-lane op runs on all 64 lanes: a DPP or bpermute source lane that is
-      // off in EXEC reads as 0)
-      const uint32_t so = wave_shr1(o);
-      const uint32_t oprev = lane == 0 ? c0r : so;                      // r0 before
-      const bool same = !act || (ll != 0 && o == oprev);
-      const uint32_t mj = wave_incl_max(same ? 0u : lane + 1);
-      const uint32_t p1 = bpermute(oprev, mj ? mj - 1 : 0u);
-      const uint32_t r1a = mj ? p1 : c1r;                               // r1 after
-      const uint32_t s1 = wave_shr1(r1a);
-      const uint32_t r1b = lane == 0 ? c1r : s1;                        // r1 before
-      const bool ev = !same && o != r1b;
-      const uint32_t mk = wave_incl_max(ev ? lane + 1 : 0u);
-      const uint32_t p2 = bpermute(r1b, mk ? mk - 1 : 0u);
-      const uint32_t r2a = mk ? p2 : c2r;                               // r2 after
-      const uint32_t s2 = wave_shr1(r2a);
-      const uint32_t r2b = lane == 0 ? c2r : s2;                        // r2 before
-      uint32_t ov;
-      if (ll) ov = o == oprev ? 1u : o == r1b ? 2u : o == r2b ? 3u : o + 3u;
-      else ov = o == r1b ? 1u : o == r2b ? 2u : o == oprev - 1u ? 3u : o + 3u;
-      c0r = readlane(o, cnt - 1);
-      c1r = readlane(r1a, cnt - 1);
-      c2r = readlane(r2a, cnt - 1);
+      // the history before this step, for zstd_emit_kernel's re-derivation of the step
+      if (lane < 3) whist[3 * (c0 >> 6) + lane] = lane == 0 ? c0r : lane == 1 ? c1r : c2r;
+      const uint32_t ov = rep_scan(ll, o, act, cnt, c0r, c1r, c2r);
       if (act) {
         const uint32_t llc = ll_code(ll), ofc = hb32(ov), mlc = ml_code(ml);
         atomicAdd(&L.sh[0][llc], 1u);
         atomicAdd(&L.sh[1][ofc], 1u);
         atomicAdd(&L.sh[2][mlc], 1u);
-        seqs[j] = make_uint2(ll | (ov << 17), ml);
         wcodes[j] = llc | (ofc << 6) | (mlc << 11);  // for zstd_walk_kernel
       }
     }
@@ -1036,6 +1035,7 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
       global_ptr(scratch + (uint64_t)i_seg * sstride + lit_cap(seg)));
   const uint32_t cap = walk_cap(seg);
   const GMEM uint16_t* outs = reinterpret_cast<const GMEM uint16_t*>(w + kWWords / 4 + cap);
+  const GMEM uint32_t* whist = w + walk_hist_at(seg) / 4;
   EntOut o;
   o.ring = obuf;
   o.dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
@@ -1062,7 +1062,12 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
       prec = seqs[(uint32_t)(c - 1) * kWave + lane];
       pw = word((uint32_t)(c - 1) * kWave + lane);
     }
-    const uint32_t ll = rec.x & 0x1FFFFu, ov = rec.x >> 17, mlb = rec.y - 3u;
+    // the step's offset values from the history before it (zstd_entropy_kernel's scan)
+    uint32_t h0 = uniform(whist[3 * (uint32_t)c]), h1 = uniform(whist[3 * (uint32_t)c + 1]),
+             h2 = uniform(whist[3 * (uint32_t)c + 2]);
+    const uint32_t cnt = nseq - (uint32_t)c * kWave < kWave ? nseq - (uint32_t)c * kWave : kWave;
+    const uint32_t ll = rec.x & 0x1FFFFu, mlb = rec.y - 3u;
+    const uint32_t ov = rep_scan(ll, rec.x >> 17, act, cnt, h0, h1, h2);
     const uint32_t llc = ll_code(ll), mlc = ml_code(rec.y), ofc = hb32(ov);
     const uint64_t stb = wd & 0x3FFFFFFu;
     const uint32_t stn = wd >> 26;
