@@ -25,7 +25,7 @@ __device__ __forceinline__ uint32_t bpermute_u32(uint32_t v, uint32_t src_lane) 
 }
 
 struct Tables {  // LDS
-  uint16_t lit_fast[1u << kLitFast];   // sym | len << 9  (0 = not a <= kLitFast-bit code)
+  uint16_t lit_fast[1u << kLitFast];   // lit_entry(sym, len) (0 = not a <= kLitFast-bit code)
   uint16_t dist_fast[1u << kDistFast];
   uint16_t cl_fast[1u << kClFast];
   uint16_t lit_count[16], dist_count[16], cl_count[16];
@@ -48,6 +48,26 @@ __device__ __forceinline__ uint32_t dist_extra(uint32_t ds) {  // 0..29
 }
 __device__ __forceinline__ uint32_t dist_base(uint32_t ds) {
   return ds < 4 ? ds + 1 : ((2 + (ds & 1u)) << dist_extra(ds)) + 1;
+}
+// A literal/length table entry, pre-decoded so the batch path's 256 candidates need no
+// symbol arithmetic: bits 9..12 the code length (0 on the slow path), bits 13..15 the kind --
+// 7 a literal (bits 0..7 the byte), 6 end of block or an invalid length symbol (bits 0..8 =
+// symbol - 256: 0, 30, 31), 0..5 a length symbol with that many extra bits (bits 0..8 its base
+// length, 3..258).  A fast entry is never 0 (its code length is not).  The distance and
+// code-length table keeps sym | len << 9.
+__device__ __forceinline__ uint32_t lit_entry(uint32_t sym, uint32_t l) {
+  if (sym < 256) return sym | (l << 9) | (7u << 13);
+  const uint32_t ls = sym - 257;
+  if (sym == 256 || ls >= 29) return (sym - 256) | (l << 9) | (6u << 13);
+  return len_base(ls) | (l << 9) | (len_extra(ls) << 13);
+}
+// A distance table entry: bits 0..4 the symbol, 5..8 its extra-bit count, 9..12 the code
+// length, 13..14 m, the base being (m << extra) + 1 (m = the symbol below 4, else 2 | its low
+// bit).
+__device__ __forceinline__ uint32_t dist_entry(uint32_t ds, uint32_t l) {
+  const uint32_t de = ds < 30 ? dist_extra(ds) : 0u;
+  const uint32_t m = ds < 4 ? ds : 2u | (ds & 1u);
+  return ds | (de << 5) | (l << 9) | (m << 13);
 }
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
@@ -136,7 +156,7 @@ __device__ __forceinline__ bool take(State& s, uint8_t* win, Bits& b, uint32_t n
 // Inlined (at two sites): an out-of-line call would make every value live across it --
 // the bit reader's state included -- sit in callee-saved VGPRs for the whole kernel.
 __device__ __forceinline__ bool build(Tables& t, const uint8_t* lens, uint32_t n, uint16_t* fast, uint32_t fbits,
-                      uint16_t* count, uint16_t* sym) {
+                      uint16_t* count, uint16_t* sym, uint32_t kind = 0) {
   const uint32_t lane = lane_id();
   lds_order();
   if (lane < 16) t.base[lane] = 0;
@@ -192,7 +212,9 @@ __device__ __forceinline__ bool build(Tables& t, const uint8_t* lens, uint32_t n
       const uint32_t c = nc + (myidx - first);
       if (l <= fbits) {
         const uint32_t r = __builtin_bitreverse32(c) >> (32 - l);
-        const uint16_t e = (uint16_t)(k | (l << 9));
+        // (kind 1: the literal/length table, 2: the distance table, 0: code lengths)
+        const uint16_t e = (uint16_t)(kind == 1 ? lit_entry(k, l) : kind == 2 ? dist_entry(k, l)
+                                                                            : k | (l << 9));
         for (uint32_t j = r; j < (1u << fbits); j += (1u << l)) fast[j] = e;
       }
     }
@@ -246,7 +268,7 @@ __device__ __forceinline__ uint32_t reg_entry(const uint32_t (&r)[N], uint32_t i
 __device__ __forceinline__ int decode_entry(State& s, Bits& b, uint32_t e, const uint16_t* count,
                                             const uint16_t* sym) {
   if (e) {
-    const uint32_t len = e >> 9;
+    const uint32_t len = (e >> 9) & 15u;
     b.buf >>= len;
     b.cnt -= len;
     return (int)(e & 511u);
@@ -282,6 +304,22 @@ __device__ __forceinline__ int decode_reg(State& s, uint8_t* win, Bits& b, const
   need(s, win, b, 15);
   const uint32_t e = reg_entry(r, (uint32_t)b.buf & ((1u << fbits) - 1));
   return decode_entry(s, b, e, count, sym);
+}
+
+// The literal/length table: the symbol's pre-decoded entry (lit_entry), < 0 if unassigned.
+template <uint32_t N>
+__device__ __forceinline__ int decode_lit_reg(State& s, uint8_t* win, Bits& b, const uint32_t (&r)[N],
+                                              const uint16_t* count, const uint16_t* sym) {
+  need(s, win, b, 15);
+  const uint32_t e = reg_entry(r, (uint32_t)b.buf & ((1u << kLitFast) - 1));
+  if (e) {
+    const uint32_t len = (e >> 9) & 15u;
+    b.buf >>= len;
+    b.cnt -= len;
+    return (int)e;
+  }
+  const int v = decode_entry(s, b, 0u, count, sym);  // (a code longer than kLitFast bits)
+  return v < 0 ? v : (int)lit_entry((uint32_t)v, 0u);
 }
 
 // pending literals, one per lane, written to the ring 64 at a time
@@ -361,25 +399,21 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
       const uint64_t bits = (uint64_t)__builtin_amdgcn_alignbit(d1, d0, sh) |
                             ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32);
       const uint32_t e = t.lit_fast[(uint32_t)bits & ((1u << kLitFast) - 1)];
-      const uint32_t l1 = e >> 9, sym = e & 511u;
-      const bool is_lit = e != 0 && sym < 256;
-      const uint32_t ls = sym - 257;
-      const bool is_len = e != 0 && sym > 256 && ls < 29;
-      const uint32_t lsc = is_len ? ls : 0u;
-      const uint32_t le = len_extra(lsc);
-      const uint32_t mlen = len_base(lsc) + ((uint32_t)(bits >> l1) & ((1u << le) - 1));
+      const uint32_t l1 = (e >> 9) & 15u, kind = e >> 13, pay = e & 511u;
+      const bool is_lit = kind == 7u;
+      const bool is_len = (kind < 6u) & (e != 0u);
+      const uint32_t le = kind & 7u;  // (only meaningful for a length symbol)
+      const uint32_t mlen = pay + ((uint32_t)(bits >> l1) & ((1u << le) - 1));
       const uint32_t o2 = l1 + le;
       const uint32_t e2 = t.dist_fast[(uint32_t)(bits >> o2) & ((1u << kDistFast) - 1)];
-      const uint32_t dl = e2 >> 9, ds = e2 & 511u;
-      const uint32_t dsc = ds < 30 ? ds : 0u;
-      const uint32_t de = dist_extra(dsc);
-      const uint32_t dist = dist_base(dsc) + ((uint32_t)(bits >> (o2 + dl)) & ((1u << de) - 1));
+      const uint32_t dl = (e2 >> 9) & 15u, ds = e2 & 31u, de = (e2 >> 5) & 15u;
+      const uint32_t dist = ((e2 >> 13) << de) + 1u + ((uint32_t)(bits >> (o2 + dl)) & ((1u << de) - 1));
       // any distance (far history -- beyond the ring's reach, stock zlib streams go to
       // 32 KiB -- is read back from HBM below)
       const bool m_ok = is_len && e2 != 0 && ds < 30 && mlen <= 64 && dist <= s.op;
       const uint32_t nb = is_lit ? l1 : o2 + dl + de;
       const uint32_t olen = is_lit ? 1u : m_ok ? mlen : 127u;
-      const uint32_t payload = is_lit ? sym : (0x8000u | (dist - 1u));
+      const uint32_t payload = is_lit ? pay : (0x8000u | (dist - 1u));
       // record: next candidate (9 bits) | olen (7 bits, 127 = stop) | payload (16 bits:
       // literal byte, or 0x8000 | distance - 1)
       rec[j] = ((c + nb) & 511u) | (olen << 9) | (payload << 16);
@@ -527,23 +561,24 @@ __device__ __forceinline__ int inflate_codes(State& s, uint8_t* win, uint8_t* ri
     bits_uniform(b);
     s.op = uniform(s.op);
     // one symbol on the scalar path
-    const int sym = decode_reg(s, win, b, rt.lit, kLitFast, t.lit_count, t.lit_sym);
-    if (sym < 0) return -1;
-    if (sym < 256) {
-      if (lane_id() == L.n) L.v = (uint32_t)sym;
+    const int ent = decode_lit_reg(s, win, b, rt.lit, t.lit_count, t.lit_sym);
+    if (ent < 0) return -1;
+    const uint32_t kind = (uint32_t)ent >> 13, pay = (uint32_t)ent & 511u;
+    if (kind == 7u) {  // a literal
+      if (lane_id() == L.n) L.v = pay;
       ++L.n;
       continue;
     }
-    if (sym == 256) return 0;
-    const uint32_t ls = (uint32_t)sym - 257;
-    if (ls >= 29) return -1;
+    if (kind == 6u) return pay == 0 ? 0 : -1;  // end of block; symbols 286 / 287 are invalid
     uint32_t e;
-    if (!take(s, win, b, len_extra(ls), e)) return -1;
-    const uint32_t len = len_base(ls) + e;
-    const int ds = decode_reg(s, win, b, rt.dist, kDistFast, t.dist_count, t.dist_sym);
-    if (ds < 0 || ds >= 30) return -1;
-    if (!take(s, win, b, dist_extra((uint32_t)ds), e)) return -1;
-    const uint32_t d = dist_base((uint32_t)ds) + e;
+    if (!take(s, win, b, kind, e)) return -1;
+    const uint32_t len = pay + e;
+    const int dsr = decode_reg(s, win, b, rt.dist, kDistFast, t.dist_count, t.dist_sym);
+    if (dsr < 0) return -1;
+    const uint32_t ds = (uint32_t)dsr & 31u;  // (a fast entry carries more above bit 4)
+    if (ds >= 30) return -1;
+    if (!take(s, win, b, dist_extra(ds), e)) return -1;
+    const uint32_t d = dist_base(ds) + e;
     if (!lits_flush(s, ring, L)) return -1;
     if (d > s.op) return -1;
     if (s.op + len > s.cap) return -1;
@@ -688,7 +723,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(
         const bool d = j == 1;
         ok = build(t, d ? t.lens + nlen : t.lens, d ? ndist : nlen, d ? t.dist_fast : t.lit_fast,
                    d ? kDistFast : kLitFast, d ? t.dist_count : t.lit_count,
-                   d ? t.dist_sym : t.lit_sym);
+                   d ? t.dist_sym : t.lit_sym, d ? 2u : 1u);
       }
       if (!ok) break;
     }
