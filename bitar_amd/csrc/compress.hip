@@ -305,13 +305,14 @@ template <uint32_t RING, uint32_t HLOG>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
-    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err, const uint32_t* __restrict__ order) {
   using namespace cmp;
   // (+ one trash entry: probe lanes past the segment insert there, see parse)
   __shared__ __attribute__((aligned(16))) uint16_t table[(1u << HLOG) + 8];
   __shared__ __attribute__((aligned(16))) uint8_t inring[RING + kInPad];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kLz4Lds + 4 * (kWave + 4)];
-  const uint32_t i_seg = blockIdx.x;
+  // cost-ordered dispatch (seg_order_kernel): workgroup b compresses segment order[b]
+  const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
@@ -337,19 +338,21 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
 }
 
 template __global__ void lz4_compress_kernel<cmp::kIn, cmp::kHashLog>(
-    const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint8_t* const*, uint32_t*, uint32_t*);
+    const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint8_t* const*, uint32_t*, uint32_t*,
+    const uint32_t*);
 template __global__ void lz4_compress_kernel<16384, 12>(
-    const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint8_t* const*, uint32_t*, uint32_t*);
+    const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint8_t* const*, uint32_t*, uint32_t*,
+    const uint32_t*);
 
 __global__ __launch_bounds__(64) void deflate_compress_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
-    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err, const uint32_t* __restrict__ order) {
   using namespace cmp;
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint32_t stage[kBitWords];
-  const uint32_t i_seg = blockIdx.x;
+  const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);

@@ -333,14 +333,14 @@ struct RowRing {
 
 __global__ __launch_bounds__(64) void deflate_dyn_parse_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
-    uint8_t* __restrict__ scratch, uint64_t scr_stride, uint32_t* __restrict__ err) {
+    uint8_t* __restrict__ scratch, uint64_t scr_stride, uint32_t* __restrict__ err, const uint32_t* __restrict__ order) {
   using namespace dyn;
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
   __shared__ __attribute__((aligned(16))) uint4 cst[64];
   __shared__ uint32_t hist[kNLit + kNDist];
-  const uint32_t i_seg = blockIdx.x;
+  const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     const uint8_t* __restrict__ scratch, uint64_t scr_stride, uint8_t* __restrict__ slab,
     uint64_t slot_stride, uint8_t* const* __restrict__ dsts, uint32_t* __restrict__ sizes,
-    uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ err, const uint32_t* __restrict__ order) {
   using namespace dyn;
   __shared__ uint32_t hist[kNLit + kNDist];
   __shared__ uint32_t ltab[288];
@@ -394,7 +394,7 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
                                                            ? sizeof(TreeLds) : kEmitLds];
   TreeLds& T = *reinterpret_cast<TreeLds*>(pool);
   const uint32_t lane = lane_id();
-  const uint32_t i_seg = blockIdx.x;
+  const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);

@@ -224,13 +224,14 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, const uint32_t* __restrict__ order) {
   using namespace lz4d;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
   uint8_t* win = lds;
   uint8_t* ring = lds + kWin;
-  const uint32_t i = blockIdx.x;
-  if (i >= nseg) return;
+  if (blockIdx.x >= nseg) return;
+  // cost-ordered dispatch (seg_order_kernel): workgroup b decodes segment order[b]
+  const uint32_t i = order ? order[blockIdx.x] : blockIdx.x;
   if (FARK && produced[i] != kDefer) return;
 
   State s;
@@ -505,10 +506,10 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
 template __global__ void lz4_decompress_kernel<false>(const uint8_t* const*, const uint8_t*,
                                                      uint64_t, const uint32_t*, uint32_t,
                                                      uint32_t, uint8_t*, uint32_t*, uint32_t*,
-                                                     unsigned long long*);
+                                                     unsigned long long*, const uint32_t*);
 template __global__ void lz4_decompress_kernel<true>(const uint8_t* const*, const uint8_t*,
                                                     uint64_t, const uint32_t*, uint32_t, uint32_t,
                                                     uint8_t*, uint32_t*, uint32_t*,
-                                                    unsigned long long*);
+                                                    unsigned long long*, const uint32_t*);
 
 }  // namespace bitar_hip

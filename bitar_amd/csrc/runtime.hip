@@ -20,31 +20,33 @@
 namespace bitar_hip {
 template <uint32_t RING, uint32_t HLOG>
 __global__ void lz4_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
-                                    uint8_t* const*, uint32_t*, uint32_t*);
+                                    uint8_t* const*, uint32_t*, uint32_t*, const uint32_t*);
 template <bool FARK>
 __global__ void lz4_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                       const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
-                                      uint32_t*, unsigned long long*);
+                                      uint32_t*, unsigned long long*, const uint32_t*);
+__global__ void seg_cost_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t, uint32_t*);
+__global__ void seg_order_kernel(const uint32_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*);
 __global__ void deflate_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
-                                        uint8_t* const*, uint32_t*, uint32_t*);
+                                        uint8_t* const*, uint32_t*, uint32_t*, const uint32_t*);
 __global__ void inflate_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
-                               uint32_t*, uint32_t, unsigned long long*);
+                               uint32_t*, uint32_t, unsigned long long*, const uint32_t*);
 template <uint32_t L>
 __global__ void inflate_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                      const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
-__global__ void zstd_parse_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint2*);
+__global__ void zstd_parse_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint2*, const uint32_t*);
 __global__ void zstd_entropy_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
                                     const uint2*, uint8_t*, uint64_t, uint8_t* const*, uint32_t*,
-                                    uint32_t*, uint8_t*, uint64_t);
+                                    uint32_t*, uint8_t*, uint64_t, const uint32_t*);
 __global__ void zstd_walk_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t, uint8_t*, uint64_t);
 __global__ void zstd_emit_kernel(const uint8_t*, uint64_t, uint32_t, const uint8_t*, uint64_t,
                                  uint8_t*, uint64_t, uint8_t* const*, uint32_t*, const uint8_t*,
-                                 uint64_t);
+                                 uint64_t, const uint32_t*);
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                        const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                        uint32_t*, uint32_t*, uint32_t, uint8_t*,
-                                       unsigned long long*);
+                                       unsigned long long*, const uint32_t*);
 template <uint32_t S>
 __global__ void zstd_hlit_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                  const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
@@ -59,15 +61,15 @@ __global__ void zstd_seqdec_kernel(const uint8_t* const*, const uint8_t*, uint64
                                    uint64_t*, uint32_t, uint32_t*, unsigned long long*);
 __global__ void zstd_exec_kernel(const uint8_t* const*, const uint8_t*, uint64_t, uint32_t,
                                  uint32_t, uint8_t*, uint32_t*, const uint8_t*,
-                                 const uint64_t*, uint32_t, uint32_t*, unsigned long long*);
+                                 const uint64_t*, uint32_t, uint32_t*, unsigned long long*, const uint32_t*);
 template <uint32_t L>
 __global__ void zstd_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                   const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
 __global__ void deflate_dyn_parse_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
-                                         uint32_t*);
+                                         uint32_t*, const uint32_t*);
 __global__ void deflate_dyn_emit_kernel(const uint8_t*, uint64_t, uint32_t, const uint8_t*,
                                         uint64_t, uint8_t*, uint64_t, uint8_t* const*, uint32_t*,
-                                        uint32_t*);
+                                        uint32_t*, const uint32_t*);
 __global__ void checksum_kernel(uint32_t, const uint8_t*, uint64_t, uint32_t, const uint32_t*,
                                 uint32_t, uint64_t*);
 __global__ void scan_sizes_kernel(const uint32_t*, uint32_t, uint64_t, uint64_t*, uint32_t*);
@@ -96,6 +98,7 @@ struct bitar_hip_ctx {
   unsigned long long* d_stats = nullptr;  // BITAR_HIP_PATH_COUNT path counters
   // decoder options (bitar_hip_decoder_options), per context
   std::atomic<uint32_t> inflate_lanes{4}, zstd_lanes{16}, zstd_seq{1}, count_paths{0};
+  std::atomic<uint32_t> cost_order{1};  // LZ4: dispatch the estimated most expensive segments first
   std::mutex mu;              // guards `words`
   std::vector<std::pair<hipStream_t, uint32_t>> words;  // stream -> error word index
 };
@@ -330,6 +333,45 @@ int bitar_hip_memcpy(bitar_hip_ctx* ctx, void* dst, const void* src, uint64_t by
   return 0;
 }
 
+// Cost-ordered dispatch (util_kernels.hip, seg_order_kernel): a launch of one wave per segment
+// ends with a drain of about one segment's duration, longest when expensive segments come
+// last.  For calls of at least kOrderMinSegs segments the LZ4 kernels take their segments in
+// the order of an estimated cost key, most expensive first.  Measured (1 GiB, kind 1 = 1 MiB
+// regions of columns / text / random data): see DESIGN.md 4.1.
+extern "C++" {
+constexpr uint32_t kOrderMinSegs = 2048;
+struct SegOrder {
+  void* scratch = nullptr;
+  uint32_t* order = nullptr;  // null: plain order
+  hipStream_t s = nullptr;
+  // order = argsort of the keys: keys[i] written by `key` (a launch), or -- csizes given --
+  // the compressed sizes' key computed by the sort itself (decompress; seg: the segment size)
+  template <class F>
+  int make(bitar_hip_ctx* ctx, hipStream_t stream, uint32_t nseg, const uint32_t* csizes, F key,
+           uint32_t seg = 0) {
+    if (!ctx->cost_order.load(std::memory_order_relaxed) || nseg < kOrderMinSegs) return 0;
+    s = stream;
+    // (an optimisation only: without scratch the call runs in plain order)
+    if (hipMallocAsync(&scratch, (csizes ? 4ull : 8ull) * nseg, s) != hipSuccess) {
+      (void)hipGetLastError();
+      scratch = nullptr;
+      return 0;
+    }
+    uint32_t* keys = csizes ? nullptr : static_cast<uint32_t*>(scratch) + nseg;
+    order = static_cast<uint32_t*>(scratch);
+    if (keys) key(keys);
+    hipLaunchKernelGGL(bitar_hip::seg_order_kernel, dim3(1), dim3(1024), 0, s, keys, csizes, seg,
+                       nseg, order);
+    return 0;
+  }
+  int release() {
+    if (scratch) HIP_TRY(hipFreeAsync(scratch, s), "order scratch release");
+    scratch = nullptr;
+    return 0;
+  }
+};
+}  // extern "C++"
+
 static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const void* d_in,
                          uint64_t n, uint32_t seg, void* d_slab, uint64_t slot_stride,
                          void* const* d_dsts, uint32_t* d_sizes) {
@@ -351,16 +393,35 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
   const auto* in = static_cast<const uint8_t*>(d_in);
   auto* slab = static_cast<uint8_t*>(d_slab);
   auto* dsts = reinterpret_cast<uint8_t* const*>(d_dsts);
-  if (codec == BITAR_HIP_CODEC_LZ4)
-    hipLaunchKernelGGL((bitar_hip::lz4_compress_kernel<4096, 10>), dim3((uint32_t)nseg), dim3(64),
-                       0, s, in, n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
-  else if (codec == BITAR_HIP_CODEC_LZ4_WIDE)
-    hipLaunchKernelGGL((bitar_hip::lz4_compress_kernel<16384, 12>), dim3((uint32_t)nseg),
-                       dim3(64), 0, s, in, n, seg, slab, slot_stride, dsts, d_sizes,
-                       err_word(ctx, s));
-  else if (codec == BITAR_HIP_CODEC_DEFLATE)
+  // cost-ordered dispatch of the segments of [cin, cin + nb): key = distinct byte values in
+  // a 128-byte sample of each segment (incompressible segments, which the parses skip
+  // through and whose stored form is a copy, show the most)
+  auto cost_order = [&](SegOrder& o, const uint8_t* cin, uint64_t nb, uint32_t cn) {
+    return o.make(ctx, s, cn, nullptr, [&](uint32_t* keys) {
+      hipLaunchKernelGGL(bitar_hip::seg_cost_kernel, dim3((cn + 255) / 256), dim3(256), 0, s,
+                         cin, nb, seg, cn, keys);
+    });
+  };
+  if (codec == BITAR_HIP_CODEC_LZ4 || codec == BITAR_HIP_CODEC_LZ4_WIDE) {
+    SegOrder ord;
+    if (int r = cost_order(ord, in, n, (uint32_t)nseg)) return r;
+    if (codec == BITAR_HIP_CODEC_LZ4)
+      hipLaunchKernelGGL((bitar_hip::lz4_compress_kernel<4096, 10>), dim3((uint32_t)nseg),
+                         dim3(64), 0, s, in, n, seg, slab, slot_stride, dsts, d_sizes,
+                         err_word(ctx, s), ord.order);
+    else
+      hipLaunchKernelGGL((bitar_hip::lz4_compress_kernel<16384, 12>), dim3((uint32_t)nseg),
+                         dim3(64), 0, s, in, n, seg, slab, slot_stride, dsts, d_sizes,
+                         err_word(ctx, s), ord.order);
+    if (int r = ord.release()) return r;
+  }
+  else if (codec == BITAR_HIP_CODEC_DEFLATE) {
+    SegOrder ord;
+    if (int r = cost_order(ord, in, n, (uint32_t)nseg)) return r;
     hipLaunchKernelGGL(bitar_hip::deflate_compress_kernel, dim3((uint32_t)nseg), dim3(64), 0, s,
-                       in, n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s));
+                       in, n, seg, slab, slot_stride, dsts, d_sizes, err_word(ctx, s), ord.order);
+    if (int r = ord.release()) return r;
+  }
   else if (codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC) {
     // pass 1 (parse -> records + histograms) and pass 2 (codes + emit) through a
     // stream-ordered scratch per segment (deflate_dyn.hip): 2 KiB plan + 16 KiB of window
@@ -376,11 +437,14 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
       const uint64_t cb = c0 * seg, nb = n - cb < cn * seg ? n - cb : cn * seg;
       uint8_t* cslab = slab ? slab + c0 * slot_stride : nullptr;
       uint8_t* const* cdsts = dsts ? dsts + c0 : nullptr;
+      SegOrder ord;
+      if (int r = cost_order(ord, in + cb, nb, (uint32_t)cn)) return r;
       hipLaunchKernelGGL(bitar_hip::deflate_dyn_parse_kernel, dim3((uint32_t)cn), dim3(64), 0, s,
-                         in + cb, nb, seg, scr, scr_stride, err_word(ctx, s));
+                         in + cb, nb, seg, scr, scr_stride, err_word(ctx, s), ord.order);
       hipLaunchKernelGGL(bitar_hip::deflate_dyn_emit_kernel, dim3((uint32_t)cn), dim3(64), 0, s,
                          in + cb, nb, seg, static_cast<const uint8_t*>(scr), scr_stride, cslab,
-                         slot_stride, cdsts, d_sizes + c0, err_word(ctx, s));
+                         slot_stride, cdsts, d_sizes + c0, err_word(ctx, s), ord.order);
+      if (int r = ord.release()) return r;
     }
     const hipError_t le = hipGetLastError();
     HIP_TRY(hipFreeAsync(scratch, s), "scratch release");
@@ -407,16 +471,19 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
       uint8_t* cslab = slab ? slab + c0 * slot_stride : nullptr;
       uint8_t* const* cdsts = dsts ? dsts + c0 : nullptr;
       const uint8_t* cin = in + cb;
+      SegOrder ord;
+      if (int r = cost_order(ord, cin, nb, (uint32_t)cn)) return r;
       hipLaunchKernelGGL(bitar_hip::zstd_parse_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin,
-                         nb, seg, scr, scr_stride, meta);
+                         nb, seg, scr, scr_stride, meta, ord.order);
       hipLaunchKernelGGL(bitar_hip::zstd_entropy_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin,
                          nb, seg, scr, scr_stride, meta, cslab, slot_stride, cdsts, d_sizes + c0,
-                         err_word(ctx, s), wscr, w_stride);
+                         err_word(ctx, s), wscr, w_stride, ord.order);
       hipLaunchKernelGGL(bitar_hip::zstd_walk_kernel, dim3((uint32_t)((cn + 15) / 16)), dim3(64),
                          0, s, scr, scr_stride, seg, (uint32_t)cn, wscr, w_stride);
       hipLaunchKernelGGL(bitar_hip::zstd_emit_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin, nb,
                          seg, scr, scr_stride, cslab, slot_stride, cdsts, d_sizes + c0, wscr,
-                         w_stride);
+                         w_stride, ord.order);
+      if (int r = ord.release()) return r;
     }
     const hipError_t le = hipGetLastError();
     HIP_TRY(hipFreeAsync(scratch, s), "scratch release");
@@ -489,6 +556,7 @@ static void init_options(bitar_hip_ctx* ctx, uint32_t flags) {
                         ? 0u : zstd_lanes_from(env_long("BITAR_HIP_ZSTD_LANES", 16));
   ctx->zstd_seq = flags & BITAR_HIP_FLAG_ZSTD_LANE_EXEC ? 0u : env_long("BITAR_HIP_ZSTD_SEQ", 1) != 0;
   ctx->count_paths = (flags & BITAR_HIP_FLAG_COUNT_PATHS) ? 1u : 0u;
+  ctx->cost_order = (flags & BITAR_HIP_FLAG_PLAIN_ORDER) ? 0u : env_long("BITAR_HIP_COST_ORDER", 1) != 0;
 }
 
 // the counters' device pointer for a launch, null (= not counted) unless count_paths is on
@@ -577,12 +645,16 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
   {
     // near-history kernel over every segment, then the far-history kernel over the segments
     // it deferred (lz4_decompress.hip)
+    // cost key: the coded size, largest first; incompressible segments (copies) last
+    SegOrder ord;
+    if (int r = ord.make(ctx, s, nseg, d_sizes, [](uint32_t*) {}, seg)) return r;
     hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<false>, dim3(nseg), dim3(64), 0, s, srcs,
                        slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
-                       stats);
+                       stats, ord.order);
     hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<true>, dim3(nseg), dim3(64), 0, s, srcs,
                        slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
-                       stats);
+                       stats, ord.order);
+    if (int r = ord.release()) return r;
   }
   else if (codec == BITAR_HIP_CODEC_DEFLATE) {
     // lane-per-segment decoder for stored / fixed-Huffman streams first; the wave decoder
@@ -599,9 +671,12 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
       else BITAR_INFL_LANES(4);
 #undef BITAR_INFL_LANES
     }
+    SegOrder ord;
+    if (int r = ord.make(ctx, s, nseg, d_sizes, [](uint32_t*) {}, seg)) return r;
     hipLaunchKernelGGL(bitar_hip::inflate_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
                        stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s), L ? 1u : 0u,
-                       stats);
+                       stats, ord.order);
+    if (int r = ord.release()) return r;
   }
   else {
     // lane-per-segment decoder first; the wave-per-segment decoder then takes the segments it
@@ -651,8 +726,11 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
       const uint32_t* csz = d_sizes + c0;
       uint8_t* cout = out + c0 * seg;
       uint32_t* cprod = d_produced + c0;
+      SegOrder ord;  // (cost key: the compressed size; allocation failure = plain order)
+      (void)ord.make(ctx, s, cn, csz, [](uint32_t*) {}, seg);
       hipLaunchKernelGGL(bitar_hip::zstd_decompress_kernel, dim3(cn), dim3(64), 0, s, csrcs,
-                         cslab, stride, csz, cn, seg, cout, cprod, ew, L ? 1u : 0u, hs, stats);
+                         cslab, stride, csz, cn, seg, cout, cprod, ew, L ? 1u : 0u, hs, stats,
+                         ord.order);
 #define BITAR_ZSTD_TAIL(K, N)                                                                 \
   hipLaunchKernelGGL(bitar_hip::K<N>, dim3((cn + N - 1) / N), dim3(64), 0, s, csrcs, cslab, stride, \
                      csz, cn, seg, cout, cprod, hs, ew)
@@ -668,8 +746,9 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
         else BITAR_SEQDEC(16);
 #undef BITAR_SEQDEC
         hipLaunchKernelGGL(bitar_hip::zstd_exec_kernel, dim3(cn), dim3(64), 0, s, csrcs, cslab,
-                           stride, cn, seg, cout, cprod, hs, rp, rcap, ew, stats);
+                           stride, cn, seg, cout, cprod, hs, rp, rcap, ew, stats, ord.order);
       }
+      (void)ord.release();
       if (ho_n == 4) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 4);
       else if (ho_n == 8) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 8);
       else BITAR_ZSTD_TAIL(zstd_handoff_kernel, 16);

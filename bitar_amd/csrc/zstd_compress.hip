@@ -555,12 +555,12 @@ __global__ __launch_bounds__(64) void zstd_parse_kernel(const uint8_t* __restric
                                                         uint64_t n_total, uint32_t seg,
                                                         uint8_t* __restrict__ scratch,
                                                         uint64_t sstride,
-                                                        uint2* __restrict__ meta) {
+                                                        uint2* __restrict__ meta, const uint32_t* __restrict__ order) {
   using namespace cmp;
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];  // + trash bytes
-  const uint32_t i_seg = blockIdx.x;
+  const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
@@ -585,12 +585,12 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     uint8_t* __restrict__ scratch, uint64_t sstride, const uint2* __restrict__ meta,
     uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ err, uint8_t* __restrict__ wscr,
-    uint64_t wstride) {
+    uint64_t wstride, const uint32_t* __restrict__ order) {
   using namespace cmp;
   using namespace zse;
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
   __shared__ __attribute__((aligned(16))) EntLds L;
-  const uint32_t i_seg = blockIdx.x;
+  const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
@@ -1014,11 +1014,11 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     const uint8_t* __restrict__ scratch, uint64_t sstride, uint8_t* __restrict__ slab,
     uint64_t slot_stride, uint8_t* const* __restrict__ dsts, uint32_t* __restrict__ sizes,
-    const uint8_t* __restrict__ wscr, uint64_t wstride) {
+    const uint8_t* __restrict__ wscr, uint64_t wstride, const uint32_t* __restrict__ order) {
   using namespace cmp;
   using namespace zse;
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
-  const uint32_t i_seg = blockIdx.x;
+  const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const GMEM uint32_t* w = global_ptr(reinterpret_cast<const uint32_t*>(wscr + (uint64_t)i_seg * wstride));

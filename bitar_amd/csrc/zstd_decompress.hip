@@ -1154,13 +1154,14 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
-    uint32_t defer_only, uint8_t* __restrict__ hscr, unsigned long long* __restrict__ stats) {
+    uint32_t defer_only, uint8_t* __restrict__ hscr, unsigned long long* __restrict__ stats, const uint32_t* __restrict__ order) {
   using namespace zsd;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
   __shared__ __attribute__((aligned(16))) Tabs t;
   uint8_t* win = lds;
   uint8_t* ring = lds + kWin;
-  const uint32_t i = blockIdx.x;
+  if (blockIdx.x >= nseg) return;
+  const uint32_t i = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   if (i >= nseg) return;
   // after zstd_lanes_kernel: only the segments it deferred (zstd_lanes.hip)
   if (defer_only && produced[i] != 0xFFFFFFFEu) return;

@@ -305,7 +305,7 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
     uint64_t slot_stride, uint32_t nseg, uint32_t seg, uint8_t* __restrict__ out,
     uint32_t* __restrict__ produced, const uint8_t* __restrict__ hscr,
     const uint64_t* __restrict__ recs, uint32_t rcap, uint32_t* __restrict__ err,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, const uint32_t* __restrict__ order) {
   using namespace zsq;
   using namespace sr;
   // (a trash byte / word per lane after the ring and the event array: lanes with nothing to
@@ -313,7 +313,8 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   // the scalar unit, shared by the CU's waves, bounds this kernel)
   __shared__ __attribute__((aligned(16))) uint8_t ring[kRing + kWave];
   __shared__ uint32_t ev[2 * kWave];
-  const uint32_t i = blockIdx.x;
+  if (blockIdx.x >= nseg) return;
+  const uint32_t i = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   if (i >= nseg || uniform(produced[i]) != kRecs) return;
   const uint32_t lane = lane_id();
   const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));

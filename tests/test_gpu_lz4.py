@@ -164,6 +164,49 @@ def test_full_size_roundtrip_1gib(eng, kind):
     torch.cuda.empty_cache()
 
 
+# ---- cost-ordered dispatch (calls of >= 2048 segments) -----------------------------------
+@pytest.mark.parametrize("codec_name", ["LZ4", "LZ4_WIDE", "DEFLATE", "DEFLATE_DYNAMIC", "ZSTD"])
+def test_cost_ordered_dispatch_same_output(eng, codec_name):
+    """Calls of >= 2048 segments dispatch the segments most-expensive-first (runtime.hip
+    SegOrder; every wave-per-segment compress and decode kernel): the slab, sizes and decoded
+    output must equal a plain-order context's (whose kernels the other tests pin to the
+    oracle), and for LZ4 sampled segments the oracle's.  Kind 1 at 2048-byte segments mixes all three of its input
+    types within the call, so the order is far from the identity."""
+    import bitar_amd
+    codec = getattr(bitar_amd, "CODEC_" + codec_name)
+    plain = bitar_amd.Engine(0, flags=bitar_amd.FLAG_PLAIN_ORDER)
+    try:
+        seg, nseg = 2048, 6000
+        n = seg * nseg - 77  # a short last segment
+        data = eng.empty(n)
+        eng.fill(1, 7, data)
+        # (1 MiB regions of kind 1 hold 512 segments of 2048 bytes: the call crosses 5 regions)
+        s1, st1, z1 = eng.compress(codec, data, seg)
+        s2, st2, z2 = plain.compress(codec, data, seg)
+        eng.sync()
+        plain.sync()
+        assert st1 == st2
+        assert torch.equal(z1, z2)
+        h1, h2, gs = down(s1), down(s2), down(z1).astype(np.uint32)
+        for i in range(nseg):  # (slot bytes past a segment's size are not written)
+            a = i * st1
+            assert np.array_equal(h1[a:a + int(gs[i])], h2[a:a + int(gs[i])]), f"segment {i}"
+        o1, p1 = eng.decompress(codec, s1, st1, z1, seg)
+        o2, p2 = plain.decompress(codec, s1, st1, z1, seg)
+        eng.sync()
+        plain.sync()
+        assert torch.equal(o1[:n], data) and torch.equal(o2[:n], data)
+        assert torch.equal(p1, p2)
+        if codec_name == "LZ4":
+            for i in (0, 511, 512, 1500, 2999, nseg - 1):
+                raw = down(data[i * seg:min((i + 1) * seg, n)])
+                r, comp = O.lz4_compress(raw.tobytes())
+                assert r == 0 and len(comp) == gs[i], f"segment {i}"
+                assert h1[i * st1:i * st1 + int(gs[i])].tobytes() == comp, f"segment {i}"
+    finally:
+        plain.close()
+
+
 # ---- the wide LZ4 parse (BITAR_HIP_CODEC_LZ4_WIDE: the ratio operating point) -------------
 @pytest.mark.parametrize("kind", [0, 1, 2, 3, 5, 6])
 @pytest.mark.parametrize("seg", [65536, 59460, 2048, 13])
