@@ -372,13 +372,15 @@ __global__ __launch_bounds__(64) void deflate_compress_kernel(
   const uint32_t eob = fixed_code(256, eb);
   o.put_one(eob, eb);
   o.flush_words((uint32_t)((o.bits + 31) >> 5));
-  // stored blocks instead when they are smaller (incompressible input: the fixed code spends
-  // 9 bits on bytes >= 144) -- zlib's rule for Z_FIXED too, and the dynamic encoder's; blocks
-  // of <= 65535 bytes, the last one final (oracle bo_deflate_fixed_block)
+  // stored blocks instead unless the fixed-Huffman block is smaller by at least n / 16
+  // (incompressible input: the fixed code spends 9 bits on bytes >= 144; a nearly
+  // incompressible segment coded anyway decodes a literal at a time, the slowest segment of
+  // its decode launch) -- blocks of <= 65535 bytes, the last one final (oracle
+  // bo_deflate_fixed_block, BO_STORE_MARGIN)
   uint32_t size = (uint32_t)((o.bits + 7) >> 3);
   const uint32_t nblk = (n + 65534u) / 65535u;
   const uint32_t stored = nblk * 5u + n;
-  if (!o.overflow && stored < size) {
+  if (!o.overflow && stored < size + (n >> 4)) {  // (oracle BO_STORE_MARGIN)
     GMEM uint8_t* d = reinterpret_cast<GMEM uint8_t*>(o.dst);
     const GMEM uint8_t* in = global_ptr(input + seg_off);
     global_fence_wave();  // the fixed-Huffman stores to this range land first

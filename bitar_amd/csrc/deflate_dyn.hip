@@ -471,7 +471,7 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
   const uint64_t stored = nblk * 5 + n;
   uint32_t mode = dyn_bits < fix_bits ? 2u : 1u;
   const uint64_t best = ((mode == 2 ? dyn_bits : fix_bits) + 7) / 8;
-  if (stored < best) mode = 0;
+  if (stored < best + (n >> 4)) mode = 0;  // unless coding saves n / 16 (oracle BO_STORE_MARGIN)
 
   if (mode == 0) {  // stored blocks of <= 65535 bytes
     if (stored > slot_stride) {

@@ -20,8 +20,8 @@
  *      run-length coded separately with symbols 16/17/18 exactly as zlib's send_tree does;
  *      the code-length code is built by the same huff_lengths (limit 7);
  *   4. block choice: dynamic if its size in bits is below the fixed-Huffman size, else fixed;
- *      then stored blocks if those are smaller in bytes.  One final block (stored: blocks of
- *      <= 65535 bytes).
+ *      then stored blocks unless the coded block is smaller by at least n / 16 bytes
+ *      (BO_STORE_MARGIN).  One final block (stored: blocks of <= 65535 bytes).
  * Codes are canonical (RFC 1951 3.2.2).  zlib / libdeflate decode every stream (tests).
  */
 #include <stdlib.h>
@@ -258,7 +258,7 @@ static int deflate_dyn(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t ca
   const uint64_t stored = nblk * 5 + n;
   int mode = dyn < fix ? 2 : 1;
   const uint64_t best = ((mode == 2 ? dyn : fix) + 7) / 8;
-  if (stored < best) mode = 0;
+  if (stored < best + BO_STORE_MARGIN(n)) mode = 0;
   if (plan) {
     plan->mode = mode;
     plan->dyn_bits = dyn;

@@ -570,10 +570,11 @@ static void dfl_emit(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t 
   put_bits(c, off - kDistBase[ds], kDistExtra[ds]);
 }
 
-/* One fixed-Huffman block -- or, when they are smaller in bytes, stored blocks of <= 65535
- * bytes (zlib's choice under Z_FIXED too, and the dynamic encoder's rule below): stored =
- * 5 * ceil(n / 65535) + n bytes against the fixed block's (bits + 7) / 8, the smaller wins,
- * the fixed block on a tie. */
+/* One fixed-Huffman block -- or stored blocks of <= 65535 bytes (stored = 5 * ceil(n / 65535)
+ * + n bytes) unless the fixed block, (bits + 7) / 8 bytes, is smaller by at least n / 16
+ * (BO_STORE_MARGIN; the dynamic encoder's rule too).  A nearly incompressible segment coded
+ * anyway decodes one literal symbol at a time: on the GPU such a segment took 2.4x the decode
+ * time of a well compressed one and bounded its whole launch. */
 int bo_deflate_fixed_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
                            uint32_t* csize) {
   dfl_ctx c = {src, dst, cap, 0, 0};
@@ -584,7 +585,7 @@ int bo_deflate_fixed_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_
   const uint64_t fixed = (c.bitpos + 7) >> 3;
   const uint64_t nblk = n ? (n + 65534u) / 65535u : 1;
   const uint64_t stored = nblk * 5 + n;
-  if (stored < fixed) {
+  if (stored < fixed + BO_STORE_MARGIN(n)) {
     uint64_t o = 0;
     uint32_t p = 0;
     for (uint64_t b = 0; b < nblk; ++b) {

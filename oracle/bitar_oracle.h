@@ -108,6 +108,8 @@ typedef void (*bo_emit_fn)(void* ctx, uint32_t lit_start, uint32_t lit_len, uint
 void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t max_mlen,
                      bo_emit_fn emit, void* ctx);
 #define BO_MAX_DIST_ALL 2560u
+/* DEFLATE encoders: a coded block is kept over stored blocks only if smaller by >= n / 16 */
+#define BO_STORE_MARGIN(n) ((uint64_t)(n) >> 4)
 #define BO_PARSE_REP 1u
 #define BO_PARSE_SKIP 2u
 #define BO_PARSE_HLOG(h) ((uint32_t)(h) << 8) /* hash table log2 size (0: 10) */

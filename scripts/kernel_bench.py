@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--bytes", type=int, default=1 << 30)
     ap.add_argument("--seg", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
     import torch
     import bitar_amd
@@ -33,7 +34,7 @@ def main():
     prod = eng.empty(nseg, dtype=torch.int32)
     s = torch.cuda.current_stream()
     for kind in [int(k) for k in a.kinds.split(",")]:
-        eng.fill(kind, 0, data)
+        eng.fill(kind, a.seed, data)
         tc, td = [], []
         for r in range(a.reps + 1):
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
