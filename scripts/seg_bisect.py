@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--kind", type=int, default=1)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--bytes", type=int, default=1 << 30)
+    ap.add_argument("--phase", default="decompress", choices=("compress", "decompress"))
     a = ap.parse_args()
     import torch
     import bitar_amd
@@ -41,8 +42,14 @@ def main():
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
-            eng.decompress_slab_into(codec, slab[lo * stride:], stride, sizes[lo:], hi - lo, seg,
-                                     out[lo * seg:], prod[lo:], capacity=(hi - lo) * seg)
+            if a.phase == "decompress":
+                eng.decompress_slab_into(codec, slab[lo * stride:], stride, sizes[lo:], hi - lo,
+                                         seg, out[lo * seg:], prod[lo:],
+                                         capacity=(hi - lo) * seg)
+            else:  # (the slots of segments lo.. are rewritten with the same bytes)
+                nb = min(hi * seg, n) - lo * seg
+                eng.compress_into(codec, data[lo * seg:], seg, slab[lo * stride:], stride,
+                                  sizes[lo:], n=nb)
             e1.record(s)
             torch.cuda.synchronize()
             best = min(best, e0.elapsed_time(e1))
