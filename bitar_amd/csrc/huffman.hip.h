@@ -14,16 +14,41 @@ namespace huf {
 constexpr uint32_t kMaxSym = 286;  // DEFLATE literal/length alphabet (the largest user)
 
 struct TreeLds {
-  uint32_t fw[kMaxSym];      // frequencies (padded)
-  uint32_t w[2 * kMaxSym];   // node weights
-  uint16_t parent[2 * kMaxSym];
-  uint16_t order[2 * kMaxSym];
-  uint16_t leaf[kMaxSym];
-  uint8_t nlen[2 * kMaxSym];
-  uint16_t blc[16];        // bl_count / next_code
+  uint32_t fw[kMaxSym];     // frequencies (padded)
+  uint32_t w[2 * kMaxSym];  // leaf weights in rank order [0, m), internal weights [m, 2m - 1)
+  uint16_t leaf[kMaxSym];   // rank -> symbol
+  uint16_t up[kMaxSym];     // internal node -> its parent (pointer jumping)
+  uint16_t dep[kMaxSym];    // internal node depth (pointer jumping)
+  uint16_t blc[16];         // bl_count
 };
 
-// Length-limited Huffman code lengths of nsym symbols (bo_huff_lengths).
+// elements of the non-decreasing a[a0, a0 + n) below x (le: not above x); branch-free binary
+// search, n < 512
+__device__ __forceinline__ uint32_t count_below(const uint32_t* a, uint32_t a0, uint32_t n,
+                                                uint32_t x, bool le) {
+  uint32_t p = 0;
+  for (uint32_t st = 256; st != 0; st >>= 1) {
+    const uint32_t q = p + st;
+    const uint32_t y = q <= n ? a[a0 + q - 1] : ~0u;
+    p = (le ? y <= x : y < x) && q <= n ? q : p;
+  }
+  return p;
+}
+
+// Length-limited Huffman code lengths of nsym symbols (bo_huff_lengths), identical to the
+// oracle's two-queue construction but with only its merge left serial:
+//   1. leaves ranked by (frequency, symbol) in parallel;
+//   2. one lane merges the two queues for the internal weights I[0, m-1) alone (no parent or
+//      order arrays);
+//   3. the merge consumed the nodes in the stable merge of the sorted leaves L and the
+//      (non-decreasing) internal weights I, leaves first on ties -- a leaf taken while its
+//      internal rival does not exist yet is that rival's child, so never heavier -- and the
+//      nodes consumed at positions 2t and 2t+1 are internal node t's children.  So every
+//      node's position is a merge rank (binary search), its parent internal node position/2,
+//      and the depths follow by pointer jumping, all lanes at once;
+//   4. zlib's gen_bitlen capping: a node deeper than maxlen counts one overflow (internal
+//      nodes too); on overflow bl_count is repaired as zlib does (one lane, <= 16 entries)
+//      and the lengths handed out to the leaves in consumption (= rank) order, in parallel.
 static __device__ void huff_lengths(const uint32_t* freq, uint32_t nsym, uint32_t maxlen, uint8_t* lens,
                              TreeLds& T) {
   const uint32_t lane = lane_id();
@@ -72,56 +97,115 @@ static __device__ void huff_lengths(const uint32_t* freq, uint32_t nsym, uint32_
   lds_order();
 #pragma unroll
   for (uint32_t c = 0; c < kMaxChunks; ++c)
-    if (key[c] != ~0u) T.leaf[rank[c]] = (uint16_t)(key[c] & 511u);
+    if (key[c] != ~0u) {
+      T.leaf[rank[c]] = (uint16_t)(key[c] & 511u);
+      T.w[rank[c]] = key[c] >> 9;
+    }
   lds_order();
+  // leaf weights T.w[0, m), internal weights T.w[m, m + ni)
+  const uint32_t ni = m - 1;  // internal nodes; the last, ni - 1, is the root
   if (lane == 0) {
-    for (uint32_t k = 0; k < m; ++k) T.w[k] = T.fw[T.leaf[k]];
-    uint32_t i = 0, j = m, next = m, no = 0;
-    for (uint32_t step = 0; step + 1 < m; ++step) {
-      uint32_t ab[2];
-      for (int t = 0; t < 2; ++t) {
-        const bool take_leaf = i < m && (j >= next || T.w[i] <= T.w[j]);
-        ab[t] = take_leaf ? i++ : j++;
-        T.order[no++] = (uint16_t)ab[t];
+    uint32_t i = 0, j = 0;
+    for (uint32_t t = 0; t < ni; ++t) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t a = T.w[i], b = T.w[m + j];
+        const bool lf = i < m && (j >= t || a <= b);
+        v += lf ? a : b;
+        i += lf ? 1u : 0u;
+        j += lf ? 0u : 1u;
       }
-      T.w[next] = T.w[ab[0]] + T.w[ab[1]];
-      T.parent[ab[0]] = (uint16_t)next;
-      T.parent[ab[1]] = (uint16_t)next;
-      ++next;
+      T.w[m + t] = v;
     }
-    const uint32_t root = 2 * m - 2;
-    T.order[no++] = (uint16_t)root;
-    for (uint32_t b = 0; b < 16; ++b) T.blc[b] = 0;
-    int overflow = 0;
-    T.nlen[root] = 0;
-    for (int k = (int)no - 2; k >= 0; --k) {
-      const uint32_t nd = T.order[k];
-      uint32_t bits = T.nlen[T.parent[nd]] + 1u;
-      if (bits > maxlen) { bits = maxlen; ++overflow; }
-      T.nlen[nd] = (uint8_t)bits;
-      if (nd < m) T.blc[bits]++;
+  }
+  lds_order();
+  // positions in the consumption order: leaf k after the internal nodes lighter than it,
+  // internal node t after the leaves not heavier than it (branch-free binary searches)
+  uint32_t dl[kMaxChunks], ti[kMaxChunks];
+#pragma unroll
+  for (uint32_t c = 0; c < kMaxChunks; ++c) {
+    const uint32_t t = c * kWave + lane;
+    ti[c] = t;
+    if (t < ni) {
+      const uint32_t up = t + 1 == ni ? t : (t + count_below(T.w, 0, m, T.w[m + t], true)) >> 1;
+      T.up[t] = (uint16_t)up;
+      T.dep[t] = t + 1 == ni ? 0u : 1u;
     }
-    if (overflow) {
+  }
+  // depths of the internal nodes: pointer jumping (the root points at itself, depth 0);
+  // a depth is < ni, so ceil(log2(ni)) rounds
+  for (uint32_t span = 1; span < ni; span <<= 1) {
+    uint32_t nd[kMaxChunks], nu[kMaxChunks];
+    lds_order();
+#pragma unroll
+    for (uint32_t c = 0; c < kMaxChunks; ++c) {
+      if (ti[c] < ni) {
+        const uint32_t u = T.up[ti[c]];
+        nd[c] = T.dep[ti[c]] + T.dep[u];
+        nu[c] = T.up[u];
+      }
+    }
+    lds_order();
+#pragma unroll
+    for (uint32_t c = 0; c < kMaxChunks; ++c) {
+      if (ti[c] < ni) {
+        T.dep[ti[c]] = (uint16_t)nd[c];
+        T.up[ti[c]] = (uint16_t)nu[c];
+      }
+    }
+  }
+  lds_order();
+  // leaf depths, capped; overflow = nodes deeper than maxlen, root excluded
+  uint32_t over = 0;
+#pragma unroll
+  for (uint32_t c = 0; c < kMaxChunks; ++c) {
+    const uint32_t k = c * kWave + lane;
+    dl[c] = 0;
+    if (k < m) dl[c] = T.dep[(k + count_below(T.w, m, ni, T.w[k], false)) >> 1] + 1u;
+    const bool deep_int = k + 1 < ni && T.dep[k] > maxlen;
+    over += (uint32_t)__builtin_popcountll(ballot(k < m && dl[c] > maxlen)) +
+            (uint32_t)__builtin_popcountll(ballot(deep_int));
+    dl[c] = dl[c] > maxlen ? maxlen : dl[c];
+  }
+  if (over) {  // (uniform)
+    // bl_count from the capped lengths (ballots: one count per length)
+    for (uint32_t b = 1; b <= maxlen; ++b) {
+      uint32_t cnt = 0;
+#pragma unroll
+      for (uint32_t c = 0; c < kMaxChunks; ++c)
+        cnt += (uint32_t)__builtin_popcountll(ballot(c * kWave + lane < m && dl[c] == b));
+      if (lane == 0) T.blc[b] = (uint16_t)cnt;
+    }
+    lds_order();
+    if (lane == 0) {
+      int32_t ov = (int32_t)over;
       do {
         uint32_t bits = maxlen - 1;
         while (T.blc[bits] == 0) --bits;
         T.blc[bits]--;
         T.blc[bits + 1] += 2;
         T.blc[maxlen]--;
-        overflow -= 2;
-      } while (overflow > 0);
-      uint32_t h = 0;
-      for (uint32_t bits = maxlen; bits != 0; --bits) {
-        uint32_t n = T.blc[bits];
-        while (n != 0) {
-          const uint32_t nd = T.order[h++];
-          if (nd >= m) continue;
-          T.nlen[nd] = (uint8_t)bits;
-          --n;
-        }
-      }
+        ov -= 2;
+      } while (ov > 0);
     }
-    for (uint32_t k = 0; k < m; ++k) lens[T.leaf[k]] = T.nlen[k];
+    lds_order();
+    // the lengths again, maxlen first, to the leaves in rank order
+    uint32_t cum = 0;
+    for (uint32_t b = maxlen; b != 0; --b) {
+      const uint32_t nb = T.blc[b];
+#pragma unroll
+      for (uint32_t c = 0; c < kMaxChunks; ++c) {
+        const uint32_t k = c * kWave + lane;
+        if (k >= cum && k < cum + nb) dl[c] = b;
+      }
+      cum += nb;
+    }
+  }
+#pragma unroll
+  for (uint32_t c = 0; c < kMaxChunks; ++c) {
+    const uint32_t k = c * kWave + lane;
+    if (k < m) lens[T.leaf[k]] = (uint8_t)dl[c];
   }
   lds_order();
 }

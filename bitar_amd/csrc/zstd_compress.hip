@@ -298,6 +298,9 @@ struct SBits {
   uint32_t pos;
   uint64_t acc;
   uint32_t nb;
+  // (a constructor, not an aggregate: {LDS address, 0, ...} may become a constant global
+  // initialised with that address, which a gfx950 code object cannot hold)
+  __device__ explicit SBits(uint8_t* o) : out(o), pos(0), acc(0), nb(0) {}
   __device__ __forceinline__ void add(uint64_t v, uint32_t n) {
     if (!n) return;
     acc |= (v & ((1ull << n) - 1)) << nb;
@@ -425,7 +428,7 @@ __device__ uint32_t weights_fse(EntLds& L, uint32_t nw) {
   const uint32_t tl = table_log(6, nw, max_w);
   int16_t* norm = L.norm;
   normalize(cnt, max_w, nw, tl, norm);
-  SBits bw{L.tmp + 1, 0, 0, 0};
+  SBits bw(L.tmp + 1);
   write_ncount(bw, norm, max_w, tl);
   uint16_t* st = L.tabs;
   uint32_t* tr = L.tr[0];
@@ -487,7 +490,7 @@ __device__ uint32_t choose_table(EntLds& L, uint32_t t, uint32_t nseq, SBits& w)
   uint32_t cost_fse = 0;
   for (uint32_t s = 0; s <= max_sym; ++s)
     if (cnt[s]) cost_fse += cnt[s] * ((tl << 8) - log2fix((uint32_t)norm[s]));
-  SBits tw{L.tmp, 0, 0, 0};
+  SBits tw(L.tmp);
   const uint32_t nb = write_ncount(tw, norm, max_sym, tl);
   cost_fse += nb * 8u * 256u;
   if (cost_fse < cost_pre) {
@@ -657,6 +660,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
   uint32_t sbytes[4] = {0, 0, 0, 0};
   if (nlit > 0 && distinct > 1) {
     huf::huff_lengths(L.hist, 256, 11, L.len, L.T);
+    ZSE_PHASE(6)
     // max length, highest used symbol, weights
     uint32_t lmax = 0, msym = 0;
     for (uint32_t s0 = 0; s0 < 256; s0 += kWave) {
@@ -715,7 +719,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       }
       // tree description: direct when possible and not larger than the FSE form
       const uint32_t nw = msym;
-      const uint32_t fsz = weights_fse(L, nw);
+      const uint32_t fsz = BITAR_ZSTD_STOP == 7 ? 0u : weights_fse(L, nw);
       const uint32_t direct = nw <= 128 ? 1 + (nw + 1) / 2 : 0u;
       uint32_t d = 0;
       if (direct && (!fsz || direct <= fsz)) {
@@ -738,6 +742,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     }
   }
   ZSE_PHASE(2)
+  ZSE_PHASE(7)
   if (huff) {
     hs = ns == 1 || nlit < 1024 ? 3u : nlit < 16384 ? 4u : 5u;
     const uint32_t sf = ns == 1 ? 0u : nlit < 1024 ? 1u : nlit < 16384 ? 2u : 3u;
@@ -852,7 +857,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     ZSE_PHASE(4)
     // tables (one lane): modes byte + descriptions in L.desc, states / transforms
     if (lane == 0) {
-      SBits w{L.desc + 1, 0, 0, 0};
+      SBits w(L.desc + 1);
       const uint32_t mll = choose_table(L, 0, nseq, w);
       const uint32_t mof = choose_table(L, 1, nseq, w);
       const uint32_t mml = choose_table(L, 2, nseq, w);

@@ -196,7 +196,10 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
   // so a reload shifts by 0..6 bytes.  Bytes below q are not masked: a stream that reads
   // them is rejected by the final count whatever they hold, a valid one never uses them.
   const int32_t lo = (int32_t)q - 8;  // q >= 12 inside the frame
-  auto at = [&](int32_t a) __attribute__((always_inline)) { return ld8(src + (a < lo ? lo : a)); };
+  // (the clamped position is >= 4: zero-extended, one 64-bit add forms the address)
+  auto at = [&](int32_t a) __attribute__((always_inline)) {
+    return ld8(src + (uint32_t)(a < lo ? lo : a));
+  };
   int32_t ptr = (int32_t)end - 8;
   uint64_t C = at(ptr), N1 = at(ptr - 8), N2 = at(ptr - 16);
   uint32_t used = 0;
@@ -261,19 +264,25 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
     // Groups of kG sequences: the records stay in registers and lane 0 of the quad stores
     // them at the group's end (the compiler waits for every outstanding store at the next
     // load use -- it does not let loads overtake stores -- so one store burst per group)
+    // (the last sequence, which updates no state, is peeled off: the loops pass `more` as
+    // a constant)
     constexpr uint32_t kG = 8;
     uint32_t k = 0;
-    for (; k + kG <= nseq; k += kG) {
+    for (; k + kG < nseq; k += kG) {
       uint64_t rb[kG];
 #pragma unroll
-      for (uint32_t g = 0; g < kG; ++g) rb[g] = step(k + g + 1 < nseq);
+      for (uint32_t g = 0; g < kG; ++g) rb[g] = step(true);
       if (j == 0) {
 #pragma unroll
         for (uint32_t g = 0; g < kG; ++g) rec[k + g] = rb[g];
       }
     }
-    for (; k < nseq; ++k) {
-      const uint64_t r = step(k + 1 < nseq);
+    for (; k + 1 < nseq; ++k) {
+      const uint64_t r = step(true);
+      if (j == 0) rec[k] = r;
+    }
+    {
+      const uint64_t r = step(false);
       if (j == 0) rec[k] = r;
     }
     ok = 8 * (ptr - (int32_t)q) + 64 - (int32_t)used == 0;  // the stream consumed exactly
