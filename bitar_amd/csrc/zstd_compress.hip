@@ -396,6 +396,79 @@ __device__ void build_ctable(const int16_t* norm, uint32_t max_sym, uint32_t al,
   }
 }
 
+// build_ctable, all lanes (symbols <= 63: one per lane).  The spread visits the positions
+// k * step & mask for k = 0, 1, ...; the c-th of them not in the high region (the "less than
+// 1" symbols' cells) takes the symbol whose run [cumN, cumN + norm) holds c.  Then each
+// symbol's cells, in position order, take its consecutive state slots from cumul: ranks
+// within a 64-cell chunk by one ballot per distinct symbol there, across chunks by a
+// per-symbol running count (lane s).  Same tables as the serial build, bit for bit.
+__device__ void build_ctable_par(const int16_t* norm, uint32_t max_sym, uint32_t al, uint16_t* st,
+                                 uint32_t* tr, uint8_t* sym_at) {
+  const uint32_t lane = lane_id();
+  const uint32_t size = 1u << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+  const int32_t nv = lane <= max_sym ? (int32_t)norm[lane] : 0;
+  const uint32_t low = nv == -1 ? 1u : 0u, pos = nv > 0 ? (uint32_t)nv : 0u;
+  const uint32_t cumul = wave_incl_sum(low + pos) - (low + pos);  // state slots before s
+  const uint32_t lowi = wave_incl_sum(low);
+  const uint32_t high = size - 1 - readlane(lowi, kWave - 1);
+  const uint32_t cum_n = wave_incl_sum(pos) - pos;                  // spread cells before s
+  if (low) sym_at[size - lowi] = (uint8_t)lane;                     // (high, downwards)
+  uint32_t c0 = 0;
+  for (uint32_t k0 = 0; k0 < size; k0 += kWave) {
+    const uint32_t k = k0 + lane;
+    const uint32_t v = (k * step) & mask;
+    const bool ok = k < size && v <= high;
+    const uint64_t bm = ballot(ok);
+    const uint32_t c = c0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+    c0 += (uint32_t)__builtin_popcountll(bm);
+    // the last symbol whose run starts at or before c (cum_n is non-decreasing over lanes)
+    uint32_t sl = 0;
+#pragma unroll
+    for (uint32_t d = 32; d != 0; d >>= 1) {
+      const uint32_t x = bpermute(cum_n, sl + d);
+      sl = x <= c ? sl + d : sl;
+    }
+    if (ok) sym_at[v] = (uint8_t)sl;
+  }
+  lds_order();
+  uint32_t run = 0;  // lane s: cells of symbol s placed so far
+  for (uint32_t u0 = 0; u0 < size; u0 += kWave) {
+    const uint32_t u = u0 + lane;
+    const bool in = u < size;
+    const uint32_t sy = in ? sym_at[u] : 0u;
+    uint64_t todo = ballot(in);
+    uint32_t rank = 0;
+    while (todo) {
+      const uint32_t y = readlane(sy, (uint32_t)__builtin_ctzll(todo));
+      const uint64_t mm = ballot(in && sy == y);
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+      rank = in && sy == y ? readlane(run, y) + below : rank;
+      run += lane == y ? (uint32_t)__builtin_popcountll(mm) : 0u;
+      todo &= ~mm;
+    }
+    const uint32_t slot = bpermute(cumul, sy) + rank;
+    if (in) st[slot] = (uint16_t)(size + u);
+  }
+  if (lane <= max_sym) {
+    int32_t dnb, dfs = 0;
+    if (nv == 0) {
+      dnb = (int32_t)(((al + 1) << 16) - size);
+    } else if (nv == -1 || nv == 1) {
+      dnb = (int32_t)((al << 16) - size);
+      dfs = (int32_t)cumul - 1;
+    } else {
+      const uint32_t mbo = al - hb32((uint32_t)nv - 1);
+      const uint32_t msp = (uint32_t)nv << mbo;
+      dnb = (int32_t)((mbo << 16) - msp);
+      dfs = (int32_t)cumul - nv;
+    }
+    tr[lane] = (uint32_t)dnb | ((uint32_t)dfs << 20);
+  }
+  lds_order();
+}
+
 __device__ __forceinline__ uint32_t tr_d(uint32_t e) { return e & 0xFFFFFu; }
 __device__ __forceinline__ int32_t tr_f(uint32_t e) { return (int32_t)e >> 20; }
 
@@ -457,8 +530,10 @@ __device__ uint32_t weights_fse(EntLds& L, uint32_t nw) {
   return bw.pos + 1;
 }
 
-// one sequence table (oracle zs_choose), lane-serial; t: 0 LL, 1 OF, 2 ML.  Appends its
-// description to w, builds its state table / transforms, returns mode | al << 8 (RLE: al 0)
+// one sequence table's choice (oracle zs_choose), lane-serial; t: 0 LL, 1 OF, 2 ML.  Appends
+// its description to w, returns mode | al << 8 | max_sym << 16 (RLE: its state table and
+// transform written here, al 0); the caller builds the FSE tables of modes 0 and 2 from
+// L.norm (2) or the predefined distribution (0) with all lanes.
 __device__ uint32_t choose_table(EntLds& L, uint32_t t, uint32_t nseq, SBits& w) {
   const uint32_t* cnt = L.sh[t];
   const uint32_t nsym = t == 0 ? 36u : t == 1 ? 32u : 53u;
@@ -495,12 +570,10 @@ __device__ uint32_t choose_table(EntLds& L, uint32_t t, uint32_t nseq, SBits& w)
   cost_fse += nb * 8u * 256u;
   if (cost_fse < cost_pre) {
     for (uint32_t k = 0; k < nb; ++k) w.add(L.tmp[k], 8);
-    build_ctable(norm, max_sym, tl, st, tr, L.sym_at, L.nxt);
-    return 2u | (tl << 8);
+    return 2u | (tl << 8) | (max_sym << 16);  // (tables: build_ctable_par over L.norm)
   }
   // predefined: its distribution (with "less than 1" symbols)
-  build_ctable(def, def_max, def_al, st, tr, L.sym_at, L.nxt);
-  return 0u | (def_al << 8);
+  return 0u | (def_al << 8) | (def_max << 16);
 }
 
 struct EntOut : ByteOut {
@@ -695,28 +768,39 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       for (uint32_t q = 0; q < 4; ++q) sbytes[q] = (bq[q] + 8) >> 3;
     }
     lds_order();
-    if (lane == 0) {
-      // codes: table ranges by increasing weight, then symbol (HUF_readDTableX1)
-      uint32_t* start = L.wk;
-      uint32_t* rc = L.wk + 16;
+    {
+      // codes: table ranges by increasing weight, then symbol (HUF_readDTableX1): a symbol
+      // of weight wt takes start[wt] >> (wt - 1) plus its rank among the weight's symbols
+      // (ballots per weight, all lanes)
+      uint32_t wv[4], rk[4];
+#pragma unroll
+      for (uint32_t c = 0; c < 4; ++c) {
+        wv[c] = L.len[64 * c + lane] ? L.w[64 * c + lane] : 0u;
+        rk[c] = 0;
+      }
       uint32_t next = 0;
-      for (uint32_t k = 0; k < 13; ++k) rc[k] = 0;
-      for (uint32_t s = 0; s < 256; ++s)
-        if (L.len[s]) rc[L.w[s]]++;
-      for (uint32_t k = 1; k <= lmax; ++k) {
-        start[k] = next;
-        next += rc[k] << (k - 1);
-      }
-      for (uint32_t s = 0; s < 256; ++s) {
-        const uint32_t l = L.len[s];
-        if (!l) {
-          L.E.code[s] = 0;
-          continue;
+      for (uint32_t wt = 1; wt <= lmax; ++wt) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c) {
+          const uint64_t mw = ballot(wv[c] == wt);
+          const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+              (uint32_t)(mw >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mw, 0u));
+          rk[c] = wv[c] == wt ? tot + below : rk[c];
+          tot += (uint32_t)__builtin_popcountll(mw);
         }
-        const uint32_t wt = L.w[s];
-        L.E.code[s] = (start[wt] >> (wt - 1)) | (l << 16);
-        start[wt] += 1u << (wt - 1);
+        if (lane == 0) L.wk[wt] = next >> (wt - 1);
+        next += tot << (wt - 1);
       }
+      lds_order();
+#pragma unroll
+      for (uint32_t c = 0; c < 4; ++c) {
+        const uint32_t s = 64 * c + lane, l = L.len[s];
+        L.E.code[s] = l ? (L.wk[wv[c]] + rk[c]) | (l << 16) : 0u;
+      }
+      lds_order();
+    }
+    if (lane == 0) {
       // tree description: direct when possible and not larger than the FSE form
       const uint32_t nw = msym;
       const uint32_t fsz = BITAR_ZSTD_STOP == 7 ? 0u : weights_fse(L, nw);
@@ -856,16 +940,27 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     lds_order();
     ZSE_PHASE(4)
     // tables (one lane): modes byte + descriptions in L.desc, states / transforms
+    SBits w(L.desc + 1);  // (lane 0's)
+    uint32_t md[3];
+#pragma unroll
+    for (uint32_t t = 0; t < 3; ++t) {
+      uint32_t mo = 0;
+      if (lane == 0) mo = choose_table(L, t, nseq, w);
+      lds_order();
+      mo = readlane(mo, 0);
+      md[t] = mo;
+      if ((mo & 3u) != 1u) {  // FSE_Compressed (from L.norm) or predefined
+        const int16_t* nrm = (mo & 3u) == 2u ? L.norm : t == 0 ? sT.ll_norm : t == 1 ? sT.of_norm : sT.ml_norm;
+        build_ctable_par(nrm, mo >> 16, (mo >> 8) & 0xFFu,
+                         L.tabs + (t == 0 ? kTabLL : t == 1 ? kTabOF : kTabML), L.tr[t], L.sym_at);
+      }
+    }
     if (lane == 0) {
-      SBits w(L.desc + 1);
-      const uint32_t mll = choose_table(L, 0, nseq, w);
-      const uint32_t mof = choose_table(L, 1, nseq, w);
-      const uint32_t mml = choose_table(L, 2, nseq, w);
-      L.desc[0] = (uint8_t)(((mll & 3u) << 6) | ((mof & 3u) << 4) | ((mml & 3u) << 2));
+      L.desc[0] = (uint8_t)(((md[0] & 3u) << 6) | ((md[1] & 3u) << 4) | ((md[2] & 3u) << 2));
       L.u[1] = w.pos + 1;
-      L.u[2] = mll >> 8;
-      L.u[3] = mof >> 8;
-      L.u[4] = mml >> 8;
+      L.u[2] = (md[0] >> 8) & 0xFFu;
+      L.u[3] = (md[1] >> 8) & 0xFFu;
+      L.u[4] = (md[2] >> 8) & 0xFFu;
       L.tabs[kTabDummy] = 0;
     }
     lds_order();
