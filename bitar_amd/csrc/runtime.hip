@@ -39,7 +39,9 @@ __global__ void zstd_parse_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, 
 __global__ void zstd_entropy_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
                                     const uint2*, uint8_t*, uint64_t, uint8_t* const*, uint32_t*,
                                     uint32_t*, uint8_t*, uint64_t, const uint32_t*);
-__global__ void zstd_walk_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t, uint8_t*, uint64_t);
+__global__ void zstd_walk_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t, uint8_t*, uint64_t,
+                                 const uint32_t*);
+__global__ void walk_key_kernel(const uint2*, uint32_t, uint32_t*);
 __global__ void zstd_emit_kernel(const uint8_t*, uint64_t, uint32_t, const uint8_t*, uint64_t,
                                  uint8_t*, uint64_t, uint8_t* const*, uint32_t*, const uint8_t*,
                                  uint64_t, const uint32_t*);
@@ -478,8 +480,15 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
       hipLaunchKernelGGL(bitar_hip::zstd_entropy_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin,
                          nb, seg, scr, scr_stride, meta, cslab, slot_stride, cdsts, d_sizes + c0,
                          err_word(ctx, s), wscr, w_stride, ord.order);
+      SegOrder word;  // (the walk's order: sequence counts, most first)
+      if (int r = word.make(ctx, s, (uint32_t)cn, nullptr, [&](uint32_t* keys) {
+            hipLaunchKernelGGL(bitar_hip::walk_key_kernel, dim3((uint32_t)((cn + 255) / 256)),
+                               dim3(256), 0, s, meta, (uint32_t)cn, keys);
+          }))
+        return r;
       hipLaunchKernelGGL(bitar_hip::zstd_walk_kernel, dim3((uint32_t)((cn + 15) / 16)), dim3(64),
-                         0, s, scr, scr_stride, seg, (uint32_t)cn, wscr, w_stride);
+                         0, s, scr, scr_stride, seg, (uint32_t)cn, wscr, w_stride, word.order);
+      if (int r = word.release()) return r;
       hipLaunchKernelGGL(bitar_hip::zstd_emit_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin, nb,
                          seg, scr, scr_stride, cslab, slot_stride, cdsts, d_sizes + c0, wscr,
                          w_stride, ord.order);

@@ -270,6 +270,17 @@ __global__ __launch_bounds__(256) void seg_cost_kernel(const uint8_t* __restrict
   keys[i] = d;
 }
 
+// Zstd chain walk (zstd_walk_kernel, 16 segments per wave, two rounds of waves at 1 GiB):
+// the sequence count, most first, so a wave walks 16 chains of similar length and the
+// longest go in the first round.
+__global__ __launch_bounds__(256) void walk_key_kernel(const uint2* __restrict__ meta, uint32_t nseg,
+                                                       uint32_t* __restrict__ keys) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nseg) return;
+  const uint32_t q = meta[i].y >> 4;
+  keys[i] = 1023u - (q < 1023u ? q : 1023u);
+}
+
 // order = 0..nseg-1 sorted by key (< 1024) ascending: a counting sort in one 1024-thread
 // workgroup (the order within a key is not fixed: it does not matter for the output).  keys
 // == null: the decompress key from the compressed sizes (csizes): the largest coded segments

@@ -486,48 +486,98 @@ __device__ __forceinline__ uint32_t enc_sym(SBits& w, const uint16_t* st, const 
   return st[(int32_t)(state >> nbo) + tr_f(tr[s])];
 }
 
-// Huffman weights in FSE form into L.tmp (oracle zs_weights_fse); 0 if not codable
+// Huffman weights in FSE form into L.tmp (oracle zs_weights_fse); 0 if not codable.  All
+// lanes: the weight counts by ballots, the table by build_ctable_par; one lane normalizes
+// and writes the header (<= 13 symbols).  The two interleaved state chains then run as
+// uniform scalar code: the weights, the state table (<= 64 cells) and the transforms (<= 13)
+// sit in VGPRs, one per lane, read with v_readlane; bits collect in a 64-bit accumulator
+// written out 4 bytes at a time (the serial writer's bytes, in its order).
 __device__ uint32_t weights_fse(EntLds& L, uint32_t nw) {
+  const uint32_t lane = lane_id();
   if (nw < 2) return 0;
-  uint32_t* cnt = L.wk;
-  for (uint32_t k = 0; k < 13; ++k) cnt[k] = 0;
+  uint32_t wv[4];
+#pragma unroll
+  for (uint32_t c = 0; c < 4; ++c) wv[c] = 64 * c + lane < nw ? L.w[64 * c + lane] : 0xFFu;
   uint32_t max_w = 0, distinct = 0;
-  for (uint32_t i = 0; i < nw; ++i) {
-    const uint32_t x = L.w[i];
-    if (!cnt[x]++) ++distinct;
-    if (x > max_w) max_w = x;
+  for (uint32_t x = 0; x <= 12; ++x) {
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c) cnt += (uint32_t)__builtin_popcountll(ballot(wv[c] == x));
+    if (lane == 0) L.wk[x] = cnt;
+    distinct += cnt ? 1u : 0u;
+    max_w = cnt ? x : max_w;
   }
   if (distinct < 2) return 0;
   const uint32_t tl = table_log(6, nw, max_w);
-  int16_t* norm = L.norm;
-  normalize(cnt, max_w, nw, tl, norm);
-  SBits bw(L.tmp + 1);
-  write_ncount(bw, norm, max_w, tl);
-  uint16_t* st = L.tabs;
-  uint32_t* tr = L.tr[0];
-  build_ctable(norm, max_w, tl, st, tr, L.sym_at, L.nxt);
+  uint32_t hdr = 0;
+  lds_order();
+  if (lane == 0) {
+    normalize(L.wk, max_w, nw, tl, L.norm);
+    SBits hw(L.tmp + 1);
+    hdr = write_ncount(hw, L.norm, max_w, tl);  // (padded to a byte)
+  }
+  lds_order();
+  hdr = readlane(hdr, 0);
+  build_ctable_par(L.norm, max_w, tl, L.tabs, L.tr[0], L.sym_at);
+  const uint32_t stv = lane < (1u << tl) ? L.tabs[lane] : 0u;
+  const uint32_t trv = lane <= max_w ? L.tr[0][lane] : 0u;
+  // the serial writer's state, as uniform values: out byte pos, accumulator, its bit count
+  uint32_t pos = 1 + hdr, nb = 0;
+  uint64_t acc = 0;
+  auto put = [&](uint32_t v, uint32_t n) __attribute__((always_inline)) {
+    acc |= (uint64_t)(v & ((1u << n) - 1u)) << nb;  // (n <= 6 here; n == 0 adds nothing)
+    nb += n;
+    if (nb >= 32) {
+      const uint32_t word = (uint32_t)acc;
+      if (lane < 4) L.tmp[pos + lane] = (uint8_t)(word >> (8 * lane));
+      pos += 4;
+      acc >>= 32;
+      nb -= 32;
+    }
+  };
+  auto wat = [&](uint32_t i) __attribute__((always_inline)) {
+    const uint32_t c = i >> 6, l = i & 63u;
+    return readlane(c == 0 ? wv[0] : c == 1 ? wv[1] : c == 2 ? wv[2] : wv[3], l);
+  };
+  auto init = [&](uint32_t sy) __attribute__((always_inline)) {
+    const uint32_t e = readlane(trv, sy);
+    const uint32_t d = tr_d(e);
+    const uint32_t nbo = (d + (1u << 15)) >> 16;
+    const uint32_t val = (nbo << 16) - d;
+    return readlane(stv, (uint32_t)((int32_t)(val >> nbo) + tr_f(e)));
+  };
+  auto enc = [&](uint32_t state, uint32_t sy) __attribute__((always_inline)) {
+    const uint32_t e = readlane(trv, sy);
+    const uint32_t nbo = (state + tr_d(e)) >> 16;
+    put(state, nbo);
+    return readlane(stv, (uint32_t)((int32_t)(state >> nbo) + tr_f(e)));
+  };
   uint32_t s1, s2;
   int32_t i = (int32_t)nw;
   if (nw & 1) {
-    s1 = enc_init(st, tr, L.w[--i]);
-    s2 = enc_init(st, tr, L.w[--i]);
-    s1 = enc_sym(bw, st, tr, s1, L.w[--i]);
+    s1 = init(wat((uint32_t)--i));
+    s2 = init(wat((uint32_t)--i));
+    s1 = enc(s1, wat((uint32_t)--i));
   } else {
-    s2 = enc_init(st, tr, L.w[--i]);
-    s1 = enc_init(st, tr, L.w[--i]);
+    s2 = init(wat((uint32_t)--i));
+    s1 = init(wat((uint32_t)--i));
   }
   while (i > 0) {
-    s2 = enc_sym(bw, st, tr, s2, L.w[--i]);
-    s1 = enc_sym(bw, st, tr, s1, L.w[--i]);
-    if (bw.pos > 200) return 0;  // far past the 128-byte limit: give up early
+    s2 = enc(s2, wat((uint32_t)--i));
+    s1 = enc(s1, wat((uint32_t)--i));
+    if (pos - 1 + (nb >> 3) > 200) return 0;  // far past the 128-byte limit: give up early
   }
-  bw.add(s2, tl);
-  bw.add(s1, tl);
-  bw.add(1, 1);
-  bw.pad();
-  if (bw.pos >= 128) return 0;
-  L.tmp[0] = (uint8_t)bw.pos;
-  return bw.pos + 1;
+  put(s2, tl);
+  put(s1, tl);
+  put(1, 1);
+  // the rest of the accumulator, then the final partial byte
+  const uint32_t nbytes = (nb + 7) >> 3;
+  if (lane < nbytes) L.tmp[pos + lane] = (uint8_t)(acc >> (8 * lane));
+  const uint32_t size = pos + nbytes - 1;  // (L.tmp[0] is the size byte)
+  if (size >= 128) return 0;
+  if (lane == 0) L.tmp[0] = (uint8_t)size;
+  lds_order();
+  return size + 1;
 }
 
 // one sequence table's choice (oracle zs_choose), lane-serial; t: 0 LL, 1 OF, 2 ML.  Appends
@@ -800,10 +850,10 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       }
       lds_order();
     }
+    const uint32_t fsz = BITAR_ZSTD_STOP == 7 ? 0u : weights_fse(L, msym);  // (all lanes)
     if (lane == 0) {
       // tree description: direct when possible and not larger than the FSE form
       const uint32_t nw = msym;
-      const uint32_t fsz = BITAR_ZSTD_STOP == 7 ? 0u : weights_fse(L, nw);
       const uint32_t direct = nw <= 128 ? 1 + (nw + 1) / 2 : 0u;
       uint32_t d = 0;
       if (direct && (!fsz || direct <= fsz)) {
@@ -1027,7 +1077,8 @@ constexpr uint32_t kWalkSegs = 16;
 __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict__ scratch,
                                                         uint64_t sstride, uint32_t seg,
                                                         uint32_t nseg, uint8_t* __restrict__ wscr,
-                                                        uint64_t wstride) {
+                                                        uint64_t wstride,
+                                                        const uint32_t* __restrict__ order) {
   using namespace cmp;
   using namespace zse;
   __shared__ __attribute__((aligned(16))) uint16_t tabs[kWalkSegs][1284];
@@ -1035,9 +1086,11 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
   const uint32_t lane = lane_id();
   for (uint32_t k = lane; k < sizeof(Tabs); k += kWave)
     reinterpret_cast<uint8_t*>(&sT)[k] = reinterpret_cast<const uint8_t*>(&kT)[k];
+  // (order: the segments by sequence count, walk_key_kernel; slot b walks segment order[b])
   for (uint32_t l = 0; l < kWalkSegs; ++l) {
-    const uint32_t il = blockIdx.x * kWalkSegs + l;
-    if (il >= nseg) break;
+    const uint32_t bl = blockIdx.x * kWalkSegs + l;
+    if (bl >= nseg) break;
+    const uint32_t il = order ? order[bl] : bl;
     const GMEM uint32_t* w = global_ptr(reinterpret_cast<const uint32_t*>(wscr + (uint64_t)il * wstride));
     if (w[kWHanded] != 1u) continue;
     for (uint32_t k = lane; k < 1284 / 2; k += kWave)
@@ -1046,8 +1099,9 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
   }
   lds_order();
   const uint32_t l = lane >> 2, j = lane & 3u;
-  const uint32_t i = blockIdx.x * kWalkSegs + l;
-  if (i >= nseg) return;  // quad-uniform
+  const uint32_t b = blockIdx.x * kWalkSegs + l;
+  if (b >= nseg) return;  // quad-uniform
+  const uint32_t i = order ? order[b] : b;
   GMEM uint32_t* w = global_ptr(reinterpret_cast<uint32_t*>(wscr + (uint64_t)i * wstride));
   if (w[kWHanded] != 1u) return;
   const uint32_t nseq = w[kWNseq];
