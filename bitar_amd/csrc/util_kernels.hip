@@ -254,14 +254,32 @@ __global__ __launch_bounds__(256) void seg_cost_kernel(const uint8_t* __restrict
   const uint64_t s0 = (uint64_t)i * seg;
   const uint32_t len = (uint32_t)(n - s0 < seg ? n - s0 : seg);
   uint32_t bm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint32_t q = 0; q < 4; ++q) {
-    const uint32_t at = (uint32_t)(((uint64_t)len * q) / 4);
-    const uint32_t cnt = len - at < 32 ? len - at : 32;
-    for (uint32_t k = 0; k < cnt; ++k) {
-      const uint32_t b = in[s0 + at + k];
-      const uint32_t bit = 1u << (b & 31u), w = b >> 5;
+  auto add = [&](uint32_t b) __attribute__((always_inline)) {
+    const uint32_t bit = 1u << (b & 31u), w = b >> 5;
 #pragma unroll
-      for (uint32_t j = 0; j < 8; ++j) bm[j] |= w == j ? bit : 0u;
+    for (uint32_t j = 0; j < 8; ++j) bm[j] |= w == j ? bit : 0u;
+  };
+  if (len >= 128) {
+    // the four 32-byte samples as eight 16-byte loads, all issued before any is used (a
+    // byte loop waits on every load: 25 us per GiB, against ~5 us)
+    uint4 v[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint32_t at = (uint32_t)(((uint64_t)len * q) / 4);
+      __builtin_memcpy(&v[2 * q], in + s0 + at, 16);
+      __builtin_memcpy(&v[2 * q + 1], in + s0 + at + 16, 16);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (uint32_t b = 0; b < 16; ++b) add((w4[b >> 2] >> (8 * (b & 3u))) & 0xFFu);
+    }
+  } else {
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint32_t at = (uint32_t)(((uint64_t)len * q) / 4);
+      const uint32_t cnt = len - at < 32 ? len - at : 32;
+      for (uint32_t k = 0; k < cnt; ++k) add(in[s0 + at + k]);
     }
   }
   uint32_t d = 0;
@@ -308,16 +326,25 @@ __global__ __launch_bounds__(1024) void seg_order_kernel(const uint32_t* __restr
   const uint32_t i1 = i0 + per < nseg ? i0 + per : nseg;
   hist[t] = 0;
   __syncthreads();
+  // (keys read 16 at a time, all loads issued before the first use: a load per loop
+  // iteration waited on each -- 23 us per sort at 16384 segments)
+  constexpr uint32_t kB = 16;
   {
     uint32_t cur = 0, cnt = 0;
-    for (uint32_t i = i0; i < i1; ++i) {
-      const uint32_t k = order_key(keys, csizes, seg, i);
-      if (cnt && k != cur) {
-        atomicAdd(&hist[cur], cnt);
-        cnt = 0;
+    for (uint32_t b = i0; b < i1; b += kB) {
+      uint32_t kk[kB];
+#pragma unroll
+      for (uint32_t j = 0; j < kB; ++j) kk[j] = b + j < i1 ? order_key(keys, csizes, seg, b + j) : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < kB; ++j) {
+        if (b + j >= i1) break;
+        if (cnt && kk[j] != cur) {
+          atomicAdd(&hist[cur], cnt);
+          cnt = 0;
+        }
+        cur = kk[j];
+        ++cnt;
       }
-      cur = k;
-      ++cnt;
     }
     if (cnt) atomicAdd(&hist[cur], cnt);
   }
@@ -347,18 +374,25 @@ __global__ __launch_bounds__(1024) void seg_order_kernel(const uint32_t* __restr
   __syncthreads();
   // scatter: one atomic per run of equal keys, then the run's indices
   uint32_t cur = 0, cnt = 0, start = i0;
-  for (uint32_t i = i0; i <= i1; ++i) {
-    const uint32_t k = i < i1 ? order_key(keys, csizes, seg, i) : 0xFFFFFFFFu;
-    if (cnt && k != cur) {
-      const uint32_t pos = atomicAdd(&hist[cur], cnt);
-      for (uint32_t j = 0; j < cnt; ++j) order[pos + j] = start + j;
-      cnt = 0;
+  auto flush = [&]() __attribute__((always_inline)) {
+    const uint32_t pos = atomicAdd(&hist[cur], cnt);
+    for (uint32_t j = 0; j < cnt; ++j) order[pos + j] = start + j;
+    cnt = 0;
+  };
+  for (uint32_t b = i0; b < i1; b += kB) {
+    uint32_t kk[kB];
+#pragma unroll
+    for (uint32_t j = 0; j < kB; ++j) kk[j] = b + j < i1 ? order_key(keys, csizes, seg, b + j) : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < kB; ++j) {
+      if (b + j >= i1) break;
+      if (cnt && kk[j] != cur) flush();
+      if (!cnt) start = b + j;
+      cur = kk[j];
+      ++cnt;
     }
-    if (i == i1) break;
-    if (!cnt) start = i;
-    cur = k;
-    ++cnt;
   }
+  if (cnt) flush();
 }
 
 }  // namespace bitar_hip

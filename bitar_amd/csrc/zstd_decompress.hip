@@ -261,17 +261,43 @@ __device__ __forceinline__ bool fse_build(Tabs& t, uint32_t* cells, uint32_t max
       high--;
     }
   }
-  // spread (scalar: the step sequence skips the reserved top cells)
   const uint32_t step = (size >> 1) + (size >> 3) + 3, mask = size - 1;
-  uint32_t pos = 0;
-  for (uint32_t sm = 0; sm <= max_sym; ++sm) {
-    const uint32_t cnt = readlane(pick4(normv, sm >> 6), sm & 63u);
-    for (uint32_t i = 0; i < cnt; ++i) {
-      if (lane == 0) cells[pos] = sm;
-      do { pos = (pos + step) & mask; } while (pos > high);
+  if (max_sym < kWave) {
+    // spread, all lanes (every sequence table and any weights table of <= 64 symbols): the
+    // positions k * step & mask, k = 0, 1, ..., that are not reserved; the c-th of them takes
+    // the symbol whose run of cells [cum, cum + norm) holds c.  The runs must fill exactly
+    // the unreserved cells (the scalar spread's "ends at 0").
+    const uint32_t cum = wave_incl_sum(normv[0]) - normv[0];
+    if (readlane(cum + normv[0], kWave - 1) != high + 1) return false;
+    uint32_t c0 = 0;
+    for (uint32_t k0 = 0; k0 < size; k0 += kWave) {
+      const uint32_t k = k0 + lane;
+      const uint32_t v = (k * step) & mask;
+      const bool ok = k < size && v <= high;
+      const uint64_t bm = ballot(ok);
+      const uint32_t c = c0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+      c0 += (uint32_t)__builtin_popcountll(bm);
+      uint32_t sl = 0;  // the last symbol whose run starts at or before c
+#pragma unroll
+      for (uint32_t d = 32; d != 0; d >>= 1) {
+        const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((sl + d) << 2), (int)cum);
+        sl = x <= c ? sl + d : sl;
+      }
+      if (ok) cells[v] = sl;
     }
+  } else {
+    // spread (scalar: the step sequence skips the reserved top cells)
+    uint32_t pos = 0;
+    for (uint32_t sm = 0; sm <= max_sym; ++sm) {
+      const uint32_t cnt = readlane(pick4(normv, sm >> 6), sm & 63u);
+      for (uint32_t i = 0; i < cnt; ++i) {
+        if (lane == 0) cells[pos] = sm;
+        do { pos = (pos + step) & mask; } while (pos > high);
+      }
+    }
+    if (pos != 0) return false;
   }
-  if (pos != 0) return false;
   lds_order();
   // states: cell u of symbol s gets next[s]++ in u order; lanes take 64 cells at a time and
   // rank equal symbols with a ballot
