@@ -400,7 +400,7 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
   // through and whose stored form is a copy, show the most)
   auto cost_order = [&](SegOrder& o, const uint8_t* cin, uint64_t nb, uint32_t cn) {
     return o.make(ctx, s, cn, nullptr, [&](uint32_t* keys) {
-      hipLaunchKernelGGL(bitar_hip::seg_cost_kernel, dim3((cn + 255) / 256), dim3(256), 0, s,
+      hipLaunchKernelGGL(bitar_hip::seg_cost_kernel, dim3((cn + 63) / 64), dim3(256), 0, s,
                          cin, nb, seg, cn, keys);
     });
   };
