@@ -474,11 +474,7 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     uint32_t k = 0, ac = 0;
     auto phase = [&](uint32_t hi, uint32_t lo32, uint32_t& slot) __attribute__((always_inline)) {
       const uint64_t c = ((uint64_t)hi << 32) | lo32;
-      while (used < 32 && k < n) {
-        uint32_t v = (uint32_t)(c >> (64 - used - log)) & mask;
-        const int32_t rem = 8 * (top - q) - (int32_t)used;  // stream bits not yet consumed
-        if (rem < (int32_t)log) v &= rem <= 0 ? 0u : ~0u << (log - (uint32_t)rem);
-        const uint32_t sym = t[v];
+      auto emit = [&](uint32_t sym) __attribute__((always_inline)) {
         used += tl[sym];
         acc |= (uint64_t)sym << (8 * ac);
         ++k;
@@ -486,6 +482,19 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
           lanes::st8(dst + k - 8, acc);
           acc = 0;
           ac = 0;
+        }
+      };
+      // A phase reads at most 31 + log <= 42 bits below the window top: with >= 43 stream
+      // bits left no peek reaches below the stream start, and the mask leaves the symbol
+      // chain (it sat between the shift and the table read of every symbol)
+      if (8 * (top - q) - (int32_t)used >= 43) {
+        while (used < 32 && k < n) emit(t[(uint32_t)(c >> (64 - used - log)) & mask]);
+      } else {
+        while (used < 32 && k < n) {
+          uint32_t v = (uint32_t)(c >> (64 - used - log)) & mask;
+          const int32_t rem = 8 * (top - q) - (int32_t)used;  // stream bits not yet consumed
+          if (rem < (int32_t)log) v &= rem <= 0 ? 0u : ~0u << (log - (uint32_t)rem);
+          emit(t[v]);
         }
       }
       // (unconditional: a conditional load is a phi the compiler settles with vmcnt(0); when
