@@ -20,7 +20,9 @@
 // HBM in 16-B blocks (stream_ring.hip.h).  No per-lane wildcopies: every output byte is
 // written once, by a coalesced store.
 //
-// Records: u64 = ll | ml << 17 | off << 34 (each <= 65536 for a segment <= 64 KiB).
+// Records: u64 = L | M << 22 | off << 44, L / M = literal-length / match-length code << 16 |
+// its extra bits (the baseline is added by the executor), off <= 2^20 - 1 (saturated: a
+// segment <= 64 KiB has offsets <= 65536).
 #include "lane_copy.hip.h"
 #include "stream_ring.hip.h"
 #include "zstd_hand.hip.h"
@@ -184,10 +186,9 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
   const uint32_t t = j == 1 ? 2u : j == 2 ? 1u : 0u;  // table in the frame's LL, OF, ML order
   const uint32_t al = (w3 >> (8 * t)) & 0xFFu;
   const uint16_t* tab = cel + l * kTab + (t == 0 ? 0u : t == 1 ? kOfAt : kMlAt);
-  // code -> baseline / extra bits: ll_code / ml_code as one formula with per-table constants
-  // (an offset code c is the formula's top range: extra bits c, baseline 2^c)
+  // code -> extra-bit count: ll_code / ml_code's bits as one formula with per-table
+  // constants (an offset code c is the formula's top range: c extra bits)
   const uint32_t c_lo = t == 0 ? 16u : t == 2 ? 32u : 0u, c_mid = t == 0 ? 25u : t == 2 ? 43u : 0u;
-  const uint32_t c_add = t == 2 ? 3u : 0u, c_mb = t == 0 ? 16u : t == 2 ? 35u : 0u;
   const uint32_t c_hs = t == 0 ? 19u : t == 2 ? 36u : 0u;
   // Backward bit reader (replicated over the quad): C = the 8 stream bytes at [ptr, ptr+8),
   // `used` bits consumed from its top; N1, N2 = the 16 bytes below.  Two reloads per
@@ -227,8 +228,6 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
       reload();
       const uint32_t sym = cell & 63u, ns = cell >> 6;
       const uint32_t m = sym - c_lo, hh = (sym - c_hs) & 31u;
-      const uint32_t base = sel(sym < c_lo, sym + c_add,
-                                sel(sym < c_mid, c_mb + 2u * mid_t_d(m), (1u << hh) + c_add));
       const uint32_t x = sel(sym < c_lo, 0u, sel(sym < c_mid, mid_bits_d(m), hh));
       const uint32_t nb0 = al - (31u - (uint32_t)__builtin_clz(ns));
       const uint32_t nbase = (ns << nb0) - (1u << al);
@@ -245,11 +244,16 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
       const uint32_t sof = xl + sel(t == 0, 0u, sel(t == 2, nbl, nbl + nbm));
       const uint32_t sbits = peek(used + sof, nb);
       used += xl + nbl + nbm + nbo;
-      const uint32_t val = base + sel(t == 0, e2, e1);
+      // the literal-length and match-length lanes send code << 16 | extra bits (the
+      // baselines are added by zstd_exec_kernel, 64 records per instruction there against 16
+      // segments per instruction here), the offset lane the offset value 2^code + extra
+      const uint32_t e = sel(t == 0, e2, e1);
+      const uint32_t val = sel(t == 1, (1u << (sym & 31u)) + e, (sym << 16) | e);
       cell = tab[nbase + sbits];
-      const uint32_t ll = qbcast<0>(val), ml = qbcast<1>(val), ofv = qbcast<2>(val);
-      // repeat offsets in select form (no exec-mask branches)
-      const uint32_t idx = ofv + (ll == 0 ? 1u : 0u);
+      const uint32_t lf = qbcast<0>(val), mf = qbcast<1>(val), ofv = qbcast<2>(val);
+      // repeat offsets in select form (no exec-mask branches); literal length 0 = LL code 0
+      // (which has no extra bits)
+      const uint32_t idx = ofv + (lf == 0 ? 1u : 0u);
       const uint32_t off =
           sel(ofv > 3, ofv - 3, sel(idx == 1, r0, sel(idx == 2, r1, sel(idx == 3, r2, r0 - 1))));
       const bool shift2 = ofv > 3 || idx >= 3, shift1 = ofv > 3 || idx >= 2;
@@ -257,9 +261,9 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
       r2 = sel(shift2, c1, c2);
       r1 = sel(shift1, c0, c1);
       r0 = off;
-      // (an offset past 2^30 - 1 is out of range anyway: saturated, zstd_exec_kernel rejects)
-      const uint32_t os = off < 0x3FFFFFFFu ? off : 0x3FFFFFFFu;
-      return (uint64_t)ll | ((uint64_t)(ml - 3) << 17) | ((uint64_t)os << 34);
+      // (an offset past 2^20 - 1 is out of range anyway: saturated, zstd_exec_kernel rejects)
+      const uint32_t os = off < 0xFFFFFu ? off : 0xFFFFFu;
+      return (uint64_t)lf | ((uint64_t)mf << 22) | ((uint64_t)os << 44);
     };
     // Groups of kG sequences: the records stay in registers and lane 0 of the quad stores
     // them at the group's end (the compiler waits for every outstanding store at the next
@@ -397,8 +401,12 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
     const uint32_t n = nseq - kb < kWave ? nseq - kb : kWave;
     const uint64_t r0 = rec[kb + (lane < n ? lane : n - 1)];
     const uint64_t r = lane < n ? r0 : 0ull;
-    const uint32_t ll = (uint32_t)r & 0x1FFFFu, ml = lane < n ? ((uint32_t)(r >> 17) & 0x1FFFFu) + 3 : 0u,
-                   off = (uint32_t)(r >> 34);
+    const uint32_t lf = (uint32_t)r & 0x3FFFFFu, mf = (uint32_t)(r >> 22) & 0x3FFFFFu;
+    uint32_t lb, lx, mb, mx;
+    ll_code(lf >> 16, lb, lx);
+    ml_code(mf >> 16, mb, mx);
+    const uint32_t ll = lb + (lf & 0xFFFFu), ml = lane < n ? mb + (mf & 0xFFFFu) : 0u,
+                   off = (uint32_t)(r >> 44);
     const uint32_t inc = wave_incl_sum(ll + ml), ex = inc - (ll + ml);
     const uint32_t linc = wave_incl_sum(ll), lex = linc - ll;
     const uint32_t T = readlane(inc, kWave - 1), LT = readlane(linc, kWave - 1);
