@@ -78,8 +78,9 @@ typedef struct {
 #define BITAR_HIP_FLAG_ZSTD_WAVE_ONLY 0x2u    /* no lane Zstd decoder in front of the wave one */
 #define BITAR_HIP_FLAG_ZSTD_LANE_EXEC 0x4u    /* handed-off sequence sections: lane executor */
 #define BITAR_HIP_FLAG_COUNT_PATHS 0x8u       /* count decoder path entries (see below) */
-#define BITAR_HIP_FLAG_PLAIN_ORDER 0x10u      /* LZ4 calls dispatch segment i as workgroup i
-                                                 (default: estimated most expensive first) */
+#define BITAR_HIP_FLAG_PLAIN_ORDER 0x10u      /* calls dispatch segment i as workgroup i
+                                                 (default, from 2048 segments: estimated most
+                                                 expensive first; the output is identical) */
 
 /* Number of visible gfx950 devices.  Replaces rte_compressdev_devices_get() in
  * CompressDriver::ListAvailableDeviceIds (reference src/driver.cc:173-190). */
