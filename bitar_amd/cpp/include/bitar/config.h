@@ -70,7 +70,8 @@ class Configuration {
   [[nodiscard]] auto burst_size() const noexcept { return burst_size_; }
   void set_burst_size(std::uint16_t burst_size) { burst_size_ = burst_size; }
 
-  /// Segments chained per op (SGL).  The HIP engine supports 1 (reference default).
+  /// Segments chained per op (SGL, reference default 1).  k > 1: the k segments of an op are
+  /// compressed as one stream and spread over k slots (device.cc, chained ops).
   [[nodiscard]] auto max_sgl_segs() const noexcept { return max_sgl_segs_; }
   void set_max_sgl_segs(std::uint16_t max_sgl_segs) { max_sgl_segs_ = max_sgl_segs; }
 
@@ -110,6 +111,12 @@ class Configuration {
   [[nodiscard]] auto codec() const noexcept { return codec_; }
   void set_codec(Codec codec) { codec_ = codec; }
 
+  /// Compression level, 1..9 (rte_comp_compress_xform.level; the reference always sets 1,
+  /// config.cc:86-88).  LZ4: 1 = the fast parse, >= 2 = the wide parse (16 KiB history, the
+  /// ratio operating point, BITAR_HIP_CODEC_LZ4_WIDE).  DEFLATE and ZSTD have one level.
+  [[nodiscard]] auto level() const noexcept { return level_; }
+  void set_level(std::uint8_t level) { level_ = level; }
+
  private:
   /// Configuration::UpdateCompressedSegSize (reference config.cc:59-73): the highest set bit
   /// of 2*seg, or seg*1.1 when that exceeds 32 KiB.
@@ -132,6 +139,7 @@ class Configuration {
   HuffmanEncoding huffman_enc_ = HuffmanEncoding::DYNAMIC;  // reference config.h:151
   std::uint16_t max_preallocate_memzones_ = 1024;
   Codec codec_ = Codec::DEFLATE;
+  std::uint8_t level_ = 1;
 };
 
 static inline constexpr std::string_view kHipConfigurationTypeName{"hip_gfx950"};

@@ -1,8 +1,14 @@
 // bitar/memory_pool.h -- arrow::MemoryPool backends (reference src/include/memory_pool.h).
 //
-// Rtemalloc / Rtememzone (DPDK hugepage memory the BlueField DMAs from) become HipHost
-// (pinned host memory, hipHostMalloc) and HipDevice (HBM on the current device, hipMalloc).
-// The reference names are kept as aliases so callers compile unchanged.
+// Rtemalloc / Rtememzone (DPDK hugepage memory: host memory the CPU writes and the BlueField
+// DMAs from, memory_pool.cc:70-188) become HipHost: pinned host memory (hipHostMalloc), which
+// the CPU reads and writes and the GPU's copy engines reach at full link rate.  The reference
+// names alias HipHost, so the demo's flow -- fill a memzone buffer on the CPU, Compress,
+// Decompress into another, compare on the CPU (demo_app.cc:121-122, 589-592) -- runs
+// unchanged.  HipDevice is HBM of the current device (hipMalloc): the fast path, but Arrow's
+// PoolBuffer tags every pool allocation with the CPU memory manager, so HipDevice buffers
+// report is_cpu() == true although the host must not touch them; bitar::AllocateDeviceBuffer
+// (hip_device.h) gives HBM buffers with the kROCM memory manager instead.
 #pragma once
 
 #include <cstddef>
@@ -22,8 +28,8 @@ enum class MemoryPoolBackend : std::uint8_t {
   Mimalloc,
   HipHost,
   HipDevice,
-  Rtemalloc = HipHost,   // reference name (memory_pool.h:65-71)
-  Rtememzone = HipDevice
+  Rtemalloc = HipHost,   // reference names (memory_pool.h:65-71): host memory the engine reads
+  Rtememzone = HipHost
 };
 
 struct HipAllocation {

@@ -40,7 +40,8 @@ std::string Configuration<Class, Enable>::ToString() const {
      << ", decompressed_seg_size: " << decompressed_seg_size_
      << ", compressed_seg_size: " << compressed_seg_size_
      << ", window_size: " << static_cast<int>(window_size_)
-     << ", huffman_enc: " << bitar::ToString(huffman_enc_) << ", codec: " << bitar::ToString(codec_);
+     << ", huffman_enc: " << bitar::ToString(huffman_enc_) << ", codec: " << bitar::ToString(codec_)
+     << ", level: " << static_cast<int>(level_);
   return os.str();
 }
 

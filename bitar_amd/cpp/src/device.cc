@@ -283,7 +283,7 @@ bool OnDevice(std::uint64_t address, int device) {
 template <typename Cfg>
 std::uint32_t AbiCodec(const Cfg& c) {
   switch (c.codec()) {
-    case Codec::LZ4: return BITAR_HIP_CODEC_LZ4;
+    case Codec::LZ4: return c.level() >= 2 ? BITAR_HIP_CODEC_LZ4_WIDE : BITAR_HIP_CODEC_LZ4;
     case Codec::ZSTD: return BITAR_HIP_CODEC_ZSTD;
     default:
       return c.huffman_enc() == HuffmanEncoding::FIXED ? BITAR_HIP_CODEC_DEFLATE
@@ -690,6 +690,8 @@ arrow::Status CompressDevice<Class, Enable>::ValidateConfiguration() {
     return arrow::Status::Invalid("window_size is not in the range of [", +window, ", ",
                                   +window, "]");
   }
+  if (configuration_->level() < 1 || configuration_->level() > 9)
+    return arrow::Status::Invalid("level is not in the range of [1, 9]");
   if (configuration_->max_preallocate_memzones() < internal::kMinPreallocateSlots) {
     return arrow::Status::Invalid("max_preallocate_memzones (",
                                   configuration_->max_preallocate_memzones(),

@@ -152,11 +152,14 @@ __device__ __forceinline__ bool take(State& s, uint8_t* win, Bits& b, uint32_t n
 }
 
 // Build the decoding tables of one code from lens[0..n) (LDS).  Returns false if the code is
-// over-subscribed.  fast: 2^fbits entries; count/sym: canonical arrays for long codes.
+// over-subscribed, or -- strict, the codes of a dynamic block -- incomplete, except a code
+// with no symbols and (kind 1 / 2) one whose longest length is 1: zlib 1.2.11's
+// inflate_table rule, as the oracle's huff_build.  fast: 2^fbits entries; count/sym:
+// canonical arrays for long codes.
 // Inlined (at two sites): an out-of-line call would make every value live across it --
 // the bit reader's state included -- sit in callee-saved VGPRs for the whole kernel.
 __device__ __forceinline__ bool build(Tables& t, const uint8_t* lens, uint32_t n, uint16_t* fast, uint32_t fbits,
-                      uint16_t* count, uint16_t* sym, uint32_t kind = 0) {
+                      uint16_t* count, uint16_t* sym, uint32_t kind, bool strict) {
   const uint32_t lane = lane_id();
   lds_order();
   if (lane < 16) t.base[lane] = 0;
@@ -183,6 +186,11 @@ __device__ __forceinline__ bool build(Tables& t, const uint8_t* lens, uint32_t n
     offs += c;
   }
   if (left < 0) return false;
+  if (strict && left > 0) {
+    const uint64_t nz = ballot(cntv != 0u);  // (lane 0's count is 0)
+    const uint32_t maxlen = nz ? 63u - (uint32_t)__builtin_clzll(nz) : 0u;
+    if (maxlen != 0 && (kind == 0 || maxlen != 1)) return false;
+  }
   lds_order();
   if (lane < 16) {
     count[lane] = (uint16_t)cntv;
@@ -682,7 +690,10 @@ __global__ __launch_bounds__(64) void inflate_kernel(
         lds_order();
       }
       if (bad) { ok = false; break; }
-      if (!build(t, t.lens, 19, t.cl_fast, kClFast, t.cl_count, t.cl_sym)) { ok = false; break; }
+      if (!build(t, t.lens, 19, t.cl_fast, kClFast, t.cl_count, t.cl_sym, 0u, true)) {
+        ok = false;
+        break;
+      }
       uint32_t idx = 0;
       while (idx < nlen + ndist) {
         const int sym = decode(s, win, b, t.cl_fast, kClFast, t.cl_count, t.cl_sym);
@@ -724,7 +735,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(
         const bool d = j == 1;
         ok = build(t, d ? t.lens + nlen : t.lens, d ? ndist : nlen, d ? t.dist_fast : t.lit_fast,
                    d ? kDistFast : kLitFast, d ? t.dist_count : t.lit_count,
-                   d ? t.dist_sym : t.lit_sym, d ? 2u : 1u);
+                   d ? t.dist_sym : t.lit_sym, d ? 2u : 1u, type == 2);
       }
       if (!ok) break;
     }

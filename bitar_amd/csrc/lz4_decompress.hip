@@ -3,7 +3,12 @@
 // Replaces the inflate op the reference hands to the BlueField engine per segment
 // (reference src/memory.cc:432-505 assembles one op per compressed buffer; output slice
 // i*seg of the caller's buffer).  Acceptance rules are exactly those of the oracle's
-// bo_lz4_decompress_block (oracle/bitar_oracle.c), so malformed input fails identically.
+// bo_lz4_decompress_block (oracle/bitar_oracle.c), so malformed input fails identically:
+// the block format's end conditions (final literal run >= 5 bytes, last match >= 12 bytes
+// before the end) and liblz4's two limits on length-extension bytes included.  Batches
+// never meet those (they stop >= 132 stream bytes before the end), so the general path
+// checks them, the last match's length coming from the general path or -- when the final
+// token directly follows a batch -- from a re-walk of that batch's headers.
 //
 // Per wave LDS (one wave per workgroup):
 //   win[kWin]   the compressed stream, staged from HBM 16 B per lane (dwordx4), refilled
@@ -254,6 +259,8 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   const uint32_t base = (uint32_t)(uintptr_t)s.dst;  // ring index = absolute address & mask
   const uint32_t src_lo = (uint32_t)(uintptr_t)s.src;
   bool want_far = false, stay_far = false;
+  // end-of-block conditions: the last match's length (0 = it was in the batch at bip)
+  uint32_t last_ml = 0, bip = 0;
   [[maybe_unused]] uint32_t p_batches = 0, p_bytes = 0, p_general = 0, p_stop_parse = 0,
                             p_stop_inel = 0;
   while (ok) {
@@ -420,6 +427,8 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         const uint32_t carry = readlane(key0, kWave - 1);
         half(std::integral_constant<uint32_t, 1>{}, key1 > carry ? key1 : carry);
       }
+      bip = s.ip;
+      last_ml = 0;
       s.ip += __builtin_amdgcn_readfirstlane(k);  // (k is an SGPR: keeps the add scalar)
       s.op += out;
       return out;
@@ -460,14 +469,33 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     // ---- general path: one sequence, any shape -----------------------------------------
     if constexpr (BITAR_LZ4D_PROFILE != 0) p_general += 1;
     if (s.ip >= s.csize) { ok = false; break; }
+    const uint32_t tok_at = s.ip;
     const uint32_t token = sv.get(s, win, s.ip);
     s.ip += 1;
     uint32_t lit = token >> 4;
-    if (lit == 15 && !ext_len(s, win, sv, lit)) { ok = false; break; }
+    // (a literal-length extension must start > 15 bytes before the end: liblz4)
+    if (lit == 15 && (s.ip + 15 >= s.csize || !ext_len(s, win, sv, lit))) { ok = false; break; }
     if ((uint64_t)s.ip + lit > s.csize || (uint64_t)s.op + lit > s.cap) { ok = false; break; }
     if (lit >= kLongLit) literals_long(s, win, ring, lit);
     else if (lit) literals_short(s, win, ring, lit);
-    if (s.ip == s.csize) break;  // last sequence: literals only
+    if (s.ip == s.csize) {  // last sequence: literals only
+      if (s.op > lit) {  // the block had a match: >= 5 final literals, last match >= 12 back
+        uint32_t ml = last_ml;
+        if (ml == 0 && lit >= 5 && lit < 8) {  // (ml >= 4 settles lit >= 8) re-walk the batch
+          for (uint32_t p = bip; p < tok_at;) {
+            const uint32_t t = sv.get(s, win, p);
+            uint32_t ll = t >> 4, mm = t & 15u;
+            p += 1;
+            if (ll == 15) ll += sv.get(s, win, p++);  // (batch sequences: <= 1 length byte)
+            p += ll + 2;
+            if (mm == 15) mm += sv.get(s, win, p++);
+            ml = mm + 4;
+          }
+        }
+        if (lit < 5 || lit + ml < 12) ok = false;
+      }
+      break;
+    }
     if (s.ip + 2 > s.csize) { ok = false; break; }
     const uint32_t o0 = sv.get(s, win, s.ip);
     const uint32_t o1 = sv.get(s, win, s.ip + 1);
@@ -475,10 +503,12 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     const uint32_t off = o0 | (o1 << 8);
     if (off == 0 || off > s.op) { ok = false; break; }
     uint32_t m = token & 15u;
-    if (m == 15 && !ext_len(s, win, sv, m)) { ok = false; break; }
+    // (a match-length extension must end > 4 bytes before the end: liblz4)
+    if (m == 15 && (!ext_len(s, win, sv, m) || s.ip + 4 >= s.csize)) { ok = false; break; }
     m += 4;
     if ((uint64_t)s.op + m > s.cap) { ok = false; break; }
     match_copy(s, ring, off, m);
+    last_ml = m;
   }
   if constexpr (BITAR_LZ4D_PROFILE != 0) {
     if (stats && lane_id() == 0) {

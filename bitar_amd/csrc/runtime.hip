@@ -9,11 +9,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <list>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/bitar_hip.h"
+#include "order.hip.h"
 #include "zstd_hand.hip.h"
 #include "zstd_layout.hip.h"
 
@@ -26,7 +28,10 @@ __global__ void lz4_decompress_kernel(const uint8_t* const*, const uint8_t*, uin
                                       const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
                                       uint32_t*, unsigned long long*, const uint32_t*);
 __global__ void seg_cost_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t, uint32_t*);
-__global__ void seg_order_kernel(const uint32_t*, const uint32_t*, uint32_t, uint32_t, uint32_t*);
+__global__ void order_hist_kernel(const uint32_t*, const uint32_t*, uint32_t, uint32_t, uint32_t,
+                                  uint32_t*);
+__global__ void order_scatter_kernel(const uint32_t*, const uint32_t*, uint32_t, uint32_t, uint32_t,
+                                     uint32_t, const uint32_t*, uint32_t*);
 __global__ void deflate_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
                                         uint8_t* const*, uint32_t*, uint32_t*, const uint32_t*);
 __global__ void inflate_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
@@ -101,8 +106,19 @@ struct bitar_hip_ctx {
   // decoder options (bitar_hip_decoder_options), per context
   std::atomic<uint32_t> inflate_lanes{4}, zstd_lanes{16}, zstd_seq{1}, count_paths{0};
   std::atomic<uint32_t> cost_order{1};  // LZ4: dispatch the estimated most expensive segments first
-  std::mutex mu;              // guards `words`
+  std::mutex mu;              // guards `words` and `order_scratch`
   std::vector<std::pair<hipStream_t, uint32_t>> words;  // stream -> error word index
+  // cost-ordered dispatch scratch, cached per (stream, slot) and reused in stream order (a
+  // call holds its entry's mutex from the sort's launch to the last launch that reads it)
+  struct OrderScratch {
+    hipStream_t stream;
+    int slot;
+    void* p = nullptr;
+    uint64_t cap = 0;
+    std::mutex m;
+    OrderScratch(hipStream_t s, int k) : stream(s), slot(k) {}
+  };
+  std::list<OrderScratch> order_scratch;
 };
 
 namespace {
@@ -187,6 +203,7 @@ int sync_error(uint32_t err) {
 }  // namespace
 
 static void init_options(bitar_hip_ctx* ctx, uint32_t flags);
+static void free_order_scratch(bitar_hip_ctx* ctx);
 
 extern "C" {
 
@@ -267,6 +284,8 @@ int bitar_hip_close(bitar_hip_ctx* ctx) {
       (void)hipStreamSynchronize(s);
       (void)hipStreamDestroy(s);
     }
+    (void)hipDeviceSynchronize();  // (order scratch may sit on foreign streams)
+    free_order_scratch(ctx);
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
   }
@@ -343,35 +362,68 @@ int bitar_hip_memcpy(bitar_hip_ctx* ctx, void* dst, const void* src, uint64_t by
 extern "C++" {
 constexpr uint32_t kOrderMinSegs = 2048;
 struct SegOrder {
-  void* scratch = nullptr;
+  bitar_hip_ctx::OrderScratch* e = nullptr;
+  std::unique_lock<std::mutex> held;
   uint32_t* order = nullptr;  // null: plain order
-  hipStream_t s = nullptr;
   // order = argsort of the keys: keys[i] written by `key` (a launch), or -- csizes given --
-  // the compressed sizes' key computed by the sort itself (decompress; seg: the segment size)
+  // the compressed sizes' key computed by the sort itself (decompress; seg: the segment size).
+  // slot: which of the stream's cached scratch areas (a call holding two orders at once
+  // uses slots 0 and 1).  The scratch is allocated once per stream and grown on demand, so
+  // steady-state calls queue no allocation.
   template <class F>
-  int make(bitar_hip_ctx* ctx, hipStream_t stream, uint32_t nseg, const uint32_t* csizes, F key,
-           uint32_t seg = 0) {
+  int make(bitar_hip_ctx* ctx, hipStream_t s, uint32_t nseg, const uint32_t* csizes, F key,
+           uint32_t seg = 0, int slot = 0) {
     if (!ctx->cost_order.load(std::memory_order_relaxed) || nseg < kOrderMinSegs) return 0;
-    s = stream;
-    // (an optimisation only: without scratch the call runs in plain order)
-    if (hipMallocAsync(&scratch, (csizes ? 4ull : 8ull) * nseg, s) != hipSuccess) {
-      (void)hipGetLastError();
-      scratch = nullptr;
-      return 0;
+    const uint32_t tile = bitar_hip::order_tile(nseg);
+    const uint32_t ntiles = (nseg + tile - 1) / tile;
+    const uint64_t need = 8ull * nseg + 4ull * bitar_hip::kOrderBins * ntiles + 64;
+    {
+      std::lock_guard<std::mutex> g(ctx->mu);
+      for (auto& x : ctx->order_scratch)
+        if (x.stream == s && x.slot == slot) e = &x;
+      if (!e) e = &ctx->order_scratch.emplace_back(s, slot);
     }
-    uint32_t* keys = csizes ? nullptr : static_cast<uint32_t*>(scratch) + nseg;
-    order = static_cast<uint32_t*>(scratch);
+    held = std::unique_lock<std::mutex>(e->m);
+    if (e->cap < need) {
+      // (an optimisation only: without scratch the call runs in plain order)
+      if (e->p) (void)hipFreeAsync(e->p, s);
+      e->p = nullptr;
+      e->cap = 0;
+      const uint64_t cap = (need + (1u << 20) - 1) & ~(uint64_t)((1u << 20) - 1);
+      if (hipMallocAsync(&e->p, cap, s) != hipSuccess) {
+        (void)hipGetLastError();
+        e->p = nullptr;
+        held.unlock();
+        return 0;
+      }
+      e->cap = cap;
+    }
+    order = static_cast<uint32_t*>(e->p);
+    uint32_t* keys = csizes ? nullptr : order + nseg;
+    auto* hist = reinterpret_cast<uint32_t*>(
+        (reinterpret_cast<uintptr_t>(order + 2ull * nseg) + 15) & ~(uintptr_t)15);
     if (keys) key(keys);
-    hipLaunchKernelGGL(bitar_hip::seg_order_kernel, dim3(1), dim3(1024), 0, s, keys, csizes, seg,
-                       nseg, order);
+    hipLaunchKernelGGL(bitar_hip::order_hist_kernel, dim3(ntiles), dim3(64), 0, s, keys, csizes,
+                       seg, nseg, tile, hist);
+    hipLaunchKernelGGL(bitar_hip::order_scatter_kernel, dim3(ntiles), dim3(64), 0, s, keys,
+                       csizes, seg, nseg, tile, ntiles, hist, order);
     return 0;
   }
+  // after the last launch that reads the order has been queued
   int release() {
-    if (scratch) HIP_TRY(hipFreeAsync(scratch, s), "order scratch release");
-    scratch = nullptr;
+    if (held.owns_lock()) held.unlock();
     return 0;
   }
+  ~SegOrder() { release(); }
 };
+
+// the context's cached order scratch, freed at close (after its streams are idle)
+static void free_order_scratch(bitar_hip_ctx* ctx) {
+  std::lock_guard<std::mutex> g(ctx->mu);
+  for (auto& x : ctx->order_scratch)
+    if (x.p) (void)hipFree(x.p);
+  ctx->order_scratch.clear();
+}
 }  // extern "C++"
 
 static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const void* d_in,
@@ -400,7 +452,7 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
   // through and whose stored form is a copy, show the most)
   auto cost_order = [&](SegOrder& o, const uint8_t* cin, uint64_t nb, uint32_t cn) {
     return o.make(ctx, s, cn, nullptr, [&](uint32_t* keys) {
-      hipLaunchKernelGGL(bitar_hip::seg_cost_kernel, dim3((cn + 63) / 64), dim3(256), 0, s,
+      hipLaunchKernelGGL(bitar_hip::seg_cost_kernel, dim3((cn + 15) / 16), dim3(64), 0, s,
                          cin, nb, seg, cn, keys);
     });
   };
@@ -482,9 +534,9 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
                          err_word(ctx, s), wscr, w_stride, ord.order);
       SegOrder word;  // (the walk's order: sequence counts, most first)
       if (int r = word.make(ctx, s, (uint32_t)cn, nullptr, [&](uint32_t* keys) {
-            hipLaunchKernelGGL(bitar_hip::walk_key_kernel, dim3((uint32_t)((cn + 255) / 256)),
-                               dim3(256), 0, s, meta, (uint32_t)cn, keys);
-          }))
+            hipLaunchKernelGGL(bitar_hip::walk_key_kernel, dim3((uint32_t)((cn + 63) / 64)),
+                               dim3(64), 0, s, meta, (uint32_t)cn, keys);
+          }, 0, 1))
         return r;
       hipLaunchKernelGGL(bitar_hip::zstd_walk_kernel, dim3((uint32_t)((cn + 15) / 16)), dim3(64),
                          0, s, scr, scr_stride, seg, (uint32_t)cn, wscr, w_stride, word.order);
@@ -803,15 +855,18 @@ int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream) {
     return sync_error(err);
   }
   // NULL: the default stream and this context's queue pairs (not other contexts' or other
-  // libraries' streams); every word of the context is read and cleared
+  // libraries' streams).  Only their words (0 = the default stream, 1..num_streams) are read
+  // and cleared: a foreign stream's word belongs to a sync of that stream, since work still
+  // running there could set it after this read and lose its error at the clear.
   HIP_TRY(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
   for (hipStream_t q : ctx->streams) HIP_TRY(hipStreamSynchronize(q), "hipStreamSynchronize");
-  std::vector<uint32_t> words(kErrWords);
-  HIP_TRY(hipMemcpy(words.data(), ctx->d_err, kErrWords * sizeof(uint32_t),
-                    hipMemcpyDeviceToHost), "read error words");
+  const size_t nw = ctx->streams.size() + 1;
+  std::vector<uint32_t> words(nw);
+  HIP_TRY(hipMemcpy(words.data(), ctx->d_err, nw * sizeof(uint32_t), hipMemcpyDeviceToHost),
+          "read error words");
   uint32_t err = 0;
   for (uint32_t x : words) err |= x;
-  if (err) HIP_TRY(hipMemset(ctx->d_err, 0, kErrWords * sizeof(uint32_t)), "clear error words");
+  if (err) HIP_TRY(hipMemset(ctx->d_err, 0, nw * sizeof(uint32_t)), "clear error words");
   return sync_error(err);
 }
 

@@ -1,4 +1,5 @@
 // util_kernels.hip -- frame packing (prefix sum + gather) and the synthetic-input generator.
+#include "order.hip.h"
 #include "wave.hip.h"
 
 namespace bitar_hip {
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(256) void fill_kernel(int kind, uint64_t seed, uint
 
 // Compress: the number of distinct byte values in a 128-byte sample of the segment (4 x 32 B
 // at its quarter points) -- incompressible data shows ~100, the parse skips through it.
-__global__ __launch_bounds__(256) void seg_cost_kernel(const uint8_t* __restrict__ in,
+__global__ __launch_bounds__(64) void seg_cost_kernel(const uint8_t* __restrict__ in,
                                                        uint64_t n, uint32_t seg, uint32_t nseg,
                                                        uint32_t* __restrict__ keys) {
   // four threads per segment, one 32-byte sample each; the four 256-bit byte sets are OR-ed
@@ -292,94 +293,47 @@ __global__ __launch_bounds__(256) void seg_cost_kernel(const uint8_t* __restrict
 // Zstd chain walk (zstd_walk_kernel, 16 segments per wave, two rounds of waves at 1 GiB):
 // the sequence count, most first, so a wave walks 16 chains of similar length and the
 // longest go in the first round.
-__global__ __launch_bounds__(256) void walk_key_kernel(const uint2* __restrict__ meta, uint32_t nseg,
-                                                       uint32_t* __restrict__ keys) {
+__global__ __launch_bounds__(64) void walk_key_kernel(const uint2* __restrict__ meta, uint32_t nseg,
+                                                      uint32_t* __restrict__ keys) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nseg) return;
-  const uint32_t q = meta[i].y >> 4;
-  keys[i] = 1023u - (q < 1023u ? q : 1023u);
+  const uint32_t q = meta[i].y >> 6;
+  keys[i] = kOrderBins - 1u - (q < kOrderBins - 1u ? q : kOrderBins - 1u);
 }
 
-// order = 0..nseg-1 sorted by key (< 1024) ascending: a counting sort in one 1024-thread
-// workgroup (the order within a key is not fixed: it does not matter for the output).  keys
-// == null: the decompress key from the compressed sizes (csizes): the largest coded segments
-// first (a decoder's cost grows with the symbols or sequences it reads), the stored /
-// incompressible ones (csize >= seg: raw blocks, stored blocks, one literal run) last, as
-// they decode as copies.  (Measured against smallest-first: LZ4 kind 1 decode 1.74 -> 1.67 ms,
-// fixed-Huffman DEFLATE 10.6 -> 7.9 ms, Zstd kind 1 6.53 -> 6.42 ms.)
-// Each thread takes a contiguous run of segments and adds runs of equal keys with one LDS
-// atomic (neighbouring segments often share a key: one address for all of them would
-// serialize 16384 atomics).
+// order = 0..nseg-1 sorted by key (< kOrderBins) ascending: a counting sort over tiles of
+// `tile` consecutive segments, in two launches of one-wave workgroups (order_hist_kernel: the
+// tiles' histograms; order_scatter_kernel: every tile's bin offsets from all histograms, then
+// its segments).  One-wave workgroups take a CU slot as soon as any wave of another grid
+// ends, so the sort of one queue pair's call no longer waits for a CU to drain while another
+// queue pair's compress grid holds the chip (a 1024-thread workgroup did: 4.7 ms per call in
+// the configs[3] record batch, 0.03 ms alone).  The order within a key is not fixed (it does
+// not matter for the output).  keys == null: the decompress key from the compressed sizes
+// (csizes): the largest coded segments first (a decoder's cost grows with the symbols or
+// sequences it reads), the stored / incompressible ones (csize >= seg: raw blocks, stored
+// blocks, one literal run) last, as they decode as copies.  (Measured against smallest-first:
+// LZ4 kind 1 decode 1.74 -> 1.67 ms, fixed-Huffman DEFLATE 10.6 -> 7.9 ms, Zstd kind 1 6.53
+// -> 6.42 ms.)  Each lane takes a contiguous run of its tile's segments and adds runs of
+// equal keys with one LDS atomic (neighbouring segments often share a key: one address for
+// all of them would serialize).
 __device__ __forceinline__ uint32_t order_key(const uint32_t* keys, const uint32_t* csizes,
                                               uint32_t seg, uint32_t i) {
-  if (keys) return keys[i] & 1023u;
+  if (keys) return keys[i] < kOrderBins ? keys[i] : kOrderBins - 1u;
   const uint32_t c = csizes[i];
-  return c >= seg ? 1023u : 1022u - (c >> 8 < 1022u ? c >> 8 : 1022u);
+  return c >= seg ? kOrderBins - 1u
+                  : kOrderBins - 2u - (uint32_t)((uint64_t)c * (kOrderBins - 2u) / seg);
 }
-__global__ __launch_bounds__(1024) void seg_order_kernel(const uint32_t* __restrict__ keys,
-                                                         const uint32_t* __restrict__ csizes,
-                                                         uint32_t seg, uint32_t nseg,
-                                                         uint32_t* __restrict__ order) {
-  __shared__ uint32_t hist[1024];
-  __shared__ uint32_t part[1024 / kWave];
-  const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-  const uint32_t per = (nseg + 1023) / 1024, i0 = t * per;
+
+// lane l of tile b visits the segments [b tile + l per, + per), per = tile / 64; runs of equal
+// keys go to f(key, run start, run length)
+template <class F>
+__device__ __forceinline__ void order_runs(const uint32_t* keys, const uint32_t* csizes,
+                                           uint32_t seg, uint32_t nseg, uint32_t tile, F f) {
+  const uint32_t per = tile / kWave;
+  const uint32_t i0 = blockIdx.x * tile + lane_id() * per;
   const uint32_t i1 = i0 + per < nseg ? i0 + per : nseg;
-  hist[t] = 0;
-  __syncthreads();
-  // (keys read 16 at a time, all loads issued before the first use: a load per loop
-  // iteration waited on each -- 23 us per sort at 16384 segments)
-  constexpr uint32_t kB = 16;
-  {
-    uint32_t cur = 0, cnt = 0;
-    for (uint32_t b = i0; b < i1; b += kB) {
-      uint32_t kk[kB];
-#pragma unroll
-      for (uint32_t j = 0; j < kB; ++j) kk[j] = b + j < i1 ? order_key(keys, csizes, seg, b + j) : 0u;
-#pragma unroll
-      for (uint32_t j = 0; j < kB; ++j) {
-        if (b + j >= i1) break;
-        if (cnt && kk[j] != cur) {
-          atomicAdd(&hist[cur], cnt);
-          cnt = 0;
-        }
-        cur = kk[j];
-        ++cnt;
-      }
-    }
-    if (cnt) atomicAdd(&hist[cur], cnt);
-  }
-  __syncthreads();
-  // exclusive scan of the 1024 counts
-  const uint32_t v = hist[t];
-  uint32_t incl = v;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  if (lane == 63) part[w] = incl;
-  __syncthreads();
-  if (t < 64) {
-    const uint32_t pv = t < 1024 / kWave ? part[t] : 0u;
-    uint32_t pin = pv;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(pin, d, 64);
-      if (t >= d) pin += y;
-    }
-    if (t < 1024 / kWave) part[t] = pin - pv;
-  }
-  __syncthreads();
-  hist[t] = part[w] + incl - v;
-  __syncthreads();
-  // scatter: one atomic per run of equal keys, then the run's indices
+  constexpr uint32_t kB = 16;  // keys read 16 at a time, all loads issued before the first use
   uint32_t cur = 0, cnt = 0, start = i0;
-  auto flush = [&]() __attribute__((always_inline)) {
-    const uint32_t pos = atomicAdd(&hist[cur], cnt);
-    for (uint32_t j = 0; j < cnt; ++j) order[pos + j] = start + j;
-    cnt = 0;
-  };
   for (uint32_t b = i0; b < i1; b += kB) {
     uint32_t kk[kB];
 #pragma unroll
@@ -387,13 +341,72 @@ __global__ __launch_bounds__(1024) void seg_order_kernel(const uint32_t* __restr
 #pragma unroll
     for (uint32_t j = 0; j < kB; ++j) {
       if (b + j >= i1) break;
-      if (cnt && kk[j] != cur) flush();
+      if (cnt && kk[j] != cur) {
+        f(cur, start, cnt);
+        cnt = 0;
+      }
       if (!cnt) start = b + j;
       cur = kk[j];
       ++cnt;
     }
   }
-  if (cnt) flush();
+  if (cnt) f(cur, start, cnt);
+}
+
+__global__ __launch_bounds__(64) void order_hist_kernel(const uint32_t* __restrict__ keys,
+                                                        const uint32_t* __restrict__ csizes,
+                                                        uint32_t seg, uint32_t nseg, uint32_t tile,
+                                                        uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kOrderBins];
+  const uint32_t lane = lane_id();
+  for (uint32_t k = lane; k < kOrderBins; k += kWave) h[k] = 0;
+  __syncthreads();
+  order_runs(keys, csizes, seg, nseg, tile,
+             [&](uint32_t key, uint32_t, uint32_t cnt) { atomicAdd(&h[key], cnt); });
+  __syncthreads();
+  for (uint32_t k = lane; k < kOrderBins; k += kWave) hist[blockIdx.x * kOrderBins + k] = h[k];
+}
+
+__global__ __launch_bounds__(64) void order_scatter_kernel(const uint32_t* __restrict__ keys,
+                                                           const uint32_t* __restrict__ csizes,
+                                                           uint32_t seg, uint32_t nseg,
+                                                           uint32_t tile, uint32_t ntiles,
+                                                           const uint32_t* __restrict__ hist,
+                                                           uint32_t* __restrict__ order) {
+  static_assert(kOrderBins == 4 * kWave, "four bins per lane");
+  __shared__ uint32_t base[kOrderBins];
+  const uint32_t lane = lane_id(), me = blockIdx.x;
+  // lane l owns bins 4l .. 4l + 3: their totals and the counts of the tiles before this one
+  uint32_t tot[4] = {0, 0, 0, 0}, pre[4] = {0, 0, 0, 0};
+  const uint4* h4 = reinterpret_cast<const uint4*>(hist);
+  for (uint32_t t = 0; t < ntiles; ++t) {
+    const uint4 v = h4[t * (kOrderBins / 4) + lane];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      tot[j] += w[j];
+      pre[j] += t < me ? w[j] : 0u;
+    }
+  }
+  // exclusive scan of the totals over the bins (4 per lane, then across the lanes)
+  const uint32_t s4 = tot[0] + tot[1] + tot[2] + tot[3];
+  uint32_t incl = s4;
+#pragma unroll
+  for (uint32_t d = 1; d < kWave; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, d, kWave);
+    if (lane >= d) incl += y;
+  }
+  uint32_t run = incl - s4;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    base[4 * lane + j] = run + pre[j];
+    run += tot[j];
+  }
+  __syncthreads();
+  order_runs(keys, csizes, seg, nseg, tile, [&](uint32_t key, uint32_t start, uint32_t cnt) {
+    const uint32_t pos = atomicAdd(&base[key], cnt);
+    for (uint32_t j = 0; j < cnt; ++j) order[pos + j] = start + j;
+  });
 }
 
 }  // namespace bitar_hip

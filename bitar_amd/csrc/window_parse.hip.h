@@ -152,6 +152,8 @@ struct Window {
   uint32_t off;     // per lane: match distance (chain lanes)
   uint32_t byte;    // per lane: input byte at x + lane
   uint32_t pos_in;  // parse position at window start: [x, pos_in) is covered by a match
+  uint32_t done;    // end of the positions earlier windows handed over (SKIP: positions in
+                    // [done, x) lay in skipped probe windows and are all literals)
 };
 
 // ---- byte output staged in an LDS ring, flushed in aligned 16-B blocks ----------------
@@ -497,6 +499,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       W.off = p - cand;
       W.byte = v.x & 0xFFu;
       W.pos_in = pos_in;
+      W.done = emitted;
       em.window(in, I, W, anchor, n);
       if (chain) anchor = pos;
       emitted = pos > x + kWave ? pos : x + kWave;

@@ -142,8 +142,11 @@ struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the lit
   __device__ __forceinline__ uint32_t pending_from(uint32_t, uint32_t emitted) const {
     return emitted;
   }
-  __device__ __forceinline__ void window(const GMEM uint8_t*, const InRing&, const Window& W,
-                                         uint32_t anchor, uint32_t n) {
+  __device__ __forceinline__ void window(const GMEM uint8_t* in, const InRing& I,
+                                         const Window& W, uint32_t anchor, uint32_t n) {
+    // SKIP: the positions of probe windows that found nothing were never handed over; they
+    // are literals and come first (the oracle's emit takes each sequence's literal run whole)
+    if (W.done < W.x) literals(in, I, W.done, W.x - W.done);
     const uint32_t lane = lane_id();
     const uint32_t q = W.x + lane;
     const bool cl = (W.chain >> lane) & 1;
@@ -677,13 +680,19 @@ struct EntOut : ByteOut {
 
 }  // namespace zse
 
+// The Zstd parse is the repeat-offset form with window skipping (oracle BO_PARSE_REP |
+// BO_PARSE_SKIP); BITAR_ZSTD_SKIP=0 builds the plain repeat-offset scan (tuning knob only).
+#ifndef BITAR_ZSTD_SKIP
+#define BITAR_ZSTD_SKIP 1
+#endif
 __global__ __launch_bounds__(64) void zstd_parse_kernel(const uint8_t* __restrict__ input,
                                                         uint64_t n_total, uint32_t seg,
                                                         uint8_t* __restrict__ scratch,
                                                         uint64_t sstride,
                                                         uint2* __restrict__ meta, const uint32_t* __restrict__ order) {
   using namespace cmp;
-  __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
+  // (+ one trash entry: probe lanes past the segment insert there, see parse)
+  __shared__ __attribute__((aligned(16))) uint16_t table[(1u << kHashLog) + 8];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];  // + trash bytes
   const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
@@ -700,7 +709,7 @@ __global__ __launch_bounds__(64) void zstd_parse_kernel(const uint8_t* __restric
   o.seqs = reinterpret_cast<GMEM uint2*>(o.dst + zse::lit_cap(seg));
   o.nseq = 0;
   const GMEM uint8_t* in = global_ptr(input + seg_off);
-  parse<zse::SeqCollect, true>(in, n, global_ptr(input + n_total), table, inring, kMaxDist,
+  parse<zse::SeqCollect, true, BITAR_ZSTD_SKIP != 0>(in, n, global_ptr(input + n_total), table, inring, kMaxDist,
                                0xFFFFFFFFu, o);
   o.flush(o.op, true);
   if (lane_id() == 0) meta[i_seg] = make_uint2(o.op, o.nseq);

@@ -430,6 +430,10 @@ __device__ __forceinline__ int huf_read(State& s, uint8_t* win, Tabs& t, uint32_
       rankv += lane == q ? c : 0u;
     }
   }
+  // the longest codes (weight 1) come in pairs, at least one (libzstd HUF_readStats; the
+  // oracle's zs_huf_read)
+  const uint32_t r1 = readlane(rankv, 1);
+  if (r1 < 2 || (r1 & 1u)) return -1;
   uint32_t startv = 0, nxt = 0;
   for (uint32_t q = 1; q <= maxb; ++q) {
     if (lane == q) startv = nxt;

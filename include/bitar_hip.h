@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define BITAR_HIP_ABI_VERSION 1
+#define BITAR_HIP_ABI_VERSION 2
 
 /* negated arrow::StatusCode */
 enum bitar_hip_status {
@@ -50,8 +50,8 @@ enum bitar_hip_codec {
                                           distance <= 14848), 4096-entry table -- the ratio
                                           operating point, within a few % of liblz4's ratio
                                           at a lower speed; the streams are ordinary LZ4 blocks
-                                          (decoded like LZ4).  The front-end selects it with a
-                                          window_size above 12 (config.h:111-114). */
+                                          (decoded like LZ4).  The C++ front-end selects it for
+                                          Codec::LZ4 at level() >= 2 (bitar/config.h). */
 };
 
 /* Per-segment marker written into sizes[] / produced[] when that segment's op failed

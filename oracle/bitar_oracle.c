@@ -30,15 +30,26 @@ uint32_t bo_compressed_seg_size(uint32_t seg) {
 /* ================================================================================ */
 uint32_t bo_lz4_bound(uint32_t n) { return n + n / 255u + 16u; }
 
+/* LZ4 block decode with the block format's rules (lz4 1.9.3 doc/lz4_Block_format.md):
+ * offset 0 and offsets before the block start are invalid, and the end-of-block conditions
+ * hold for any block with a match -- the last sequence is literals only, at least 5 of them
+ * ("the last 5 bytes are always literals"), and the last match starts at least 12 bytes
+ * before the end of the block.  liblz4's LZ4_decompress_safe checks the same conditions
+ * against its output capacity (equal to the block size for a full segment); its two
+ * input-side limits on length-extension bytes are applied as it applies them
+ * (read_variable_length: a literal-length extension must start more than 15 bytes before
+ * the end of the input, and a match-length extension byte must end more than 4 bytes before
+ * it).  tests/test_oracle_vs_stock.py pins these verdicts to liblz4's over mutation corpora. */
 int bo_lz4_decompress_block(const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t cap,
                             uint32_t* produced) {
-  uint64_t ip = 0, op = 0;
+  uint64_t ip = 0, op = 0, last_ml = 0;
   if (csize == 0) return BO_ERR_IO;
   for (;;) {
     if (ip >= csize) return BO_ERR_IO; /* truncated: no token */
     uint32_t token = src[ip++];
     uint64_t lit = token >> 4;
     if (lit == 15) {
+      if (ip + 15 >= csize) return BO_ERR_IO;
       uint32_t b;
       do {
         if (ip >= csize) return BO_ERR_IO;
@@ -51,7 +62,10 @@ int bo_lz4_decompress_block(const uint8_t* src, uint32_t csize, uint8_t* dst, ui
     memcpy(dst + op, src + ip, (size_t)lit);
     ip += lit;
     op += lit;
-    if (ip == csize) break; /* last sequence: literals only */
+    if (ip == csize) { /* last sequence: literals only */
+      if (op > lit && (lit < 5 || lit + last_ml < 12)) return BO_ERR_IO; /* end of block */
+      break;
+    }
     if (ip + 2 > csize) return BO_ERR_IO;
     uint32_t off = (uint32_t)src[ip] | ((uint32_t)src[ip + 1] << 8);
     ip += 2;
@@ -62,6 +76,7 @@ int bo_lz4_decompress_block(const uint8_t* src, uint32_t csize, uint8_t* dst, ui
       do {
         if (ip >= csize) return BO_ERR_IO;
         b = src[ip++];
+        if (ip + 4 >= csize) return BO_ERR_IO;
         mlen += b;
       } while (b == 255);
     }
@@ -69,6 +84,7 @@ int bo_lz4_decompress_block(const uint8_t* src, uint32_t csize, uint8_t* dst, ui
     if (op + mlen > cap) return BO_ERR_IO;
     for (uint64_t i = 0; i < mlen; ++i) dst[op + i] = dst[op - off + i]; /* overlap-safe */
     op += mlen;
+    last_ml = mlen;
   }
   *produced = (uint32_t)op;
   return BO_OK;
@@ -150,7 +166,7 @@ void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
     memset(table, 0, sizeof(uint32_t) << hlog);
     const uint32_t last_start = n - BO_MFLIMIT;        /* match start must be <= n-12 */
     const uint32_t match_limit = n - BO_LASTLITERALS;  /* match end must be <= n-5 */
-    uint32_t pos = 0, g = 0;
+    uint32_t pos = 0, g = 0, done = 0;
     for (uint32_t x = 0; x <= last_start; x += BO_WIN) {
       if (skip) {
         if (pos >= x + BO_WIN) continue; /* inside the current match */
@@ -170,6 +186,7 @@ void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
           g = x + BO_WIN * (s - 1) - 127u;
         }
       }
+      if ((flags & BO_PARSE_GAPS) && done < x) emit(ctx, done, x - done, BO_GAP_OFF, 0);
       uint32_t cnt = last_start - x + 1;
       if (cnt > BO_WIN) cnt = BO_WIN;
       uint32_t cand[BO_WIN], h[BO_WIN];
@@ -228,6 +245,7 @@ void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist,
         }
       }
       if (pos > g) g = pos;
+      done = pos > x + BO_WIN ? pos : x + BO_WIN;
     }
   }
   emit(ctx, anchor, n - anchor, 0, 0); /* last sequence: literals only */
@@ -358,9 +376,12 @@ typedef struct {
   uint16_t symbol[320];
 } bo_huff;
 
-/* Build from code lengths.  Over-subscribed sets are an error; incomplete sets are
- * accepted (decoding an unassigned code is then an error). */
-static int huff_build(bo_huff* h, const uint8_t* lens, int n) {
+/* Build from code lengths.  Over-subscribed sets are an error.  type < 0 (the fixed codes):
+ * incomplete sets are accepted.  Dynamic blocks follow zlib 1.2.11's inflate_table: an
+ * incomplete set is an error too, except a code with no symbols at all (decoding one is then
+ * an error) and -- type 1 literal/length, type 2 distance codes, not type 0 the code-length
+ * code -- a code whose longest length is 1 (a single one-bit code). */
+static int huff_build(bo_huff* h, const uint8_t* lens, int n, int type) {
   uint16_t offs[16];
   memset(h->count, 0, sizeof(h->count));
   for (int s = 0; s < n; ++s) h->count[lens[s]]++;
@@ -371,6 +392,9 @@ static int huff_build(bo_huff* h, const uint8_t* lens, int n) {
     left -= h->count[len];
     if (left < 0) return -1;
   }
+  int max = 15;
+  while (max >= 1 && !h->count[max]) --max;
+  if (type >= 0 && left > 0 && max > 0 && (type == 0 || max != 1)) return -1;
   offs[1] = 0;
   for (int len = 1; len < 15; ++len) offs[len + 1] = (uint16_t)(offs[len] + h->count[len]);
   for (int s = 0; s < n; ++s)
@@ -459,8 +483,8 @@ int bo_inflate_raw(const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t ca
     } else if (type == 1) {
       uint8_t ll[288], dl[30];
       fixed_lengths(ll, dl);
-      huff_build(&lit, ll, 288);
-      huff_build(&dist, dl, 30);
+      huff_build(&lit, ll, 288, -1);
+      huff_build(&dist, dl, 30, -1);
       int r = inflate_codes(&b, &lit, &dist, dst, cap, &op);
       if (r) return r;
     } else if (type == 2) {
@@ -476,7 +500,7 @@ int bo_inflate_raw(const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t ca
         cl[kClOrder[i]] = (uint8_t)v;
       }
       bo_huff clh;
-      if (huff_build(&clh, cl, 19)) return BO_ERR_IO;
+      if (huff_build(&clh, cl, 19, 0)) return BO_ERR_IO;
       uint8_t lens[320];
       int idx = 0;
       while (idx < nlen + ndist) {
@@ -507,8 +531,8 @@ int bo_inflate_raw(const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t ca
         while (rep--) lens[idx++] = val;
       }
       if (lens[256] == 0) return BO_ERR_IO; /* no end-of-block code */
-      if (huff_build(&lit, lens, nlen)) return BO_ERR_IO;
-      if (huff_build(&dist, lens + nlen, ndist)) return BO_ERR_IO;
+      if (huff_build(&lit, lens, nlen, 1)) return BO_ERR_IO;
+      if (huff_build(&dist, lens + nlen, ndist, 2)) return BO_ERR_IO;
       int r = inflate_codes(&b, &lit, &dist, dst, cap, &op);
       if (r) return r;
     } else {
@@ -586,6 +610,8 @@ int bo_deflate_fixed_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_
   const uint64_t nblk = n ? (n + 65534u) / 65535u : 1;
   const uint64_t stored = nblk * 5 + n;
   if (stored < fixed + BO_STORE_MARGIN(n)) {
+    /* (stored can exceed a cap the fixed block just fit in by up to n / 16 bytes) */
+    if (stored > cap) return BO_ERR_IO;
     uint64_t o = 0;
     uint32_t p = 0;
     for (uint64_t b = 0; b < nblk; ++b) {

@@ -94,6 +94,10 @@ void bo_huff_lengths(const uint32_t* freq, int nsym, int maxlen, uint8_t* lens);
 int bo_zstd_decompress(const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t cap,
                        uint32_t* produced);
 uint64_t bo_xxh64(const uint8_t* p, uint64_t len, uint64_t seed);
+/* tests: why the last bo_zstd_decompress on this thread rejected (0: another reason) */
+#define BO_ZSTD_REJECT_HUF_END 1      /* a Huffman stream not consumed exactly (detail: bits left) */
+#define BO_ZSTD_REJECT_SEQ_OVERREAD 2 /* the sequence bitstream read past its start */
+int bo_zstd_last_reject(int64_t* detail);
 /* Encode one segment as one Zstandard frame, exactly as the HIP kernel does (bitar
  * window-scan parse; blocks of <= 512 sequences; raw literals; predefined FSE sequence
  * codes; no repeat offsets; a block that does not shrink is stored raw).  cap must be
@@ -113,7 +117,18 @@ void bo_window_parse(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t
 #define BO_PARSE_REP 1u
 #define BO_PARSE_SKIP 2u
 #define BO_PARSE_HLOG(h) ((uint32_t)(h) << 8) /* hash table log2 size (0: 10) */
+/* test hook: before each window it scans, the parse reports the positions [done, x) that
+ * skipped probe windows covered since the last scanned window, as emit(ctx, done, x - done,
+ * BO_GAP_OFF, 0) */
+#define BO_PARSE_GAPS (1u << 16)
+#define BO_GAP_OFF 0xFFFFFFFFu
 uint32_t bo_set_lz4_parse_flags(uint32_t flags);
+/* Zstd parse flags (default BO_PARSE_REP | BO_PARSE_SKIP, the shipped zstd_parse_kernel).
+ * BO_ZSTD_DROP_GAP_LITERALS reproduces the round-3 experimental GPU emitter (its literal
+ * section lacked the bytes of skipped probe windows): the tests check that such frames are
+ * rejected by libzstd and by bo_zstd_decompress alike. */
+#define BO_ZSTD_DROP_GAP_LITERALS (1u << 17)
+uint32_t bo_set_zstd_parse_flags(uint32_t flags);
 void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t max_mlen,
                            uint32_t flags, bo_emit_fn emit, void* ctx);
 

@@ -307,6 +307,10 @@ static int zs_huf_read(zs_huf* h, const uint8_t* src, uint32_t len) {
   /* HUF_readDTableX1 */
   uint32_t rank[13] = {0};
   for (uint32_t i = 0; i < nw; ++i) rank[w[i]]++;
+  /* the longest codes (weight 1) come in pairs, at least one: libzstd's HUF_readStats
+   * rejects any other description ("tree construction validity"), though such weights can
+   * still form a complete code (e.g. 2 2 3: lengths 2 2 1 under a table log of 3) */
+  if (rank[1] < 2 || (rank[1] & 1)) return -1;
   uint32_t next = 0;
   for (uint32_t n = 1; n <= maxb; ++n) {
     const uint32_t cur = next;
@@ -329,6 +333,16 @@ static int zs_huf_read(zs_huf* h, const uint8_t* src, uint32_t len) {
   return used;
 }
 
+/* why the last bo_zstd_decompress on this thread rejected its frame (tests only): a Huffman
+ * literal stream that was not consumed exactly records BO_ZSTD_REJECT_HUF_END and the
+ * remaining bit count (negative: read past the stream's start) */
+static __thread int g_zs_reject;
+static __thread int64_t g_zs_reject_detail;
+int bo_zstd_last_reject(int64_t* detail) {
+  if (detail) *detail = g_zs_reject_detail;
+  return g_zs_reject;
+}
+
 static int zs_huf_stream(const zs_huf* h, const uint8_t* src, uint32_t len, uint8_t* out,
                          uint32_t n) {
   zs_bwd b;
@@ -338,7 +352,12 @@ static int zs_huf_stream(const zs_huf* h, const uint8_t* src, uint32_t len, uint
     out[i] = h->sym[v];
     b.pos -= h->nbits[v];
   }
-  return b.pos == 0 ? 0 : -1;
+  if (b.pos != 0) {
+    g_zs_reject = BO_ZSTD_REJECT_HUF_END;
+    g_zs_reject_detail = b.pos;
+    return -1;
+  }
+  return 0;
 }
 
 /* ================================================================================ */
@@ -477,7 +496,7 @@ static int zs_block(zs_ctx* z, const uint8_t* src, uint32_t len, uint8_t* dst, u
                sml = (uint32_t)zs_read(&b, z->ml.al);
       for (uint32_t k = 0; k < nseq; ++k) {
         const uint32_t llc = z->ll.t[sll].sym, ofc = z->of.t[sof].sym, mlc = z->ml.t[sml].sym;
-        if (llc > 35 || mlc > 52 || ofc > 31) goto out;
+        if (llc > 35 || mlc > 52 || ofc > 31) goto seq_fail;
         const uint32_t ofv = (1u << ofc) + (uint32_t)zs_read(&b, ofc);
         const uint32_t ml = kMLBase[mlc] + (uint32_t)zs_read(&b, kMLBits[mlc]);
         const uint32_t ll = kLLBase[llc] + (uint32_t)zs_read(&b, kLLBits[llc]);
@@ -502,19 +521,26 @@ static int zs_block(zs_ctx* z, const uint8_t* src, uint32_t len, uint8_t* dst, u
             z->rep[2] = z->rep[1]; z->rep[1] = z->rep[0]; z->rep[0] = off;
           } else {
             off = z->rep[0] - 1;
-            if (off == 0) goto out;
+            if (off == 0) goto seq_fail;
             z->rep[2] = z->rep[1]; z->rep[1] = z->rep[0]; z->rep[0] = off;
           }
         }
-        if (lp + ll > regen || (uint64_t)op + ll + ml > cap) goto out;
+        if (lp + ll > regen || (uint64_t)op + ll + ml > cap) goto seq_fail;
         memcpy(dst + op, lit + lp, ll);
         op += ll;
         lp += ll;
-        if (off == 0 || off > op) goto out;  /* no dictionary: history is this frame */
+        if (off == 0 || off > op) goto seq_fail;  /* no dictionary: history is this frame */
         for (uint32_t i = 0; i < ml; ++i) dst[op + i] = dst[op - off + i];
         op += ml;
       }
-      if (b.pos != 0) goto out;
+      if (b.pos == 0) goto seq_done;
+    seq_fail:
+      if (b.pos < 0) { /* the sequence bitstream was read past its start */
+        g_zs_reject = BO_ZSTD_REJECT_SEQ_OVERREAD;
+        g_zs_reject_detail = b.pos;
+      }
+      goto out;
+    seq_done:;
     } else if (p != len) {
       goto out;
     }
@@ -532,6 +558,8 @@ out:
 
 int bo_zstd_decompress(const uint8_t* src, uint32_t csize, uint8_t* dst, uint32_t cap,
                        uint32_t* produced) {
+  g_zs_reject = 0;
+  g_zs_reject_detail = 0;
   if (csize < 6 || rd32le(src) != 0xFD2FB528u) return BO_ERR_IO;
   uint32_t p = 4;
   const uint32_t fhd = src[p++];
@@ -1028,12 +1056,16 @@ typedef struct {
   uint32_t* ll;
   uint32_t* ml;
   uint32_t* off;
+  uint8_t* drop;  /* BO_ZSTD_DROP_GAP_LITERALS: positions whose literal byte is left out */
 } zs_parsed;
 
 static void zs_collect(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_t off,
                        uint32_t mlen) {
   zs_parsed* z = (zs_parsed*)vctx;
-  (void)lit_start;
+  if (off == BO_GAP_OFF && !mlen) { /* (BO_PARSE_GAPS: only with a drop map) */
+    memset(z->drop + lit_start, 1, lit_len);
+    return;
+  }
   z->nlit += lit_len;  /* bytes are gathered from the positions afterwards */
   if (mlen) {
     z->ll[z->nseq] = lit_len;
@@ -1041,6 +1073,17 @@ static void zs_collect(void* vctx, uint32_t lit_start, uint32_t lit_len, uint32_
     z->off[z->nseq] = off;
     z->nseq++;
   }
+}
+
+/* The parse of the Zstd encoder: the repeat-offset form with window skipping (the shipped
+ * zstd_parse_kernel).  Round 3 tried this combination on the GPU and its frames failed
+ * libzstd: the kernel's literal collector staged literal bytes window by window and had no
+ * case for the positions of skipped probe windows (BO_ZSTD_DROP_GAP_LITERALS restates it). */
+static uint32_t g_zstd_parse_flags = BO_PARSE_REP | BO_PARSE_SKIP;
+uint32_t bo_set_zstd_parse_flags(uint32_t flags) {
+  const uint32_t old = g_zstd_parse_flags;
+  g_zstd_parse_flags = flags;
+  return old;
 }
 
 uint32_t bo_zstd_bound(uint32_t n) {
@@ -1062,7 +1105,15 @@ int bo_zstd_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_
   uint32_t* ov = (uint32_t*)malloc(4u * maxseq);
   int rc = BO_ERR_OUT_OF_MEMORY;
   if (!z.lit || !z.ll || !z.ml || !z.off || !codes || !ov) goto out;
-  bo_window_parse_flags(src, n, BO_MAX_DIST_ALL, 0xFFFFFFFFu, BO_PARSE_REP, zs_collect, &z);
+  {
+    const uint32_t fl = g_zstd_parse_flags;
+    if (fl & BO_ZSTD_DROP_GAP_LITERALS) {
+      z.drop = (uint8_t*)calloc(n + 1, 1);
+      if (!z.drop) goto out;
+    }
+    bo_window_parse_flags(src, n, BO_MAX_DIST_ALL, 0xFFFFFFFFu,
+                          (fl & 0xFFFFu) | (z.drop ? BO_PARSE_GAPS : 0u), zs_collect, &z);
+  }
   {
     /* literal bytes: everything outside the matches */
     uint32_t ip = 0, lp = 0;
@@ -1074,6 +1125,18 @@ int bo_zstd_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_
     memcpy(z.lit + lp, src + ip, n - ip);
     lp += n - ip;
     if (lp != z.nlit) { rc = BO_ERR_IO; goto out; }
+    if (z.drop) { /* the broken collector: literal bytes of the gaps never reached the section */
+      uint32_t q = 0;
+      ip = 0;
+      for (uint32_t i = 0; i <= z.nseq; ++i) {
+        const uint32_t ll = i < z.nseq ? z.ll[i] : n - ip;
+        for (uint32_t k = 0; k < ll; ++k) {
+          if (!z.drop[ip + k]) z.lit[q++] = src[ip + k];
+        }
+        ip += ll + (i < z.nseq ? z.ml[i] : 0);
+      }
+      z.nlit = q;
+    }
   }
   /* repeat offsets (RFC 8878 3.1.2.5) */
   {
@@ -1139,7 +1202,7 @@ int bo_zstd_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_
         }
         const uint32_t mp = p++;  /* Symbol_Compression_Modes */
         zs_bw w = {dst, p, cap, 0, 0, 0};
-        static zs_seqtab tll, tof, tml;  /* (large: not on the stack) */
+        static __thread zs_seqtab tll, tof, tml;  /* (large: not on the stack; per thread) */
         zs_choose(&tll, llc, nseq, 35, 9, kLLDefault, 35, ZS_LL_AL, &w);
         zs_choose(&tof, ofc, nseq, 31, 8, kOFDefault, 28, ZS_OF_AL, &w);
         zs_choose(&tml, mlc, nseq, 52, 9, kMLDefault, 52, ZS_ML_AL, &w);
@@ -1188,6 +1251,6 @@ int bo_zstd_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_
     rc = BO_OK;
   }
 out:
-  free(z.lit); free(z.ll); free(z.ml); free(z.off); free(codes); free(ov);
+  free(z.lit); free(z.ll); free(z.ml); free(z.off); free(codes); free(ov); free(z.drop);
   return rc;
 }

@@ -62,9 +62,15 @@ void CpuTests() {
   CHECK(bitar::internal::kMaxSegSize == 59460);
   CHECK(c.ToString().find("checksum_type: NONE") != std::string::npos);
   CHECK(c.type_name() == bitar::kHipConfigurationTypeName);
-  // memory pools exist and the reference names alias the HIP ones
+  // memory pools exist; the reference's DPDK pools are host memory the engine reads
+  // (memory_pool.cc:70-188), so both names alias the pinned host pool
   CHECK(bitar::GetMemoryPool(bitar::MemoryPoolBackend::Rtememzone) ==
-        bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipDevice));
+        bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipHost));
+  CHECK(bitar::GetMemoryPool(bitar::MemoryPoolBackend::Rtemalloc) ==
+        bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipHost));
+  CHECK(bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipDevice) !=
+        bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipHost));
+  CHECK(c.level() == 1 && c.ToString().find("level: 1") != std::string::npos);
   CHECK(bitar::GetMemoryPool(bitar::MemoryPoolBackend::System) != nullptr);
   uint8_t* p = nullptr;
   CHECK_OK(bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipDevice)->Allocate(0, 64, &p));
@@ -333,6 +339,60 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
             std::memcmp((*back)->data(), data.data(), data.size()) == 0);
     CHECK(d->Recycle(*comp) == comp->size());
     CHECK(d->Recycle(*comp2) == comp2->size());
+  }
+  // the reference's demo flow over its memzone pool (demo_app.cc:121-122, 589-592): the
+  // input is written on the CPU into an Rtememzone buffer, compressed, decompressed into
+  // another Rtememzone buffer and compared on the CPU
+  {
+    auto fresh = driver->GetDevices({(*ids)[0]});
+    CHECK_OK(fresh.status());
+    auto& d = (*fresh)[0];
+    CHECK_OK(d->Initialize(MakeConfig(bitar::Codec::LZ4, 65536)));
+    auto* pool = bitar::GetMemoryPool(bitar::MemoryPoolBackend::Rtememzone);
+    auto in = arrow::AllocateBuffer(static_cast<int64_t>(data.size()), pool);
+    CHECK_OK(in.status());
+    std::shared_ptr<arrow::Buffer> zin = std::move(*in);
+    std::memcpy(zin->mutable_data(), data.data(), data.size());  // host write (rte_memcpy)
+    auto comp = d->Compress(0, zin);
+    CHECK_OK(comp.status());
+    const auto nseg = (data.size() + 65535) / 65536;
+    auto out = arrow::AllocateResizableBuffer(static_cast<int64_t>(nseg * 65536), pool);
+    CHECK_OK(out.status());
+    std::unique_ptr<arrow::ResizableBuffer> zout = std::move(*out);
+    if (comp.ok()) {
+      CHECK_OK(d->Decompress(0, *comp, zout));
+      CHECK(zout->size() == static_cast<int64_t>(data.size()) &&
+            std::memcmp(zout->data(), data.data(), data.size()) == 0);  // host read
+      CHECK(d->Recycle(*comp) == comp->size());
+    }
+    // Reallocate keeps the bytes (the reference copies memzones with rte_memcpy, 151-174)
+    CHECK_OK(zout->Resize(static_cast<int64_t>(nseg * 65536 + 4096)));
+    CHECK(std::memcmp(zout->data(), data.data(), data.size()) == 0);
+  }
+  // LZ4 at level 2 = the wide parse (the ratio point): smaller output, same round trip;
+  // <outdir>/lz4_wide.segs is checked against the oracle's wide parse by the Python side
+  {
+    auto fresh = driver->GetDevices({(*ids)[0]});
+    CHECK_OK(fresh.status());
+    auto& d = (*fresh)[0];
+    auto cfg = MakeConfig(bitar::Codec::LZ4, 65536);
+    cfg->set_level(2);
+    CHECK_OK(d->Initialize(std::move(cfg)));
+    auto comp = d->Compress(0, host_in);
+    CHECK_OK(comp.status());
+    if (comp.ok()) {
+      WriteSegments(outdir + "/lz4_wide.segs", *comp);
+      auto out = arrow::AllocateResizableBuffer(static_cast<int64_t>(comp->size() * 65536));
+      std::unique_ptr<arrow::ResizableBuffer> o = std::move(*out);
+      CHECK_OK(d->Decompress(0, *comp, o));
+      CHECK(o->size() == static_cast<int64_t>(data.size()) &&
+            std::memcmp(o->data(), data.data(), data.size()) == 0);
+    }
+    auto bad = driver->GetDevices({(*ids)[0]});
+    CHECK_OK(bad.status());
+    auto cfg0 = MakeConfig(bitar::Codec::LZ4, 65536);
+    cfg0->set_level(0);
+    CHECK((*bad)[0]->Initialize(std::move(cfg0)).IsInvalid());
   }
   // empty input -> empty vector (device.cc:161-164); empty vector -> OK
   auto& d0 = (*devs)[0];

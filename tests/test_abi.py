@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_slot_sizes():
     L = bitar_amd.lib()
-    assert L.bitar_hip_abi_version() == 1
+    assert L.bitar_hip_abi_version() == 2
     # LZ4_compressBound(65536) = 65809 -> 256-B rounded slot
     assert bitar_amd.slot_size(bitar_amd.CODEC_LZ4, 65536) == 66048
     assert bitar_amd.slot_size(bitar_amd.CODEC_LZ4, 59460) >= 59460 + 59460 // 255 + 16

@@ -71,6 +71,13 @@ def test_frontend_on_gpu(tmp_path):
     for i, s in enumerate(segs):
         rc, plain = O.lz4_decompress(s, seg)
         assert rc == 0 and plain == data[i * seg:(i + 1) * seg]
+        assert O.lz4_compress(plain) == (0, s), ("lz4", i)
+    # Codec::LZ4 at level 2: the wide parse, bit-exact with the oracle's, smaller in total
+    wide = _segments(tmp_path / "lz4_wide.segs")
+    assert len(wide) == len(segs)
+    for i, s in enumerate(wide):
+        assert O.lz4_wide_compress(data[i * seg:(i + 1) * seg]) == (0, s), ("lz4_wide", i)
+    assert sum(map(len, wide)) < sum(map(len, segs))
     # configured checksums: CRC32 | Adler32 << 32 of every 64 KiB segment (vs zlib)
     cs = np.fromfile(tmp_path / "checksums.bin", dtype=np.uint64)
     assert cs.size == (len(data) + 65535) // 65536
@@ -82,6 +89,7 @@ def test_frontend_on_gpu(tmp_path):
     for i, s in enumerate(segs):
         rc, plain = O.zstd_decompress(s, seg)
         assert rc == 0 and plain == data[i * seg:(i + 1) * seg]
+        assert O.zstd_compress(plain) == (0, s), ("zstd", i)
     # chained ops (max_sgl_segs = 4 over 16 KiB segments): the 4 buffers of op j joined are
     # one stream of input bytes [j*64Ki, (j+1)*64Ki), the oracle's own encoding of them
     seg, k = 16384, 4

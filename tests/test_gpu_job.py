@@ -1,11 +1,12 @@
 """GPU tests of the sharded job (bitar_amd.job.ShardedJob): BASELINE configs[3] at full
 size on one GPU -- an 8 GiB Arrow record-batch job of 64 KiB chunks, round-robin batches,
 four concurrent queue-pair streams -- with a byte-exact round trip, a frame index spanning
-the job, and sampled chunks bit-exact against the oracle; plus the offset generator the
-ranks use to materialise only their batches."""
+the job, and EVERY chunk bit-exact against the oracle (tests/gpu_parity.py); plus the offset
+generator the ranks use to materialise only their batches."""
 import numpy as np
 import pytest
 
+import gpu_parity as P
 import oracle_lib as O
 from test_gpu_lz4 import down, eng  # noqa: F401  (fixture reuse)
 
@@ -41,12 +42,9 @@ def test_recordbatch_8gib_four_streams():
         sizes = down(job.sizes).astype(np.uint32)
         assert int(job.index[-1].item()) == int(sizes.astype(np.int64).sum())
         assert np.array_equal(np.diff(down(job.index)), sizes.astype(np.int64))
-        for g in (0, 255, 256, 32767, 32768, 65537, 131071):  # part boundaries included
-            plain = down(job.data[g * seg:(g + 1) * seg])
-            r, comp = O.lz4_compress(plain.tobytes())
-            assert r == 0 and len(comp) == sizes[g], g
-            got = down(job.slab[g * job.stride:g * job.stride + int(sizes[g])]).tobytes()
-            assert got == comp, g
+        # every one of the 131072 chunks (all four parts, their boundaries included)
+        P.assert_every_segment_matches_oracle(bitar_amd.CODEC_LZ4, job.data, 8 << 30, seg,
+                                              job.slab, job.stride, job.sizes)
         job.free()
     finally:
         e.close()
@@ -56,7 +54,7 @@ def test_zstd_column_8gib_configs4():
     """BASELINE configs[4] at its full 8 GiB job size on one GPU: level-1-class Zstd frames
     per 64 KiB chunk of an int64 column buffer (kind 5, the Parquet-column shape), dealt in
     round-robin batches over two queue-pair streams, byte-exact round trip, the job-wide frame
-    index, and sampled chunks bit-exact against the oracle's encoder."""
+    index, and every chunk bit-exact against the oracle's encoder."""
     import bitar_amd
     from bitar_amd.job import ShardedJob
     if not torch.cuda.is_available():
@@ -73,12 +71,8 @@ def test_zstd_column_8gib_configs4():
         sizes = down(job.sizes).astype(np.uint32)
         assert int(job.index[-1].item()) == int(sizes.astype(np.int64).sum())
         assert sizes.astype(np.int64).sum() < (8 << 30) // 3  # a column compresses > 3x
-        for g in (0, 255, 256, 65535, 65536, 131071):
-            plain = down(job.data[g * seg:(g + 1) * seg])
-            r, comp = O.zstd_compress(plain.tobytes())
-            assert r == 0 and len(comp) == sizes[g], g
-            got = down(job.slab[g * job.stride:g * job.stride + int(sizes[g])]).tobytes()
-            assert got == comp, g
+        P.assert_every_segment_matches_oracle(bitar_amd.CODEC_ZSTD, job.data, 8 << 30, seg,
+                                              job.slab, job.stride, job.sizes)
         job.free()
     finally:
         e.close()

@@ -14,12 +14,10 @@ byte-equal output when accepted -- the reference's per-op rule (src/device.cc:51
 failed op fails the call, never yields wrong bytes).  The context's path counters
 (bitar_hip_path_counters) show that the mutations reached the targeted kernels.
 """
-import ctypes
-import zlib
-
 import numpy as np
 import pytest
 
+import mutation_corpora as M
 import oracle_lib as O
 from test_gpu_lz4 import _decode_blobs, eng  # noqa: F401  (fixture reuse)
 
@@ -30,30 +28,7 @@ torch = pytest.importorskip("torch")
 SEG = 65536
 
 
-def _mutations(frame, rng, count, hot=None):
-    """count seeded mutations of frame: bit flips, byte sets, truncations, and bit flips in
-    `hot` = (lo, hi), the byte range that holds the structure under test (block / table
-    headers, the sequence bitstream)."""
-    out = []
-    for _ in range(count):
-        b = bytearray(frame)
-        kind = int(rng.integers(0, 5))
-        if kind == 0:  # bit flip anywhere
-            i = int(rng.integers(0, len(b)))
-            b[i] ^= 1 << int(rng.integers(0, 8))
-        elif kind == 1:  # byte set
-            i = int(rng.integers(0, len(b)))
-            b[i] = int(rng.integers(0, 256))
-        elif kind == 2:  # truncation
-            b = b[:int(rng.integers(0, len(b)))]
-        else:  # one or two bit flips in the hot range
-            lo, hi = hot if hot else (0, len(b))
-            hi = max(lo + 1, min(hi, len(b)))
-            for _ in range(1 + (kind == 4)):
-                i = int(rng.integers(lo, hi))
-                b[i] ^= 1 << int(rng.integers(0, 8))
-        out.append(bytes(b) if b else b"\x00")
-    return out
+_mutations = M.mutations  # (tests/mutation_corpora.py: the corpora the CPU test pins to stock)
 
 
 def _check_like_oracle(eng, codec, cases, oracle):
@@ -79,17 +54,7 @@ def counting_inflate(request, eng):
     eng.set_decoder_options(**old)
 
 
-def _dynamic_sources():
-    srcs = []
-    for kind, n, seed in ((1, 59460, 11), (2, 59460, 12), (6, 40000, 13), (5, 30000, 14),
-                          (1, 20000, 15)):
-        plain = O.fill(kind, seed, n).tobytes()
-        r, ours = O.deflate_dynamic(plain)  # == deflate_dyn_*_kernel's stream (bit-exact)
-        assert r == 0 and O.deflate_dynamic_mode(plain) == 2  # a dynamic block
-        z = zlib.compressobj(1, zlib.DEFLATED, -15, 8, zlib.Z_DEFAULT_STRATEGY)
-        stock = z.compress(plain) + z.flush()  # zlib level 1: the reference's frame
-        srcs += [(ours, plain), (stock, plain)]
-    return srcs
+_dynamic_sources = M.dynamic_sources
 
 
 def test_inflate_batch_mutations_like_oracle(eng, counting_inflate):
@@ -117,16 +82,7 @@ def test_inflate_batch_mutations_like_oracle(eng, counting_inflate):
 
 def test_inflate_fixed_and_stored_mutations_like_oracle(eng, counting_inflate):
     """Fixed-Huffman (the lane inflater's own path) and stored streams, mutated."""
-    rng = np.random.default_rng(1952)
-    cases = []
-    for kind, n, seed in ((1, 59460, 21), (6, 30000, 22), (0, 20000, 23)):
-        plain = O.fill(kind, seed, n).tobytes()
-        r, fixed = O.deflate_fixed(plain)
-        assert r == 0
-        z = zlib.compressobj(1, zlib.DEFLATED, -15, 8, zlib.Z_FIXED)
-        cases += _mutations(fixed, rng, 32, hot=(0, 64))
-        cases += _mutations(z.compress(plain) + z.flush(), rng, 32, hot=(0, 64))
-    _check_like_oracle(eng, O.CODEC_DEFLATE, cases, O.inflate)
+    _check_like_oracle(eng, O.CODEC_DEFLATE, M.inflate_fixed_cases(), O.inflate)
 
 
 # ---- Zstd: hand-off -> phase A (seqdec) -> phase B (exec) ---------------------------------
@@ -138,45 +94,8 @@ def counting_zstd(request, eng):
     eng.set_decoder_options(**old)
 
 
-def _libzstd():
-    try:
-        L = ctypes.CDLL("/opt/conda/lib/libzstd.so.1.4.9")
-    except OSError:
-        return None
-    L.ZSTD_compress.restype = ctypes.c_size_t
-    L.ZSTD_compress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
-                                ctypes.c_size_t, ctypes.c_int]
-    L.ZSTD_isError.restype = ctypes.c_uint
-    L.ZSTD_isError.argtypes = [ctypes.c_size_t]
-    return L
-
-
-def _zstd_sources():
-    srcs = []
-    Z = _libzstd()
-    for kind, n, seed in ((2, 65536, 31), (1, 65536, 32), (5, 65536, 33), (6, 50000, 34),
-                          (2, 30000, 35)):
-        plain = O.fill(kind, seed, n).tobytes()
-        r, ours = O.zstd_compress(plain)  # == the GPU encoder's frame (bit-exact), no checksum
-        assert r == 0
-        srcs.append((ours, plain))
-        if Z is not None:  # libzstd level 1, ZSTD_compress: no checksum by default
-            buf = ctypes.create_string_buffer(n + 1024)
-            r = Z.ZSTD_compress(buf, n + 1024, plain, n, 1)
-            assert not Z.ZSTD_isError(r)
-            srcs.append((buf.raw[:r], plain))
-    return srcs
-
-
-def _fcs_flip(frame):
-    """frame with the low bit of its Frame_Content_Size flipped (RFC 8878 3.1.1.1)"""
-    fhd = frame[4]
-    single, fcs_flag, did = (fhd >> 5) & 1, fhd >> 6, fhd & 3
-    at = 5 + (0 if single else 1) + (0, 1, 2, 4)[did]
-    assert single or fcs_flag, "frame without a content size"
-    b = bytearray(frame)
-    b[at] ^= 1
-    return bytes(b)
+_zstd_sources = M.zstd_sources
+_fcs_flip = M.fcs_flip
 
 
 def test_zstd_sequence_path_mutations_like_oracle(eng, counting_zstd):
@@ -254,30 +173,11 @@ def test_lz4_far_path_mutations_like_oracle(eng):
     old = eng.set_decoder_options(count_paths=1)
     try:
         eng.path_counters()
-        rng = np.random.default_rng(1977)
-        bases = []
-        for kind, n, seed in ((1, 65536, 41), (2, 65536, 42), (5, 65536, 43), (6, 40000, 44)):
-            plain = O.fill(kind, seed, n).tobytes()
-            r, wide = O.lz4_wide_compress(plain)
-            assert r == 0
-            bases.append(wide)
-        try:
-            L = ctypes.CDLL("liblz4.so.1")
-            L.LZ4_compress_default.restype = ctypes.c_int
-            for kind, n, seed in ((1, 65536, 45), (5, 65536, 46)):
-                plain = O.fill(kind, seed, n).tobytes()
-                buf = ctypes.create_string_buffer(n + n // 255 + 16)
-                r = L.LZ4_compress_default(plain, buf, n, len(buf))
-                assert r > 0
-                bases.append(buf.raw[:r])
-        except OSError:
-            pass
+        bases = [b for b, _ in M.lz4_far_sources()]
         _check_like_oracle(eng, O.CODEC_LZ4, bases, O.lz4_decompress)
         c0 = eng.path_counters()
         assert c0["lz4_far"] > 0, c0
-        cases = []
-        for b in bases:
-            cases += _mutations(b, rng, 40, hot=(len(b) // 2, len(b)))
+        cases = M.lz4_far_cases()
         n_ok = _check_like_oracle(eng, O.CODEC_LZ4, cases, O.lz4_decompress)
         c = eng.path_counters()
         assert c["lz4_far"] > len(cases) // 4, c
@@ -285,3 +185,17 @@ def test_lz4_far_path_mutations_like_oracle(eng):
         print(f"lz4 far mutations: {len(cases)} cases, {n_ok} accepted, counters {c}")
     finally:
         eng.set_decoder_options(**old)
+
+
+def test_lz4_near_mutations_and_end_rules_like_oracle(eng):
+    """Our own LZ4 blocks mutated near their end (the batch -> general path hand-over) and
+    crafted blocks around the block format's end conditions (final literal run >= 5, last
+    match >= 12 bytes before the end; the oracle's bo_lz4_decompress_block, pinned to liblz4
+    by tests/test_oracle_vs_stock.py): the near kernel's verdicts and bytes are the oracle's,
+    including blocks whose last match was decoded inside a batch (re-walked at the end)."""
+    cases = M.lz4_near_cases()
+    n_ok = _check_like_oracle(eng, O.CODEC_LZ4, cases, O.lz4_decompress)
+    assert 0 < n_ok < len(cases)
+    crafted = M.lz4_end_rule_cases()
+    n_ok = _check_like_oracle(eng, O.CODEC_LZ4, crafted, O.lz4_decompress)
+    assert 0 < n_ok < len(crafted)

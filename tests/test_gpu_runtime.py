@@ -272,3 +272,57 @@ def test_copy_batch_any_alignment(eng):
     for so, do, n in entries:
         want[do:do + n] = s[so:so + n]
     assert np.array_equal(d, want)
+
+
+def test_sync_null_leaves_foreign_stream_errors():
+    """sync(NULL) reads and clears only the default stream's and the queue pairs' error words:
+    a failure on a foreign (torch side) stream is reported exactly once, by a sync of that
+    stream, whether or not a sync(NULL) came first (a NULL sync that cleared it could lose it
+    to work still running there)."""
+    import bitar_amd
+    e = bitar_amd.Engine(0, num_streams=1)
+    try:
+        seg = 65536
+        side = torch.cuda.Stream()
+        bs, bz = _slab([bytes([0, 0, 0])], 512)
+        torch.cuda.synchronize()
+        bo, bp = e.empty(seg), e.empty(1, dtype=torch.int32)
+        e.decompress_slab_into(O.CODEC_LZ4, bs, 512, bz, 1, seg, bo, bp, stream=side)
+        side.synchronize()
+        e.sync(False)  # NULL: not this stream's word
+        with pytest.raises(bitar_amd.BitarError) as ex:
+            e.sync(side)
+        assert ex.value.code == -5
+        e.sync(side)  # reported once
+        e.sync(False)
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("codec", [O.CODEC_ZSTD, O.CODEC_DEFLATE_DYN])
+def test_two_scratch_chunks_bit_exact(codec):
+    """Calls above 32768 segments run in chunks over one scratch allocation (runtime.hip
+    kChunkSegs): 64 MiB at seg 1024 = 65536 segments = two chunks; every segment's stream
+    equals the oracle's, and the decode of the whole call is byte-exact."""
+    import bitar_amd
+    e = bitar_amd.Engine(0)
+    try:
+        seg, n = 1024, 64 << 20
+        data = O.fill(O.KIND_ARROW, 77, n)
+        d = up(data)
+        slab, stride, sizes = e.compress(codec, d, seg)
+        out, prod = e.decompress(codec, slab, stride, sizes, seg)
+        e.sync()
+        assert torch.equal(out[:n], d)
+        assert np.array_equal(down(prod).astype(np.uint32), np.full(n // seg, seg, np.uint32))
+        r, oslab, osz = O.compress_segments(codec, data, seg, stride, 16)
+        assert r == 0
+        gsz = down(sizes).astype(np.uint32)
+        assert np.array_equal(gsz, osz)
+        g = down(slab).reshape(-1, stride)
+        o = oslab.reshape(-1, stride)
+        col = np.arange(stride)[None, :]
+        mask = col < osz[:, None]
+        assert np.array_equal(g[mask], o[mask])
+    finally:
+        e.close()

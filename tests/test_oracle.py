@@ -408,3 +408,78 @@ def test_lz4_wide_parse_ratio_and_streams():
         blobs = [slabw[i * stride:i * stride + sizesw[i]] for i in range(sizesw.size)]
         r, out, prod = O.decompress_segments(O.CODEC_LZ4_WIDE, blobs, seg, n, 4)
         assert r == 0 and np.array_equal(out, d)
+
+
+def _set_zstd_flags(flags):
+    L = O.lib()
+    L.bo_set_zstd_parse_flags.restype = ctypes.c_uint32
+    L.bo_set_zstd_parse_flags.argtypes = [ctypes.c_uint32]
+    return L.bo_set_zstd_parse_flags(flags)
+
+
+REP, SKIP, DROP = 1, 2, 1 << 17
+
+
+def test_zstd_skip_parse_frames_and_ratio():
+    """The Zstd parse is the repeat-offset form with window skipping (REP | SKIP, the shipped
+    zstd_parse_kernel): libzstd decodes every frame it writes on every kind, and skipping costs
+    at most 0.5 % of ratio against the plain repeat-offset scan."""
+    Z = _libzstd()
+    seg, n = 65536, 2 << 20
+    old = _set_zstd_flags(REP | SKIP)
+    try:
+        assert old == REP | SKIP  # the default
+        for kind in range(7):
+            data = O.fill(kind, 21, n).tobytes()
+            sizes = {}
+            for flags in (REP, REP | SKIP):
+                _set_zstd_flags(flags)
+                tot = 0
+                for i in range(0, n, seg):
+                    s = data[i:i + seg]
+                    r, f = O.zstd_compress(s)
+                    assert r == 0
+                    tot += len(f)
+                    if flags & SKIP:
+                        out = ctypes.create_string_buffer(seg)
+                        rr = Z.ZSTD_decompress(out, seg, f, len(f))
+                        assert not Z.ZSTD_isError(rr) and out.raw[:rr] == s, (kind, i)
+                sizes[flags] = tot
+            assert sizes[REP | SKIP] <= 1.005 * sizes[REP], (kind, sizes)
+    finally:
+        _set_zstd_flags(old)
+
+
+def test_zstd_dropped_gap_literals_are_rejected():
+    """Root cause of round 3's REP + SKIP corruption: the GPU literal collector left out the
+    literal bytes of skipped probe windows, so a frame's sequences declared more literals than
+    its literal section held.  Restated by BO_ZSTD_DROP_GAP_LITERALS, such frames are rejected
+    by libzstd ("corruption detected") AND by the oracle's decoder -- the oracle's RFC 8878
+    acceptance is not looser than libzstd's on this class."""
+    Z = _libzstd()
+    seg = 65536
+    old = _set_zstd_flags(REP | SKIP | DROP)
+    bad = 0
+    try:
+        for kind in (2,):  # (its float64 column: probes that miss, then a hit)
+            data = O.fill(kind, 3, 64 * seg).tobytes()
+            for i in range(0, len(data), seg):
+                s = data[i:i + seg]
+                _set_zstd_flags(REP | SKIP | DROP)
+                r, f = O.zstd_compress(s)
+                _set_zstd_flags(REP | SKIP)
+                r0, good = O.zstd_compress(s)
+                assert r == 0 and r0 == 0
+                if f == good:
+                    continue  # no gap before a scanned window in this segment
+                bad += 1
+                out = ctypes.create_string_buffer(seg)
+                rr = Z.ZSTD_decompress(out, seg, f, len(f))
+                assert Z.ZSTD_isError(rr) or out.raw[:rr] != s, (kind, i)
+                r2, back = O.zstd_decompress(f, seg)
+                assert (r2 != 0) == bool(Z.ZSTD_isError(rr)), (kind, i, r2)
+                if r2 == 0:
+                    assert back == out.raw[:rr]
+    finally:
+        _set_zstd_flags(old)
+    assert bad >= 4
