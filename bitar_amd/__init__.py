@@ -96,6 +96,8 @@ def lib():
         "bitar_hip_get_decoder_options": (i32, [vp, ctypes.POINTER(DecoderOptions)]),
         "bitar_hip_set_decoder_options": (i32, [vp, ctypes.POINTER(DecoderOptions)]),
         "bitar_hip_path_counters": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), u32]),
+        "bitar_hip_compress_host": (i32, [vp, vp, u32, vp, u64, u32, vp, vp, vp, u64, vp]),
+        "bitar_hip_decompress_host": (i32, [vp, vp, u32, vp, vp, u32, u32, vp, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -115,7 +117,8 @@ ABI_SYMBOLS = ("bitar_hip_abi_version", "bitar_hip_last_error", "bitar_hip_devic
                "bitar_hip_sync", "bitar_hip_pack", "bitar_hip_pack_lz4f", "bitar_hip_fill",
                "bitar_hip_fill_at", "bitar_hip_checksum", "bitar_hip_copy_batch",
                "bitar_hip_lz4_chain", "bitar_hip_get_decoder_options",
-               "bitar_hip_set_decoder_options", "bitar_hip_path_counters")
+               "bitar_hip_set_decoder_options", "bitar_hip_path_counters",
+               "bitar_hip_compress_host", "bitar_hip_decompress_host")
 
 
 def check(rc):
@@ -215,6 +218,21 @@ class Engine:
         n = data.numel() * data.element_size() if n is None else n
         check(lib().bitar_hip_compress(self.ctx, self._stream(stream), codec, _ptr(data), n, seg,
                                        _ptr(slab), stride, _ptr(sizes)))
+
+    def compress_host_into(self, codec, host, n, seg, stage, slab, stride, sizes, stream=None):
+        """compress n bytes of host memory (a pinned torch CPU tensor, or an address) through
+        the HBM staging tensor `stage`, link and kernels overlapped"""
+        check(lib().bitar_hip_compress_host(self.ctx, self._stream(stream), codec, _ptr(host),
+                                            n, seg, _ptr(stage), _ptr(slab), None, stride,
+                                            _ptr(sizes)))
+
+    def decompress_host_into(self, codec, srcs, sizes, nseg, seg, stage, host, produced,
+                             capacity=None, stream=None):
+        """decompress into host memory (nseg*seg bytes at `host`) through `stage`"""
+        cap = nseg * seg if capacity is None else capacity
+        check(lib().bitar_hip_decompress_host(self.ctx, self._stream(stream), codec, _ptr(srcs),
+                                              _ptr(sizes), nseg, seg, _ptr(stage), _ptr(host),
+                                              cap, _ptr(produced)))
 
     def decompress_slab_into(self, codec, slab, stride, sizes, nseg, seg, out, produced,
                              capacity=None, stream=None):

@@ -383,11 +383,14 @@ arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
   const auto nseg = static_cast<std::uint32_t>((n + seg - 1) / seg);
   const auto codec = internal::AbiCodec(*configuration_);
 
-  // input: read HBM in place, else stage it (the reference attaches it zero-copy, 380-399)
-  const void* d_in = reinterpret_cast<const void*>(decompressed_buffer->address());
-  if (!internal::OnDevice(*decompressed_buffer, device_id_)) {
+  // input: read HBM in place; host memory (the reference attaches it zero-copy, 380-399) is
+  // staged into HBM chunk by chunk with each chunk's compress overlapping the next one's
+  // copy (bitar_hip_compress_host)
+  const void* h_in = reinterpret_cast<const void*>(decompressed_buffer->address());
+  const void* d_in = h_in;
+  const bool host_in = !internal::OnDevice(*decompressed_buffer, device_id_);
+  if (host_in) {
     ARROW_RETURN_NOT_OK(m->Stage(n));
-    BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_stage, d_in, n, m->stream), "stage input");
     d_in = m->d_stage;
   }
 
@@ -419,13 +422,18 @@ arrow::Result<BufferVector> CompressDevice<Class, Enable>::Compress(
     for (std::uint32_t i = 0; i < nseg; ++i)
       m->h_ptrs[i] = static_cast<std::uint64_t>(reinterpret_cast<uintptr_t>(slots[i]));
     rc = m->UploadPtrs(nseg);
-    if (rc == 0)
-      rc = bitar_hip_compress_scattered(ctx_, m->stream, codec, d_in, n, seg,
-                                        reinterpret_cast<void* const*>(m->d_ptrs), slot_size_,
+    const auto* dsts = reinterpret_cast<void* const*>(m->d_ptrs);
+    if (rc == 0 && host_in)
+      rc = bitar_hip_compress_host(ctx_, m->stream, codec, h_in, n, seg, m->d_stage, nullptr,
+                                   dsts, slot_size_, m->d_sizes);
+    else if (rc == 0)
+      rc = bitar_hip_compress_scattered(ctx_, m->stream, codec, d_in, n, seg, dsts, slot_size_,
                                         m->d_sizes);
   } else {
-    rc = bitar_hip_compress(ctx_, m->stream, codec, d_in, n, static_cast<std::uint32_t>(opseg),
-                            m->d_chain, stride, m->d_sizes);
+    if (host_in) rc = bitar_hip_memcpy(ctx_, m->d_stage, h_in, n, m->stream);
+    if (rc == 0)
+      rc = bitar_hip_compress(ctx_, m->stream, codec, d_in, n, static_cast<std::uint32_t>(opseg),
+                              m->d_chain, stride, m->d_sizes);
   }
   if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sizes, m->d_sizes, 4ull * nops, m->stream);
   auto mm = hip_memory_manager(device_id_);
@@ -517,17 +525,25 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
   const std::uint32_t k = configuration_->max_sgl_segs();
   const std::uint64_t opseg = std::uint64_t{k} * seg;
   const std::uint32_t nops = (nseg + k - 1) / k, nfull = nseg / k, tail = nseg % k;
-  ARROW_RETURN_NOT_OK(m->Tables(k > 1 ? 2ull * nseg + nops : nseg));
+  ARROW_RETURN_NOT_OK(m->Tables(k > 1 ? 2ull * nseg + nops : 3ull * nseg));
 
-  // sources: HBM buffers in place; host buffers staged behind the output area
+  // sources: HBM buffers in place; host buffers staged behind the output area -- pinned ones
+  // (the HipHost / Rtememzone pool) gathered by ONE copy kernel reading host memory over the
+  // link, pageable ones by a copy each (memory.cc:459-500 attaches them zero-copy)
   std::uint64_t host_bytes = 0;
-  std::vector<bool> on_dev(nseg);
+  std::vector<std::uint8_t> where(nseg);  // 2 HBM, 1 pinned host, 0 pageable host
   const arrow::MemoryManager* own_mm = hip_memory_manager(device_id_).get();
   for (std::uint32_t i = 0; i < nseg; ++i) {
+    const auto& b = *compressed_buffers[i];
     // (our own slot views: their memory manager says so without a query)
-    on_dev[i] = compressed_buffers[i]->memory_manager().get() == own_mm ||
-                internal::OnDevice(*compressed_buffers[i], device_id_);
-    if (!on_dev[i]) host_bytes += (static_cast<std::uint64_t>(compressed_buffers[i]->size()) + 15) & ~15ull;
+    if (b.memory_manager().get() == own_mm || internal::OnDevice(b, device_id_)) {
+      where[i] = 2;
+      continue;
+    }
+    int kind = 0, dev = -1;
+    (void)bitar_hip_pointer_info(reinterpret_cast<const void*>(b.address()), &kind, &dev);
+    where[i] = kind == 1 ? 1 : 0;
+    host_bytes += (static_cast<std::uint64_t>(b.size()) + 15) & ~15ull;
   }
   const auto out_addr = decompressed_buffer->mutable_address();
   const bool out_on_dev = internal::OnDevice(out_addr, device_id_);
@@ -535,31 +551,61 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
   if (host_bytes + out_bytes) ARROW_RETURN_NOT_OK(m->Stage(host_bytes + out_bytes));
   auto* stage = static_cast<std::uint8_t*>(m->d_stage);
   std::uint64_t off = out_bytes;
+  std::uint32_t ngather = 0;  // pinned sources: table entries at [nseg, 3 nseg)
   for (std::uint32_t i = 0; i < nseg; ++i) {
     const auto& b = compressed_buffers[i];
     if (static_cast<std::uint64_t>(b->size()) >= BITAR_HIP_SEGMENT_ERROR)
       return arrow::Status::Invalid("compressed buffer ", i, " is too large");
     m->h_sizes[i] = static_cast<std::uint32_t>(b->size());
-    if (on_dev[i]) {
+    if (where[i] == 2) {
       m->h_ptrs[i] = b->address();
+      continue;
+    }
+    if (where[i] == 1 && k == 1) {
+      m->h_ptrs[nseg + ngather] = b->address();
+      m->h_ptrs[2ull * nseg + ngather] = reinterpret_cast<std::uint64_t>(stage + off);
+      m->h_sizes[nseg + ngather] = static_cast<std::uint32_t>(b->size());
+      ++ngather;
     } else {
       BITAR_ABI(bitar_hip_memcpy(ctx_, stage + off, reinterpret_cast<const void*>(b->address()),
                                  static_cast<std::uint64_t>(b->size()), m->stream),
                 "stage compressed input");
-      m->h_ptrs[i] = reinterpret_cast<std::uint64_t>(stage + off);
-      off += (static_cast<std::uint64_t>(b->size()) + 15) & ~15ull;
     }
+    m->h_ptrs[i] = reinterpret_cast<std::uint64_t>(stage + off);
+    off += (static_cast<std::uint64_t>(b->size()) + 15) & ~15ull;
+  }
+  if (ngather) {
+    if (m->ptr_mirror.size() > nseg) m->ptr_mirror.resize(nseg);
+    BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_ptrs + nseg, m->h_ptrs + nseg, 8ull * ngather, m->stream),
+              "tables");
+    BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_ptrs + 2ull * nseg, m->h_ptrs + 2ull * nseg,
+                               8ull * ngather, m->stream), "tables");
+    BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_sizes + nseg, m->h_sizes + nseg, 4ull * ngather,
+                               m->stream), "tables");
+    BITAR_ABI(bitar_hip_copy_batch(ctx_, m->stream,
+                                   reinterpret_cast<const void* const*>(m->d_ptrs + nseg),
+                                   reinterpret_cast<void* const*>(m->d_ptrs + 2ull * nseg),
+                                   m->d_sizes + nseg, ngather),
+              "gather compressed input");
   }
   void* d_out = out_on_dev ? reinterpret_cast<void*>(out_addr) : m->d_stage;
   int rc = 0;
   std::uint32_t nunits = nseg;  // ops, one produced size / checksum each
   std::uint64_t unit = seg;
+  bool out_copied = false;  // the output already went to host memory (decompress_host)
   if (k == 1) {
     BITAR_ABI(m->UploadPtrs(nseg), "tables");
     BITAR_ABI(bitar_hip_memcpy(ctx_, m->d_sizes, m->h_sizes, 4ull * nseg, m->stream), "tables");
-    rc = bitar_hip_decompress(ctx_, m->stream, codec,
-                              reinterpret_cast<const void* const*>(m->d_ptrs), m->d_sizes, nseg,
-                              seg, d_out, static_cast<std::uint64_t>(min_capacity), m->d_prod);
+    const auto* srcs = reinterpret_cast<const void* const*>(m->d_ptrs);
+    if (!out_on_dev) {  // host output: decode chunks, each copied out while the next decodes
+      rc = bitar_hip_decompress_host(ctx_, m->stream, codec, srcs, m->d_sizes, nseg, seg, d_out,
+                                     reinterpret_cast<void*>(out_addr),
+                                     static_cast<std::uint64_t>(min_capacity), m->d_prod);
+      out_copied = true;
+    } else {
+      rc = bitar_hip_decompress(ctx_, m->stream, codec, srcs, m->d_sizes, nseg, seg, d_out,
+                                static_cast<std::uint64_t>(min_capacity), m->d_prod);
+    }
   } else {
     nunits = nops;
     unit = opseg;
@@ -611,7 +657,7 @@ arrow::Status CompressDevice<Class, Enable>::Decompress(
                             static_cast<std::uint32_t>(unit), m->d_prod, nunits, m->d_sums);
     if (rc == 0) rc = bitar_hip_memcpy(ctx_, m->h_sums, m->d_sums, 8ull * nunits, m->stream);
   }
-  if (rc == 0 && !out_on_dev)
+  if (rc == 0 && !out_on_dev && !out_copied)
     rc = bitar_hip_memcpy(ctx_, reinterpret_cast<void*>(out_addr), d_out,
                           static_cast<std::uint64_t>(min_capacity), m->stream);
   if (rc == 0) rc = bitar_hip_sync(ctx_, m->stream);

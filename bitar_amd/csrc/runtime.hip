@@ -119,6 +119,9 @@ struct bitar_hip_ctx {
     OrderScratch(hipStream_t s, int k) : stream(s), slot(k) {}
   };
   std::list<OrderScratch> order_scratch;
+  // host-memory calls (bitar_hip_compress_host / _decompress_host): the copy stream paired
+  // with each caller stream, created on first use
+  std::vector<std::pair<hipStream_t, hipStream_t>> copy_streams;
 };
 
 namespace {
@@ -286,6 +289,8 @@ int bitar_hip_close(bitar_hip_ctx* ctx) {
     }
     (void)hipDeviceSynchronize();  // (order scratch may sit on foreign streams)
     free_order_scratch(ctx);
+    for (auto& cs : ctx->copy_streams) (void)hipStreamDestroy(cs.second);
+    ctx->copy_streams.clear();
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
   }
@@ -839,6 +844,100 @@ int bitar_hip_decompress_slab(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
   if (nseg && !d_slab) return fail(BITAR_HIP_INVALID, "null d_slab");
   return decompress_impl(ctx, stream, codec, nullptr, d_slab, slot_stride, d_sizes, nseg, seg,
                          d_out, capacity, d_produced);
+}
+
+// ---- host-memory calls: the PCIe link and the kernels overlapped ---------------------------
+// The caller's stream s and a copy stream paired with it: the copy stream first waits for
+// everything queued on s (the staging area may still be read by an earlier call), then per
+// chunk of whole segments one copy + one event, and s waits on each chunk's event before the
+// chunk's kernels (compress) -- or the copy stream waits on the chunk's decode before copying
+// it out (decompress).  s finally waits on the copy stream, so a sync of s covers the call.
+static hipStream_t copy_stream_for(bitar_hip_ctx* ctx, hipStream_t s) {
+  std::lock_guard<std::mutex> g(ctx->mu);
+  for (auto& cs : ctx->copy_streams)
+    if (cs.first == s) return cs.second;
+  hipStream_t c = nullptr;
+  if (hipStreamCreateWithFlags(&c, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  ctx->copy_streams.emplace_back(s, c);
+  return c;
+}
+
+// b waits for what is queued on a now
+static int stream_after(hipStream_t b, hipStream_t a) {
+  hipEvent_t e;
+  HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  hipError_t r = hipEventRecord(e, a);
+  if (r == hipSuccess) r = hipStreamWaitEvent(b, e, 0);
+  (void)hipEventDestroy(e);  // (released once recorded work completes)
+  HIP_TRY(r, "stream ordering");
+  return 0;
+}
+
+// chunks of whole segments: about 1/8 of the call, at least 32 MiB
+static uint64_t host_chunk_segs(uint64_t nseg, uint32_t seg) {
+  uint64_t c = (nseg + 7) / 8;
+  const uint64_t lo = ((32ull << 20) + seg - 1) / seg;
+  return c < lo ? lo : c;
+}
+
+int bitar_hip_compress_host(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const void* h_in,
+                            uint64_t n, uint32_t seg, void* d_stage, void* d_slab,
+                            void* const* d_dsts, uint64_t slot_stride, uint32_t* d_sizes) {
+  if (int r = enter(ctx)) return r;
+  if (n == 0) return 0;
+  if (!h_in || !d_stage || (!d_slab && !d_dsts) || !d_sizes)
+    return fail(BITAR_HIP_INVALID, "null buffer");
+  if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
+  const hipStream_t s = pick_stream(ctx, stream);
+  const hipStream_t c = copy_stream_for(ctx, s);
+  if (!c) return fail(BITAR_HIP_UNKNOWN_ERROR, "copy stream");
+  if (int r = stream_after(c, s)) return r;
+  const uint64_t nseg = (n + seg - 1) / seg, per = host_chunk_segs(nseg, seg);
+  auto* stage = static_cast<uint8_t*>(d_stage);
+  const auto* src = static_cast<const uint8_t*>(h_in);
+  auto* slab = static_cast<uint8_t*>(d_slab);
+  for (uint64_t c0 = 0; c0 < nseg; c0 += per) {
+    const uint64_t cn = nseg - c0 < per ? nseg - c0 : per;
+    const uint64_t off = c0 * seg, nb = n - off < cn * seg ? n - off : cn * seg;
+    HIP_TRY(hipMemcpyAsync(stage + off, src + off, nb, hipMemcpyHostToDevice, c), "stage input");
+    if (int r = stream_after(s, c)) return r;
+    if (int r = compress_impl(ctx, s, codec, stage + off, nb, seg,
+                              slab ? slab + c0 * slot_stride : nullptr, slot_stride,
+                              d_dsts ? d_dsts + c0 : nullptr, d_sizes + c0))
+      return r;
+  }
+  return 0;
+}
+
+int bitar_hip_decompress_host(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
+                              const void* const* d_srcs, const uint32_t* d_sizes, uint32_t nseg,
+                              uint32_t seg, void* d_stage, void* h_out, uint64_t capacity,
+                              uint32_t* d_produced) {
+  if (int r = enter(ctx)) return r;
+  if (nseg == 0) return 0;
+  if (capacity < (uint64_t)nseg * seg)  // reference device.cc:248-254
+    return fail(BITAR_HIP_CAPACITY_ERROR, "The decompressed_buffer is required to be >= " +
+                                              std::to_string((uint64_t)nseg * seg) + " bytes");
+  if (!d_srcs || !d_sizes || !d_stage || !h_out || !d_produced)
+    return fail(BITAR_HIP_INVALID, "null buffer");
+  if (seg == 0 || seg > kMaxSeg) return fail(BITAR_HIP_INVALID, "seg must be in [1, 65536]");
+  const hipStream_t s = pick_stream(ctx, stream);
+  const hipStream_t c = copy_stream_for(ctx, s);
+  if (!c) return fail(BITAR_HIP_UNKNOWN_ERROR, "copy stream");
+  if (int r = stream_after(c, s)) return r;  // (h_out / d_stage users queued before)
+  const uint64_t per = host_chunk_segs(nseg, seg);
+  auto* stage = static_cast<uint8_t*>(d_stage);
+  auto* out = static_cast<uint8_t*>(h_out);
+  for (uint64_t c0 = 0; c0 < nseg; c0 += per) {
+    const uint64_t cn = nseg - c0 < per ? nseg - c0 : per;
+    if (int r = decompress_impl(ctx, s, codec, d_srcs + c0, nullptr, 0, d_sizes + c0,
+                                (uint32_t)cn, seg, stage + c0 * seg, cn * seg, d_produced + c0))
+      return r;
+    if (int r = stream_after(c, s)) return r;
+    HIP_TRY(hipMemcpyAsync(out + c0 * seg, stage + c0 * seg, cn * seg, hipMemcpyDeviceToHost, c),
+            "output copy");
+  }
+  return stream_after(s, c);
 }
 
 int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream) {

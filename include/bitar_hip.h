@@ -154,11 +154,37 @@ int bitar_hip_decompress_slab(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                               const uint32_t* d_sizes, uint32_t nseg, uint32_t seg,
                               void* d_out, uint64_t capacity, uint32_t* d_produced);
 
+/* Compress n bytes of HOST memory (pinned or pageable) at h_in with the PCIe link and the
+ * kernels overlapped: the input is copied into d_stage (device memory, >= n bytes) in chunks
+ * of whole segments (about 1/8 of the call, >= 32 MiB) on a copy stream paired with
+ * `stream`, and each chunk is compressed on `stream` as soon as it has landed, so a call
+ * takes about the link time plus one chunk's compress.  The output is a slab (d_slab, as
+ * bitar_hip_compress) or scattered slots (d_dsts with d_slab NULL, as
+ * bitar_hip_compress_scattered; slot_stride is then the slots' capacity).  Asynchronous on
+ * `stream`; bitar_hip_sync(stream) covers the copies too.  Replaces the zero-copy attach of
+ * host input slices the BlueField DMAs from (reference src/memory.cc:380-399,
+ * rte_mem_virt2iova at 388). */
+int bitar_hip_compress_host(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const void* h_in,
+                            uint64_t n, uint32_t seg, void* d_stage, void* d_slab,
+                            void* const* d_dsts, uint64_t slot_stride, uint32_t* d_sizes);
+
+/* Decompress into HOST memory: the segments decode into d_stage (device memory, >= nseg*seg
+ * bytes) in chunks, and each decoded chunk is copied to h_out on the paired copy stream while
+ * the next one decodes; nseg*seg bytes land at h_out (capacity >= nseg*seg, else
+ * BITAR_HIP_CAPACITY_ERROR).  Otherwise as bitar_hip_decompress; bitar_hip_sync(stream)
+ * covers the copies.  Replaces decompression into host-memory output slices (reference
+ * src/memory.cc:482-493). */
+int bitar_hip_decompress_host(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
+                              const void* const* d_srcs, const uint32_t* d_sizes, uint32_t nseg,
+                              uint32_t seg, void* d_stage, void* h_out, uint64_t capacity,
+                              uint32_t* d_produced);
+
 /* Wait for `stream` and return BITAR_HIP_IO_ERROR if a segment op launched on THAT stream
  * failed since its last sync (each stream has its own sticky device-side error word, read
  * and cleared in stream order, so concurrent queue pairs never see each other's failures).
- * NULL waits for the default stream and the context's queue pairs, and reports/clears
- * every stream's word.  Replaces the
+ * NULL waits for the default stream and the context's queue pairs and reports / clears
+ * their words only: a foreign stream's word (e.g. a torch side stream) is left to a sync of
+ * that stream, which reports it exactly once.  Replaces the
  * completion polling of DequeueBurst + GetErrorCount (reference src/device.cc:84-110,
  * 490-535). */
 int bitar_hip_sync(bitar_hip_ctx* ctx, void* stream);

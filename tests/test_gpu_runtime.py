@@ -326,3 +326,49 @@ def test_two_scratch_chunks_bit_exact(codec):
         assert np.array_equal(g[mask], o[mask])
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("pinned", [True, False], ids=["pinned", "pageable"])
+@pytest.mark.parametrize("codec", [O.CODEC_LZ4, O.CODEC_ZSTD, O.CODEC_DEFLATE_DYN])
+def test_host_memory_calls_overlap_and_match(codec, pinned):
+    """bitar_hip_compress_host / _decompress_host: host input staged chunk by chunk with each
+    chunk's compress overlapping the next chunk's copy, and the decode copied out chunk by
+    chunk -- the same slab and sizes as a compress of the HBM copy, and the input back in host
+    memory (the reference attaches host slices zero-copy, src/memory.cc:380-399, 482-493)."""
+    import bitar_amd
+    e = bitar_amd.Engine(0)
+    try:
+        seg = 59460 if codec == O.CODEC_DEFLATE_DYN else 65536
+        # ~12 MiB: one chunk; 96 MiB: three chunks of >= 32 MiB (the last one short)
+        for n in (200 * seg + 777, (96 << 20) + 12345):
+            data = O.fill(O.KIND_MIXED, 61, n)
+            host = torch.from_numpy(data)
+            if pinned:
+                host = host.pin_memory()
+            nseg = (n + seg - 1) // seg
+            stride = bitar_amd.slot_size(codec, seg)
+            stage = e.empty(nseg * seg)
+            slab = e.empty(nseg * stride)
+            sizes = e.empty(nseg, dtype=torch.int32)
+            e.compress_host_into(codec, host.data_ptr(), n, seg, stage, slab, stride, sizes)
+            e.sync()
+            d = up(data)
+            slab2, stride2, sizes2 = e.compress(codec, d[:n], seg)
+            e.sync()
+            assert torch.equal(sizes, sizes2)
+            g1, g2, gs = down(slab), down(slab2), down(sizes).astype(np.uint32)
+            for i in range(nseg):
+                assert np.array_equal(g1[i * stride:i * stride + gs[i]],
+                                      g2[i * stride:i * stride + gs[i]]), i
+            srcs = torch.tensor([slab.data_ptr() + i * stride for i in range(nseg)],
+                                dtype=torch.int64).cuda()
+            out = torch.zeros(nseg * seg, dtype=torch.uint8)
+            if pinned:
+                out = out.pin_memory()
+            prod = e.empty(nseg, dtype=torch.int32)
+            e.decompress_host_into(codec, srcs, sizes, nseg, seg, stage, out.data_ptr(), prod)
+            e.sync()
+            assert np.array_equal(out.numpy()[:n], data)
+            assert int(prod.to(torch.int64).sum().item()) == n
+    finally:
+        e.close()
