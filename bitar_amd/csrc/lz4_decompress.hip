@@ -29,6 +29,11 @@
 #ifndef BITAR_LZ4D_PROFILE
 #define BITAR_LZ4D_PROFILE 0
 #endif
+// tuning knob: 0 builds a decoder WITHOUT the end-of-block checks (timing A/B only; it is
+// looser than the oracle)
+#ifndef BITAR_LZ4D_ENDRULES
+#define BITAR_LZ4D_ENDRULES 1
+#endif
 
 namespace bitar_hip {
 
@@ -260,7 +265,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   const uint32_t src_lo = (uint32_t)(uintptr_t)s.src;
   bool want_far = false, stay_far = false;
   // end-of-block conditions: the last match's length (0 = it was in the batch at bip)
-  uint32_t last_ml = 0, bip = 0;
+  uint32_t last_ml = 0, bip = 0, fin_lit = 0, fin_tok = 0;
   [[maybe_unused]] uint32_t p_batches = 0, p_bytes = 0, p_general = 0, p_stop_parse = 0,
                             p_stop_inel = 0;
   while (ok) {
@@ -427,8 +432,10 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         const uint32_t carry = readlane(key0, kWave - 1);
         half(std::integral_constant<uint32_t, 1>{}, key1 > carry ? key1 : carry);
       }
-      bip = s.ip;
-      last_ml = 0;
+      if constexpr (BITAR_LZ4D_ENDRULES == 1 || BITAR_LZ4D_ENDRULES == 2) {
+        bip = s.ip;
+        last_ml = 0;
+      }
       s.ip += __builtin_amdgcn_readfirstlane(k);  // (k is an SGPR: keeps the add scalar)
       s.op += out;
       return out;
@@ -478,22 +485,9 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     if ((uint64_t)s.ip + lit > s.csize || (uint64_t)s.op + lit > s.cap) { ok = false; break; }
     if (lit >= kLongLit) literals_long(s, win, ring, lit);
     else if (lit) literals_short(s, win, ring, lit);
-    if (s.ip == s.csize) {  // last sequence: literals only
-      if (s.op > lit) {  // the block had a match: >= 5 final literals, last match >= 12 back
-        uint32_t ml = last_ml;
-        if (ml == 0 && lit >= 5 && lit < 8) {  // (ml >= 4 settles lit >= 8) re-walk the batch
-          for (uint32_t p = bip; p < tok_at;) {
-            const uint32_t t = sv.get(s, win, p);
-            uint32_t ll = t >> 4, mm = t & 15u;
-            p += 1;
-            if (ll == 15) ll += sv.get(s, win, p++);  // (batch sequences: <= 1 length byte)
-            p += ll + 2;
-            if (mm == 15) mm += sv.get(s, win, p++);
-            ml = mm + 4;
-          }
-        }
-        if (lit < 5 || lit + ml < 12) ok = false;
-      }
+    if (s.ip == s.csize) {  // last sequence: literals only (end conditions: below)
+      fin_lit = lit;
+      fin_tok = tok_at;
       break;
     }
     if (s.ip + 2 > s.csize) { ok = false; break; }
@@ -518,6 +512,26 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       atomicAdd(stats + BITAR_HIP_PATH_LZ4_STOP_PARSE, (unsigned long long)p_stop_parse);
       atomicAdd(stats + BITAR_HIP_PATH_LZ4_STOP_INELIGIBLE, (unsigned long long)p_stop_inel);
     }
+  }
+  // the block format's end conditions, if the block had a match: >= 5 final literals, the
+  // last match >= 12 bytes before the end (its length: from the general path, or -- the
+  // final token right after a batch -- re-walked from that batch's first token; ml >= 4
+  // settles fin_lit >= 8).  Out of the decode loop: inside it, this code cost the loop 6 %.
+  if ((BITAR_LZ4D_ENDRULES == 1 || BITAR_LZ4D_ENDRULES == 3) && ok && s.op > fin_lit &&
+      !(!FARK && want_far)) {
+    uint32_t ml = last_ml;
+    if (ml == 0 && fin_lit >= 5 && fin_lit < 8) {
+      for (uint32_t p = bip; p < fin_tok;) {
+        const uint32_t t = sv.get(s, win, p);
+        uint32_t ll = t >> 4, mm = t & 15u;
+        p += 1;
+        if (ll == 15) ll += sv.get(s, win, p++);  // (batch sequences: <= 1 length byte)
+        p += ll + 2;
+        if (mm == 15) mm += sv.get(s, win, p++);
+        ml = mm + 4;
+      }
+    }
+    if (fin_lit < 5 || fin_lit + ml < 12) ok = false;
   }
   if (!FARK && want_far) {
     if (lane_id() == 0) {
