@@ -22,29 +22,55 @@ namespace bitar_hip {
 
 namespace cmp {
 
-// ---- LZ4 emitter ---------------------------------------------------------------------
 // m's bit for this lane ? a : b (m an SGPR pair used directly as the lane mask)
 __device__ __forceinline__ uint32_t lane_sel(uint64_t m, uint32_t a, uint32_t b) {
   uint32_t r;
   __asm__("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
   return r;
 }
-// LDS of the LZ4 emitter past its output ring: the spill area (a window writes at most
-// 269 + 64 literals and 17 sequence headers: unwrapped addresses reach kLz4Obuf - 1 + 421), the
-// trash bytes (lane + 0..2), and the literal bases by chain rank (kWave dwords, then one
-// trash dword every other lane writes: a per-lane one measured slower, more LDS)
-// The output ring is 512 B (1 KiB before the round-3 emitter: the smaller LDS footprint
-// measured 2-3 % faster than the same emitter on 1 KiB; the flushes stay per input row).
-#ifndef BITAR_CMP_LZ4_OBUF
-#define BITAR_CMP_LZ4_OBUF 512
-#endif
-constexpr uint32_t kLz4Obuf = BITAR_CMP_LZ4_OBUF;
-constexpr uint32_t kSpill = 448;
-constexpr uint32_t kTrash = kLz4Obuf + kSpill;
-constexpr uint32_t kLz4Lds = kLz4Obuf + kSpill + 80;  // bytes before the literal-base table
+
+// ---- LZ4 emitter: sequences batched, output gathered byte by byte ----------------------
+// The parse hands each window's matches over as sequence records {match start, distance,
+// length}: the chain lanes append them to an LDS list (one store, one mbcnt).  Every <= 64
+// records (and before the tail) one flush turns them into LZ4 sequences, one record per
+// lane: literal run = [previous match end, match start), sizes by one prefix sum, and then
+// the output is GATHERED 64 bytes per step -- output byte o finds its sequence (the latest one
+// starting at or before o: sequence starts marked in LDS, a prefix max), fetches that
+// sequence's packed header fields (ds_bpermute) and writes exactly one byte: token, length
+// byte, literal (from the input ring), offset byte or match-length byte.  Rare sequences --
+// literal run >= 270 bytes or outside the input ring, match >= 274 bytes -- and a flush that
+// would overrun the slot take the general path, one sequence at a time.
+// Round 3's per-window emitter wrote six bytes per POSITION lane (token, length bytes,
+// offset, literal; trash bytes for the rest) after two prefix scans per window; with the
+// emitter removed the parse ran 30 % faster (1 GiB kinds 1 / 5 / 6), so that is what this
+// batching takes aim at.  The output bytes are the same.
+constexpr uint32_t kLz4Obuf = 512;  // output ring (flushed to HBM in 16-B blocks)
+constexpr uint32_t kSeqCap = 64;    // records per flush (a window adds <= 16)
+struct Lz4Lds {
+  uint8_t ring[kLz4Obuf + kWave];  // + one trash byte per lane
+  uint2 seqs[kSeqCap + 1];         // + a trash record
+  uint32_t marks[kWave + 1];       // sequence starts of the current output step; + trash
+};
 
 struct Lz4Out : ByteOutT<kLz4Obuf> {
-  uint32_t* scr;  // literal bases by chain rank (LDS)
+  Lz4Lds* L;
+  uint32_t nseq;      // pending records
+  uint32_t last_end;  // end of the last match emitted (the next literal run's start)
+  uint32_t step_id;   // output steps so far (tags the marks, so they never need clearing)
+
+  __device__ __forceinline__ void init(Lz4Lds* lds, GMEM uint8_t* d, uint64_t c) {
+    L = lds;
+    ring = lds->ring;
+    dst = d;
+    cap = c;
+    op = flushed = 0;
+    overflow = false;
+    nseq = 0;
+    last_end = 0;
+    step_id = 0;
+    lds->marks[lane_id()] = 0;  // (tag 0 never matches a step)
+    lds_order();
+  }
   __device__ __forceinline__ void put_ext(uint32_t v) {  // 255 ... 255, v % 255
     const uint32_t cnt = v / 255u + 1;
     for (uint32_t k = 0; k < cnt; k += kWave) {
@@ -55,9 +81,8 @@ struct Lz4Out : ByteOutT<kLz4Obuf> {
     }
   }
   // One sequence, general path: any literal run (long runs HBM -> HBM), any lengths.
-  __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I,
-                                           uint32_t lit_start, uint32_t lit_len, uint32_t off,
-                                           uint32_t mlen) {
+  __device__ __forceinline__ void one(const GMEM uint8_t* in, const InRing& I, uint32_t lit_start,
+                                      uint32_t lit_len, uint32_t off, uint32_t mlen) {
     if (overflow) return;
     const uint32_t ml = mlen ? mlen - kMinMatch : 0;
     const uint32_t token = ((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15);
@@ -88,93 +113,121 @@ struct Lz4Out : ByteOutT<kLz4Obuf> {
     put(lane_id() ? off >> 8 : off & 0xFF, 2);
     if (ml >= 15) put_ext(ml - 15);
   }
+
+  // records of lanes [lo, hi) (all ordinary) as LZ4 sequences, gathered 64 output bytes per
+  // step; false (nothing written) if they would overrun the slot
+  __device__ __forceinline__ bool bulk(const InRing& I, uint32_t lo, uint32_t hi, uint32_t q,
+                                       uint32_t lit_start, uint32_t off, uint32_t mlen) {
+    const uint32_t lane = lane_id();
+    const bool in = (lane >= lo) & (lane < hi);
+    const uint32_t lit_len = q - lit_start, ml = mlen - kMinMatch;
+    const uint32_t nlx = lit_len >= 15 ? 1u : 0u, nmx = ml >= 15 ? 1u : 0u;
+    const uint32_t e = in ? 3u + nlx + nmx + lit_len : 0u;
+    const uint32_t incl = wave_incl_sum(e);
+    const uint32_t total = readlane(incl, kWave - 1);
+    if ((uint64_t)op + total > cap) return false;
+    const uint32_t a = incl - e;  // output offset of the sequence's token
+    const uint32_t tok = ((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15);
+    const uint32_t p0 = a | (lit_len << 16) | (nlx << 25) | (nmx << 26);
+    const uint32_t p1 = lit_start | (tok << 16);
+    const uint32_t p2 = (off & 0xFFFFu) | (((ml - 15u) & 0xFFu) << 16) | ((lit_len - 15u) << 24);
+    for (uint32_t R = 0; R < total; R += kWave) {
+      room(kWave);
+      step_id += 1;
+      // the sequences starting in this step mark their first byte; every byte then takes the
+      // latest sequence starting at or before it (those before the step: counted by a ballot)
+      const bool st = in & (a - R < kWave);
+      lds_order();
+      L->marks[st ? a - R : kWave] = (step_id << 8) | (lane + 1);
+      lds_order();
+      const uint32_t mk = L->marks[lane];
+      const uint32_t before = (uint32_t)__builtin_popcountll(ballot(in & (a < R)));
+      const uint32_t carry = before ? lo + before : 0u;
+      const uint32_t v = (mk >> 8) == step_id ? (mk & 0xFFu) : 0u;
+      const uint32_t s1 = max(wave_incl_max(v), carry);  // >= 1: lane lo starts at offset 0
+      const int src = (int)((s1 - 1) << 2);
+      const uint32_t q0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)p0);
+      const uint32_t q1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)p1);
+      const uint32_t q2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)p2);
+      const uint32_t r = R + lane - (q0 & 0xFFFFu);  // byte of its sequence
+      const uint32_t ll = (q0 >> 16) & 511u;
+      const uint32_t L0 = 1u + ((q0 >> 25) & 1u), h = L0 + ll;
+      const uint32_t litb = I.byte((q1 & 0xFFFFu) + r - L0);
+      uint32_t b = r == h + 2 ? (q2 >> 16) & 0xFFu : (q2 >> 8) & 0xFFu;  // ml byte / off high
+      b = r == h ? q2 & 0xFFu : b;
+      b = r < h ? litb : b;
+      b = r < L0 ? q2 >> 24 : b;  // (r == 1 with a literal-length byte)
+      b = r == 0 ? (q1 >> 16) & 0xFFu : b;
+      const uint32_t nb = total - R < kWave ? total - R : kWave;
+      lds_order();
+      ring[lane < nb ? at(op + lane) : kLz4Obuf + lane] = (uint8_t)b;
+      lds_order();
+      op += nb;
+    }
+    return true;
+  }
+
+  // every pending record as LZ4 sequences
+  __device__ __forceinline__ void flush_seqs(const GMEM uint8_t* in, const InRing& I) {
+    const uint32_t cnt = nseq;
+    nseq = 0;
+    if (!cnt || overflow) return;
+    const uint32_t lane = lane_id();
+    lds_order();
+    const uint2 rec = L->seqs[lane < cnt ? lane : kSeqCap];
+    const uint32_t q = rec.x & 0xFFFFu, off = rec.x >> 16, mlen = rec.y;
+    const uint32_t end = q + mlen;
+    const uint32_t prev = wave_shr1(end);
+    const uint32_t lit_start = lane == 0 ? last_end : prev;
+    const uint32_t lit_len = q - lit_start;
+    last_end = readlane(end, cnt - 1);
+    // rare sequences (and a flush that would overrun the slot) take the general path
+    const uint64_t live = cnt < kWave ? (1ull << cnt) - 1 : ~0ull;
+    uint64_t special = (ballot(lit_len >= 270u) | ballot(mlen >= 270u + kMinMatch) |
+                        ballot(lit_start < I.lo)) & live;
+    uint32_t lo = 0;
+    for (;;) {
+      const uint32_t k = special ? (uint32_t)__builtin_ctzll(special) : cnt;
+      if (k > lo && !bulk(I, lo, k, q, lit_start, off, mlen)) {
+        for (uint32_t j = lo; j < k && !overflow; ++j)  // (the slot's end: exact checks)
+          one(in, I, readlane(lit_start, j), readlane(lit_len, j), readlane(off, j),
+              readlane(mlen, j));
+      }
+      if (k >= cnt || overflow) break;
+      one(in, I, readlane(lit_start, k), readlane(lit_len, k), readlane(off, k),
+          readlane(mlen, k));
+      special &= special - 1;
+      lo = k + 1;
+    }
+  }
+
+  // the tail literals (and whatever is pending before them)
+  __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I,
+                                           uint32_t lit_start, uint32_t lit_len, uint32_t off,
+                                           uint32_t mlen) {
+    flush_seqs(in, I);
+    one(in, I, lit_start, lit_len, off, mlen);
+  }
   // the tail sequence starts at the last match's end
   __device__ __forceinline__ uint32_t pending_from(uint32_t anchor, uint32_t) const { return anchor; }
 
-  // All sequences of one window.  Fast path (every literal run < 270 bytes and in the
-  // input ring, every match < 274 bytes: at most one length byte each): each match lane
-  // writes its header bytes and each literal lane its own byte, all lanes at once, at
-  // offsets from a prefix sum of the sequence sizes.
-  //
-  // Addresses are relative to the ring index of op WITHOUT wrapping (at most ~420 bytes per
-  // window land past the ring's end, in the spill area, and are copied back to the ring's
-  // head afterwards), so a sequence's five header bytes take one address and immediate
-  // offsets.  A header byte a sequence does not have (no literal-length / match-length byte)
-  // is written anyway, before the bytes that overwrite its position: the first literal or the
-  // offset, and the next sequence's token.  Lanes with nothing to write use the trash bytes.
-  // A literal lane finds its sequence's literal base in LDS, written there by the sequence's
-  // match lane at its rank among the window's match lanes (v_mbcnt), which is also the
-  // literal lane's own rank.
-  __device__ __forceinline__ void window(const GMEM uint8_t* in, const InRing& I, const Window& W,
-                                         uint32_t anchor, uint32_t) {
-    if (!W.chain || overflow) return;
-    const uint32_t lane = lane_id();
-    const uint32_t q = W.x + lane;
+  // between windows: flush the records once the next window could overfill the list
+  __device__ __forceinline__ void between(const GMEM uint8_t* in, const InRing& I) {
+    if (nseq > kSeqCap - 16) flush_seqs(in, I);
+  }
+  // One window: its matches appended as records (<= 16: matches are >= 4 bytes)
+  __device__ __forceinline__ void window(const GMEM uint8_t*, const InRing&, const Window& W,
+                                         uint32_t, uint32_t) {
+    if (!W.chain) return;
     const uint64_t chain = W.chain;
-    // match ends increase along the chain, so "end of the previous match" is a prefix max
-    const uint32_t end_incl = wave_incl_max(lane_sel(chain, q + W.mlen, 0u));
-    const uint32_t end_excl = wave_shr1(end_incl);
-    const uint32_t lit_start = max(anchor, lane_sel(chain, end_excl, end_incl));
-    const uint32_t lit_len = q - lit_start;  // chain lanes: their literal run
-    const uint32_t ml = W.mlen - kMinMatch;
-    const uint32_t nlx = lit_len >= 15 ? 1u : 0u, nmx = ml >= 15 ? 1u : 0u;
-    const uint32_t hoff = 1 + nlx + lit_len;  // chain lanes: the offset, vs the token
-    const uint32_t e = lane_sel(chain, hoff + 2 + nmx, 0u);
-    const uint32_t incl = wave_incl_sum(e);
-    const uint32_t total = readlane(incl, 63);
-    if (((ballot(lit_len >= 270) | ballot(ml >= 270)) & chain) || anchor < I.lo ||
-        (uint64_t)op + total > cap) {
-      // general path, one sequence at a time
-      uint64_t m = chain;
-      uint32_t a = anchor;
-      while (m) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        const uint32_t i = W.x + l, mlen = readlane(W.mlen, l);
-        sequence(in, I, a, i - a, readlane(W.off, l), mlen);
-        a = i + mlen;
-      }
-      return;
-    }
-    room(total);
-    const uint32_t base = at(op);  // unwrapped addresses from here: base + [0, total)
-    // chain lanes: token at a, literal-length byte at a + 1, literals, offset at h, h + 1,
-    // match-length byte at h + 2; other lanes write into the trash bytes
-    const uint32_t a = lane_sel(chain, base + incl - e, kTrash + lane);
-    const uint32_t h = a + lane_sel(chain, hoff, 0u);
-    lds_order();
-    ring[h + 2] = (uint8_t)(ml - 15);       // (no such byte: the next token overwrites it)
-    ring[a + 1] = (uint8_t)(lit_len - 15);  // (no such byte: a literal or the offset does)
-    ring[a] = (uint8_t)(((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15));
-    ring[h] = (uint8_t)W.off;
-    ring[h + 1] = (uint8_t)(W.off >> 8);
-    // a literal lane (not a match start, not inside a match) belongs to the sequence of the
-    // lowest chain lane above it, whose rank among the chain lanes equals its own
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)chain, 0u));
-    const uint32_t nch = (uint32_t)__builtin_popcountll(chain);
-    scr[lane_sel(chain, rank, kWave)] = a + 1 + nlx - lit_start;  // (kWave: trash slot)
+    const uint32_t lane = lane_id();
     lds_order();
-    const uint64_t litm = ~chain & ballot(rank < nch) & ballot(q >= lit_start);
-    ring[lane_sel(litm, scr[rank] + q, kTrash + lane)] = (uint8_t)W.byte;
-    // literals of the first sequence that precede the window (anchor < x): from the ring
-    if (anchor < W.x) {
-      const uint32_t l0 = lowbit(chain);
-      const uint32_t d0 = base + 1 + (W.x + l0 - anchor >= 15 ? 1u : 0u) - anchor;
-      for (uint32_t k = anchor; k < W.x; k += kWave) {
-        const uint32_t qq = k + lane;
-        if (qq < W.x) ring[d0 + qq] = (uint8_t)I.byte(qq);
-      }
-    }
-    // bytes that went past the ring's end belong at its head
-    if (base + total > kLz4Obuf) {
-      lds_order();
-      const uint32_t nd = (base + total - kLz4Obuf + 3) / 4;
-      uint32_t* r32 = reinterpret_cast<uint32_t*>(ring);
-      for (uint32_t k = lane; k < nd; k += kWave) r32[k] = r32[kLz4Obuf / 4 + k];
-    }
+    L->seqs[lane_sel(chain, nseq + rank, kSeqCap)] =
+        make_uint2((W.x + lane) | (W.off << 16), W.mlen);
     lds_order();
-    op += total;
+    nseq += (uint32_t)__builtin_popcountll(chain);
   }
 };
 
@@ -278,6 +331,7 @@ struct DflOut {
   }
   // literals are emitted window by window: the tail starts where output stopped
   __device__ __forceinline__ uint32_t pending_from(uint32_t, uint32_t emitted) const { return emitted; }
+  __device__ __forceinline__ void between(const GMEM uint8_t*, const InRing&) {}
 
   // One window: each position contributes its literal code, its match symbol (a selected
   // match starts there) or nothing (inside a match); one prefix sum places them all.
@@ -310,20 +364,14 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   // (+ one trash entry: probe lanes past the segment insert there, see parse)
   __shared__ __attribute__((aligned(16))) uint16_t table[(1u << HLOG) + 8];
   __shared__ __attribute__((aligned(16))) uint8_t inring[RING + kInPad];
-  __shared__ __attribute__((aligned(16))) uint8_t obuf[kLz4Lds + 4 * (kWave + 4)];
+  __shared__ __attribute__((aligned(16))) Lz4Lds olds;
   // cost-ordered dispatch (seg_order_kernel): workgroup b compresses segment order[b]
   const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
   Lz4Out o;
-  o.ring = obuf;
-  o.scr = reinterpret_cast<uint32_t*>(obuf + kLz4Lds);
-  o.dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
-  o.cap = slot_stride;
-  o.op = 0;
-  o.flushed = 0;
-  o.overflow = false;
+  o.init(&olds, global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride), slot_stride);
 #ifndef BITAR_CMP_LZ4_SKIP
 #define BITAR_CMP_LZ4_SKIP 1  // tuning knob: 0 = the plain window scan (not the oracle's LZ4 parse)
 #endif

@@ -139,6 +139,7 @@ struct RecOut : ByteOut {  // the byte ring carries the match records
       lds_order();
     }
   }
+  __device__ __forceinline__ void between(const GMEM uint8_t*, const InRing&) {}
   __device__ __forceinline__ uint32_t pending_from(uint32_t, uint32_t emitted) const { return emitted; }
 };
 

@@ -17,7 +17,8 @@
 //      lanes still matching extend in parallel up to 32 bytes;
 //   3. a scalar chain walk picks the greedy matches in lane order (one ctz per match,
 //      cooperative extension only for matches reaching 32 bytes);
-//   4. the codec's emitter (E::window) writes the window's output lane-parallel.
+//   4. the codec's emitter (E::window) writes the window's output lane-parallel (or, the LZ4
+//      emitter, records the matches and writes batches of them in E::between).
 // Output is staged in LDS and flushed with aligned 16-B stores once per input row (E::drain),
 // right before the next row's load is issued.
 #pragma once
@@ -500,7 +501,9 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       W.byte = v.x & 0xFFu;
       W.pos_in = pos_in;
       W.done = emitted;
+#ifndef BITAR_CMP_TIMING_NOEMIT  // (timing knob only: no output)
       em.window(in, I, W, anchor, n);
+#endif
       if (chain) anchor = pos;
       emitted = pos > x + kWave ? pos : x + kWave;
       // same-slot writes of this window: re-write until the largest position holds the slot
@@ -547,6 +550,8 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
         nxt = load_row(k + 2);
         next_load += kRow;
       }
+      // the emitter's batched work, between windows (fewer live registers than inside one)
+      em.between(in, I);
       if constexpr (SKIP) {
         if (x - g + (kWave - 1) >= kSkipProbe + kWave - 1) {  // g >= x + 64, or x >= g + 128
           if (pos >= x + kWave) {  // inside the current match

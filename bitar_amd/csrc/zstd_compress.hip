@@ -139,6 +139,7 @@ struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the lit
                                            uint32_t len, uint32_t, uint32_t) {
     literals(in, I, s, len);
   }
+  __device__ __forceinline__ void between(const GMEM uint8_t*, const InRing&) {}
   __device__ __forceinline__ uint32_t pending_from(uint32_t, uint32_t emitted) const {
     return emitted;
   }

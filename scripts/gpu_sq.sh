@@ -1,12 +1,14 @@
 #!/bin/bash
-# GPU-box step: SQ instruction-mix counters of the headline kernels (one --pmc pass).
+# GPU-box step: SQ instruction-mix counters of the headline kernels (one --pmc pass), or of
+# ARGS for scripts/prof_one.py (e.g. ARGS="--kind 5 --codec lz4 --which compress").
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${TAG:-sq}
+if [ -n "$ARGS" ]; then PROG="scripts/prof_one.py $ARGS"; else PROG="bench.py --only headline --steps 2 --warmup 1 ${BENCH_ARGS}"; fi
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SMEM SQ_INSTS_BRANCH \
-  -d gpurun_out/$TAG -o pmc --output-format csv -- python3 bench.py --only headline --steps 2 --warmup 1 ${BENCH_ARGS} \
+  -d gpurun_out/$TAG -o pmc --output-format csv -- python3 $PROG \
   > gpurun_out/$TAG.log 2>&1 || { echo "sq pass failed"; tail -20 gpurun_out/$TAG.log; exit 1; }
 python3 - gpurun_out/$TAG/pmc_counter_collection.csv <<'PY'
 import csv, sys
