@@ -122,6 +122,8 @@ struct bitar_hip_ctx {
   // host-memory calls (bitar_hip_compress_host / _decompress_host): the copy stream paired
   // with each caller stream, created on first use
   std::vector<std::pair<hipStream_t, hipStream_t>> copy_streams;
+  // per caller stream: a stream for kernels forked off it (Zstd literals beside sequences)
+  std::vector<std::pair<hipStream_t, hipStream_t>> aux_streams;
 };
 
 namespace {
@@ -291,6 +293,8 @@ int bitar_hip_close(bitar_hip_ctx* ctx) {
     free_order_scratch(ctx);
     for (auto& cs : ctx->copy_streams) (void)hipStreamDestroy(cs.second);
     ctx->copy_streams.clear();
+    for (auto& cs : ctx->aux_streams) (void)hipStreamDestroy(cs.second);
+    ctx->aux_streams.clear();
     if (ctx->d_err) (void)hipFree(ctx->d_err);
     if (ctx->d_stats) (void)hipFree(ctx->d_stats);
   }
@@ -679,6 +683,29 @@ static uint32_t handoff_lanes() {
   return v;
 }
 
+// the stream paired with the caller's stream s in `list` (created on first use; null if that
+// fails)
+static hipStream_t side_stream_for(bitar_hip_ctx* ctx,
+                                   std::vector<std::pair<hipStream_t, hipStream_t>>& list,
+                                   hipStream_t s) {
+  std::lock_guard<std::mutex> g(ctx->mu);
+  for (auto& cs : list)
+    if (cs.first == s) return cs.second;
+  hipStream_t c = nullptr;
+  if (hipStreamCreateWithFlags(&c, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  list.emplace_back(s, c);
+  return c;
+}
+static int stream_after(hipStream_t b, hipStream_t a);
+
+// Zstd: zstd_hlit_kernel on a stream of its own, beside zstd_seqdec_kernel (both latency-bound
+// with about one wave per SIMD, and independent: the sequences need no literal);
+// BITAR_HIP_ZSTD_FORK=0 queues them one after the other
+static bool zstd_fork() {
+  static const bool v = env_long("BITAR_HIP_ZSTD_FORK", 1) != 0;
+  return v;
+}
+
 static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            const void* const* d_srcs, const void* d_slab, uint64_t stride,
                            const uint32_t* d_sizes, uint32_t nseg, uint32_t seg, void* d_out,
@@ -800,9 +827,16 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
 #define BITAR_ZSTD_TAIL(K, N)                                                                 \
   hipLaunchKernelGGL(bitar_hip::K<N>, dim3((cn + N - 1) / N), dim3(64), 0, s, csrcs, cslab, stride, \
                      csz, cn, seg, cout, cprod, hs, ew)
-      if (hs_n == 4) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 4);
-      else if (hs_n == 8) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 8);
-      else BITAR_ZSTD_TAIL(zstd_hlit_kernel, 16);
+      // the literal streams: beside the sequences' phase A on the aux stream when it exists
+      const hipStream_t main_s = s;
+      hipStream_t a = seq && zstd_fork() ? side_stream_for(ctx, ctx->aux_streams, s) : nullptr;
+      if (a && stream_after(a, s)) a = nullptr;
+      {
+        const hipStream_t s = a ? a : main_s;  // (the launch macro's stream)
+        if (hs_n == 4) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 4);
+        else if (hs_n == 8) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 8);
+        else BITAR_ZSTD_TAIL(zstd_hlit_kernel, 16);
+      }
       if (seq) {
 #define BITAR_SEQDEC(N)                                                                       \
   hipLaunchKernelGGL(bitar_hip::zstd_seqdec_kernel<N>, dim3((cn + N - 1) / N), dim3(64), 0, s,  \
@@ -811,6 +845,7 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
         else if (sd == 8) BITAR_SEQDEC(8);
         else BITAR_SEQDEC(16);
 #undef BITAR_SEQDEC
+        if (a && stream_after(s, a)) (void)hipStreamSynchronize(a);  // (join failed: wait here)
         hipLaunchKernelGGL(bitar_hip::zstd_exec_kernel, dim3(cn), dim3(64), 0, s, csrcs, cslab,
                            stride, cn, seg, cout, cprod, hs, rp, rcap, ew, stats, ord.order);
       }
@@ -853,13 +888,7 @@ int bitar_hip_decompress_slab(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
 // chunk's kernels (compress) -- or the copy stream waits on the chunk's decode before copying
 // it out (decompress).  s finally waits on the copy stream, so a sync of s covers the call.
 static hipStream_t copy_stream_for(bitar_hip_ctx* ctx, hipStream_t s) {
-  std::lock_guard<std::mutex> g(ctx->mu);
-  for (auto& cs : ctx->copy_streams)
-    if (cs.first == s) return cs.second;
-  hipStream_t c = nullptr;
-  if (hipStreamCreateWithFlags(&c, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  ctx->copy_streams.emplace_back(s, c);
-  return c;
+  return side_stream_for(ctx, ctx->copy_streams, s);
 }
 
 // b waits for what is queued on a now

@@ -16,6 +16,7 @@ constexpr uint32_t kRec = 32, kCells = 512, kHufWords = 1024;
 constexpr uint32_t kCellsAt = kRec, kHufAt = kRec + 3 * kCells;
 constexpr uint64_t kStride = 4ull * (kRec + 3 * kCells + kHufWords);
 constexpr uint32_t kHanded = 0xFFFFFFFDu;  // produced[i] while the lane kernels own segment i
+constexpr uint32_t kRecs = 0xFFFFFFFCu;    // produced[i]: zstd_seqdec_kernel's records ready
 
 // record words
 enum : uint32_t {

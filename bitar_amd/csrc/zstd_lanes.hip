@@ -401,6 +401,12 @@ __device__ __forceinline__ uint32_t word_raw(const GMEM uint8_t* s, int32_t a, i
 // lane decodes its stream backward (one table lookup per symbol, 8 symbols per 8-byte store)
 // into the tail of the segment's output slot, where zstd_handoff_kernel reads the literals.
 // Acceptance: the stream is consumed exactly (the wave decoder's huf_stream rule).
+// It may run alongside zstd_seqdec_kernel (runtime.hip), which needs no literal and moves a
+// segment from kHanded to kRecs (records ready) by compare-and-swap: the streams of both
+// states are decoded here, and a failure overwrites either.
+__device__ __forceinline__ bool lits_pending(uint32_t p) {
+  return p == zhand::kHanded || p == zhand::kRecs;
+}
 template <uint32_t S>
 __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
@@ -417,7 +423,7 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
   const uint32_t lane = lane_id();
   for (uint32_t l = 0; l < S; ++l) {
     const uint32_t il = blockIdx.x * S + l;
-    if (il >= nseg || produced[il] != kHanded) continue;
+    if (il >= nseg || !lits_pending(produced[il])) continue;
     const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
     if (h[kLitPend] != 1u) continue;
     const uint32_t nw = (1u << (h[kHufLog] & 0xFFu)) / 2;
@@ -431,7 +437,7 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
   lds_order();
   const uint32_t l = lane >> 2, j = lane & 3u;
   const uint32_t i = blockIdx.x * S + l;
-  if (l >= S || i >= nseg || produced[i] != kHanded) return;
+  if (l >= S || i >= nseg || !lits_pending(produced[i])) return;
   const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
   if (h[kLitPend] != 1u) return;
   const uint32_t hl = h[kHufLog], log = hl & 0xFFu, ns = hl >> 8;
@@ -516,7 +522,7 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     ok = 8 * (top - q) - (int32_t)used == 0;
   }
   if (!ok) {
-    produced[i] = 0xFFFFFFFFu;
+    atomicExch(&produced[i], 0xFFFFFFFFu);  // (over zstd_seqdec_kernel's kRecs, see above)
     atomicOr(err, 1u);
   }
 }

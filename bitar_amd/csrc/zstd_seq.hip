@@ -33,7 +33,6 @@ namespace zsq {
 
 using namespace zhand;
 
-constexpr uint32_t kRecs = 0xFFFFFFFCu;  // produced[i]: phase A done, records ready
 constexpr uint32_t kTab = 1280;          // cells per segment: LL 512 | OF 256 | ML 512
 constexpr uint32_t kOfAt = 512, kMlAt = 768;
 
@@ -293,7 +292,8 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
   }
   if (j == 0) {
     if (ok) {
-      produced[i] = kRecs;
+      // (zstd_hlit_kernel may run alongside and mark the segment failed first)
+      atomicCAS(&produced[i], kHanded, kRecs);
     } else {
       produced[i] = 0xFFFFFFFFu;
       atomicOr(err, 1u);
