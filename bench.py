@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--no-zstd", action="store_true")
     p.add_argument("--no-deflate", action="store_true")
     p.add_argument("--no-recordbatch", action="store_true")
+    p.add_argument("--no-lz4-arrow", action="store_true",
+                   help="skip the kind-2 (Arrow record batch) LZ4 round-trip line")
     p.add_argument("--no-lz4-wide", action="store_true",
                    help="skip the wide-parse LZ4 leg (the ratio operating point)")
     p.add_argument("--no-stock", action="store_true",
@@ -617,6 +619,12 @@ def main():
         # the reference's default frame: dynamic Huffman (config.h:151)
         dd = run_job(eng, "deflate_dyn", args.kind, world * n, 59460, 1, args.steps,
                      args.warmup, world, rank, seed=2000)
+    ka = None
+    if args.codec == "lz4" and args.kind != 2 and not args.no_lz4_arrow and want(args, "lz4_arrow"):
+        # the Arrow record-batch input (kind 2) through the headline's LZ4 round trip, one
+        # 1-GiB call per GPU (the harder, more representative LZ4 number)
+        ka = run_job(eng, "lz4", 2, world * n, seg, 1, args.steps, args.warmup, world, rank,
+                     seed=3)
     lw = None
     if args.codec == "lz4" and not args.no_lz4_wide and want(args, "lz4_wide"):
         # the ratio operating point: the same job through the wide LZ4 parse
@@ -705,6 +713,12 @@ def main():
             "the reference's DEFAULT frame: raw DEFLATE with dynamic Huffman codes "
             "(HuffmanEncoding::DYNAMIC, config.h:151) per 59460-B segment, compress + "
             "decompress, same input and sharding as the headline")
+    if ka is not None:
+        res["lz4_arrow"] = leg_summary(
+            "lz4", ka, world, args.steps, args.traffic_json,
+            "the headline's LZ4 round trip on the Arrow record-batch input (kind 2: int64 / "
+            "float64 / dictionary / string columns), 1 GiB per GPU, 64 KiB segments, one "
+            "call", leg="lz4_arrow")
     if lw is not None:
         res["lz4_wide"] = leg_summary(
             "lz4_wide", lw, world, args.steps, args.traffic_json,
