@@ -396,7 +396,7 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
     const uint32_t wd = (uint32_t)(s.wb >> 2);  // window base, in absolute dwords
     const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win);
     // (1) speculative decode of 4 candidates per lane
-    uint32_t rec[4];
+    uint32_t rec[4], mlv[4];
     lds_order();
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
@@ -418,9 +418,12 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
       const uint32_t dist = ((e2 >> 13) << de) + 1u + ((uint32_t)(bits >> (o2 + dl)) & ((1u << de) - 1));
       // any distance (far history -- beyond the ring's reach, stock zlib streams go to
       // 32 KiB -- is read back from HBM below)
-      const bool m_ok = is_len && e2 != 0 && ds < 30 && mlen <= 64 && dist <= s.op;
+      const bool d_ok = is_len && e2 != 0 && ds < 30 && dist <= s.op;
+      const bool m_ok = d_ok && mlen <= 64;
       const uint32_t nb = is_lit ? l1 : o2 + dl + de;
-      const uint32_t olen = is_lit ? 1u : m_ok ? mlen : 127u;
+      // 126: a match longer than a batch -- the walk stops on it and it is copied below
+      const uint32_t olen = is_lit ? 1u : m_ok ? mlen : d_ok ? 126u : 127u;
+      mlv[j] = mlen;
       const uint32_t payload = is_lit ? pay : (0x8000u | (dist - 1u));
       // record: next candidate (9 bits) | olen (7 bits, 127 = stop) | payload (16 bits:
       // literal byte, or 0x8000 | distance - 1)
@@ -507,7 +510,25 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
     // the batch continues only when that symbol was cut by a full batch
     const uint32_t olxu = __builtin_amdgcn_readfirstlane(olx);
     const bool taken_all = olxu == 0 || (olxu != 0x17Fu && lim == 64u);
-    if (out == 0) break;
+    // a long match (65..258 bytes) stopped the walk: its symbol at candidate k
+    const bool long_next = olxu == 0x17Eu;
+    auto long_match = [&]() __attribute__((always_inline)) -> bool {
+      const uint32_t ku = __builtin_amdgcn_readfirstlane(k);
+      const uint32_t jr = ku >> 6;
+      const uint32_t rv = jr == 0 ? readlane(rec[0], ku) : jr == 1 ? readlane(rec[1], ku)
+                          : jr == 2 ? readlane(rec[2], ku) : readlane(rec[3], ku);
+      const uint32_t ml = jr == 0 ? readlane(mlv[0], ku) : jr == 1 ? readlane(mlv[1], ku)
+                          : jr == 2 ? readlane(mlv[2], ku) : readlane(mlv[3], ku);
+      if (s.op + ml > s.cap) return false;  // (the scalar path rejects it)
+      match_copy(s, ring, ((rv >> 16) & 0x7FFFu) + 1u, ml);
+      P += (rv & 511u) - ku;  // past the symbol and its extra bits
+      moved = true;
+      return true;
+    };
+    if (out == 0) {
+      if (long_next && long_match()) continue;
+      break;
+    }
     // every output byte takes the payload of the latest symbol starting at or before it
     // (one symbol -- a batch cut short by a far match or a long code: its record for all)
     const uint32_t key = __builtin_amdgcn_readfirstlane(ns) == 1u
@@ -554,6 +575,10 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
     P += k;
     moved = true;
     ++s.nbatch;
+    if (long_next) {
+      if (long_match()) continue;
+      break;
+    }
     if (!taken_all) break;  // stopped on a symbol the batch does not take
   }
   if (moved) seek(s, win, b, P);
