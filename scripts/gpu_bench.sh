@@ -5,9 +5,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${TAG:-r01}
+if [ -z "$NO_BENCH" ]; then  # (NO_BENCH=1: profile passes only, e.g. a second call)
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; cat gpurun_out/smoke.log; exit 1; }
 timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { echo bench failed; tail -30 gpurun_out/bench_${TAG}.err; exit 1; }
 cat gpurun_out/bench_${TAG}.json
+fi
 if [ -n "$PROFILE" ]; then
   # one kernel-trace pass and one pass per PMC counter for each leg on its own (--only), so a
   # kernel's averages never mix launches of different legs (the record-batch leg also runs
