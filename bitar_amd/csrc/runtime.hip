@@ -701,9 +701,9 @@ static int stream_after(hipStream_t b, hipStream_t a);
 // Zstd: zstd_hlit_kernel on a stream of its own, beside zstd_seqdec_kernel (both latency-bound
 // with about one wave per SIMD, and independent: the sequences need no literal);
 // BITAR_HIP_ZSTD_FORK=0 queues them one after the other
-static bool zstd_fork() {
-  static const bool v = env_long("BITAR_HIP_ZSTD_FORK", 1) != 0;
-  return v;
+static uint32_t zstd_fork() {
+  static const uint32_t v = (uint32_t)env_long("BITAR_HIP_ZSTD_FORK", 1);
+  return v > 2 ? 1u : v;
 }
 
 static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
@@ -827,17 +827,17 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
 #define BITAR_ZSTD_TAIL(K, N)                                                                 \
   hipLaunchKernelGGL(bitar_hip::K<N>, dim3((cn + N - 1) / N), dim3(64), 0, s, csrcs, cslab, stride, \
                      csz, cn, seg, cout, cprod, hs, ew)
-      // the literal streams: beside the sequences' phase A on the aux stream when it exists
-      const hipStream_t main_s = s;
-      hipStream_t a = seq && zstd_fork() ? side_stream_for(ctx, ctx->aux_streams, s) : nullptr;
+      // the literal streams beside the sequences' phase A: one of the two on the aux stream
+      // (zstd_fork() 1: the literals there, launched first; 2: phase A there, first)
+      const uint32_t fork = seq ? zstd_fork() : 0u;
+      hipStream_t a = fork ? side_stream_for(ctx, ctx->aux_streams, s) : nullptr;
       if (a && stream_after(a, s)) a = nullptr;
-      {
-        const hipStream_t s = a ? a : main_s;  // (the launch macro's stream)
+      auto hlit = [&](hipStream_t s) {
         if (hs_n == 4) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 4);
         else if (hs_n == 8) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 8);
         else BITAR_ZSTD_TAIL(zstd_hlit_kernel, 16);
-      }
-      if (seq) {
+      };
+      auto seqdec = [&](hipStream_t s) {
 #define BITAR_SEQDEC(N)                                                                       \
   hipLaunchKernelGGL(bitar_hip::zstd_seqdec_kernel<N>, dim3((cn + N - 1) / N), dim3(64), 0, s,  \
                      csrcs, cslab, stride, csz, cn, seg, cprod, hs, rp, rcap, ew, stats)
@@ -845,6 +845,15 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
         else if (sd == 8) BITAR_SEQDEC(8);
         else BITAR_SEQDEC(16);
 #undef BITAR_SEQDEC
+      };
+      if (a && fork == 2) {
+        seqdec(a);
+        hlit(s);
+      } else {
+        hlit(a ? a : s);
+        if (seq) seqdec(s);
+      }
+      if (seq) {
         if (a && stream_after(s, a)) (void)hipStreamSynchronize(a);  // (join failed: wait here)
         hipLaunchKernelGGL(bitar_hip::zstd_exec_kernel, dim3(cn), dim3(64), 0, s, csrcs, cslab,
                            stride, cn, seg, cout, cprod, hs, rp, rcap, ew, stats, ord.order);
