@@ -398,12 +398,17 @@ __device__ __forceinline__ void huff_batch(State& s, uint8_t* win, uint8_t* ring
     // (1) speculative decode of 4 candidates per lane
     uint32_t rec[4], mlv[4];
     lds_order();
+    // candidate j's bits start 64 j bits (2 j dwords) after candidate 0's: the nine dwords
+    // they span are read once
+    const uint64_t ab0 = absbit0 + lane;
+    const uint32_t di0 = (uint32_t)(ab0 >> 5) - wd, sh = (uint32_t)(ab0 & 31u);
+    uint32_t dw[9];
+#pragma unroll
+    for (uint32_t k = 0; k < 9; ++k) dw[k] = w32[di0 + k];
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
       const uint32_t c = lane + kWave * j;
-      const uint64_t ab = absbit0 + c;
-      const uint32_t di = (uint32_t)(ab >> 5) - wd, sh = (uint32_t)(ab & 31u);
-      const uint32_t d0 = w32[di], d1 = w32[di + 1], d2 = w32[di + 2];
+      const uint32_t d0 = dw[2 * j], d1 = dw[2 * j + 1], d2 = dw[2 * j + 2];
       const uint64_t bits = (uint64_t)__builtin_amdgcn_alignbit(d1, d0, sh) |
                             ((uint64_t)__builtin_amdgcn_alignbit(d2, d1, sh) << 32);
       const uint32_t e = t.lit_fast[(uint32_t)bits & ((1u << kLitFast) - 1)];
