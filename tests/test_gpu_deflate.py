@@ -109,15 +109,32 @@ def test_full_size_deflate_roundtrip(eng, kind):
 
 
 # ---- dynamic Huffman (HuffmanEncoding::DYNAMIC, the reference default) ---------------------
+# (compress parity does not depend on the decoder: the dynamic-Huffman tests run under the
+# lanes4 decoder, and the reference's 59460-B segments under the other two as well)
+def _by_decoders(*ds):
+    ids = {4: "lanes4", 16: "lanes16", 0: "wave"}
+    return pytest.mark.parametrize("inflate_decoder", list(ds), indirect=True,
+                                   ids=[ids[d] for d in ds])
+
+
+@_by_decoders(4)
 @pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("seg", [59460, 65536, 2048, 100, 13, 8])
-def test_deflate_dynamic_bit_exact_vs_oracle(eng, kind, seg, inflate_decoder):
+def test_deflate_dynamic_bit_exact_vs_oracle(eng, kind, seg):
     """deflate_dyn_parse_kernel + deflate_dyn_emit_kernel emit the oracle's exact stream
     (dynamic, fixed or stored block, whichever is smallest); zlib decodes every segment and
     our inflaters round-trip it."""
+    _dynamic_bit_exact(eng, kind, seg)
+
+
+@_by_decoders(16, 0)
+@pytest.mark.parametrize("kind", [0, 1, 2, 3, 4, 5, 6])
+def test_deflate_dynamic_bit_exact_other_decoders(eng, kind):
+    _dynamic_bit_exact(eng, kind, 59460)
+
+
+def _dynamic_bit_exact(eng, kind, seg):
     import bitar_amd
-    if inflate_decoder != 4 and seg != 59460:
-        pytest.skip("compress parity is decoder-independent: one decoder per extra size")
     n = 3 * seg + seg // 3 + 1 if seg > 100 else 700
     data = O.fill(kind, 93, n)
     slab, stride, sizes = eng.compress(bitar_amd.CODEC_DEFLATE_DYNAMIC, up(data)[:n], seg)
@@ -138,12 +155,11 @@ def test_deflate_dynamic_bit_exact_vs_oracle(eng, kind, seg, inflate_decoder):
     assert np.array_equal(down(out)[:n], data)
 
 
-def test_deflate_dynamic_covers_every_block_type(eng, inflate_decoder):
+@_by_decoders(4)
+def test_deflate_dynamic_covers_every_block_type(eng):
     """Inputs that make the encoder choose stored (random), fixed (tiny) and dynamic blocks,
     in one ragged batch, including a 65536-B stored segment (two stored blocks)."""
     import bitar_amd
-    if inflate_decoder != 4:
-        pytest.skip("one decoder suffices")
     seg = 65536
     parts = [O.fill(0, 1, seg), O.fill(1, 2, 40), O.fill(6, 3, seg), O.fill(3, 4, seg),
              O.fill(0, 5, 5000), bytes([7]) * 1 + b"", O.fill(2, 6, 20000)]
@@ -160,11 +176,10 @@ def test_deflate_dynamic_covers_every_block_type(eng, inflate_decoder):
     assert modes == {0, 1, 2}
 
 
-def test_deflate_dynamic_scattered_slots(eng, inflate_decoder):
+@_by_decoders(4)
+def test_deflate_dynamic_scattered_slots(eng):
     """compress_scattered (the C++ slot pool's form) writes the same streams."""
     import bitar_amd
-    if inflate_decoder != 4:
-        pytest.skip("one decoder suffices")
     seg = 59460
     n = 5 * seg + 99
     data = O.fill(2, 8, n)
@@ -190,12 +205,11 @@ def test_deflate_dynamic_scattered_slots(eng, inflate_decoder):
         assert (0, blob) == O.deflate_dynamic(plain), i
 
 
+@_by_decoders(4, 0)
 @pytest.mark.parametrize("kind", [1, 2])
-def test_full_size_deflate_dynamic_roundtrip(eng, kind, inflate_decoder):
+def test_full_size_deflate_dynamic_roundtrip(eng, kind):
     """1 GiB at 59460-B segments with dynamic Huffman: round trip + zlib + oracle samples."""
     import bitar_amd
-    if inflate_decoder == 16:
-        pytest.skip("lanes4 and wave decoders cover the full size")
     n = 1 << 30
     seg = 59460
     data = eng.empty(n)
