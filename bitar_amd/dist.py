@@ -147,7 +147,7 @@ class SizeGather:
         elif coll:
             dist.all_gather_into_tensor(gathered, padded, group=group)
         else:
-            gathered.copy_(padded)
+            gathered = padded  # (one rank, no group: the sizes are the whole gather)
         src = self.src if self.src.device == dev else self.src.to(dev)
         return gathered.index_select(0, src).to(torch.int64) & 0xFFFFFFFF
 
