@@ -23,6 +23,7 @@ MAX_SEG_SIZE = 65536
 # bitar_hip_config.flags (initial decoder options of a context)
 FLAG_INFLATE_WAVE_ONLY, FLAG_ZSTD_WAVE_ONLY, FLAG_ZSTD_LANE_EXEC, FLAG_COUNT_PATHS = 1, 2, 4, 8
 FLAG_PLAIN_ORDER = 0x10  # segment i is workgroup i (no cost-ordered dispatch; same output)
+FLAG_ZSTD_SERIAL = 0x20  # Zstd literals and phase A in series (default: side by side)
 # bitar_hip_path_counter indices
 PATHS = ("inflate_wave", "inflate_wave_reject", "inflate_batch_segs", "inflate_batches",
          "zstd_wave", "zstd_handed", "zstd_seqdec", "zstd_seqdec_reject", "zstd_exec",

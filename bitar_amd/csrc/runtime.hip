@@ -105,6 +105,7 @@ struct bitar_hip_ctx {
   unsigned long long* d_stats = nullptr;  // BITAR_HIP_PATH_COUNT path counters
   // decoder options (bitar_hip_decoder_options), per context
   std::atomic<uint32_t> inflate_lanes{4}, zstd_lanes{16}, zstd_seq{1}, count_paths{0};
+  std::atomic<uint32_t> zstd_fork{1};  // Zstd literals beside phase A (decompress_impl)
   std::atomic<uint32_t> cost_order{1};  // LZ4: dispatch the estimated most expensive segments first
   std::mutex mu;              // guards `words` and `order_scratch`
   std::vector<std::pair<hipStream_t, uint32_t>> words;  // stream -> error word index
@@ -613,6 +614,15 @@ static long env_long(const char* name, long dflt) {
   return e ? std::strtol(e, nullptr, 10) : dflt;
 }
 
+// Zstd: zstd_hlit_kernel on a stream of its own, beside zstd_seqdec_kernel (both latency-bound
+// with about one wave per SIMD, and independent: the sequences need no literal).  Per
+// context: BITAR_HIP_FLAG_ZSTD_SERIAL (or BITAR_HIP_ZSTD_FORK=0) queues them one after the
+// other; BITAR_HIP_ZSTD_FORK=2 (timing runs) puts phase A on the side stream instead.
+static uint32_t zstd_fork_env() {
+  static const uint32_t v = (uint32_t)env_long("BITAR_HIP_ZSTD_FORK", 1);
+  return v > 2 ? 1u : v;
+}
+
 static void init_options(bitar_hip_ctx* ctx, uint32_t flags) {
   // The lane inflater in front of the wave inflater is off by default since the wave
   // inflater's batches take far matches (round 3): 1 GiB fixed-Huffman decode, wave alone vs
@@ -625,6 +635,7 @@ static void init_options(bitar_hip_ctx* ctx, uint32_t flags) {
   ctx->zstd_lanes = flags & BITAR_HIP_FLAG_ZSTD_WAVE_ONLY
                         ? 0u : zstd_lanes_from(env_long("BITAR_HIP_ZSTD_LANES", 16));
   ctx->zstd_seq = flags & BITAR_HIP_FLAG_ZSTD_LANE_EXEC ? 0u : env_long("BITAR_HIP_ZSTD_SEQ", 1) != 0;
+  ctx->zstd_fork = flags & BITAR_HIP_FLAG_ZSTD_SERIAL ? 0u : zstd_fork_env();
   ctx->count_paths = (flags & BITAR_HIP_FLAG_COUNT_PATHS) ? 1u : 0u;
   ctx->cost_order = (flags & BITAR_HIP_FLAG_PLAIN_ORDER) ? 0u : env_long("BITAR_HIP_COST_ORDER", 1) != 0;
 }
@@ -698,13 +709,6 @@ static hipStream_t side_stream_for(bitar_hip_ctx* ctx,
 }
 static int stream_after(hipStream_t b, hipStream_t a);
 
-// Zstd: zstd_hlit_kernel on a stream of its own, beside zstd_seqdec_kernel (both latency-bound
-// with about one wave per SIMD, and independent: the sequences need no literal);
-// BITAR_HIP_ZSTD_FORK=0 queues them one after the other
-static uint32_t zstd_fork() {
-  static const uint32_t v = (uint32_t)env_long("BITAR_HIP_ZSTD_FORK", 1);
-  return v > 2 ? 1u : v;
-}
 
 static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            const void* const* d_srcs, const void* d_slab, uint64_t stride,
@@ -828,8 +832,8 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
   hipLaunchKernelGGL(bitar_hip::K<N>, dim3((cn + N - 1) / N), dim3(64), 0, s, csrcs, cslab, stride, \
                      csz, cn, seg, cout, cprod, hs, ew)
       // the literal streams beside the sequences' phase A: one of the two on the aux stream
-      // (zstd_fork() 1: the literals there, launched first; 2: phase A there, first)
-      const uint32_t fork = seq ? zstd_fork() : 0u;
+      // (zstd_fork 1: the literals there, launched first; 2: phase A there, first)
+      const uint32_t fork = seq ? ctx->zstd_fork.load(std::memory_order_relaxed) : 0u;
       hipStream_t a = fork ? side_stream_for(ctx, ctx->aux_streams, s) : nullptr;
       if (a && stream_after(a, s)) a = nullptr;
       auto hlit = [&](hipStream_t s) {

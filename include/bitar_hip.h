@@ -81,6 +81,10 @@ typedef struct {
 #define BITAR_HIP_FLAG_PLAIN_ORDER 0x10u      /* calls dispatch segment i as workgroup i
                                                  (default, from 2048 segments: estimated most
                                                  expensive first; the output is identical) */
+#define BITAR_HIP_FLAG_ZSTD_SERIAL 0x20u      /* Zstd decode: the Huffman literal streams and
+                                                 the sequences' phase A one after the other on
+                                                 the call's stream (default: side by side, the
+                                                 literals on a paired stream; same output) */
 
 /* Number of visible gfx950 devices.  Replaces rte_compressdev_devices_get() in
  * CompressDriver::ListAvailableDeviceIds (reference src/driver.cc:173-190). */

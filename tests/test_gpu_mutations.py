@@ -125,6 +125,35 @@ def test_zstd_sequence_path_mutations_like_oracle(eng, counting_zstd):
     print(f"zstd mutations: {len(cases)} cases, {n_ok} accepted, counters {c}")
 
 
+def test_zstd_literal_mutations_forked_and_serial(eng):
+    """The Huffman literal streams (zstd_hlit_kernel) decode beside the sequences' phase A
+    (zstd_seqdec_kernel), on a side stream; the only word they share is produced[i] (phase A
+    moves it kHanded -> kRecs by compare-and-swap, a literal failure overwrites it).
+    Mutations aimed at the literal section must get the oracle's verdicts with the kernels
+    side by side, and a context that runs them in series (BITAR_HIP_FLAG_ZSTD_SERIAL) must
+    produce the same bytes and verdicts."""
+    import bitar_amd
+    srcs = _zstd_sources()
+    rng = np.random.default_rng(8879)
+    cases = []
+    for frame, _ in srcs:
+        # hot range: the middle third -- the last block's literal section (Huffman tree and
+        # streams) sits before its sequence section
+        cases += _mutations(frame, rng, 32, hot=(len(frame) // 3, 2 * len(frame) // 3))
+    n_ok = _check_like_oracle(eng, O.CODEC_ZSTD, cases, O.zstd_decompress)
+    assert 0 < n_ok < len(cases)
+    ok_a, out_a, prod_a = _decode_blobs(eng, O.CODEC_ZSTD, cases, SEG)
+    serial = bitar_amd.Engine(0, num_streams=1, flags=bitar_amd.FLAG_ZSTD_SERIAL)
+    ok_b, out_b, prod_b = _decode_blobs(serial, O.CODEC_ZSTD, cases, SEG)
+    assert ok_a == ok_b
+    assert np.array_equal(prod_a, prod_b)
+    for k in range(len(cases)):
+        if prod_a[k] != 0xFFFFFFFF:
+            n = int(prod_a[k])
+            assert out_a[k * SEG:k * SEG + n].tobytes() == out_b[k * SEG:k * SEG + n].tobytes(), k
+    del serial
+
+
 def test_two_engines_with_different_decoders_concurrently(eng):
     """Decoder options are per context: two engines, one with the lane decoders and one with
     the wave decoders alone, decode the same batch at the same time on their own streams;
