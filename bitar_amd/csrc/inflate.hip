@@ -12,13 +12,28 @@
 // matches / stored blocks reuse the window + ring machinery of stream_ring.hip.h.
 #include "stream_ring.hip.h"
 
+// Fast-table sizes, namespace and kernel name: inflate_fixed.hip builds this file a second
+// time with 9 / 8-bit tables for fixed-Huffman streams (inflate_fixed_kernel)
+#ifndef BITAR_INFL_NS
+#define BITAR_INFL_NS infl
+#endif
+#ifndef BITAR_INFL_KERNEL
+#define BITAR_INFL_KERNEL inflate_kernel
+#endif
+
 namespace bitar_hip {
 
-namespace infl {
+namespace BITAR_INFL_NS {
 
 using namespace sr;
 
-constexpr uint32_t kLitFast = 10, kDistFast = 9, kClFast = 7;
+#ifndef BITAR_INFL_LIT_FAST
+#define BITAR_INFL_LIT_FAST 10
+#endif
+#ifndef BITAR_INFL_DIST_FAST
+#define BITAR_INFL_DIST_FAST 9
+#endif
+constexpr uint32_t kLitFast = BITAR_INFL_LIT_FAST, kDistFast = BITAR_INFL_DIST_FAST, kClFast = 7;
 
 __device__ __forceinline__ uint32_t bpermute_u32(uint32_t v, uint32_t src_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
@@ -258,6 +273,9 @@ __device__ __forceinline__ uint32_t pick(const uint32_t (&r)[8], uint32_t j) {
   const uint32_t a2 = b0 ? r[5] : r[4], a3 = b0 ? r[7] : r[6];
   const uint32_t c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
   return b2 ? c1 : c0;
+}
+__device__ __forceinline__ uint32_t pick(const uint32_t (&r)[2], uint32_t j) {
+  return (j & 1u) ? r[1] : r[0];
 }
 __device__ __forceinline__ uint32_t pick(const uint32_t (&r)[4], uint32_t j) {
   const bool b0 = j & 1u, b1 = j & 2u;
@@ -624,14 +642,14 @@ __device__ __forceinline__ int inflate_codes(State& s, uint8_t* win, uint8_t* ri
   }
 }
 
-}  // namespace infl
+}  // namespace BITAR_INFL_NS
 
-__global__ __launch_bounds__(64) void inflate_kernel(
+__global__ __launch_bounds__(64) void BITAR_INFL_KERNEL(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
     uint32_t defer_only, unsigned long long* __restrict__ stats, const uint32_t* __restrict__ order) {
-  using namespace infl;
+  using namespace BITAR_INFL_NS;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
   __shared__ __attribute__((aligned(16))) Tables t;
   uint8_t* win = lds;

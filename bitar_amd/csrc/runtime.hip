@@ -37,6 +37,9 @@ __global__ void deflate_compress_kernel(const uint8_t*, uint64_t, uint32_t, uint
 __global__ void inflate_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
                                uint32_t*, uint32_t, unsigned long long*, const uint32_t*);
+__global__ void inflate_fixed_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
+                               const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
+                               uint32_t*, uint32_t, unsigned long long*, const uint32_t*);
 template <uint32_t L>
 __global__ void inflate_lanes_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                      const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
@@ -715,7 +718,10 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            const uint32_t* d_sizes, uint32_t nseg, uint32_t seg, void* d_out,
                            uint64_t capacity, uint32_t* d_produced) {
   if (int r = enter(ctx)) return r;
-  if (codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC) codec = BITAR_HIP_CODEC_DEFLATE;  // same decoder
+  // the caller's FIXED hint picks the inflater built for fixed-Huffman streams (9 / 8-bit
+  // fast tables, more waves per CU; any stream still decodes, inflate_fixed.hip)
+  const bool fixed_hint = codec == BITAR_HIP_CODEC_DEFLATE;
+  if (codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC) codec = BITAR_HIP_CODEC_DEFLATE;  // same format
   if (codec == BITAR_HIP_CODEC_LZ4_WIDE) codec = BITAR_HIP_CODEC_LZ4;              // same format
   if (codec != BITAR_HIP_CODEC_LZ4 && codec != BITAR_HIP_CODEC_DEFLATE &&
       codec != BITAR_HIP_CODEC_ZSTD)
@@ -770,9 +776,9 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
     }
     SegOrder ord;
     if (int r = ord.make(ctx, s, nseg, d_sizes, [](uint32_t*) {}, seg)) return r;
-    hipLaunchKernelGGL(bitar_hip::inflate_kernel, dim3(nseg), dim3(64), 0, s, srcs, slab,
-                       stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s), L ? 1u : 0u,
-                       stats, ord.order);
+    hipLaunchKernelGGL(fixed_hint ? bitar_hip::inflate_fixed_kernel : bitar_hip::inflate_kernel,
+                       dim3(nseg), dim3(64), 0, s, srcs, slab, stride, d_sizes, nseg, seg, out,
+                       d_produced, err_word(ctx, s), L ? 1u : 0u, stats, ord.order);
     if (int r = ord.release()) return r;
   }
   else {

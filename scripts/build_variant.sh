@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/../bitar_amd"
 name=$1; defs=$2
 mkdir -p build_$name lib/variants
-for f in runtime lz4_decompress inflate compress util_kernels zstd_decompress zstd_compress zstd_lanes inflate_lanes deflate_dyn checksum lz4_chain zstd_seq; do
+for f in runtime lz4_decompress inflate inflate_fixed compress util_kernels zstd_decompress zstd_compress zstd_lanes inflate_lanes deflate_dyn checksum lz4_chain zstd_seq; do
   extra=""
   case " ${ILP_FILES:-lz4_decompress zstd_seq zstd_lanes} " in *" $f "*) extra="-mllvm -amdgpu-sched-strategy=max-ilp";; esac  # (as the Makefile; ILP_FILES overrides)
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics $extra $defs -c csrc/$f.hip -o build_$name/$f.o &

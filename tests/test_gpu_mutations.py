@@ -57,10 +57,13 @@ def counting_inflate(request, eng):
 _dynamic_sources = M.dynamic_sources
 
 
-def test_inflate_batch_mutations_like_oracle(eng, counting_inflate):
+@pytest.mark.parametrize("codec", [O.CODEC_DEFLATE_DYN, O.CODEC_DEFLATE], ids=["dyn", "fixed-hint"])
+def test_inflate_batch_mutations_like_oracle(eng, counting_inflate, codec):
+    """Both inflaters: inflate_kernel (the DYNAMIC hint) and inflate_fixed_kernel (the FIXED
+    hint, whose 9 / 8-bit fast tables send these streams' longer codes to the slow path)."""
     srcs = _dynamic_sources()
     # the unmutated streams decode and run the batch path
-    _check_like_oracle(eng, O.CODEC_DEFLATE, [s for s, _ in srcs], O.inflate)
+    _check_like_oracle(eng, codec, [s for s, _ in srcs], O.inflate)
     c0 = eng.path_counters()
     assert c0["inflate_wave"] == len(srcs) and c0["inflate_wave_reject"] == 0
     assert c0["inflate_batch_segs"] == len(srcs), c0
@@ -69,7 +72,7 @@ def test_inflate_batch_mutations_like_oracle(eng, counting_inflate):
     for stream, _ in srcs:
         # hot range: the block header and the code-length / literal-length tables
         cases += _mutations(stream, rng, 48, hot=(0, 80))
-    n_ok = _check_like_oracle(eng, O.CODEC_DEFLATE, cases, O.inflate)
+    n_ok = _check_like_oracle(eng, codec, cases, O.inflate)
     c = eng.path_counters()
     # every mutated stream went to inflate_kernel (dynamic blocks: the lane inflater defers
     # them all), most of them ran batches, and the oracle both accepted and rejected some
