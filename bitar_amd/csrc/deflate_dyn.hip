@@ -74,10 +74,13 @@ constexpr uint32_t kMaskBytes = 16384;  // <= 1024 windows (n <= 65536)
 constexpr uint32_t kPlanWindows = kPlanRecBytes + 1;  // word index of the window count
 constexpr uint32_t kPlanTail = kPlanRecBytes + 2;     // word index of the tail start
 
-struct RecOut : ByteOut {  // the byte ring carries the match records
+// (a 512-B byte ring and a 32-window mask ring: 8.4 KiB of LDS, 19 waves per CU instead of
+// 17 -- the parse is latency-bound; a row of input adds <= 16 windows between drains)
+constexpr uint32_t kRecBuf = 512, kMaskRing = 32;
+struct RecOut : ByteOutT<kRecBuf> {  // the byte ring carries the match records
   uint32_t* lh;          // LDS literal/length histogram (286)
   uint32_t* dh;          // LDS distance histogram (30)
-  uint4* cst;            // LDS ring of 64 window mask pairs
+  uint4* cst;            // LDS ring of kMaskRing window mask pairs
   GMEM uint4* cdst;      // mask area
   uint32_t nwin, cflushed;
 
@@ -100,7 +103,7 @@ struct RecOut : ByteOut {  // the byte ring carries the match records
       atomicAdd(&dh[ds], 1u);
     }
     if (lane == 0)
-      cst[nwin & 63u] = make_uint4((uint32_t)W.chain, (uint32_t)(W.chain >> 32), (uint32_t)litm,
+      cst[nwin & (kMaskRing - 1)] = make_uint4((uint32_t)W.chain, (uint32_t)(W.chain >> 32), (uint32_t)litm,
                                    (uint32_t)(litm >> 32));
     lds_order();
     ++nwin;
@@ -118,11 +121,11 @@ struct RecOut : ByteOut {  // the byte ring carries the match records
   __device__ __forceinline__ void flush_masks(uint32_t upto) {
     const uint32_t lane = lane_id();
     lds_order();
-    for (uint32_t w = cflushed + lane; w < upto; w += kWave) cdst[w] = cst[w & 63u];
+    for (uint32_t w = cflushed + lane; w < upto; w += kWave) cdst[w] = cst[w & (kMaskRing - 1)];
     cflushed = upto;
   }
   __device__ __forceinline__ void drain() {
-    ByteOut::drain();
+    ByteOutT<kRecBuf>::drain();
     flush_masks(nwin);
   }
   // the tail literals [s, s + n)
@@ -221,7 +224,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return readlane(wave_
 
 // ---- pass 2 output: LDS bit ring of 64-bit lane contributions -----------------------------
 constexpr uint32_t kB = 4;  // windows per emit step
-constexpr uint32_t kStageWords = 1024, kStageMask = kStageWords - 1;
+constexpr uint32_t kStageWords = 512, kStageMask = kStageWords - 1;
 // one window adds <= 64 lanes x 45 bits = 90 words (+2 for the spill)
 constexpr uint32_t kFlushMargin = kB * 92 + 8;
 
@@ -290,25 +293,29 @@ struct BitOut {
   }
 };
 
-// A global byte range streamed through a 2 KiB LDS ring in 1 KiB rows (16 B per lane, the
-// next row prefetched into registers a whole row ahead): the emit pass's per-window reads
-// are LDS reads, never a dependent HBM round trip.  Byte k of the range (relative to the
-// 16-B aligned base) lives at ring[k & 2047] once ensure(k + 1) has run.
+// A global byte range streamed through an LDS ring of two rows of RB bytes (RB = 1024: 16 B
+// per lane, 512: 8 B), the next row prefetched into registers a whole row ahead: the emit
+// pass's per-window reads are LDS reads, never a dependent HBM round trip.  Byte k of the
+// range (relative to its 16-B aligned base) lives at ring[k & (2 RB - 1)] once ensure(k + 1)
+// has run.
+template <uint32_t RB>
 struct RowRing {
-  const GMEM uint4* src16;  // 16-B aligned base of the range
-  uint32_t limit;           // bytes readable from src16 (blocks at or past it are not loaded)
-  uint8_t* ring;            // 2 KiB of LDS
-  uint32_t loaded;          // [0, loaded) committed; the ring holds [loaded - 2048, loaded)
-  uint4 nxt;                // the next row, in flight
+  using V = typename std::conditional<RB == 1024, uint4, uint2>::type;
+  static constexpr uint32_t kPer = RB / 64, kMask = 2 * RB - 1;
+  const GMEM V* srcv;  // the range's aligned base
+  uint32_t limit;      // bytes readable from it (blocks at or past it are not loaded)
+  uint8_t* ring;       // 2 RB bytes of LDS
+  uint32_t loaded;     // [0, loaded) committed; the ring holds [loaded - 2 RB, loaded)
+  V nxt;               // the next row, in flight
 
-  __device__ __forceinline__ uint4 load_row(uint32_t r) const {
-    const uint32_t o = 1024u * r + 16u * lane_id();
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (o < limit) v = src16[o >> 4];
+  __device__ __forceinline__ V load_row(uint32_t r) const {
+    const uint32_t o = RB * r + kPer * lane_id();
+    V v{};
+    if (o < limit) v = srcv[o / kPer];
     return v;
   }
   __device__ __forceinline__ void init(const GMEM uint4* base, uint32_t lim, uint8_t* lds) {
-    src16 = base;
+    srcv = reinterpret_cast<const GMEM V*>(base);
     limit = lim;
     ring = lds;
     loaded = 0;
@@ -316,17 +323,17 @@ struct RowRing {
   }
   __device__ __forceinline__ void ensure(uint32_t end) {
     while (loaded < end) {
-      const uint32_t r = loaded >> 10;
+      const uint32_t r = loaded / RB;
       lds_order();
-      reinterpret_cast<uint4*>(ring)[((r & 1u) << 6) + lane_id()] = nxt;
+      reinterpret_cast<V*>(ring)[((r & 1u) << 6) + lane_id()] = nxt;
       lds_order();
-      loaded += 1024;
+      loaded += RB;
       nxt = load_row(r + 1);
     }
   }
-  __device__ __forceinline__ uint32_t byte(uint32_t k) const { return ring[k & 2047u]; }
+  __device__ __forceinline__ uint32_t byte(uint32_t k) const { return ring[k & kMask]; }
   __device__ __forceinline__ uint32_t word(uint32_t k) const {  // k 4-aligned
-    return reinterpret_cast<const uint32_t*>(ring)[(k & 2047u) >> 2];
+    return reinterpret_cast<const uint32_t*>(ring)[(k & kMask) >> 2];
   }
 };
 
@@ -338,8 +345,8 @@ __global__ __launch_bounds__(64) void deflate_dyn_parse_kernel(
   using namespace dyn;
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
-  __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
-  __shared__ __attribute__((aligned(16))) uint4 cst[64];
+  __shared__ __attribute__((aligned(16))) uint8_t obuf[kRecBuf + kWave];
+  __shared__ __attribute__((aligned(16))) uint4 cst[kMaskRing];
   __shared__ uint32_t hist[kNLit + kNDist];
   const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
@@ -389,8 +396,10 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
   __shared__ uint16_t cls[kNLit + kNDist + 4];
   __shared__ uint32_t clf[kNCl];
   // the tree scratch and the output bit ring share LDS: codes are built before any output
-  // (codes first; then the bit ring + the chain, record and input rings, 2 KiB each)
-  constexpr uint32_t kEmitLds = kStageWords * 4 + 3 * 2048;
+  // (codes first; then the 2-KiB bit ring + the window-mask and input rings, 1 KiB each,
+  // and the record ring, 2 KiB: a step may read 1 KiB of records).  6 KiB instead of 10:
+  // 16 workgroups per CU instead of 11 (the pass is latency-bound: 8 cost it 10 %)
+  constexpr uint32_t kEmitLds = kStageWords * 4 + 1024 + 2048 + 1024;
   __shared__ __attribute__((aligned(16))) uint8_t pool[sizeof(TreeLds) > kEmitLds
                                                            ? sizeof(TreeLds) : kEmitLds];
   TreeLds& T = *reinterpret_cast<TreeLds*>(pool);
@@ -548,7 +557,8 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
 
   // symbols, kB windows per step (independent LDS reads and prefix sums across the
   // windows of a step); window masks, match records and input bytes stream through LDS rings
-  RowRing C, R, I;
+  RowRing<512> C, I;
+  RowRing<1024> R;
   const uint32_t s0 = (uint32_t)((uintptr_t)in & 15u);
   const uint32_t nwin = plan[kPlanWindows];
   uint32_t emitted = plan[kPlanTail];
@@ -556,10 +566,10 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
     uint8_t* rings = pool + kStageWords * 4;
     C.init(reinterpret_cast<const GMEM uint4*>(scr + kPlanBytes), 16 * nwin, rings);
     R.init(reinterpret_cast<const GMEM uint4*>(scr + kPlanBytes + kMaskBytes),
-           (plan[kPlanRecBytes] + 15u) & ~15u, rings + 2048);
+           (plan[kPlanRecBytes] + 15u) & ~15u, rings + 1024);
     const uint64_t span = (uint64_t)(global_ptr(input + n_total) - (in - s0));
     I.init(reinterpret_cast<const GMEM uint4*>(in - s0),
-           (uint32_t)(span < (uint64_t)n + s0 ? span : (uint64_t)n + s0), rings + 4096);
+           (uint32_t)(span < (uint64_t)n + s0 ? span : (uint64_t)n + s0), rings + 3072);
   }
   if (BITAR_DYN_VARIANT == 1) emitted = n;  // timing experiment: no symbol emission
   if (BITAR_DYN_VARIANT != 1) {
