@@ -236,9 +236,10 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ order) {
   using namespace lz4d;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
-  uint8_t* win = lds;
-  uint8_t* ring = lds + kWin;
+  // the ring at LDS address 0: a history source is then (address & mask), one add fewer
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing + kWin];
+  uint8_t* ring = lds;
+  uint8_t* win = lds + kRing;
   if (blockIdx.x >= nseg) return;
   // cost-ordered dispatch (seg_order_kernel): workgroup b decodes segment order[b]
   const uint32_t i = order ? order[blockIdx.x] : blockIdx.x;
@@ -321,9 +322,10 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       // kMaxEligibleNext; the walk stops at a lane >= 64, which was not parsed, after
       // consuming the sequence) | output length (255: not eligible, the walk's one compare
       // then stops; an ineligible token's wider nxt only ORs into those already-set bits).
-      // Sequence record (stays in the token lane): offset (16 bits) | literal count.
+      // Sequence record (stays in the token lane): offset (16 bits) | literal count (byte 2;
+      // <= 60 when eligible) | lane of the first literal (byte 3: lane + 1 + lx <= 64).
       const uint32_t nxt = lane + 3 + (lx ? 1u : 0u) + (mx ? 1u : 0u) + cL;
-      const uint32_t pr = coff | (cL << 16);
+      const uint32_t pr = coff | (cL << 16) | ((lane + 1u + (lx ? 1u : 0u)) << 24);
       // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
       const uint32_t room = s.cap - s.op;
       const uint32_t lim = room < kBatchOut ? room : kBatchOut;
@@ -358,26 +360,26 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         // an LDS byte address.  Bytes of the first half are in the ring already when the
         // second half reads them.
         const uint32_t ostart = key >> 24;
-        const uint32_t seqlane = key & 63u;
         // the record from its token lane (ds_bpermute reads address bits 2..7 only)
         const uint32_t rec =
             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(key << 2), (int)pr);
-        const uint32_t jL = rec >> 16;
         const uint32_t joff = rec & 0xFFFFu;
-        const uint32_t r = q - ostart;  // < kSeqOut: a sequence is at most 64 bytes
-        const bool is_lit = r < jL;
-        const uint32_t m = r - jL;
-        // overlapping copy (offset <= match position): fold the source into the first period
-        // (m mod off, exact in fp32 for m, off < 64); skipped when no byte needs it
-        uint32_t mm = m;
-        if (ballot(!is_lit && joff <= m && q < out)) {
-          const float qf = floorf(((float)(m & 63u) + 0.5f) *
+        const uint32_t ms = ostart + ((rec >> 16) & 0xFFu);  // the match's first byte (vs op)
+        const bool is_lit = q < ms;
+        // a match byte's source: q - off (vs op)
+        int32_t srel = (int32_t)q - (int32_t)joff;
+        // overlapping copy (source inside the match itself: q - off >= ms): fold the source
+        // into the first period, ms + (m mod off) - off with m = q - ms (exact in fp32 for
+        // m, off < 64); skipped when no byte needs it
+        if (ballot(srel >= (int32_t)ms && q < out)) {
+          const uint32_t m = (q - ms) & 63u;
+          const float qf = floorf(((float)m + 0.5f) *
                                   __builtin_amdgcn_rcpf((float)(joff > 1u ? joff : 1u)));
-          mm = joff <= m ? (m & 63u) - (uint32_t)qf * joff : m;
+          const int32_t sf = (int32_t)(ms + m - (uint32_t)qf * joff) - (int32_t)joff;
+          srel = srel >= (int32_t)ms ? sf : srel;  // (a select: no exec-mask branch)
         }
-        const int32_t srel = (int32_t)(ostart + jL + mm) - (int32_t)joff;  // vs op
-        const uint32_t hist = kWin + ((base + s.op + (uint32_t)srel) & kRingMask);
-        const uint32_t lit_addr = wrel + seqlane + 1 + (jL >= 15u ? 1u : 0u) + r;
+        const uint32_t hist = (base + s.op + (uint32_t)srel) & kRingMask;  // ring at 0
+        const uint32_t lit_addr = kRing + wrel + (rec >> 24) + (q - ostart);
         // every form computed before the selects (the empty asm pins them), so the compiler
         // does not turn the selects into an exec-mask if / else
         uint32_t lit_a = lit_addr, hist_a = hist, alias_a = (uint32_t)srel | 0x80000000u;
@@ -408,7 +410,8 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         }
         // one gather (LDS, or HBM for far history), one store
         lds_order();
-        uint32_t g = lds[st & 0x3FFFu];
+        // (near batches: every resolved source is an LDS address < kRing + kWin)
+        uint32_t g = lds[big ? st & 0x3FFFu : st];
         if (big) {
           const bool gfar = (st >> 30) == 1u && q < out;
           const uint64_t farm = ballot(gfar);
