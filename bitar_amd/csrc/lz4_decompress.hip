@@ -300,6 +300,10 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       //     length byte, literals, offset, optional match length byte
       lds_order();
       const uint32_t wc = wrel + lane;
+      // the literal gather's base, LDS address of this lane's stream byte (kept in a VGPR
+      // of its own: folded into the parse's reads, it costs every literal address an add)
+      uint32_t wck = kRing + wc;
+      __asm__("" : "+v"(wck));
       const uint32_t tok = win[wc];
       const uint32_t b1 = win[wc + 1];
       const uint32_t cm4 = tok & 15u;
@@ -329,7 +333,8 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       // (2) scalar walk over the real tokens (capacity: checked once for the whole batch)
       const uint32_t room = s.cap - s.op;
       const uint32_t lim = room < kBatchOut ? room : kBatchOut;
-      uint32_t k, vrec0 = 0, vrec1 = 0;
+      // (lanes the walk does not write keep bit 31: negative keys for the signed prefix max)
+      uint32_t k, vrec0 = 0x80000000u, vrec1 = 0x80000000u;
       const bool celig = csimple && lane < kWave - 1;  // lane 63: the walk's sentinel
       const uint32_t pw = (nxt < kWave - 1 ? nxt : kWave - 1) | ((celig ? colen : 255u) << 6) |
                           kWordTag | (nxt << 24);
@@ -363,15 +368,18 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         // the record from its token lane (ds_bpermute reads address bits 2..7 only)
         const uint32_t rec =
             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(key << 2), (int)pr);
-        const uint32_t joff = rec & 0xFFFFu;
         const uint32_t ms = ostart + ((rec >> 16) & 0xFFu);  // the match's first byte (vs op)
         const bool is_lit = q < ms;
-        // a match byte's source: q - off (vs op)
-        int32_t srel = (int32_t)q - (int32_t)joff;
+        // a match byte's source: q - off (vs op; SDWA takes the offset's 16 bits in place)
+        int32_t srel;
+        __asm__("v_sub_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD "
+                "src0_sel:DWORD src1_sel:WORD_0"
+                : "=v"(srel) : "v"(q), "v"(rec));
         // overlapping copy (source inside the match itself: q - off >= ms): fold the source
         // into the first period, ms + (m mod off) - off with m = q - ms (exact in fp32 for
         // m, off < 64); skipped when no byte needs it
         if (ballot(srel >= (int32_t)ms && q < out)) {
+          const uint32_t joff = rec & 0xFFFFu;
           const uint32_t m = (q - ms) & 63u;
           const float qf = floorf(((float)m + 0.5f) *
                                   __builtin_amdgcn_rcpf((float)(joff > 1u ? joff : 1u)));
@@ -379,7 +387,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
           srel = srel >= (int32_t)ms ? sf : srel;  // (a select: no exec-mask branch)
         }
         const uint32_t hist = (base + s.op + (uint32_t)srel) & kRingMask;  // ring at 0
-        const uint32_t lit_addr = kRing + wrel + (rec >> 24) + (q - ostart);
+        const uint32_t lit_addr = wck + H * kWave + (rec >> 24) - ostart;
         // every form computed before the selects (the empty asm pins them), so the compiler
         // does not turn the selects into an exec-mask if / else
         uint32_t lit_a = lit_addr, hist_a = hist, alias_a = (uint32_t)srel | 0x80000000u;
@@ -427,13 +435,17 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         lds_order();
       };
       // every output byte takes the record of the latest sequence starting at or before it
-      const uint32_t key0 = wave_incl_max(vrec0 ? (vrec0 & 63u) | (lane << 24) : 0u);
+      // (a written word has bit 31 clear, so its key is >= 0; the first sequence's, at lane
+      // 0, is 0, so every half-0 key ends >= 0)
+      const uint32_t key0 =
+          (uint32_t)wave_incl_max_i((int32_t)((vrec0 & 0x8000003Fu) | (lane << 24)));
       half(std::integral_constant<uint32_t, 0>{}, key0);
       if (out > kWave) {
         // second half: its own starts (all past byte 64), else the first half's last record
-        const uint32_t key1 = wave_incl_max(vrec1 ? (vrec1 & 63u) | ((lane + kWave) << 24) : 0u);
-        const uint32_t carry = readlane(key0, kWave - 1);
-        half(std::integral_constant<uint32_t, 1>{}, key1 > carry ? key1 : carry);
+        const int32_t key1 =
+            wave_incl_max_i((int32_t)((vrec1 & 0x8000003Fu) | ((lane + kWave) << 24)));
+        const int32_t carry = (int32_t)readlane(key0, kWave - 1);
+        half(std::integral_constant<uint32_t, 1>{}, (uint32_t)(key1 > carry ? key1 : carry));
       }
       if constexpr (BITAR_LZ4D_ENDRULES == 1 || BITAR_LZ4D_ENDRULES == 2) {
         bip = s.ip;

@@ -184,6 +184,18 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
   x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
   return x;
 }
+// signed form (lanes out of the DPP pattern read INT_MIN, the identity of the max)
+__device__ __forceinline__ int32_t wave_incl_max_i(int32_t v) {
+  constexpr int32_t lo = (int32_t)0x80000000u;
+  int32_t x = v;
+  x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x111, 0xf, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x112, 0xf, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x114, 0xf, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x118, 0xf, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x142, 0xa, 0xf, false));
+  x = max(x, __builtin_amdgcn_update_dpp(lo, x, 0x143, 0xc, 0xf, false));
+  return x;
+}
 // lane l gets lane l-1's value, lane 0 gets 0 (DPP wave_shr:1)
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
