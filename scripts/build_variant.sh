@@ -7,7 +7,12 @@ name=$1; defs=$2
 mkdir -p build_$name lib/variants
 for f in runtime lz4_decompress inflate inflate_fixed compress util_kernels zstd_decompress zstd_compress zstd_lanes inflate_lanes deflate_dyn checksum lz4_chain zstd_seq; do
   extra=""
-  case " ${ILP_FILES:-lz4_decompress zstd_seq zstd_lanes} " in *" $f "*) extra="-mllvm -amdgpu-sched-strategy=max-ilp";; esac  # (as the Makefile; ILP_FILES overrides)
+  case $f in  # (the Makefile's per-file scheduler; FLAGS_<file> below overrides)
+    lz4_decompress) extra="-mllvm -amdgpu-sched-strategy=max-ilp";;
+    zstd_seq|zstd_lanes) extra="-mllvm -amdgpu-sched-strategy=max-memory-clause";;
+    compress) extra="-mllvm -amdgpu-sched-strategy=iterative-maxocc";;
+  esac
+  eval "extra=\${FLAGS_$f:-\$extra}"  # FLAGS_<file>="..." replaces a file's extra flags
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics $extra $defs -c csrc/$f.hip -o build_$name/$f.o &
 done
 wait
