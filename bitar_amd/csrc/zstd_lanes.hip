@@ -421,25 +421,46 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
   __shared__ uint16_t tab[S][kHufWords];  // two symbol bytes per entry pair
   __shared__ uint8_t len8[S][256];
   const uint32_t lane = lane_id();
-  for (uint32_t l = 0; l < S; ++l) {
+  // The wave's segment headers, one lane per segment, loaded together, and each table's
+  // words issued before any is used: at about one wave per SIMD every serial load is
+  // exposed, and the per-segment form chained three header loads and 16 table loads.
+  uint32_t p0 = 0, pend = 0, hlg = 0;
+  {
+    const uint32_t il = blockIdx.x * S + lane;
+    if (lane < S && il < nseg) {
+      const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
+      p0 = produced[il];
+      pend = h[kLitPend];
+      hlg = h[kHufLog];
+    }
+  }
+  const uint64_t tm = ballot(lits_pending(p0) && pend == 1u);
+  for (uint64_t m = tm; m; m &= m - 1) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(m);
     const uint32_t il = blockIdx.x * S + l;
-    if (il >= nseg || !lits_pending(produced[il])) continue;
     const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
-    if (h[kLitPend] != 1u) continue;
-    const uint32_t nw = (1u << (h[kHufLog] & 0xFFu)) / 2;
-    for (uint32_t u = lane; u < nw; u += kWave) {
-      const uint32_t w = h[kHufAt + u];
-      tab[l][u] = (uint16_t)((w & 0xFFu) | ((w >> 8) & 0xFF00u));
-      len8[l][w & 0xFFu] = (uint8_t)(w >> 8);  // (every entry of a symbol: the same length)
-      len8[l][(w >> 16) & 0xFFu] = (uint8_t)(w >> 24);
+    const uint32_t nw = (1u << (readlane(hlg, l) & 0xFFu)) / 2;
+    uint32_t wv[kHufWords / kWave];
+#pragma unroll
+    for (uint32_t k = 0; k < kHufWords / kWave; ++k) {
+      const uint32_t u = lane + k * kWave;
+      wv[k] = h[kHufAt + (u < nw ? u : 0u)];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kHufWords / kWave; ++k) {
+      const uint32_t u = lane + k * kWave, w = wv[k];
+      if (u < nw) {
+        tab[l][u] = (uint16_t)((w & 0xFFu) | ((w >> 8) & 0xFF00u));
+        len8[l][w & 0xFFu] = (uint8_t)(w >> 8);  // (every entry of a symbol: the same length)
+        len8[l][(w >> 16) & 0xFFu] = (uint8_t)(w >> 24);
+      }
     }
   }
   lds_order();
   const uint32_t l = lane >> 2, j = lane & 3u;
   const uint32_t i = blockIdx.x * S + l;
-  if (l >= S || i >= nseg || !lits_pending(produced[i])) return;
+  if (l >= S || i >= nseg || !((tm >> l) & 1u)) return;
   const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
-  if (h[kLitPend] != 1u) return;
   const uint32_t hl = h[kHufLog], log = hl & 0xFFu, ns = hl >> 8;
   if (j >= ns) return;
   const uint32_t regen = h[kRegen], qq = h[kQQ];

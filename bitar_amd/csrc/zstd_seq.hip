@@ -141,24 +141,52 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
   using lanes::ld8;
   __shared__ __attribute__((aligned(16))) uint16_t cel[L * kTab];
   const uint32_t lane = lane_id();
-  // stage the decode tables of the wave's segments, 4 cells per lane per step
-  for (uint32_t l = 0; l < L; ++l) {
+  // stage the decode tables of the wave's segments, 4 cells per lane per step.  The headers
+  // are loaded one lane per segment, together, and a segment's table loads are all issued
+  // before the first is used: at about one wave per SIMD every serial load is exposed.
+  uint32_t p0 = 0, nq0 = 0, als0 = 0;
+  {
+    const uint32_t il = blockIdx.x * L + lane;
+    if (lane < L && il < nseg) {
+      const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
+      p0 = produced[il];
+      nq0 = h[kNseq];
+      als0 = h[kAls];
+    }
+  }
+  const uint64_t tm = ballot(p0 == kHanded && nq0 <= rcap);
+  for (uint64_t mm = tm; mm; mm &= mm - 1) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(mm);
     const uint32_t il = blockIdx.x * L + l;
-    if (il >= nseg || produced[il] != kHanded) continue;
     const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
-    if (h[kNseq] > rcap) continue;
-    const uint32_t als = h[kAls];
+    const uint32_t als = readlane(als0, l);
+    constexpr uint32_t kPer = (kCells / 4 + kWave - 1) / kWave;  // uint4 loads per lane per table
+    uint4 cv[3][kPer];
 #pragma unroll
     for (uint32_t k = 0; k < 3; ++k) {
       const uint32_t al = (als >> (8 * k)) & 0xFFu;
       const uint32_t n4 = al >= 2 ? (1u << al) / 4 : 1u;
       const GMEM uint4* t = reinterpret_cast<const GMEM uint4*>(h + kCellsAt + k * kCells);
+#pragma unroll
+      for (uint32_t e = 0; e < kPer; ++e) {
+        const uint32_t u = lane + e * kWave;
+        cv[k][e] = t[u < n4 ? u : 0u];
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) {
+      const uint32_t al = (als >> (8 * k)) & 0xFFu;
+      const uint32_t n4 = al >= 2 ? (1u << al) / 4 : 1u;
       uint16_t* d = cel + l * kTab + (k == 0 ? 0u : k == 1 ? kOfAt : kMlAt);
-      for (uint32_t u = lane; u < n4; u += kWave) {
-        const uint4 c = t[u];
-        const uint32_t lo = cell16(c.x, al) | (cell16(c.y, al) << 16);
-        const uint32_t hi = cell16(c.z, al) | (cell16(c.w, al) << 16);
-        *reinterpret_cast<uint2*>(d + 4 * u) = make_uint2(lo, hi);
+#pragma unroll
+      for (uint32_t e = 0; e < kPer; ++e) {
+        const uint32_t u = lane + e * kWave;
+        if (u < n4) {
+          const uint4 c = cv[k][e];
+          const uint32_t lo = cell16(c.x, al) | (cell16(c.y, al) << 16);
+          const uint32_t hi = cell16(c.z, al) | (cell16(c.w, al) << 16);
+          *reinterpret_cast<uint2*>(d + 4 * u) = make_uint2(lo, hi);
+        }
       }
     }
   }
@@ -172,10 +200,9 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
   // advances all three FSE chains of 16 segments.
   const uint32_t l = lane >> 2, j = lane & 3u;
   const uint32_t i = blockIdx.x * L + l;
-  if (l >= L || i >= nseg || produced[i] != kHanded) return;  // quad-uniform
+  if (l >= L || i >= nseg || !((tm >> l) & 1u)) return;  // quad-uniform
   GMEM uint32_t* h = global_ptr(reinterpret_cast<uint32_t*>(hscr + (uint64_t)i * kStride));
   const uint32_t nseq = h[kNseq];
-  if (nseq > rcap) return;
   const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
   GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap);
   const uint32_t cs = csizes[i];
