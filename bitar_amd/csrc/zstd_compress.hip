@@ -1097,23 +1097,45 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
   for (uint32_t k = lane; k < sizeof(Tabs); k += kWave)
     reinterpret_cast<uint8_t*>(&sT)[k] = reinterpret_cast<const uint8_t*>(&kT)[k];
   // (order: the segments by sequence count, walk_key_kernel; slot b walks segment order[b])
-  for (uint32_t l = 0; l < kWalkSegs; ++l) {
-    const uint32_t bl = blockIdx.x * kWalkSegs + l;
-    if (bl >= nseg) break;
-    const uint32_t il = order ? order[bl] : bl;
+  // The wave's segments are looked up one lane each, together, and each segment's table loads
+  // are issued before the first is stored: at one wave per SIMD every serial load is exposed.
+  uint32_t il0 = 0, hd0 = 0;
+  {
+    const uint32_t bl = blockIdx.x * kWalkSegs + lane;
+    if (lane < kWalkSegs && bl < nseg) {
+      il0 = order ? order[bl] : bl;
+      hd0 = global_ptr(reinterpret_cast<const uint32_t*>(wscr + (uint64_t)il0 * wstride))[kWHanded];
+    }
+  }
+  const uint64_t hm = ballot(hd0 == 1u);
+  for (uint64_t m = hm; m; m &= m - 1) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(m);
+    const uint32_t il = readlane(il0, l);
     const GMEM uint32_t* w = global_ptr(reinterpret_cast<const uint32_t*>(wscr + (uint64_t)il * wstride));
-    if (w[kWHanded] != 1u) continue;
-    for (uint32_t k = lane; k < 1284 / 2; k += kWave)
-      reinterpret_cast<uint32_t*>(tabs[l])[k] = w[kWTabs / 4 + k];
-    for (uint32_t k = lane; k < 3 * 64; k += kWave) (&trs[l][0][0])[k] = w[kWTr / 4 + k];
+    constexpr uint32_t kTw = 1284 / 2, kTn = (kTw + kWave - 1) / kWave;
+    uint32_t tv[kTn], rv[3];
+#pragma unroll
+    for (uint32_t e = 0; e < kTn; ++e) {
+      const uint32_t k = lane + e * kWave;
+      tv[e] = w[kWTabs / 4 + (k < kTw ? k : 0u)];
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < 3; ++e) rv[e] = w[kWTr / 4 + lane + e * kWave];
+#pragma unroll
+    for (uint32_t e = 0; e < kTn; ++e) {
+      const uint32_t k = lane + e * kWave;
+      if (k < kTw) reinterpret_cast<uint32_t*>(tabs[l])[k] = tv[e];
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < 3; ++e) (&trs[l][0][0])[lane + e * kWave] = rv[e];
   }
   lds_order();
   const uint32_t l = lane >> 2, j = lane & 3u;
   const uint32_t b = blockIdx.x * kWalkSegs + l;
-  if (b >= nseg) return;  // quad-uniform
-  const uint32_t i = order ? order[b] : b;
+  // (fetched while every lane is active: a disabled source lane reads as 0)
+  const uint32_t i = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(l << 2), (int)il0);
+  if (b >= nseg || !((hm >> l) & 1u)) return;  // quad-uniform
   GMEM uint32_t* w = global_ptr(reinterpret_cast<uint32_t*>(wscr + (uint64_t)i * wstride));
-  if (w[kWHanded] != 1u) return;
   const uint32_t nseq = w[kWNseq];
   const uint32_t cap = walk_cap(seg);
   const GMEM uint32_t* codes = w + kWWords / 4;
