@@ -81,9 +81,10 @@ KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
            # the wide parse (16 KiB history): same kernels, other template instance; offsets
            # past the decoder's LDS ring take lz4_decompress_kernel<true> (far history)
            "lz4_wide": ("lz4_compress_kernel", "lz4_decompress_kernel"),
-           # decompress = inflate_kernel (wave per segment; the lane-per-segment
+           # decompress = inflate_fixed_kernel (inflate.hip built with the 9/8-bit tables of
+           # the fixed code, picked on the FIXED hint; the lane-per-segment
            # inflate_lanes_kernel runs in front only when a context turns it on)
-           "deflate": ("deflate_compress_kernel", "inflate_lanes_kernel+inflate_kernel"),
+           "deflate": ("deflate_compress_kernel", "inflate_fixed_kernel"),
            # compress = zstd_parse_kernel + zstd_entropy_kernel + zstd_walk_kernel (FSE state
            # chains, a lane per chain) + zstd_emit_kernel (sequence bitstream); decompress =
            # zstd_lanes_kernel (predefined-table frames) + zstd_decompress_kernel (headers,
@@ -94,9 +95,9 @@ KERNELS = {"lz4": ("lz4_compress_kernel", "lz4_decompress_kernel"),
                     "zstd_lanes_kernel+zstd_decompress_kernel+zstd_hlit_kernel+"
                     "zstd_seqdec_kernel+zstd_exec_kernel+zstd_handoff_kernel"),
            # compress = deflate_dyn_parse_kernel + deflate_dyn_emit_kernel (one event pair
-           # brackets both); decompress = inflate_kernel (as for "deflate")
+           # brackets both); decompress = inflate_kernel (10/9-bit tables, the DYNAMIC hint)
            "deflate_dyn": ("deflate_dyn_parse_kernel+deflate_dyn_emit_kernel",
-                           "inflate_lanes_kernel+inflate_kernel")}
+                           "inflate_kernel")}
 CODEC_NAMES = {"lz4": "lz4-block", "deflate": "deflate-raw-fixed", "zstd": "zstd-frame",
                "deflate_dyn": "deflate-raw-dynamic", "lz4_wide": "lz4-block (wide parse)"}
 
@@ -224,7 +225,14 @@ def kernel_lines(codec_name, r, traffic_json, leg="headline"):
         pass
     roof = {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic, "algorithmic_bytes_per_launch": dominant[1],
+            "traffic": traffic,
+            # traffic is not measured in this run: a bench run under --pmc would perturb the
+            # timing, so it is the per-launch PMC figure of this leg's kernels from the
+            # committed profile (scripts/gpu_bench.sh PROFILE=1 -> scripts/collect_profile.py)
+            "traffic_source": (f"committed PMC profile {os.path.relpath(traffic_json, HERE)} "
+                               f"(FETCH_SIZE x2 + WRITE_SIZE per launch, separate --pmc passes)"
+                               if traffic is not None else None),
+            "algorithmic_bytes_per_launch": dominant[1],
             "avg_launch_ms": round(dominant[2] * 1e3, 4)}
     kernels = {kc: {"avg_ms": round(t_comp * 1e3, 4), "alg_GBs": round(comp_bytes / t_comp / 1e9, 2)},
                kd: {"avg_ms": round(t_dec * 1e3, 4), "alg_GBs": round(dec_bytes / t_dec / 1e9, 2)}}

@@ -77,6 +77,7 @@ def lib():
         "bitar_hip_stream": (i32, [vp, u32, ctypes.POINTER(vp)]),
         "bitar_hip_device": (i32, [vp, ctypes.POINTER(i32)]),
         "bitar_hip_slot_size": (u64, [u32, u32]),
+        "bitar_hip_max_distance": (u32, [u32]),
         "bitar_hip_alloc": (i32, [vp, u64, ctypes.POINTER(vp)]),
         "bitar_hip_free": (i32, [vp, vp]),
         "bitar_hip_host_alloc": (i32, [vp, u64, ctypes.POINTER(vp)]),
@@ -111,7 +112,7 @@ def lib():
 # every symbol include/bitar_hip.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("bitar_hip_abi_version", "bitar_hip_last_error", "bitar_hip_device_count",
                "bitar_hip_open", "bitar_hip_close", "bitar_hip_stream", "bitar_hip_device",
-               "bitar_hip_slot_size", "bitar_hip_alloc", "bitar_hip_free",
+               "bitar_hip_slot_size", "bitar_hip_max_distance", "bitar_hip_alloc", "bitar_hip_free",
                "bitar_hip_host_alloc", "bitar_hip_host_free", "bitar_hip_memcpy",
                "bitar_hip_compress", "bitar_hip_compress_scattered", "bitar_hip_pointer_info",
                "bitar_hip_decompress", "bitar_hip_decompress_slab",
@@ -130,6 +131,11 @@ def check(rc):
 
 def slot_size(codec, seg):
     return int(lib().bitar_hip_slot_size(codec, seg))
+
+
+def max_distance(codec):
+    """largest match distance the encoder of `codec` emits (its window's reach)"""
+    return int(lib().bitar_hip_max_distance(codec))
 
 
 def device_count():

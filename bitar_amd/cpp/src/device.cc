@@ -701,8 +701,8 @@ CompressDevice<Class, Enable>::CompressDevice(std::uint8_t device_id,
 
 template <typename Class, typename Enable>
 arrow::Status CompressDevice<Class, Enable>::ValidateConfiguration() {
-  // device capabilities: <= 64 queue pairs, no chained segments, window 2^15 (DEFLATE) or
-  // 2^16 (LZ4), fixed or dynamic Huffman (reference device.cc:352-415, 566-574)
+  // device capabilities: <= 64 queue pairs, chained ops of <= 64 KiB (max_sgl_segs * seg),
+  // the encoder's window, fixed or dynamic Huffman (reference device.cc:352-415, 566-574)
   constexpr std::uint16_t kMaxQueuePairs = 64;
   if (num_qps() == 0 || num_qps() > kMaxQueuePairs) {
     return arrow::Status::Invalid("The requested number of queue pairs (", num_qps(),
@@ -728,16 +728,28 @@ arrow::Status CompressDevice<Class, Enable>::ValidateConfiguration() {
     return arrow::Status::Invalid("decompressed_seg_size is not in the range of [",
                                   internal::kMinSegSize, ", ", internal::kMaxSegSize32, "]");
   }
-  // window log: DEFLATE 2^15; LZ4 offsets and single-segment Zstd frames reach 2^16
-  const std::uint8_t window = configuration_->codec() == Codec::DEFLATE ? 15 : 16;
-  if (configuration_->window_size() == 0) {
-    configuration_->set_window_size(window);
-  } else if (configuration_->window_size() != window) {
-    return arrow::Status::Invalid("window_size is not in the range of [", +window, ", ",
-                                  +window, "]");
-  }
+  // level: LZ4 1..9 (>= 2 selects the wide parse); DEFLATE and ZSTD have one level, so any
+  // other value is refused rather than ignored (the reference always sets 1)
   if (configuration_->level() < 1 || configuration_->level() > 9)
     return arrow::Status::Invalid("level is not in the range of [1, 9]");
+  if (configuration_->codec() != Codec::LZ4 && configuration_->level() != 1)
+    return arrow::Status::Invalid("level is not in the range of [1, 1] for this codec");
+  // window log: the reach of the encoder this configuration runs (bitar_hip_max_distance:
+  // 2560 B -> 2^12, the wide LZ4 parse 14848 B -> 2^14).  The reference sets the device
+  // maximum (device.cc:389-393); here the configured value reports what the encoder actually
+  // uses.  A caller may ask for any window from that up to the format's maximum (DEFLATE 2^15,
+  // LZ4 / single-segment Zstd 2^16): the streams are valid for it, and window_size() then
+  // reports the reach.  A smaller window cannot be honoured and is refused.
+  const std::uint32_t reach = bitar_hip_max_distance(internal::AbiCodec(*configuration_));
+  std::uint8_t window = 1;
+  while ((1u << window) < reach) ++window;
+  const std::uint8_t max_window = configuration_->codec() == Codec::DEFLATE ? 15 : 16;
+  if (configuration_->window_size() != 0 &&
+      (configuration_->window_size() < window || configuration_->window_size() > max_window)) {
+    return arrow::Status::Invalid("window_size is not in the range of [", +window, ", ",
+                                  +max_window, "]");
+  }
+  configuration_->set_window_size(window);
   if (configuration_->max_preallocate_memzones() < internal::kMinPreallocateSlots) {
     return arrow::Status::Invalid("max_preallocate_memzones (",
                                   configuration_->max_preallocate_memzones(),

@@ -332,6 +332,20 @@ uint64_t bitar_hip_slot_size(uint32_t codec, uint32_t seg) {
   return (bound + 255u) & ~(uint64_t)255u;
 }
 
+uint32_t bitar_hip_max_distance(uint32_t codec) {
+  // the window-scan parse verifies candidates in its LDS input ring, which runs up to 1536 B
+  // ahead of the scan: a 4 KiB ring (window_parse.hip.h kMaxDist) for the fast parses of LZ4,
+  // DEFLATE and Zstd, a 16 KiB ring for the wide LZ4 parse (compress.hip, lz4_wide)
+  switch (codec) {
+    case BITAR_HIP_CODEC_LZ4:
+    case BITAR_HIP_CODEC_DEFLATE:
+    case BITAR_HIP_CODEC_DEFLATE_DYNAMIC:
+    case BITAR_HIP_CODEC_ZSTD: return 4096u - 1536u;
+    case BITAR_HIP_CODEC_LZ4_WIDE: return 16384u - 1536u;
+    default: return 0;
+  }
+}
+
 int bitar_hip_alloc(bitar_hip_ctx* ctx, uint64_t bytes, void** ptr) {
   if (int r = enter(ctx)) return r;
   if (!ptr) return fail(BITAR_HIP_INVALID, "null ptr");

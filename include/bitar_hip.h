@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define BITAR_HIP_ABI_VERSION 2
+#define BITAR_HIP_ABI_VERSION 3
 
 /* negated arrow::StatusCode */
 enum bitar_hip_status {
@@ -108,6 +108,13 @@ int bitar_hip_device(bitar_hip_ctx* ctx, int* device);
  * fixed-Huffman bound), rounded up to 256 B.  Plays the role of compressed_seg_size
  * (reference src/config.cc:59-73): the stride of output slots in a slab. */
 uint64_t bitar_hip_slot_size(uint32_t codec, uint32_t seg);
+
+/* Largest match distance the encoder of `codec` emits (0 for an unknown codec): the reach of
+ * its sliding window, 2560 for the fast parses of LZ4 / DEFLATE / Zstd and 14848 for the
+ * wide LZ4 parse.  The front-end reports ceil(log2) of it as the configured window_size
+ * (the reference sets the device maximum, src/device.cc:389-393; its streams are valid for
+ * any window at least this large, and the decoders accept the full 32 KiB / 64 KiB). */
+uint32_t bitar_hip_max_distance(uint32_t codec);
 
 /* HBM / pinned-host allocations on the context's device.  Replace the memzone reservation
  * of RtememzoneAllocator::AllocateAligned / rte_malloc (reference src/memory_pool.cc:70-188).

@@ -58,7 +58,7 @@ def per_call(d):
     return out
 
 
-LEGS = ("headline", "zstd", "deflate", "deflate_dyn", "recordbatch")
+LEGS = ("headline", "zstd", "deflate", "deflate_dyn", "recordbatch", "lz4_arrow")
 # legs whose kernels also run in the headline job of the same pass: only their own launches
 # (by grid size) are averaged -- the record-batch job's parts are 8 GiB / 4 streams = 32768
 # segments of 64 KiB, one 64-lane workgroup each
@@ -66,7 +66,8 @@ LEG_GRID = {"recordbatch": 32768 * 64}
 # the kernels each leg is about (every pass also runs the headline's LZ4 kernels)
 LEG_KERNELS = {"headline": ("lz4_",), "zstd": ("zstd_",),
                "deflate": ("deflate_compress", "inflate"),
-               "deflate_dyn": ("deflate_dyn_", "inflate"), "recordbatch": ("lz4_",)}
+               "deflate_dyn": ("deflate_dyn_", "inflate"), "recordbatch": ("lz4_",),
+               "lz4_arrow": ("lz4_",)}
 
 
 def main():

@@ -48,6 +48,50 @@ std::unique_ptr<bitar::HipConfiguration> MakeConfig(bitar::Codec codec, std::uin
   return c;
 }
 
+// INTEGRATION.md's minimal program, verbatim between the markers (tests/test_frontend.py
+// checks that the two texts are identical)
+// --- INTEGRATION.md minimal program ---
+// `data`, `n`: the caller's bytes on the host
+arrow::Status RoundTrip(const std::uint8_t* data, std::int64_t n) {
+  auto* driver = bitar::CompressDriver<bitar::Class_HIP_GFX950>::Instance();
+  ARROW_ASSIGN_OR_RAISE(auto ids, driver->ListAvailableDeviceIds());
+  ARROW_ASSIGN_OR_RAISE(auto devices, driver->GetDevices({ids[0]}));
+  auto& dev = devices[0];
+  auto cfg = std::make_unique<bitar::HipConfiguration>(bitar::HipConfiguration::Defaults());
+  cfg->set_codec(bitar::Codec::LZ4);
+  cfg->set_decompressed_seg_size32(65536);
+  ARROW_RETURN_NOT_OK(dev->Initialize(std::move(cfg)));
+
+  // (a) host-filled buffers: the pinned HipHost pool (= the reference's Rtememzone), written
+  //     and read by the CPU; Compress / Decompress stream them over PCIe in chunks
+  auto* pinned = bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipHost);
+  ARROW_ASSIGN_OR_RAISE(std::shared_ptr<arrow::Buffer> input, arrow::AllocateBuffer(n, pinned));
+  std::memcpy(input->mutable_data(), data, static_cast<std::size_t>(n));  // host write
+  ARROW_ASSIGN_OR_RAISE(auto frames, dev->Compress(/*qp=*/0, input));
+  const auto cap = static_cast<std::int64_t>(frames.size()) * 65536;
+  ARROW_ASSIGN_OR_RAISE(std::unique_ptr<arrow::ResizableBuffer> out,
+                        arrow::AllocateResizableBuffer(cap, pinned));
+  ARROW_RETURN_NOT_OK(dev->Decompress(0, frames, out));
+  if (out->size() != n || std::memcmp(out->data(), data, static_cast<std::size_t>(n)) != 0)
+    return arrow::Status::IOError("round trip differs");
+  dev->Recycle(frames);
+
+  // (b) HBM-resident buffers (the fast path: no PCIe): copy in through the ROCm memory
+  //     manager, decompress into an HBM buffer; both report is_cpu() == false
+  ARROW_ASSIGN_OR_RAISE(auto d_in, arrow::Buffer::Copy(input, bitar::hip_memory_manager(0)));
+  ARROW_ASSIGN_OR_RAISE(auto frames2, dev->Compress(0, d_in));
+  ARROW_ASSIGN_OR_RAISE(std::unique_ptr<arrow::ResizableBuffer> d_out,
+                        bitar::AllocateResizableDeviceBuffer(cap, 0));
+  ARROW_RETURN_NOT_OK(dev->Decompress(0, frames2, d_out));
+  ARROW_ASSIGN_OR_RAISE(auto back, arrow::Buffer::Copy(std::shared_ptr<arrow::Buffer>(std::move(d_out)),
+                                                       arrow::default_cpu_memory_manager()));
+  if (back->size() != n || std::memcmp(back->data(), data, static_cast<std::size_t>(n)) != 0)
+    return arrow::Status::IOError("HBM round trip differs");
+  dev->Recycle(frames2);
+  return arrow::Status::OK();
+}
+// --- end ---
+
 void CpuTests() {
   // slot sizing rule of the reference (config.cc:59-73)
   bitar::HipConfiguration c;
@@ -377,6 +421,7 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
     auto& d = (*fresh)[0];
     auto cfg = MakeConfig(bitar::Codec::LZ4, 65536);
     cfg->set_level(2);
+    const auto* wide_cfg = cfg.get();  // (owned by the device after Initialize)
     CHECK_OK(d->Initialize(std::move(cfg)));
     auto comp = d->Compress(0, host_in);
     CHECK_OK(comp.status());
@@ -388,12 +433,40 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
       CHECK(o->size() == static_cast<int64_t>(data.size()) &&
             std::memcmp(o->data(), data.data(), data.size()) == 0);
     }
+    CHECK(wide_cfg->window_size() == 14);  // the wide parse reaches 14848 B
     auto bad = driver->GetDevices({(*ids)[0]});
     CHECK_OK(bad.status());
     auto cfg0 = MakeConfig(bitar::Codec::LZ4, 65536);
     cfg0->set_level(0);
     CHECK((*bad)[0]->Initialize(std::move(cfg0)).IsInvalid());
   }
+  // window_size reports the encoder's reach (2560 B -> 12); a larger requested window is
+  // accepted (the streams are valid for it), a smaller one or one past the format's maximum is
+  // refused; DEFLATE and ZSTD refuse levels other than 1 instead of ignoring them
+  {
+    struct W {
+      bitar::Codec codec;
+      int window, level;
+      bool ok;
+    };
+    for (const W& w : {W{bitar::Codec::LZ4, 0, 1, true}, W{bitar::Codec::DEFLATE, 15, 1, true},
+                       W{bitar::Codec::ZSTD, 16, 1, true}, W{bitar::Codec::LZ4, 11, 1, false},
+                       W{bitar::Codec::DEFLATE, 16, 1, false}, W{bitar::Codec::DEFLATE, 0, 2, false},
+                       W{bitar::Codec::ZSTD, 0, 3, false}, W{bitar::Codec::LZ4, 0, 9, true}}) {
+      auto fresh = driver->GetDevices({(*ids)[0]});
+      CHECK_OK(fresh.status());
+      auto& d = (*fresh)[0];
+      auto cfg = MakeConfig(w.codec, w.codec == bitar::Codec::DEFLATE ? 59460 : 65536);
+      cfg->set_window_size(static_cast<std::uint8_t>(w.window));
+      cfg->set_level(static_cast<std::uint8_t>(w.level));
+      const auto* c = cfg.get();
+      const auto st = d->Initialize(std::move(cfg));
+      CHECK(st.ok() == w.ok);
+      if (st.ok()) CHECK(c->window_size() == (w.level >= 2 ? 14 : 12));
+    }
+  }
+  // INTEGRATION.md's minimal program, run as written
+  CHECK_OK(RoundTrip(data.data(), static_cast<std::int64_t>(data.size())));
   // empty input -> empty vector (device.cc:161-164); empty vector -> OK
   auto& d0 = (*devs)[0];
   CHECK_OK(d0->Initialize(MakeConfig(bitar::Codec::LZ4, 65536)));

@@ -28,12 +28,22 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_slot_sizes():
     L = bitar_amd.lib()
-    assert L.bitar_hip_abi_version() == 2
+    assert L.bitar_hip_abi_version() == 3
     # LZ4_compressBound(65536) = 65809 -> 256-B rounded slot
     assert bitar_amd.slot_size(bitar_amd.CODEC_LZ4, 65536) == 66048
     assert bitar_amd.slot_size(bitar_amd.CODEC_LZ4, 59460) >= 59460 + 59460 // 255 + 16
     assert bitar_amd.slot_size(bitar_amd.CODEC_DEFLATE, 59460) >= (59460 * 9 + 7) // 8 + 16
     assert bitar_amd.slot_size(99, 100) == 0
+
+
+def test_encoder_reach():
+    """bitar_hip_max_distance: the encoders' match-distance cap, which the oracle restates
+    (BO_MAX_DIST / the wide parse's cap) and the front-end reports as its window."""
+    B = bitar_amd
+    for c in (B.CODEC_LZ4, B.CODEC_DEFLATE, B.CODEC_DEFLATE_DYNAMIC, B.CODEC_ZSTD):
+        assert B.max_distance(c) == 2560
+    assert B.max_distance(B.CODEC_LZ4_WIDE) == 14848
+    assert B.max_distance(99) == 0
 
 
 def test_no_device_is_not_an_error_for_count():

@@ -34,6 +34,22 @@ def test_frontend_builds_and_cpu_rules():
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_integration_example_is_the_tested_code():
+    """INTEGRATION.md's minimal program is the function frontend_test runs in GPU mode, word
+    for word (so the documented flow is the tested one)."""
+    with open(os.path.join(ROOT, "INTEGRATION.md")) as f:
+        doc = f.read()
+    a = doc.index('```cpp\n#include "bitar/bitar.h"\n\n// `data`')
+    block = doc[a + len("```cpp\n"):doc.index("```", a + 6)]
+    body = block.split("\n", 2)[2]
+    with open(os.path.join(ROOT, "tests", "cpp", "frontend_test.cc")) as f:
+        src = f.read()
+    s = src.index("// --- INTEGRATION.md minimal program ---\n") + len(
+        "// --- INTEGRATION.md minimal program ---\n")
+    assert src[s:src.index("// --- end ---", s)] == body
+    assert "CHECK_OK(RoundTrip(" in src
+
+
 def _segments(path):
     out = []
     with open(path, "rb") as f:
