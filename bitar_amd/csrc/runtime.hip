@@ -112,8 +112,9 @@ struct bitar_hip_ctx {
   std::atomic<uint32_t> cost_order{1};  // LZ4: dispatch the estimated most expensive segments first
   std::mutex mu;              // guards `words` and `order_scratch`
   std::vector<std::pair<hipStream_t, uint32_t>> words;  // stream -> error word index
-  // cost-ordered dispatch scratch, cached per (stream, slot) and reused in stream order (a
-  // call holds its entry's mutex from the sort's launch to the last launch that reads it)
+  // cost-ordered dispatch scratch of the context's own streams (and the default stream),
+  // cached per (stream, slot) and reused in stream order (a call holds its entry's mutex from
+  // the sort's launch to the last launch that reads it); foreign streams get per-call scratch
   struct OrderScratch {
     hipStream_t stream;
     int slot;
@@ -391,6 +392,8 @@ constexpr uint32_t kOrderMinSegs = 2048;
 struct SegOrder {
   bitar_hip_ctx::OrderScratch* e = nullptr;
   std::unique_lock<std::mutex> held;
+  void* transient = nullptr;  // a foreign stream's scratch (freed by release(), stream-ordered)
+  hipStream_t tstream = nullptr;
   uint32_t* order = nullptr;  // null: plain order
   // order = argsort of the keys: keys[i] written by `key` (a launch), or -- csizes given --
   // the compressed sizes' key computed by the sort itself (decompress; seg: the segment size).
@@ -404,28 +407,42 @@ struct SegOrder {
     const uint32_t tile = bitar_hip::order_tile(nseg);
     const uint32_t ntiles = (nseg + tile - 1) / tile;
     const uint64_t need = 8ull * nseg + 4ull * bitar_hip::kOrderBins * ntiles + 64;
-    {
-      std::lock_guard<std::mutex> g(ctx->mu);
-      for (auto& x : ctx->order_scratch)
-        if (x.stream == s && x.slot == slot) e = &x;
-      if (!e) e = &ctx->order_scratch.emplace_back(s, slot);
-    }
-    held = std::unique_lock<std::mutex>(e->m);
-    if (e->cap < need) {
-      // (an optimisation only: without scratch the call runs in plain order)
-      if (e->p) (void)hipFreeAsync(e->p, s);
-      e->p = nullptr;
-      e->cap = 0;
-      const uint64_t cap = (need + (1u << 20) - 1) & ~(uint64_t)((1u << 20) - 1);
-      if (hipMallocAsync(&e->p, cap, s) != hipSuccess) {
+    bool own = s == nullptr;
+    for (hipStream_t q : ctx->streams) own = own || q == s;
+    if (!own) {
+      // a foreign stream (e.g. a torch side stream): no cache entry, which would pin HBM for
+      // the context's life and be inherited by a later stream reusing the handle -- the
+      // scratch is allocated and freed in this stream's order by this call
+      if (hipMallocAsync(&transient, need, s) != hipSuccess) {
         (void)hipGetLastError();
-        e->p = nullptr;
-        held.unlock();
-        return 0;
+        transient = nullptr;
+        return 0;  // (an optimisation only: the call runs in plain order)
       }
-      e->cap = cap;
+      tstream = s;
+    } else {
+      {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        for (auto& x : ctx->order_scratch)
+          if (x.stream == s && x.slot == slot) e = &x;
+        if (!e) e = &ctx->order_scratch.emplace_back(s, slot);
+      }
+      held = std::unique_lock<std::mutex>(e->m);
+      if (e->cap < need) {
+        // (an optimisation only: without scratch the call runs in plain order)
+        if (e->p) (void)hipFreeAsync(e->p, s);
+        e->p = nullptr;
+        e->cap = 0;
+        const uint64_t cap = (need + (1u << 20) - 1) & ~(uint64_t)((1u << 20) - 1);
+        if (hipMallocAsync(&e->p, cap, s) != hipSuccess) {
+          (void)hipGetLastError();
+          e->p = nullptr;
+          held.unlock();
+          return 0;
+        }
+        e->cap = cap;
+      }
     }
-    order = static_cast<uint32_t*>(e->p);
+    order = static_cast<uint32_t*>(transient ? transient : e->p);
     uint32_t* keys = csizes ? nullptr : order + nseg;
     auto* hist = reinterpret_cast<uint32_t*>(
         (reinterpret_cast<uintptr_t>(order + 2ull * nseg) + 15) & ~(uintptr_t)15);
@@ -439,6 +456,8 @@ struct SegOrder {
   // after the last launch that reads the order has been queued
   int release() {
     if (held.owns_lock()) held.unlock();
+    if (transient) (void)hipFreeAsync(transient, tstream);
+    transient = nullptr;
     return 0;
   }
   ~SegOrder() { release(); }
@@ -610,7 +629,11 @@ int bitar_hip_pointer_info(const void* ptr, int* kind, int* device) {
   if (a.type == hipMemoryTypeDevice) {
     *kind = 2;
     *device = a.device;
-  } else if (a.type == hipMemoryTypeHost) {
+  } else if (a.type == hipMemoryTypeHost && a.devicePointer == ptr) {
+    // pinned host memory the device reaches at the same address (hipHostMalloc, torch
+    // pin_memory): kernels may read it in place.  Memory pinned by hipHostRegister can have
+    // another device address; it is reported as pageable (kind 0), so callers stage it with a
+    // copy (hipMemcpyDefault) instead of handing its host address to a kernel.
     *kind = 1;
     *device = a.device;
   }
@@ -961,7 +984,7 @@ int bitar_hip_compress_host(bitar_hip_ctx* ctx, void* stream, uint32_t codec, co
   for (uint64_t c0 = 0; c0 < nseg; c0 += per) {
     const uint64_t cn = nseg - c0 < per ? nseg - c0 : per;
     const uint64_t off = c0 * seg, nb = n - off < cn * seg ? n - off : cn * seg;
-    HIP_TRY(hipMemcpyAsync(stage + off, src + off, nb, hipMemcpyHostToDevice, c), "stage input");
+    HIP_TRY(hipMemcpyAsync(stage + off, src + off, nb, hipMemcpyDefault, c), "stage input");
     if (int r = stream_after(s, c)) return r;
     if (int r = compress_impl(ctx, s, codec, stage + off, nb, seg,
                               slab ? slab + c0 * slot_stride : nullptr, slot_stride,
@@ -996,7 +1019,7 @@ int bitar_hip_decompress_host(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                                 (uint32_t)cn, seg, stage + c0 * seg, cn * seg, d_produced + c0))
       return r;
     if (int r = stream_after(c, s)) return r;
-    HIP_TRY(hipMemcpyAsync(out + c0 * seg, stage + c0 * seg, cn * seg, hipMemcpyDeviceToHost, c),
+    HIP_TRY(hipMemcpyAsync(out + c0 * seg, stage + c0 * seg, cn * seg, hipMemcpyDefault, c),
             "output copy");
   }
   return stream_after(s, c);
