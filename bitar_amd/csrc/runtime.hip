@@ -45,8 +45,7 @@ __global__ void inflate_lanes_kernel(const uint8_t* const*, const uint8_t*, uint
                                      const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*);
 __global__ void zstd_parse_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t, uint2*, const uint32_t*);
 __global__ void zstd_entropy_kernel(const uint8_t*, uint64_t, uint32_t, uint8_t*, uint64_t,
-                                    const uint2*, uint8_t*, uint64_t, uint8_t* const*, uint32_t*,
-                                    uint32_t*, uint8_t*, uint64_t, const uint32_t*);
+                                    const uint2*, uint8_t*, uint64_t, const uint32_t*);
 __global__ void zstd_walk_kernel(const uint8_t*, uint64_t, uint32_t, uint32_t, uint8_t*, uint64_t,
                                  const uint32_t*);
 __global__ void walk_key_kernel(const uint2*, uint32_t, uint32_t*);
@@ -56,19 +55,20 @@ __global__ void zstd_emit_kernel(const uint8_t*, uint64_t, uint32_t, const uint8
 __global__ void zstd_decompress_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                        const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                        uint32_t*, uint32_t*, uint32_t, uint8_t*,
-                                       unsigned long long*, const uint32_t*);
-template <uint32_t S>
+                                       unsigned long long*, const uint32_t*, uint32_t);
+template <uint32_t S, uint32_t B>
 __global__ void zstd_hlit_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                  const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
-                                 const uint8_t*, uint32_t*);
+                                 const uint8_t*, uint32_t*, const uint32_t*);
+__global__ void hand_key_kernel(const uint32_t*, const uint8_t*, uint32_t, uint32_t, uint32_t*);
 template <uint32_t L>
 __global__ void zstd_handoff_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                     const uint32_t*, uint32_t, uint32_t, uint8_t*, uint32_t*,
                                     const uint8_t*, uint32_t*);
-template <uint32_t L>
+template <uint32_t L, uint32_t B>
 __global__ void zstd_seqdec_kernel(const uint8_t* const*, const uint8_t*, uint64_t,
                                    const uint32_t*, uint32_t, uint32_t, uint32_t*, uint8_t*,
-                                   uint64_t*, uint32_t, uint32_t*, unsigned long long*);
+                                   uint64_t*, uint32_t, uint32_t*, unsigned long long*, const uint32_t*);
 __global__ void zstd_exec_kernel(const uint8_t* const*, const uint8_t*, uint64_t, uint32_t,
                                  uint32_t, uint8_t*, uint32_t*, const uint8_t*,
                                  const uint64_t*, uint32_t, uint32_t*, unsigned long long*, const uint32_t*);
@@ -555,8 +555,8 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
     // stream-ordered scratch: per segment the literal area + records (zstd_compress.hip),
     // then {nlit, nseq} per segment
     const uint64_t scr_stride = bitar_hip::zse::scratch_stride(seg);
-    // + the chain-walk scratch (zstd_layout.hip.h: a 3400-byte header with the tables, then
-    // 10 bytes per sequence and 12 per step of 64 sequences)
+    // + the chain-walk scratch (zstd_layout.hip.h: a 5000-byte header with the record, the
+    // literal codes and the FSE tables, then 10 bytes per sequence and 12 per step of <= 64)
     const uint64_t w_stride = bitar_hip::zse::walk_stride(seg);
     const Chunks ch(nseg);
     void* scratch = nullptr;
@@ -576,15 +576,14 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
       hipLaunchKernelGGL(bitar_hip::zstd_parse_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin,
                          nb, seg, scr, scr_stride, meta, ord.order);
       hipLaunchKernelGGL(bitar_hip::zstd_entropy_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin,
-                         nb, seg, scr, scr_stride, meta, cslab, slot_stride, cdsts, d_sizes + c0,
-                         err_word(ctx, s), wscr, w_stride, ord.order);
+                         nb, seg, scr, scr_stride, meta, wscr, w_stride, ord.order);
       SegOrder word;  // (the walk's order: sequence counts, most first)
       if (int r = word.make(ctx, s, (uint32_t)cn, nullptr, [&](uint32_t* keys) {
             hipLaunchKernelGGL(bitar_hip::walk_key_kernel, dim3((uint32_t)((cn + 63) / 64)),
                                dim3(64), 0, s, meta, (uint32_t)cn, keys);
           }, 0, 1))
         return r;
-      hipLaunchKernelGGL(bitar_hip::zstd_walk_kernel, dim3((uint32_t)((cn + 15) / 16)), dim3(64),
+      hipLaunchKernelGGL(bitar_hip::zstd_walk_kernel, dim3((uint32_t)((cn + 3) / 4)), dim3(64),
                          0, s, scr, scr_stride, seg, (uint32_t)cn, wscr, w_stride, word.order);
       if (int r = word.release()) return r;
       hipLaunchKernelGGL(bitar_hip::zstd_emit_kernel, dim3((uint32_t)cn), dim3(64), 0, s, cin, nb,
@@ -791,9 +790,16 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
     hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<false>, dim3(nseg), dim3(64), 0, s, srcs,
                        slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
                        stats, ord.order);
-    hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<true>, dim3(nseg), dim3(64), 0, s, srcs,
-                       slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
-                       stats, ord.order);
+    // the far kernel: at most kFarGrid workgroups, each striding over the dispatch slots for
+    // the segments the near kernel deferred.  A 1 GiB call keeps one workgroup per slot
+    // (stock liblz4 streams defer ~2/3 of their segments: 7168 workgroups striding over them,
+    // 28 waves per CU, decoded them 7 % slower); larger calls (the configs[3] record batch's
+    // 2 GiB parts) launch half the workgroups or fewer
+    constexpr uint32_t kFarGrid = 16384;
+    hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<true>,
+                       dim3(nseg > kFarGrid ? kFarGrid : nseg), dim3(64), 0, s, srcs, slab,
+                       stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s), stats,
+                       ord.order);
     if (int r = ord.release()) return r;
   }
   else if (codec == BITAR_HIP_CODEC_DEFLATE) {
@@ -868,29 +874,52 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
       uint32_t* cprod = d_produced + c0;
       SegOrder ord;  // (cost key: the compressed size; allocation failure = plain order)
       (void)ord.make(ctx, s, cn, csz, [](uint32_t*) {}, seg);
+      // (multi-block hand-offs -- every block of this engine's frames -- need the two-phase
+      // sequence path; the lane executor takes last blocks only)
       hipLaunchKernelGGL(bitar_hip::zstd_decompress_kernel, dim3(cn), dim3(64), 0, s, csrcs,
                          cslab, stride, csz, cn, seg, cout, cprod, ew, L ? 1u : 0u, hs, stats,
-                         ord.order);
+                         ord.order, seq ? 1u : 0u);
 #define BITAR_ZSTD_TAIL(K, N)                                                                 \
   hipLaunchKernelGGL(bitar_hip::K<N>, dim3((cn + N - 1) / N), dim3(64), 0, s, csrcs, cslab, stride, \
                      csz, cn, seg, cout, cprod, hs, ew)
+#define BITAR_HLIT(N, B, O)                                                                   \
+  hipLaunchKernelGGL((bitar_hip::zstd_hlit_kernel<N, B>), dim3((cn + N - 1) / N), dim3(64), 0, s,  \
+                     csrcs, cslab, stride, csz, cn, seg, cout, cprod, hs, ew, O)
       // the literal streams beside the sequences' phase A: one of the two on the aux stream
       // (zstd_fork 1: the literals there, launched first; 2: phase A there, first)
+      // the multi-block lane kernels take their segments most expensive first (by sequences /
+      // by literals: the column types of a record batch alternate in runs of segments, and
+      // index order would give whole CUs the same kind of segment)
+      SegOrder oseq, olit;
+      if (seq) {
+        (void)oseq.make(ctx, s, cn, nullptr, [&](uint32_t* keys) {
+          hipLaunchKernelGGL(bitar_hip::hand_key_kernel, dim3((cn + 63) / 64), dim3(64), 0, s,
+                             cprod, hs, cn, 0u, keys);
+        }, 0, 1);
+        (void)olit.make(ctx, s, cn, nullptr, [&](uint32_t* keys) {
+          hipLaunchKernelGGL(bitar_hip::hand_key_kernel, dim3((cn + 63) / 64), dim3(64), 0, s,
+                             cprod, hs, cn, 1u, keys);
+        }, 0, 2);
+      }
       const uint32_t fork = seq ? ctx->zstd_fork.load(std::memory_order_relaxed) : 0u;
       hipStream_t a = fork ? side_stream_for(ctx, ctx->aux_streams, s) : nullptr;
       if (a && stream_after(a, s)) a = nullptr;
+      // single-block hand-offs (16 segments x 4 streams / chains per wave) and, with the
+      // two-phase path, the multi-block ones (4 segments x 4 blocks x 4 per wave)
       auto hlit = [&](hipStream_t s) {
-        if (hs_n == 4) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 4);
-        else if (hs_n == 8) BITAR_ZSTD_TAIL(zstd_hlit_kernel, 8);
-        else BITAR_ZSTD_TAIL(zstd_hlit_kernel, 16);
+        if (hs_n == 4) BITAR_HLIT(4, 1, nullptr);
+        else if (hs_n == 8) BITAR_HLIT(8, 1, nullptr);
+        else BITAR_HLIT(16, 1, nullptr);
+        if (seq) BITAR_HLIT(4, 4, olit.order);
       };
       auto seqdec = [&](hipStream_t s) {
-#define BITAR_SEQDEC(N)                                                                       \
-  hipLaunchKernelGGL(bitar_hip::zstd_seqdec_kernel<N>, dim3((cn + N - 1) / N), dim3(64), 0, s,  \
-                     csrcs, cslab, stride, csz, cn, seg, cprod, hs, rp, rcap, ew, stats)
-        if (sd == 4) BITAR_SEQDEC(4);
-        else if (sd == 8) BITAR_SEQDEC(8);
-        else BITAR_SEQDEC(16);
+#define BITAR_SEQDEC(N, B, O)                                                                 \
+  hipLaunchKernelGGL((bitar_hip::zstd_seqdec_kernel<N, B>), dim3((cn + N - 1) / N), dim3(64), 0, s, \
+                     csrcs, cslab, stride, csz, cn, seg, cprod, hs, rp, rcap, ew, stats, O)
+        if (sd == 4) BITAR_SEQDEC(4, 1, nullptr);
+        else if (sd == 8) BITAR_SEQDEC(8, 1, nullptr);
+        else BITAR_SEQDEC(16, 1, nullptr);
+        BITAR_SEQDEC(4, 4, oseq.order);
 #undef BITAR_SEQDEC
       };
       if (a && fork == 2) {
@@ -906,10 +935,13 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
                            stride, cn, seg, cout, cprod, hs, rp, rcap, ew, stats, ord.order);
       }
       (void)ord.release();
+      (void)oseq.release();
+      (void)olit.release();
       if (ho_n == 4) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 4);
       else if (ho_n == 8) BITAR_ZSTD_TAIL(zstd_handoff_kernel, 8);
       else BITAR_ZSTD_TAIL(zstd_handoff_kernel, 16);
 #undef BITAR_ZSTD_TAIL
+#undef BITAR_HLIT
     }
     const hipError_t le = hipGetLastError();
     if (recs) (void)hipFreeAsync(recs, s);

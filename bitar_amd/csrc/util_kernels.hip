@@ -290,9 +290,8 @@ __global__ __launch_bounds__(64) void seg_cost_kernel(const uint8_t* __restrict_
   if (live && q == 0) keys[i] = d;
 }
 
-// Zstd chain walk (zstd_walk_kernel, 16 segments per wave, two rounds of waves at 1 GiB):
-// the sequence count, most first, so a wave walks 16 chains of similar length and the
-// longest go in the first round.
+// Zstd chain walk (zstd_walk_kernel, 4 segments x 4 blocks per wave): the sequence count,
+// most first, so a wave walks chains of similar length and the longest go in the first round.
 __global__ __launch_bounds__(64) void walk_key_kernel(const uint2* __restrict__ meta, uint32_t nseg,
                                                       uint32_t* __restrict__ keys) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -32,7 +32,7 @@ using namespace cmp;
 #endif
 #define ZSE_PHASE(k)                             \
   if constexpr (BITAR_ZSTD_STOP == (k)) {        \
-    if (lane == 0) sizes[i_seg] = 16u;           \
+    if (lane == 0) wrec[zse::kWHanded] = 0u;     \
     return;                                      \
   }
 
@@ -719,79 +719,50 @@ __global__ __launch_bounds__(64) void zstd_parse_kernel(const uint8_t* __restric
 __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     uint8_t* __restrict__ scratch, uint64_t sstride, const uint2* __restrict__ meta,
-    uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
-    uint32_t* __restrict__ sizes, uint32_t* __restrict__ err, uint8_t* __restrict__ wscr,
-    uint64_t wstride, const uint32_t* __restrict__ order) {
+    uint8_t* __restrict__ wscr, uint64_t wstride, const uint32_t* __restrict__ order) {
   using namespace cmp;
   using namespace zse;
-  __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
   __shared__ __attribute__((aligned(16))) EntLds L;
   const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
   const uint32_t lane = lane_id();
-  const GMEM uint8_t* src = global_ptr(input + seg_off);
   GMEM uint8_t* lits = global_ptr(scratch + (uint64_t)i_seg * sstride);
   GMEM uint2* seqs = reinterpret_cast<GMEM uint2*>(lits + lit_cap(seg));
+  GMEM uint32_t* wrec = global_ptr(reinterpret_cast<uint32_t*>(wscr + (uint64_t)i_seg * wstride));
+  GMEM uint8_t* wbytes = reinterpret_cast<GMEM uint8_t*>(wrec);
   for (uint32_t k = lane; k < sizeof(Tabs); k += kWave)
     reinterpret_cast<uint8_t*>(&sT)[k] = reinterpret_cast<const uint8_t*>(&kT)[k];
   lds_order();
   const uint2 mt = meta[i_seg];
   const uint32_t nlit = mt.x, nseq = mt.y;
-  EntOut o;
-  o.ring = obuf;
-  o.dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
-  o.cap = slot_stride;
-  o.op = 0;
-  o.flushed = 0;
-  o.overflow = false;
-  // frame header: magic, Single_Segment with the content size (1 byte below 256, else 2)
-  const uint32_t fh = n < 256 ? 6u : 7u;
-  const uint32_t fcs = n < 256 ? n : n - 256u;
-  const uint32_t hb = lane < 4 ? (0xFD2FB528u >> (8 * lane)) & 0xFFu
-                      : lane == 4 ? (n < 256 ? 0x20u : 0x60u)
-                      : lane == 5 ? fcs & 0xFFu : fcs >> 8;
-  o.put(hb, fh);
-  const uint32_t blk = o.op;
-  o.op += 3;  // block header, written last
 
-  // ---- literal histogram, per stream quarter (one read of the literals: the quarters' code
-  // lengths -- the stream sizes -- follow from these counts once the code is built) ----
-  for (uint32_t k = lane; k < 2 * 256; k += kWave) (&L.hq[0][0])[k] = 0;
+  // ---- the literal code (shared by the frame's blocks): histogram, code lengths, codes,
+  // tree description.  Which blocks use it, and the literal sections themselves, are
+  // zstd_emit_kernel's (oracle zs_littab_build / zs_literals_block). ----
+  for (uint32_t k = lane; k < 256; k += kWave) L.hist[k] = 0;
   lds_order();
-  const uint32_t qs = (nlit + 3) / 4;
   for (uint32_t b0 = 0; b0 < nlit; b0 += 16u * kWave) {
     const uint32_t at = b0 + 16u * lane;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (at < nlit) v = *reinterpret_cast<const GMEM uint4*>(lits + at);
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) {
-      const uint32_t idx = at + j;
-      // (a quarter holds <= 16384 literals: its count fits 16 bits)
-      const uint32_t q = idx < qs ? 0u : idx < 2 * qs ? 1u : idx < 3 * qs ? 2u : 3u;
-      if (idx < nlit)
-        atomicAdd(&L.hq[q >> 1][(wv[j >> 2] >> (8 * (j & 3))) & 0xFFu], (q & 1u) ? 0x10000u : 1u);
-    }
-  }
-  lds_order();
-  for (uint32_t k = lane; k < 256; k += kWave) {
-    const uint32_t a = L.hq[0][k], b = L.hq[1][k];
-    L.hist[k] = (a & 0xFFFFu) + (a >> 16) + (b & 0xFFFFu) + (b >> 16);
+    for (uint32_t j = 0; j < 16; ++j)
+      if (at + j < nlit) atomicAdd(&L.hist[(wv[j >> 2] >> (8 * (j & 3))) & 0xFFu], 1u);
   }
   lds_order();
   uint32_t distinct = 0;
   for (uint32_t s0 = 0; s0 < 256; s0 += kWave)
     distinct += (uint32_t)__builtin_popcountll(ballot(L.hist[s0 + lane] != 0));
   lds_order();
-
   ZSE_PHASE(1)
-  // ---- literals section ----
-  bool huff = false;
-  uint32_t ns = 1, dsz = 0, hs = 0, total = 0;
-  uint32_t sbytes[4] = {0, 0, 0, 0};
-  if (nlit > 0 && distinct > 1) {
+  uint32_t lmode = 0, lrle = 0, dsz = 0;
+  if (nlit > 0 && distinct == 1) {
+    lmode = 1;
+    lrle = lits[0];
+  } else if (nlit > 0) {
     huf::huff_lengths(L.hist, 256, 11, L.len, L.T);
     ZSE_PHASE(6)
     // max length, highest used symbol, weights
@@ -807,25 +778,6 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     for (uint32_t s0 = 0; s0 < 256; s0 += kWave) {
       const uint32_t l = L.len[s0 + lane];
       L.w[s0 + lane] = (uint8_t)(l ? lmax + 1 - l : 0u);
-    }
-    // stream sizes: each quarter's bits = sum over symbols of code length x its count there
-    ns = nlit < 256 ? 1u : 4u;
-    uint32_t bq[4] = {0, 0, 0, 0};
-    lds_order();
-    for (uint32_t s0 = 0; s0 < 256; s0 += kWave) {
-      const uint32_t l = L.len[s0 + lane], a = L.hq[0][s0 + lane], b = L.hq[1][s0 + lane];
-      bq[0] += l * (a & 0xFFFFu);
-      bq[1] += l * (a >> 16);
-      bq[2] += l * (b & 0xFFFFu);
-      bq[3] += l * (b >> 16);
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) bq[q] = readlane(wave_incl_sum(bq[q]), 63);
-    if (ns == 1) {
-      sbytes[0] = (bq[0] + bq[1] + bq[2] + bq[3] + 8) >> 3;
-    } else {
-#pragma unroll
-      for (uint32_t q = 0; q < 4; ++q) sbytes[q] = (bq[q] + 8) >> 3;
     }
     lds_order();
     {
@@ -856,7 +808,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
 #pragma unroll
       for (uint32_t c = 0; c < 4; ++c) {
         const uint32_t s = 64 * c + lane, l = L.len[s];
-        L.E.code[s] = l ? (L.wk[wv[c]] + rk[c]) | (l << 16) : 0u;
+        wrec[kWCodeAt + s] = l ? (L.wk[wv[c]] + rk[c]) | (l << 16) : 0u;
       }
       lds_order();
     }
@@ -879,122 +831,51 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     }
     lds_order();
     dsz = L.u[0];
-    if (dsz) {
-      total = dsz + (ns == 4 ? 6u : 0u) + sbytes[0] + sbytes[1] + sbytes[2] + sbytes[3];
-      const int32_t limit = (int32_t)nlit - (int32_t)((nlit >> 6) + 2);
-      huff = (int32_t)total < limit;
-    }
+    for (uint32_t k = lane; k < dsz; k += kWave) wbytes[4 * kWTreeAt + k] = L.desc[k];
+    if (dsz) lmode = 2;
   }
   ZSE_PHASE(2)
-  ZSE_PHASE(7)
-  if (huff) {
-    hs = ns == 1 || nlit < 1024 ? 3u : nlit < 16384 ? 4u : 5u;
-    const uint32_t sf = ns == 1 ? 0u : nlit < 1024 ? 1u : nlit < 16384 ? 2u : 3u;
-    const uint64_t h = 2u | (sf << 2) | ((uint64_t)nlit << 4) |
-                       ((uint64_t)total << (hs == 3 ? 14 : hs == 4 ? 18 : 22));
-    o.room(hs);
-    o.put((uint32_t)(h >> (8 * (lane < 8 ? lane : 0u))) & 0xFFu, hs);
-    o.put_lds(L.desc, dsz);
-    if (ns == 4) {
-      const uint32_t j = lane >> 1;
-      const uint32_t sv = j == 0 ? sbytes[0] : j == 1 ? sbytes[1] : sbytes[2];
-      o.room(6);
-      o.put((lane & 1) ? sv >> 8 : sv & 0xFFu, 6);
-    }
-    // the streams: symbols from the last, 64 per step (the highest index first)
-    for (uint32_t k = 0; k < ns && !o.overflow; ++k) {
-      const uint32_t a = ns == 1 ? 0u : k * qs;
-      const uint32_t b = ns == 1 ? nlit : (k == 3 ? nlit : (k + 1) * qs);
-      const uint32_t p0 = o.op;
-      uint32_t bits = 0, zeroed = p0;
-      // 1 KiB blocks of aligned 16-B groups, staged in LDS, the next one loaded during the
-      // current one
-      const GMEM uint4* l16 = reinterpret_cast<const GMEM uint4*>(lits);
-      const int32_t gA = (int32_t)(a >> 4), gB = (int32_t)((b + 15) >> 4);
-      int32_t g0 = gB - (int32_t)kWave;
-      uint4 blkv = make_uint4(0, 0, 0, 0);
-      if (g0 + (int32_t)lane >= gA) blkv = l16[g0 + (int32_t)lane];
-      for (;;) {
-        lds_order();
-        reinterpret_cast<uint4*>(L.E.lst)[lane] = blkv;
-        const int32_t g1 = g0 - (int32_t)kWave;
-        if (g0 > gA && g1 + (int32_t)lane >= gA) blkv = l16[g1 + (int32_t)lane];
-        const int32_t lo = max((int32_t)a, 16 * g0), hi = min((int32_t)b, 16 * (g0 + (int32_t)kWave));
-        for (int32_t e = hi; e > lo && !o.overflow; e -= (int32_t)kWave) {
-          const int32_t idx = e - (int32_t)kWave + (int32_t)lane;
-          const bool act = idx >= lo;
-          lds_order();
-          const uint32_t sym = act ? L.E.lst[idx - 16 * g0] : 0u;
-          const uint32_t cw = L.E.code[sym];
-          o.put_bits(act ? (cw & 0xFFFFu) : 0u, act ? cw >> 16 : 0u, 0, 0, p0, bits, zeroed);
-        }
-        if (g0 <= gA || o.overflow) break;
-        g0 = g1;
-      }
-      o.put_bits(lane == 0 ? 1u : 0u, lane == 0 ? 1u : 0u, 0, 0, p0, bits, zeroed);  // end mark
-      o.op = p0 + ((bits + 7) >> 3);
-    }
-  } else if (nlit > 0 && distinct == 1) {  // RLE
-    const uint32_t h = nlit < 32 ? 1u | (nlit << 3)
-                       : nlit < 4096 ? 1u | (1u << 2) | ((nlit & 15u) << 4) | ((nlit >> 4) << 8)
-                                     : 1u | (3u << 2) | ((nlit & 15u) << 4) | ((nlit >> 4) << 8);
-    const uint32_t hsz = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
-    const uint32_t byte0 = lits[0];
-    o.room(hsz + 1);
-    o.put(lane < hsz ? (h >> (8 * lane)) & 0xFFu : byte0, hsz + 1);
-  } else {  // raw
-    const uint32_t h = nlit < 32 ? (nlit << 3)
-                       : nlit < 4096 ? (1u << 2) | ((nlit & 15u) << 4) | ((nlit >> 4) << 8)
-                                     : (3u << 2) | ((nlit & 15u) << 4) | ((nlit >> 4) << 8);
-    const uint32_t hsz = nlit < 32 ? 1u : nlit < 4096 ? 2u : 3u;
-    o.room(hsz);
-    o.put((h >> (8 * (lane < 4 ? lane : 0u))) & 0xFFu, hsz);
-    if (nlit) {
-      if ((uint64_t)o.op + nlit > o.cap) {
-        o.overflow = true;
-      } else {
-        o.flush(o.op, true);
-        wave_copy_global(o.dst + o.op, lits, nlit);
-        o.op += nlit;
-        o.flushed = o.op;
-      }
-    }
-  }
 
-  ZSE_PHASE(3)
-  // ---- sequences section ----
-  if (!o.overflow) {
-    const uint32_t nh = nseq < 128 ? 1u : 2u;
-    o.room(nh);
-    o.put(nh == 1 ? nseq : lane == 0 ? (nseq >> 8) + 128u : nseq & 0xFFu, nh);
-  }
-  if (nseq && !o.overflow) {
-    // repeat offsets (rep_scan), codes, histograms, 64 sequences per step; the history
-    // before each step goes to the walk scratch (the records stay as the parse wrote them)
+  // ---- sequences: the blocks (equal sequence counts), repeat offsets (rep_scan), codes,
+  // histograms, 64 sequences per step from each block's first; the history before each step
+  // goes to the walk scratch (the records stay as the parse wrote them) ----
+  const uint32_t nb = nseq >= kMultiMin ? kBlocks : 1u;
+  uint32_t tdesc = 0;
+  if (nseq) {
     for (uint32_t k = lane; k < 3 * 64; k += kWave) (&L.sh[0][0])[k] = 0;
     lds_order();
     uint32_t c0r = 1, c1r = 4, c2r = 8;  // the history before the step (uniform)
-    GMEM uint32_t* wcodes = reinterpret_cast<GMEM uint32_t*>(
-        global_ptr(wscr + (uint64_t)i_seg * wstride + kWWords));
-    GMEM uint32_t* whist = reinterpret_cast<GMEM uint32_t*>(
-        global_ptr(wscr + (uint64_t)i_seg * wstride + walk_hist_at(seg)));
+    GMEM uint32_t* wcodes = reinterpret_cast<GMEM uint32_t*>(wbytes + kWWords);
+    GMEM uint32_t* whist = reinterpret_cast<GMEM uint32_t*>(wbytes + walk_hist_at(seg));
+    uint32_t st = 0, lsum = 0;
     uint2 nrec = lane < nseq ? seqs[lane] : make_uint2(0, 3);
-    for (uint32_t c0 = 0; c0 < nseq; c0 += kWave) {
-      const uint32_t j = c0 + lane;
-      const bool act = j < nseq;
-      const uint2 rec = nrec;
-      if (c0 + kWave + lane < nseq) nrec = seqs[c0 + kWave + lane];  // prefetch the next step
-      const uint32_t ll = rec.x & 0x1FFFFu, o = rec.x >> 17, ml = rec.y;
-      const uint32_t cnt = nseq - c0 < kWave ? nseq - c0 : kWave;
-      // the history before this step, for zstd_emit_kernel's re-derivation of the step
-      if (lane < 3) whist[3 * (c0 >> 6) + lane] = lane == 0 ? c0r : lane == 1 ? c1r : c2r;
-      const uint32_t ov = rep_scan(ll, o, act, cnt, c0r, c1r, c2r);
-      if (act) {
-        const uint32_t llc = ll_code(ll), ofc = hb32(ov), mlc = ml_code(ml);
-        atomicAdd(&L.sh[0][llc], 1u);
-        atomicAdd(&L.sh[1][ofc], 1u);
-        atomicAdd(&L.sh[2][mlc], 1u);
-        wcodes[j] = llc | (ofc << 6) | (mlc << 11);  // for zstd_walk_kernel
+    for (uint32_t b = 0; b < nb; ++b) {
+      const uint32_t s0 = (uint32_t)((uint64_t)b * nseq / nb);
+      const uint32_t s1 = (uint32_t)((uint64_t)(b + 1) * nseq / nb);
+      if (lane == 0) {
+        wrec[kWSb + b] = s0;
+        wrec[kWLb + b] = lsum;
+        wrec[kWStep + b] = st;
+      }
+      for (uint32_t c0 = s0; c0 < s1; c0 += kWave, ++st) {
+        const uint32_t j = c0 + lane;
+        const uint32_t cnt = s1 - c0 < kWave ? s1 - c0 : kWave;
+        const bool act = lane < cnt;
+        const uint2 rec = nrec;
+        // prefetch the next step (it starts right after this one's last sequence)
+        if (c0 + cnt + lane < nseq) nrec = seqs[c0 + cnt + lane];
+        const uint32_t ll = act ? rec.x & 0x1FFFFu : 0u, o = rec.x >> 17, ml = rec.y;
+        // the history before this step, for zstd_emit_kernel's re-derivation of the step
+        if (lane < 3) whist[3 * st + lane] = lane == 0 ? c0r : lane == 1 ? c1r : c2r;
+        const uint32_t ov = rep_scan(ll, o, act, cnt, c0r, c1r, c2r);
+        if (act) {
+          const uint32_t llc = ll_code(ll), ofc = hb32(ov), mlc = ml_code(ml);
+          atomicAdd(&L.sh[0][llc], 1u);
+          atomicAdd(&L.sh[1][ofc], 1u);
+          atomicAdd(&L.sh[2][mlc], 1u);
+          wcodes[j] = llc | (ofc << 6) | (mlc << 11);  // for zstd_walk_kernel
+        }
+        lsum += readlane(wave_incl_sum(ll), kWave - 1);
       }
     }
     lds_order();
@@ -1025,48 +906,30 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     }
     lds_order();
     ZSE_PHASE(5)
-    o.put_lds(L.desc, L.u[1]);
-    const uint32_t al_ll = L.u[2], al_of = L.u[3], al_ml = L.u[4];
-    // The sequence bitstream goes to two more launches (the state chains walked on four
-    // lanes per segment by zstd_walk_kernel, the fields placed by zstd_emit_kernel): hand
-    // the tables and where the bitstream starts over, with everything before it in HBM.
-    if (!o.overflow) {
-      GMEM uint32_t* w = global_ptr(reinterpret_cast<uint32_t*>(wscr + (uint64_t)i_seg * wstride));
-      o.flush(o.op, true);
-      lds_order();
-      for (uint32_t k = lane; k < (kTabDummy + 1 + 1) / 2; k += kWave)
-        w[kWTabs / 4 + k] = reinterpret_cast<const uint32_t*>(L.tabs)[k];
-      for (uint32_t k = lane; k < 3 * 64; k += kWave) w[kWTr / 4 + k] = (&L.tr[0][0])[k];
-      const uint32_t rv = lane == kWHanded ? 1u : lane == kWP0 ? o.op : lane == kWBlk ? blk
-                          : lane == kWN ? n : lane == kWNseq ? nseq
-                          : al_ll | (al_of << 8) | (al_ml << 16);
-      if (lane <= kWAls) w[lane] = rv;
-      return;
-    }
+    tdesc = L.u[1];
+    for (uint32_t k = lane; k < tdesc; k += kWave) wbytes[4 * kWDescAt + k] = L.desc[k];
+    // the state tables and transforms for zstd_walk_kernel
+    for (uint32_t k = lane; k < (kTabDummy + 1 + 1) / 2; k += kWave)
+      wrec[kWTabs / 4 + k] = reinterpret_cast<const uint32_t*>(L.tabs)[k];
+    for (uint32_t k = lane; k < 3 * 64; k += kWave) wrec[kWTr / 4 + k] = (&L.tr[0][0])[k];
+  } else if (lane == 0) {
+    wrec[kWSb] = 0;
+    wrec[kWLb] = 0;
+    wrec[kWStep] = 0;
   }
-  // nothing handed over (no sequences, or the slot overflowed): the record says so
-  if (lane == 0)
-    reinterpret_cast<GMEM uint32_t*>(global_ptr(wscr + (uint64_t)i_seg * wstride))[kWHanded] = 0u;
-
-  // ---- the block: compressed, or raw when that is not smaller ----
-  const bool stored = o.overflow || o.op - (blk + 3) >= n;
-  uint32_t hdr;
-  if (stored) {
-    o.overflow = false;
-    if (o.flushed < blk) o.flush(blk, true);  // the frame header is still staged
-    global_fence_wave();                       // earlier stores to this range land first
-    wave_copy_global(o.dst + blk + 3, src, n);
-    o.op = blk + 3 + n;
-    o.flushed = o.op;
-    hdr = 1u | (n << 3);
-  } else {
-    hdr = 1u | (2u << 1) | ((o.op - (blk + 3)) << 3);
-    o.flush(o.op, true);
+  // the record: everything zstd_emit_kernel needs to write the frame
+  if (lane == 0) {
+    wrec[kWN] = n;
+    wrec[kWNseq] = nseq;
+    wrec[kWAls] = nseq ? L.u[2] | (L.u[3] << 8) | (L.u[4] << 16) : 0u;
+    wrec[kWNb] = nb;
+    wrec[kWLit] = lmode | (lrle << 8) | (dsz << 16);
+    wrec[kWNlit] = nlit;
+    wrec[kWTdesc] = tdesc;
+    wrec[kWSb + nb] = nseq;
+    wrec[kWLb + nb] = nlit;
+    wrec[kWHanded] = 1u;
   }
-  global_fence_wave();
-  if (lane < 3) o.dst[blk + lane] = (uint8_t)(hdr >> (8 * lane));
-  if (lane == 0) sizes[i_seg] = o.op;
-  (void)err;
 }
 
 template <int K>
@@ -1074,16 +937,16 @@ __device__ __forceinline__ uint32_t zsq_qbcast(uint32_t v) {  // lane K of each 
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, K * 0x55, 0xF, 0xF, false);
 }
 
-// ---- pass 3: the FSE state chains, four lanes per segment ----------------------------------
-// Lane 4 l + j of the wave walks chain j (0 offsets, 1 match lengths, 2 literal lengths; 3
-// repeats 0) of segment blockIdx.x * 16 + l, last sequence first, with the segment's state
-// table and transforms in LDS: the three chains of a segment are independent, so each is a
-// lane's own loop (the wave kernel walked them one sequence at a time with readlanes).  Per
-// sequence the quad packs the three chains' state bits into one word (OF, then ML, then LL,
-// count << 26) -- the `stb` / `stn` of the old walk -- stored 8 at a time; the final states
-// go to the segment's record.  Same arithmetic as the walk it replaces (oracle
-// bo_zstd_compress_block), so the bitstream is unchanged bit for bit.
-constexpr uint32_t kWalkSegs = 16;
+// ---- pass 3: the FSE state chains, four lanes per chain set --------------------------------
+// Lane 16 l + 4 b + j of the wave walks chain j (0 offsets, 1 match lengths, 2 literal
+// lengths; 3 repeats 0) of block b of segment blockIdx.x * 4 + l, the block's last sequence
+// first, with the segment's state table and transforms in LDS: the chains of a block are
+// independent of each other and of the other blocks' (each block's states start from its own
+// last sequence), so each is a lane's own loop.  Per sequence the lane stores its chain's
+// state bits | count << 12 (u16), 8 at a time; each block's final states go to the segment's
+// record.  Same arithmetic as the oracle's per-block walk (bo_zstd_compress_block), bit for
+// bit.
+constexpr uint32_t kWalkSegs = 4;
 __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict__ scratch,
                                                         uint64_t sstride, uint32_t seg,
                                                         uint32_t nseg, uint8_t* __restrict__ wscr,
@@ -1091,23 +954,23 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
                                                         const uint32_t* __restrict__ order) {
   using namespace cmp;
   using namespace zse;
+  static_assert(kWalkSegs * kBlocks * 4 == kWave, "a lane per chain");
   __shared__ __attribute__((aligned(16))) uint16_t tabs[kWalkSegs][1284];
   __shared__ uint32_t trs[kWalkSegs][3][64];
   const uint32_t lane = lane_id();
-  for (uint32_t k = lane; k < sizeof(Tabs); k += kWave)
-    reinterpret_cast<uint8_t*>(&sT)[k] = reinterpret_cast<const uint8_t*>(&kT)[k];
   // (order: the segments by sequence count, walk_key_kernel; slot b walks segment order[b])
   // The wave's segments are looked up one lane each, together, and each segment's table loads
-  // are issued before the first is stored: at one wave per SIMD every serial load is exposed.
+  // are issued before the first is stored.
   uint32_t il0 = 0, hd0 = 0;
   {
     const uint32_t bl = blockIdx.x * kWalkSegs + lane;
     if (lane < kWalkSegs && bl < nseg) {
       il0 = order ? order[bl] : bl;
-      hd0 = global_ptr(reinterpret_cast<const uint32_t*>(wscr + (uint64_t)il0 * wstride))[kWHanded];
+      const GMEM uint32_t* w0 = global_ptr(reinterpret_cast<const uint32_t*>(wscr + (uint64_t)il0 * wstride));
+      hd0 = w0[kWHanded] == 1u && w0[kWNseq] != 0u;
     }
   }
-  const uint64_t hm = ballot(hd0 == 1u);
+  const uint64_t hm = ballot(hd0 != 0u);
   for (uint64_t m = hm; m; m &= m - 1) {
     const uint32_t l = (uint32_t)__builtin_ctzll(m);
     const uint32_t il = readlane(il0, l);
@@ -1130,13 +993,14 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
     for (uint32_t e = 0; e < 3; ++e) (&trs[l][0][0])[lane + e * kWave] = rv[e];
   }
   lds_order();
-  const uint32_t l = lane >> 2, j = lane & 3u;
+  const uint32_t l = lane >> 4, blk = (lane >> 2) & 3u, j = lane & 3u;
   const uint32_t b = blockIdx.x * kWalkSegs + l;
   // (fetched while every lane is active: a disabled source lane reads as 0)
   const uint32_t i = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(l << 2), (int)il0);
-  if (b >= nseg || !((hm >> l) & 1u)) return;  // quad-uniform
+  if (b >= nseg || !((hm >> l) & 1u)) return;  // uniform over the segment's 16 lanes
   GMEM uint32_t* w = global_ptr(reinterpret_cast<uint32_t*>(wscr + (uint64_t)i * wstride));
-  const uint32_t nseq = w[kWNseq];
+  if (blk >= w[kWNb]) return;  // quad-uniform
+  const uint32_t s0 = w[kWSb + blk], s1 = w[kWSb + blk + 1];
   const uint32_t cap = walk_cap(seg);
   const GMEM uint32_t* codes = w + kWWords / 4;
   GMEM uint16_t* outs = reinterpret_cast<GMEM uint16_t*>(w + kWWords / 4 + cap) + (j < 3 ? j : 0u) * cap;
@@ -1146,8 +1010,8 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
   // this chain's code in the code word (LL 6 bits, OF 5, ML 6)
   const uint32_t csh = c == 0 ? 6u : c == 1 ? 11u : 0u, cmask = c == 0 ? 31u : 63u;
   auto code = [&](uint32_t cw) __attribute__((always_inline)) { return (cw >> csh) & cmask; };
-  // the last sequence initialises the states (no state bits)
-  const uint32_t top = nseq - 1;
+  // the block's last sequence initialises the states (no state bits)
+  const uint32_t top = s1 - 1;
   uint32_t st;
   {
     const uint32_t e = tr[code(codes[top])];
@@ -1165,19 +1029,21 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
     return out;
   };
   if (j < 3) outs[top] = 0;
+  // k: sequences top - 1 .. s0, as offsets below top (kk = top - 1 - k')
+  const int32_t lo = (int32_t)s0;
   int32_t k = (int32_t)top - 1;
   constexpr int32_t kG = 8;
   // groups of 8: the transforms looked up together (independent of the states), then the
   // chain; the lane's 8 outputs stored together
   uint32_t r[kG];
 #pragma unroll
-  for (int32_t g = 0; g < kG; ++g) r[g] = codes[k - g >= 0 ? k - g : 0];
-  for (; k >= kG - 1; k -= kG) {
+  for (int32_t g = 0; g < kG; ++g) r[g] = codes[k - g >= lo ? k - g : lo];
+  for (; k >= lo + kG - 1; k -= kG) {
     uint32_t e[kG], o[kG];
 #pragma unroll
     for (int32_t g = 0; g < kG; ++g) e[g] = tr[code(r[g])];
 #pragma unroll
-    for (int32_t g = 0; g < kG; ++g) r[g] = codes[k - kG - g >= 0 ? k - kG - g : 0];  // next group
+    for (int32_t g = 0; g < kG; ++g) r[g] = codes[k - kG - g >= lo ? k - kG - g : lo];  // next group
 #pragma unroll
     for (int32_t g = 0; g < kG; ++g) o[g] = walk(e[g]);
     if (j < 3) {
@@ -1185,17 +1051,21 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
       for (int32_t g = 0; g < kG; ++g) outs[k - g] = (uint16_t)o[g];
     }
   }
-  for (; k >= 0; --k) {
+  for (; k >= lo; --k) {
     const uint32_t o = walk(tr[code(codes[k])]);
     if (j < 3) outs[k] = (uint16_t)o;
   }
-  if (j < 3) w[kWSt0 + j] = st;
+  if (j < 3) w[kWFin + 3 * blk + j] = st;
 }
 
-// ---- pass 4: the sequence bitstream ---------------------------------------------------------
-// One wave per handed-over segment: the fields of 64 sequences per step (highest first), the
-// final states and end mark, then the block header (or the raw block when the compressed one
-// is not smaller) -- the tail of zstd_entropy_kernel, with the state bits from pass 3.
+// ---- pass 4: the frame -----------------------------------------------------------------------
+// One wave per segment writes the whole frame: the frame header, then per block its literal
+// section (Huffman streams of the block's literals with the shared code -- the tree in the
+// first Huffman-coded block, Treeless after it -- or raw / RLE, oracle zs_literals_block),
+// its sequence section header, the table descriptions (first block) or Repeat_Mode, and its
+// sequence bitstream: the fields of 64 sequences per step (highest first) with the state bits
+// from pass 3, the final states and the end mark.  Then the block headers, or one raw block
+// when the compressed blocks are not smaller than the segment.
 __global__ __launch_bounds__(64) void zstd_emit_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     const uint8_t* __restrict__ scratch, uint64_t sstride, uint8_t* __restrict__ slab,
@@ -1204,21 +1074,32 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
   using namespace cmp;
   using namespace zse;
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];
+  __shared__ __attribute__((aligned(16))) uint32_t hcode[256];  // code | length << 16
+  __shared__ __attribute__((aligned(16))) uint8_t lst[16 * kWave];  // literal block being encoded
+  __shared__ __attribute__((aligned(16))) uint8_t bytes[132 + 256];  // tree; table descriptions
   const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const GMEM uint32_t* w = global_ptr(reinterpret_cast<const uint32_t*>(wscr + (uint64_t)i_seg * wstride));
+  const GMEM uint8_t* wb = reinterpret_cast<const GMEM uint8_t*>(w);
   if (uniform(w[kWHanded]) != 1u) return;
   const uint32_t lane = lane_id();
   for (uint32_t k = lane; k < sizeof(Tabs); k += kWave)
     reinterpret_cast<uint8_t*>(&sT)[k] = reinterpret_cast<const uint8_t*>(&kT)[k];
-  lds_order();
-  const uint32_t p0 = uniform(w[kWP0]), blk = uniform(w[kWBlk]), n = uniform(w[kWN]);
-  const uint32_t nseq = uniform(w[kWNseq]), als = uniform(w[kWAls]);
+  const uint32_t n = uniform(w[kWN]), als = uniform(w[kWAls]);
+  const uint32_t nb = uniform(w[kWNb]), litw = uniform(w[kWLit]);
+  const uint32_t tdesc = uniform(w[kWTdesc]);
+  const uint32_t lmode = litw & 0xFFu, lrle = (litw >> 8) & 0xFFu, dsz = litw >> 16;
   const uint32_t al_ll = als & 0xFFu, al_of = (als >> 8) & 0xFFu, al_ml = als >> 16;
+  if (lmode == 2) {
+    for (uint32_t k = lane; k < 256; k += kWave) hcode[k] = w[kWCodeAt + k];
+    for (uint32_t k = lane; k < dsz; k += kWave) bytes[k] = wb[4 * kWTreeAt + k];
+  }
+  for (uint32_t k = lane; k < tdesc; k += kWave) bytes[132 + k] = wb[4 * kWDescAt + k];
+  lds_order();
   const GMEM uint8_t* src = global_ptr(input + seg_off);
-  const GMEM uint2* seqs = reinterpret_cast<const GMEM uint2*>(
-      global_ptr(scratch + (uint64_t)i_seg * sstride + lit_cap(seg)));
+  const GMEM uint8_t* lits = global_ptr(scratch + (uint64_t)i_seg * sstride);
+  const GMEM uint2* seqs = reinterpret_cast<const GMEM uint2*>(lits + lit_cap(seg));
   const uint32_t cap = walk_cap(seg);
   const GMEM uint16_t* outs = reinterpret_cast<const GMEM uint16_t*>(w + kWWords / 4 + cap);
   const GMEM uint32_t* whist = w + walk_hist_at(seg) / 4;
@@ -1226,71 +1107,223 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
   o.ring = obuf;
   o.dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
   o.cap = slot_stride;
-  o.op = p0;
-  o.flushed = p0;  // the frame up to p0 is in the slot (zstd_entropy_kernel)
+  o.op = 0;
+  o.flushed = 0;
   o.overflow = false;
-  uint32_t bits = 0, zeroed = p0;
-  const uint32_t top = nseq - 1;
-  uint2 prec = seqs[(top >> 6) * kWave + lane < nseq ? (top >> 6) * kWave + lane : top];
-  auto word = [&](uint32_t j) __attribute__((always_inline)) {  // OF | ML | LL bits, counts
-    const uint32_t oo = outs[j], om = outs[cap + j], ol = outs[2 * cap + j];
-    const uint32_t nof = oo >> 12, nml = om >> 12, nll = ol >> 12;
-    return (oo & 0xFFFu) | ((om & 0xFFFu) << nof) | ((ol & 0xFFFu) << (nof + nml)) |
-           ((nof + nml + nll) << 26);
-  };
-  uint32_t pw = word((top >> 6) * kWave + lane < nseq ? (top >> 6) * kWave + lane : top);
-  for (int32_t c = (int32_t)(top >> 6); c >= 0 && !o.overflow; --c) {
-    const uint32_t j = (uint32_t)c * kWave + lane;
-    const bool act = j < nseq;
-    const uint2 rec = prec;
-    const uint32_t wd = pw;
-    if (c > 0) {  // prefetch the next step
-      prec = seqs[(uint32_t)(c - 1) * kWave + lane];
-      pw = word((uint32_t)(c - 1) * kWave + lane);
+  // frame header: magic, Single_Segment with the content size (1 byte below 256, else 2)
+  const uint32_t fh = n < 256 ? 6u : 7u;
+  {
+    const uint32_t fcs = n < 256 ? n : n - 256u;
+    const uint32_t hb = lane < 4 ? (0xFD2FB528u >> (8 * lane)) & 0xFFu
+                        : lane == 4 ? (n < 256 ? 0x20u : 0x60u)
+                        : lane == 5 ? fcs & 0xFFu : fcs >> 8;
+    o.put(hb, fh);
+  }
+  uint32_t bpos[kBlocks], bhdr[kBlocks];
+  bool tree_sent = false;
+  // literals [a, a + m) of the segment's literal area as a Huffman stream (oracle
+  // zs_literals_block): symbols from the last, 64 per step, from 1 KiB blocks of aligned
+  // 16-B groups staged in LDS, the next one loaded during the current one
+  auto huff_stream = [&](uint32_t a, uint32_t b) __attribute__((always_inline)) {
+    const uint32_t p0 = o.op;
+    uint32_t bits = 0, zeroed = p0;
+    const GMEM uint4* l16 = reinterpret_cast<const GMEM uint4*>(lits);
+    const int32_t gA = (int32_t)(a >> 4), gB = (int32_t)((b + 15) >> 4);
+    int32_t g0 = gB - (int32_t)kWave;
+    uint4 blkv = make_uint4(0, 0, 0, 0);
+    if (g0 + (int32_t)lane >= gA) blkv = l16[g0 + (int32_t)lane];
+    for (;;) {
+      lds_order();
+      reinterpret_cast<uint4*>(lst)[lane] = blkv;
+      const int32_t g1 = g0 - (int32_t)kWave;
+      if (g0 > gA && g1 + (int32_t)lane >= gA) blkv = l16[g1 + (int32_t)lane];
+      const int32_t lo = max((int32_t)a, 16 * g0), hi = min((int32_t)b, 16 * (g0 + (int32_t)kWave));
+      for (int32_t e = hi; e > lo && !o.overflow; e -= (int32_t)kWave) {
+        const int32_t idx = e - (int32_t)kWave + (int32_t)lane;
+        const bool act = idx >= lo;
+        lds_order();
+        const uint32_t sym = act ? lst[idx - 16 * g0] : 0u;
+        const uint32_t cw = hcode[sym];
+        o.put_bits(act ? (cw & 0xFFFFu) : 0u, act ? cw >> 16 : 0u, 0, 0, p0, bits, zeroed);
+      }
+      if (g0 <= gA || o.overflow) break;
+      g0 = g1;
     }
-    // the step's offset values from the history before it (zstd_entropy_kernel's scan)
-    uint32_t h0 = uniform(whist[3 * (uint32_t)c]), h1 = uniform(whist[3 * (uint32_t)c + 1]),
-             h2 = uniform(whist[3 * (uint32_t)c + 2]);
-    const uint32_t cnt = nseq - (uint32_t)c * kWave < kWave ? nseq - (uint32_t)c * kWave : kWave;
-    const uint32_t ll = rec.x & 0x1FFFFu, mlb = rec.y - 3u;
-    const uint32_t ov = rep_scan(ll, rec.x >> 17, act, cnt, h0, h1, h2);
-    const uint32_t llc = ll_code(ll), mlc = ml_code(rec.y), ofc = hb32(ov);
-    const uint64_t stb = wd & 0x3FFFFFFu;
-    const uint32_t stn = wd >> 26;
-    const uint32_t llb = sT.ll_bits[llc], mlbits = sT.ml_bits[mlc];
-    // part 0: state bits + literal-length extra (<= 26 + 16); part 1: match-length extra,
-    // then offset extra (<= 16 + 16)
-    const uint64_t f0 = stb | ((uint64_t)(ll & ((1u << llb) - 1u)) << stn);
-    const uint64_t f1 = (uint64_t)(mlb & ((1u << mlbits) - 1u)) |
-                        ((uint64_t)(ov & ((1u << ofc) - 1u)) << mlbits);
-    o.put_bits(act ? f0 : 0u, act ? stn + llb : 0u, act ? f1 : 0u, act ? mlbits + ofc : 0u,
-               p0, bits, zeroed);
-  }
-  if (!o.overflow) {
-    // final states (ML, OF, LL: the decoder reads LL first) and the end mark
-    const uint32_t sOF = uniform(w[kWSt0]), sML = uniform(w[kWSt1]), sLL = uniform(w[kWSt2]);
-    const uint64_t fin = (uint64_t)(sML & ((1u << al_ml) - 1u)) |
-                         ((uint64_t)(sOF & ((1u << al_of) - 1u)) << al_ml) |
-                         ((uint64_t)(sLL & ((1u << al_ll) - 1u)) << (al_ml + al_of)) |
-                         (1ull << (al_ml + al_of + al_ll));
-    const uint32_t fn = al_ml + al_of + al_ll + 1;
-    o.put_bits(lane == 0 ? fin : 0u, lane == 0 ? fn : 0u, 0, 0, p0, bits, zeroed);
+    o.put_bits(lane == 0 ? 1u : 0u, lane == 0 ? 1u : 0u, 0, 0, p0, bits, zeroed);  // end mark
     o.op = p0 + ((bits + 7) >> 3);
+  };
+  auto lit_header = [&](uint32_t type, uint32_t m) __attribute__((always_inline)) {
+    const uint32_t h = m < 32 ? type | (m << 3)
+                       : m < 4096 ? type | (1u << 2) | ((m & 15u) << 4) | ((m >> 4) << 8)
+                                  : type | (3u << 2) | ((m & 15u) << 4) | ((m >> 4) << 8);
+    const uint32_t hsz = m < 32 ? 1u : m < 4096 ? 2u : 3u;
+    o.room(hsz + 1);
+    o.put(lane < hsz ? (h >> (8 * (lane < 4 ? lane : 0u))) & 0xFFu : lrle,
+          hsz + (type == 1 ? 1u : 0u));
+  };
+  for (uint32_t b = 0; b < nb && !o.overflow; ++b) {
+    const uint32_t blk = o.op;
+    bpos[b] = blk;
+    o.room(3);
+    o.op += 3;  // the block header, written last
+    // ---- literal section ----
+    const uint32_t a = uniform(w[kWLb + b]), m = uniform(w[kWLb + b + 1]) - a;
+    bool coded = false;
+    if (lmode == 1 && m > 0) {
+      lit_header(1u, m);
+      coded = true;
+    } else if (lmode == 2 && m > 0) {
+      // the streams' sizes: code lengths summed per quarter (one pass over the literals)
+      const uint32_t ns = m < 256 ? 1u : 4u, q = (m + 3) / 4;
+      uint32_t bq[4] = {0, 0, 0, 0};
+      for (uint32_t g = a & ~15u; g < a + m; g += 16u * kWave) {
+        const uint32_t at = g + 16u * lane;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (at < a + m) v = *reinterpret_cast<const GMEM uint4*>(lits + at);
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t jj = 0; jj < 16; ++jj) {
+          const uint32_t r = at + jj - a;  // (wraps for positions before a: >= m)
+          const uint32_t ln = hcode[(wv[jj >> 2] >> (8 * (jj & 3))) & 0xFFu] >> 16;
+          const uint32_t qi = ns == 1 ? 0u : r < q ? 0u : r < 2 * q ? 1u : r < 3 * q ? 2u : 3u;
+          const uint32_t add = r < m ? ln : 0u;
+          bq[0] += qi == 0 ? add : 0u;
+          bq[1] += qi == 1 ? add : 0u;
+          bq[2] += qi == 2 ? add : 0u;
+          bq[3] += qi == 3 ? add : 0u;
+        }
+      }
+      uint32_t sb[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) sb[k] = (readlane(wave_incl_sum(bq[k]), kWave - 1) + 8) >> 3;
+      const uint32_t tsz = tree_sent ? 0u : dsz;
+      const uint32_t total = tsz + (ns == 4 ? 6u + sb[0] + sb[1] + sb[2] + sb[3] : sb[0]);
+      const int32_t limit = (int32_t)m - (int32_t)((m >> 6) + 2);
+      if ((int32_t)total < limit) {
+        const uint32_t hs = ns == 1 || m < 1024 ? 3u : m < 16384 ? 4u : 5u;
+        const uint32_t sf = ns == 1 ? 0u : m < 1024 ? 1u : m < 16384 ? 2u : 3u;
+        const uint64_t h = (tree_sent ? 3u : 2u) | (sf << 2) | ((uint64_t)m << 4) |
+                           ((uint64_t)total << (hs == 3 ? 14 : hs == 4 ? 18 : 22));
+        o.room(hs);
+        o.put((uint32_t)(h >> (8 * (lane < 8 ? lane : 0u))) & 0xFFu, hs);
+        o.put_lds(bytes, tsz);
+        if (ns == 4) {
+          const uint32_t jj = lane >> 1;
+          const uint32_t sv = jj == 0 ? sb[0] : jj == 1 ? sb[1] : sb[2];
+          o.room(6);
+          o.put((lane & 1) ? sv >> 8 : sv & 0xFFu, 6);
+          for (uint32_t k = 0; k < 4 && !o.overflow; ++k)
+            huff_stream(a + k * q, k == 3 ? a + m : a + (k + 1) * q);
+        } else {
+          huff_stream(a, a + m);
+        }
+        tree_sent = true;
+        coded = true;
+      }
+    }
+    if (!coded) {  // raw
+      lit_header(0u, m);
+      if (m) {
+        if ((uint64_t)o.op + m > o.cap) {
+          o.overflow = true;
+        } else {
+          o.flush(o.op, true);
+          wave_copy_global(o.dst + o.op, lits + a, m);
+          o.op += m;
+          o.flushed = o.op;
+        }
+      }
+    }
+    // ---- sequences section ----
+    const uint32_t s0 = uniform(w[kWSb + b]), s1 = uniform(w[kWSb + b + 1]), bn = s1 - s0;
+    if (!o.overflow) {
+      const uint32_t nh = bn < 128 ? 1u : 2u;
+      o.room(nh);
+      o.put(nh == 1 ? bn : lane == 0 ? (bn >> 8) + 128u : bn & 0xFFu, nh);
+    }
+    if (bn && !o.overflow) {
+      if (b == 0) {
+        o.put_lds(bytes + 132, tdesc);  // modes byte + table descriptions
+      } else {
+        o.room(1);
+        o.put(0xFCu, 1);  // Repeat_Mode for all three tables
+      }
+      const uint32_t p0 = o.op;
+      uint32_t bits = 0, zeroed = p0;
+      const uint32_t st0 = uniform(w[kWStep + b]);
+      auto word = [&](uint32_t j) __attribute__((always_inline)) {  // OF | ML | LL bits, counts
+        const uint32_t oo = outs[j], om = outs[cap + j], ol = outs[2 * cap + j];
+        const uint32_t nof = oo >> 12, nml = om >> 12, nll = ol >> 12;
+        return (oo & 0xFFFu) | ((om & 0xFFFu) << nof) | ((ol & 0xFFFu) << (nof + nml)) |
+               ((nof + nml + nll) << 26);
+      };
+      const uint32_t lastc = (bn - 1) >> 6;
+      uint32_t jn = s0 + lastc * kWave + lane;
+      uint2 prec = seqs[jn < s1 ? jn : s1 - 1];
+      uint32_t pw = word(jn < s1 ? jn : s1 - 1);
+      for (int32_t c = (int32_t)lastc; c >= 0 && !o.overflow; --c) {
+        const uint32_t j = s0 + (uint32_t)c * kWave + lane;
+        const bool act = j < s1;
+        const uint2 rec = prec;
+        const uint32_t wd = pw;
+        if (c > 0) {  // prefetch the next step
+          prec = seqs[j - kWave];
+          pw = word(j - kWave);
+        }
+        // the step's offset values from the history before it (zstd_entropy_kernel's scan)
+        const uint32_t hs = 3 * (st0 + (uint32_t)c);
+        uint32_t h0 = uniform(whist[hs]), h1 = uniform(whist[hs + 1]), h2 = uniform(whist[hs + 2]);
+        const uint32_t cnt = s1 - (s0 + (uint32_t)c * kWave) < kWave ? s1 - (s0 + (uint32_t)c * kWave) : kWave;
+        const uint32_t ll = rec.x & 0x1FFFFu, mlb = rec.y - 3u;
+        const uint32_t ov = rep_scan(ll, rec.x >> 17, act, cnt, h0, h1, h2);
+        const uint32_t llc = ll_code(ll), mlc = ml_code(rec.y), ofc = hb32(ov);
+        const uint64_t stb = wd & 0x3FFFFFFu;
+        const uint32_t stn = wd >> 26;
+        const uint32_t llb = sT.ll_bits[llc], mlbits = sT.ml_bits[mlc];
+        // part 0: state bits + literal-length extra (<= 26 + 16); part 1: match-length extra,
+        // then offset extra (<= 16 + 16)
+        const uint64_t f0 = stb | ((uint64_t)(ll & ((1u << llb) - 1u)) << stn);
+        const uint64_t f1 = (uint64_t)(mlb & ((1u << mlbits) - 1u)) |
+                            ((uint64_t)(ov & ((1u << ofc) - 1u)) << mlbits);
+        o.put_bits(act ? f0 : 0u, act ? stn + llb : 0u, act ? f1 : 0u, act ? mlbits + ofc : 0u,
+                   p0, bits, zeroed);
+      }
+      if (!o.overflow) {
+        // final states (ML, OF, LL: the decoder reads LL first) and the end mark
+        const uint32_t sOF = uniform(w[kWFin + 3 * b]), sML = uniform(w[kWFin + 3 * b + 1]),
+                       sLL = uniform(w[kWFin + 3 * b + 2]);
+        const uint64_t fin = (uint64_t)(sML & ((1u << al_ml) - 1u)) |
+                             ((uint64_t)(sOF & ((1u << al_of) - 1u)) << al_ml) |
+                             ((uint64_t)(sLL & ((1u << al_ll) - 1u)) << (al_ml + al_of)) |
+                             (1ull << (al_ml + al_of + al_ll));
+        const uint32_t fn = al_ml + al_of + al_ll + 1;
+        o.put_bits(lane == 0 ? fin : 0u, lane == 0 ? fn : 0u, 0, 0, p0, bits, zeroed);
+        o.op = p0 + ((bits + 7) >> 3);
+      }
+    }
+    bhdr[b] = (b + 1 == nb ? 1u : 0u) | (2u << 1) | ((o.op - (blk + 3)) << 3);
   }
-  // the block: compressed, or raw when that is not smaller
-  const bool stored = o.overflow || o.op - (blk + 3) >= n;
-  uint32_t hdr;
+  // the blocks, or one raw block when they are not smaller than the segment
+  const bool stored = o.overflow || o.op - (fh + 3) >= n;
   if (stored) {
-    global_fence_wave();  // earlier stores to this range land first
-    wave_copy_global(o.dst + blk + 3, src, n);
-    o.op = blk + 3 + n;
-    hdr = 1u | (n << 3);
+    o.overflow = false;
+    if (o.flushed < fh) o.flush(fh, true);  // the frame header may still be staged
+    global_fence_wave();                     // earlier stores to this range land first
+    wave_copy_global(o.dst + fh + 3, src, n);
+    o.op = fh + 3 + n;
+    bpos[0] = fh;
+    bhdr[0] = 1u | (n << 3);
   } else {
-    hdr = 1u | (2u << 1) | ((o.op - (blk + 3)) << 3);
     o.flush(o.op, true);
   }
   global_fence_wave();
-  if (lane < 3) o.dst[blk + lane] = (uint8_t)(hdr >> (8 * lane));
+  const uint32_t nh = stored ? 1u : nb;
+  if (lane < 3 * nh) {
+    const uint32_t bi = lane / 3, byte = lane - 3 * bi;
+    const uint32_t at = bi == 0 ? bpos[0] : bi == 1 ? bpos[1] : bi == 2 ? bpos[2] : bpos[3];
+    const uint32_t hv = bi == 0 ? bhdr[0] : bi == 1 ? bhdr[1] : bi == 2 ? bhdr[2] : bhdr[3];
+    o.dst[at + byte] = (uint8_t)(hv >> (8 * byte));
+  }
   if (lane == 0) sizes[i_seg] = o.op;
 }
 

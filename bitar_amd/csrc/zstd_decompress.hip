@@ -711,7 +711,7 @@ struct Frame {
 // hand != null, i.e. no checksum, and last block)
 __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs& t, Frame& fr, uint32_t p,
                       uint32_t len, GMEM uint32_t* hand, bool last_block, uint32_t fsz,
-                      uint32_t fcs) {
+                      uint32_t fcs, uint32_t& h_nseq, uint32_t& h_regen) {
   const uint32_t lane = lane_id();
   p = uniform(p);
   len = uniform(len);
@@ -908,6 +908,8 @@ __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs
                           : lane == 5 ? regen : lane == 6 ? s.op : lane == 7 ? fr.rep0
                           : lane == 8 ? fr.rep1 : lane == 9 ? fr.rep2 : lane == 10 ? fsz : fcs;
       if (lane < 12) hand[lane] = rv;
+      h_nseq = nseq;
+      h_regen = regen;
       return 2;
     }
     // FSE tables of <= 64 cells (every predefined one) move into registers: lane u holds cell
@@ -1106,11 +1108,158 @@ __device__ __forceinline__ int block(State& s, uint8_t* win, uint8_t* ring, Tabs
                         : lane == 5 ? regen : lane == 6 ? s.op : lane == 7 ? fr.rep0
                         : lane == 8 ? fr.rep1 : lane == 9 ? fr.rep2 : lane == 10 ? fsz : fcs;
     if (lane < 12) hand[lane] = rv;
+    h_nseq = 0;
+    h_regen = regen;
     return 2;
   }
   if ((uint64_t)s.op + (regen - lp) > s.cap) return 0;
   copy_lits(regen - lp);
   return 1;
+}
+
+// Frames whose blocks can all be handed over (zstd_hand.hip.h): 2..kMaxBlocks compressed
+// blocks ending exactly at the frame's end, where the blocks after the first define no table
+// and no Huffman tree (Repeat_Mode or no sequences; Treeless, raw or RLE literals) -- the
+// frames of this engine's encoder.  Returns the block count, else 0.  Only the headers are
+// read here; every other rule is checked where the blocks run.
+__device__ uint32_t multi_blocks(State& s, uint8_t* win, uint32_t p, uint32_t cs) {
+  uint32_t nb = 0;
+  for (;;) {
+    if (nb == zhand::kMaxBlocks || p + 3 > cs) return 0;
+    const uint32_t bh = load_le(s, win, p, 3);
+    const uint32_t last = bh & 1u, type = (bh >> 1) & 3u, bsz = bh >> 3;
+    p += 3;
+    if (type != 2 || bsz > (128u << 10) || bsz < 2 || p + bsz > cs) return 0;
+    if (nb > 0) {
+      const uint32_t end = p + bsz;
+      const uint32_t b0 = load_le(s, win, p, 1);
+      const uint32_t lt = b0 & 3u, sf = (b0 >> 2) & 3u;
+      if (lt == 2) return 0;  // a new tree
+      uint32_t hsz, size;
+      if (lt < 2) {
+        hsz = (sf == 0 || sf == 2) ? 1u : sf == 1 ? 2u : 3u;
+        if (p + hsz > end) return 0;
+        const uint32_t regen = hsz == 1 ? b0 >> 3 : load_le(s, win, p, hsz) >> 4;
+        size = lt == 0 ? regen : 1u;
+      } else {
+        hsz = sf <= 1 ? 3u : sf == 2 ? 4u : 5u;
+        if (p + hsz > end) return 0;
+        const uint64_t c = (uint64_t)load_le(s, win, p, hsz < 4 ? hsz : 4u) |
+                           (hsz == 5 ? (uint64_t)load_le(s, win, p + 4, 1) << 32 : 0ull);
+        size = (uint32_t)(hsz == 3 ? (c >> 14) & 0x3FFu : hsz == 4 ? (c >> 18) & 0x3FFFu
+                                                                 : (c >> 22) & 0x3FFFFu);
+      }
+      const uint32_t q = p + hsz + size;
+      if (q >= end) return 0;
+      uint32_t nseq = load_le(s, win, q, 1), qm = q + 1;
+      if (nseq >= 128) {
+        if (nseq < 255) { nseq = 1; qm = q + 2; }
+        else { nseq = 1; qm = q + 3; }
+      }
+      if (nseq && (qm >= end || load_le(s, win, qm, 1) != 0xFCu)) return 0;  // Repeat_Mode
+    }
+    ++nb;
+    p += bsz;
+    if (last) return (nb >= 2 && p == cs) ? nb : 0u;
+  }
+}
+
+// A block after the first of a multi-block hand-off (multi_blocks): its headers into the
+// sub-record hb (zstd_hand.hip.h), with the checks the wave decoder would apply to them
+// (block()).  False = malformed.
+__device__ bool hand_header(State& s, uint8_t* win, const Frame& fr, GMEM uint32_t* hb,
+                            uint32_t p, uint32_t len, uint32_t& nseq_o, uint32_t& regen_o) {
+  const uint32_t lane = lane_id();
+  p = uniform(p);
+  len = uniform(len);
+  const uint32_t end = p + len;
+  const uint32_t b0 = load_le(s, win, p, 1);
+  const uint32_t lt = b0 & 3u, sf = (b0 >> 2) & 3u;
+  uint32_t regen, csz = 0, hsz, nstreams = 1;
+  if (lt < 2) {
+    if (sf == 0 || sf == 2) { regen = b0 >> 3; hsz = 1; }
+    else if (sf == 1) { if (len < 2) return false; regen = load_le(s, win, p, 2) >> 4; hsz = 2; }
+    else { if (len < 3) return false; regen = load_le(s, win, p, 3) >> 4; hsz = 3; }
+  } else {
+    if (sf <= 1) {
+      if (len < 3) return false;
+      const uint32_t c = load_le(s, win, p, 3);
+      regen = (c >> 4) & 0x3FFu; csz = (c >> 14) & 0x3FFu; hsz = 3; nstreams = sf == 0 ? 1 : 4;
+    } else if (sf == 2) {
+      if (len < 4) return false;
+      const uint32_t c = load_le(s, win, p, 4);
+      regen = (c >> 4) & 0x3FFFu; csz = (c >> 18) & 0x3FFFu; hsz = 4; nstreams = 4;
+    } else {
+      if (len < 5) return false;
+      const uint64_t c = (uint64_t)load_le(s, win, p, 4) | ((uint64_t)load_le(s, win, p + 4, 1) << 32);
+      regen = (uint32_t)(c >> 4) & 0x3FFFFu; csz = (uint32_t)(c >> 22) & 0x3FFFFu; hsz = 5; nstreams = 4;
+    }
+  }
+  if (regen > (128u << 10)) return false;
+  uint32_t q = p + hsz;
+  uint32_t litv = 0, st = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, qq = regen;
+  bool pend = false;
+  if (lt == 0) {
+    if (q + regen > end) return false;
+    litv = q;
+    q += regen;
+  } else if (lt == 1) {
+    if (q + 1 > end) return false;
+    litv = load_le(s, win, q, 1);
+    q += 1;
+  } else {  // Treeless: the first block's tree
+    if (q + csz > end || !fr.huf_log) return false;
+    st = q;
+    s1 = csz;
+    if (nstreams != 1) {
+      if (csz < 6) return false;
+      const uint32_t j = load_le(s, win, q, 4);
+      s1 = j & 0xFFFFu;
+      s2 = j >> 16;
+      s3 = load_le(s, win, q + 4, 2);
+      if (6ull + s1 + s2 + s3 > csz) return false;
+      s4 = csz - 6 - s1 - s2 - s3;
+      qq = (regen + 3) / 4;
+      if (3 * qq > regen) return false;
+      st = q + 6;
+    }
+    pend = true;
+    q += csz;
+  }
+  if (q >= end) return false;
+  uint32_t nseq = load_le(s, win, q, 1);
+  if (nseq < 128) {
+    q += 1;
+  } else if (nseq < 255) {
+    if (q + 2 > end) return false;
+    nseq = ((nseq - 128) << 8) + load_le(s, win, q + 1, 1);
+    q += 2;
+  } else {
+    if (q + 3 > end) return false;
+    nseq = load_le(s, win, q + 1, 2) + 0x7F00u;
+    q += 3;
+  }
+  if (nseq) {
+    // Repeat_Mode for all three tables (multi_blocks), which the first block must have had
+    if (q >= end || !fr.have[0] || !fr.have[1] || !fr.have[2]) return false;
+    q += 1;
+    if (q >= end) return false;
+  } else if (q != end) {
+    return false;
+  }
+  const uint32_t rv = lane == zhand::kQ ? q : lane == zhand::kEnd ? end
+                      : lane == zhand::kNseq ? nseq
+                      : lane == zhand::kAls ? fr.al[0] | (fr.al[1] << 8) | (fr.al[2] << 16) | (lt << 24)
+                      : lane == zhand::kLitV ? litv : lane == zhand::kRegen ? regen
+                      : lane == zhand::kLitPend ? (pend ? 1u : 0u)
+                      : lane == zhand::kHufLog ? fr.huf_log | (nstreams << 8)
+                      : lane == zhand::kStreams ? st : lane == zhand::kS1 ? s1
+                      : lane == zhand::kS2 ? s2 : lane == zhand::kS3 ? s3
+                      : lane == zhand::kS4 ? s4 : qq;
+  if (lane < zhand::kBlkW && (lane < zhand::kOp || lane >= zhand::kLitPend)) hb[lane] = rv;
+  nseq_o = nseq;
+  regen_o = regen;
+  return true;
 }
 
 // XXH64 of the first n output bytes (already flushed to HBM and fenced), low 32 bits
@@ -1184,7 +1333,8 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
-    uint32_t defer_only, uint8_t* __restrict__ hscr, unsigned long long* __restrict__ stats, const uint32_t* __restrict__ order) {
+    uint32_t defer_only, uint8_t* __restrict__ hscr, unsigned long long* __restrict__ stats,
+    const uint32_t* __restrict__ order, uint32_t multi) {
   using namespace zsd;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kWin + kRing];
   __shared__ __attribute__((aligned(16))) Tabs t;
@@ -1244,6 +1394,9 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
     bool bad = false, last = false, handed = false;
     GMEM uint32_t* hand = hscr && !cks ? global_ptr(reinterpret_cast<uint32_t*>(hscr + (uint64_t)i * zhand::kStride))
                                        : nullptr;
+    // all blocks to the lane kernels (the two-phase sequence path only), else the last one
+    const uint32_t nbm = hand && multi ? multi_blocks(s, win, p, cs) : 0u;
+    uint32_t h_nseq = 0, h_regen = 0;
     while (!last) {
       if (p + 3 > cs) { bad = true; break; }
       const uint32_t bh = load_le(s, win, p, 3);
@@ -1266,9 +1419,42 @@ __global__ __launch_bounds__(64) void zstd_decompress_kernel(
       } else if (type == 2) {
         if (bsz > (128u << 10) || p + bsz > cs) { bad = true; break; }
         ZP_BEGIN(tb);
-        const int r = block(s, win, ring, t, fr, p, bsz, hand, last, fsz, (uint32_t)fcs);
+        const int r = block(s, win, ring, t, fr, p, bsz, hand, last || nbm != 0, fsz, (uint32_t)fcs,
+                            h_nseq, h_regen);
         if (r == 0) { bad = true; break; }
-        if (r == 2) { handed = true; break; }
+        if (r == 2) {
+          handed = true;
+          // the frame-level words (zstd_hand.hip.h), and the later blocks' sub-records
+          uint32_t nsa = h_nseq, lsa = h_regen, nb = 1;
+          uint32_t xv = 0;  // lane 8 b + k: block b's extra word k
+          if (lane_id() == 0) xv = 0u;  // block 0: records and literals from 0
+          for (uint32_t q = p + bsz; nb < nbm; ++nb) {
+            const uint32_t bh2 = load_le(s, win, q, 3);
+            const uint32_t bsz2 = bh2 >> 3;
+            q += 3;
+            uint32_t ns2 = 0, rg2 = 0;
+            if (!hand_header(s, win, fr, hand + zhand::blk_at(nb), q, bsz2, ns2, rg2)) {
+              bad = true;
+              break;
+            }
+            const uint32_t ln = lane_id();
+            xv = ln == zhand::kXW * nb + zhand::kXRec ? nsa : ln == zhand::kXW * nb + zhand::kXLit ? lsa : xv;
+            nsa += ns2;
+            lsa += rg2;
+            q += bsz2;
+          }
+          if (bad) break;
+          if (lsa > s.cap - s.op) { bad = true; break; }  // (the slot tail holds them all)
+          const uint32_t ln = lane_id();
+          const bool xs = ln < zhand::kXW * nb && (ln % zhand::kXW) <= zhand::kXLit;
+          if (xs) hand[zhand::kX0 + ln] = xv;
+          if (ln == 0) {
+            hand[zhand::kNb] = nb;
+            hand[zhand::kNseqAll] = nsa;
+            hand[zhand::kLitAll] = lsa;
+          }
+          break;
+        }
         ZP_END(1, tb);
         ZP_ADD(13, 1);
         p += bsz;

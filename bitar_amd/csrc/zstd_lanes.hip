@@ -407,13 +407,19 @@ __device__ __forceinline__ uint32_t word_raw(const GMEM uint8_t* s, int32_t a, i
 __device__ __forceinline__ bool lits_pending(uint32_t p) {
   return p == zhand::kHanded || p == zhand::kRecs;
 }
-template <uint32_t S>
+// B: the blocks of a segment in the wave (lane 4 B l + 4 b + j = stream j of block b of
+// segment l): B = 1 takes the frames that handed their last block only (kNb == 1), B = 4 the
+// multi-block hand-offs (kNb >= 2: the streams of all of a frame's blocks run at once, their
+// literals going to each block's place in the slot tail, zstd_hand.hip.h kXLit).
+template <uint32_t S, uint32_t B>
 __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced,
-    const uint8_t* __restrict__ hscr, uint32_t* __restrict__ err) {
+    const uint8_t* __restrict__ hscr, uint32_t* __restrict__ err,
+    const uint32_t* __restrict__ order) {
   using namespace zhand;
+  static_assert(S * B * 4 <= kWave, "a lane per stream");
   // Per segment: the 2^11-entry table as symbol bytes plus each symbol's code length, 2.25
   // KiB instead of 4 KiB of (symbol | length) entries, so 16 segments take 36 KiB and four
   // workgroups share a CU: every stream of a GiB is resident in one round (two lookups per
@@ -424,20 +430,34 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
   // The wave's segment headers, one lane per segment, loaded together, and each table's
   // words issued before any is used: at about one wave per SIMD every serial load is
   // exposed, and the per-segment form chained three header loads and 16 table loads.
-  uint32_t p0 = 0, pend = 0, hlg = 0;
+  // (pend: any block's streams pending; hlg: the table log, the same for every block)
+  // (order: the segments by literal count, most first, hand_key_kernel: slot x takes
+  // segment order[x])
+  uint32_t p0 = 0, pend = 0, hlg = 0, nbh = 0, il0 = 0;
   {
-    const uint32_t il = blockIdx.x * S + lane;
+    const uint32_t bl = blockIdx.x * S + lane;
+    const uint32_t il = bl < nseg ? (order ? order[bl] : bl) : bl;
+    il0 = il;
     if (lane < S && il < nseg) {
       const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
       p0 = produced[il];
-      pend = h[kLitPend];
-      hlg = h[kHufLog];
+      nbh = h[kNb];
+      uint32_t pd = 0, lg = 0;
+#pragma unroll
+      for (uint32_t b = 0; b < B; ++b) {
+        const uint32_t pb = h[blk_at(b) + kLitPend], lb = h[blk_at(b) + kHufLog];
+        const bool in = b < nbh && pb == 1u;
+        pd |= in ? 1u : 0u;
+        lg = in ? lb : lg;
+      }
+      pend = pd;
+      hlg = lg;
     }
   }
-  const uint64_t tm = ballot(lits_pending(p0) && pend == 1u);
+  const uint64_t tm = ballot(lits_pending(p0) && pend == 1u && (B == 1 ? nbh == 1u : nbh >= 2u));
   for (uint64_t m = tm; m; m &= m - 1) {
     const uint32_t l = (uint32_t)__builtin_ctzll(m);
-    const uint32_t il = blockIdx.x * S + l;
+    const uint32_t il = readlane(il0, l);
     const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
     const uint32_t nw = (1u << (readlane(hlg, l) & 0xFFu)) / 2;
     uint32_t wv[kHufWords / kWave];
@@ -457,10 +477,14 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     }
   }
   lds_order();
-  const uint32_t l = lane >> 2, j = lane & 3u;
-  const uint32_t i = blockIdx.x * S + l;
-  if (l >= S || i >= nseg || !((tm >> l) & 1u)) return;
-  const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
+  const uint32_t l = lane / (4 * B), bk = (lane >> 2) % B, j = lane & 3u;
+  // (fetched while every lane is active: a disabled source lane reads as 0)
+  const uint32_t i = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l < S ? l : 0u) << 2), (int)il0);
+  if (l >= S || blockIdx.x * S + l >= nseg || !((tm >> l) & 1u)) return;
+  const GMEM uint32_t* h0 = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
+  if (bk >= h0[kNb]) return;
+  const GMEM uint32_t* h = h0 + blk_at(bk);
+  if (h[kLitPend] != 1u) return;  // (this block's literals are raw / RLE)
   const uint32_t hl = h[kHufLog], log = hl & 0xFFu, ns = hl >> 8;
   if (j >= ns) return;
   const uint32_t regen = h[kRegen], qq = h[kQQ];
@@ -468,8 +492,10 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
   const uint32_t start = h[kStreams] + (j >= 1 ? s1 : 0u) + (j >= 2 ? s2 : 0u) + (j >= 3 ? s3 : 0u);
   const uint32_t len = j == 0 ? s1 : j == 1 ? s2 : j == 2 ? s3 : s4;
   const uint32_t n = ns == 1 ? regen : j < 3 ? qq : regen - 3 * qq;
+  // the block's literals: [cap - kLitAll + kXLit, + regen) of the slot
+  const uint32_t lat = (seg - h0[kLitAll]) + h0[kX0 + kXW * bk + kXLit];
   const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
-  GMEM uint8_t* dst = global_ptr(out + (uint64_t)i * seg + (seg - regen) + j * qq);
+  GMEM uint8_t* dst = global_ptr(out + (uint64_t)i * seg + lat + j * qq);
   const uint8_t* t = reinterpret_cast<const uint8_t*>(tab[l]);
   const uint8_t* tl = len8[l];
   bool ok = len > 0;
@@ -566,6 +592,11 @@ __global__ __launch_bounds__(64) void zstd_handoff_kernel(
   const uint32_t i = blockIdx.x * L + lane;
   if (lane >= L || i >= nseg || produced[i] != kHanded) return;
   const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kHandStride));
+  if (h[zhand::kNb] != 1u) {  // (multi-block hand-offs belong to zstd_seqdec_kernel, which
+    produced[i] = 0xFFFFFFFFu;  // takes or rejects every one: defensive)
+    atomicOr(err, 1u);
+    return;
+  }
   const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
   GMEM uint8_t* dst = global_ptr(out + (uint64_t)i * seg);
   const uint32_t cs = csizes[i];
@@ -584,7 +615,8 @@ __global__ __launch_bounds__(64) void zstd_handoff_kernel(
   // part of it
   const GMEM uint8_t* tail = dst + (cap - regen);
   uint32_t lp = 0;
-  auto limit = [&]() __attribute__((always_inline)) { return lt == 2 ? cap - (regen - lp) : capw; };
+  // (lt 2 and 3 -- a Treeless block reuses the previous block's code -- are both Huffman)
+  auto limit = [&]() __attribute__((always_inline)) { return lt >= 2 ? cap - (regen - lp) : capw; };
   auto lits = [&](uint32_t n) __attribute__((always_inline)) {
     if (n == 0) return;
     if (lt == 0) {
@@ -690,7 +722,7 @@ __global__ __launch_bounds__(64) void zstd_handoff_kernel(
   if (ok && (uint64_t)op + (regen - lp) > cap) ok = false;
   if (ok) {
     const uint32_t n = regen - lp;
-    if (lt == 2) {  // the tail literals may overlap their destination: forward, 8 B only
+    if (lt >= 2) {  // the tail literals may overlap their destination: forward, 8 B only
                     // where the gap allows
       const uint32_t gap = (cap - (regen - lp)) - op;
       if (gap >= 8) {
@@ -723,15 +755,16 @@ template __global__ void zstd_handoff_kernel<4>(const uint8_t* const*, const uin
 template __global__ void zstd_handoff_kernel<8>(const uint8_t* const*, const uint8_t*, uint64_t,
                                                  const uint32_t*, uint32_t, uint32_t, uint8_t*,
                                                  uint32_t*, const uint8_t*, uint32_t*);
-template __global__ void zstd_hlit_kernel<4>(const uint8_t* const*, const uint8_t*, uint64_t,
-                                            const uint32_t*, uint32_t, uint32_t, uint8_t*,
-                                            uint32_t*, const uint8_t*, uint32_t*);
-template __global__ void zstd_hlit_kernel<8>(const uint8_t* const*, const uint8_t*, uint64_t,
-                                            const uint32_t*, uint32_t, uint32_t, uint8_t*,
-                                            uint32_t*, const uint8_t*, uint32_t*);
-template __global__ void zstd_hlit_kernel<16>(const uint8_t* const*, const uint8_t*, uint64_t,
-                                             const uint32_t*, uint32_t, uint32_t, uint8_t*,
-                                             uint32_t*, const uint8_t*, uint32_t*);
+#define BITAR_HLIT_INST(S, B)                                                                  \
+  template __global__ void zstd_hlit_kernel<S, B>(const uint8_t* const*, const uint8_t*, uint64_t, \
+                                                  const uint32_t*, uint32_t, uint32_t, uint8_t*,  \
+                                                  uint32_t*, const uint8_t*, uint32_t*,           \
+                                                  const uint32_t*);
+BITAR_HLIT_INST(4, 1)
+BITAR_HLIT_INST(8, 1)
+BITAR_HLIT_INST(16, 1)
+BITAR_HLIT_INST(4, 4)
+#undef BITAR_HLIT_INST
 
 template __global__ void zstd_lanes_kernel<64>(const uint8_t* const*, const uint8_t*, uint64_t,
                                                const uint32_t*, uint32_t, uint32_t, uint8_t*,

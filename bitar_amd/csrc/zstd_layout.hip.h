@@ -13,16 +13,42 @@ __host__ __device__ constexpr uint64_t scratch_stride(uint32_t seg) {
   return (lit_cap(seg) + 8ull * (seg / 4u + 2u) + 255u) & ~255ull;
 }
 
-// walk scratch (pass 2 -> zstd_walk_kernel -> zstd_emit_kernel), per segment: a 16-word record
-// (kW*), the FSE state tables (u16, kTabDummy + 1) and transforms (3 x 64 u32); then per
-// sequence its three codes (u32: LL | OF << 6 | ML << 11, written by pass 2) and each
-// chain's state bits | their count << 12 (u16, chains OF, ML, LL one array each); then per
-// step of 64 sequences the repeat-offset history before it (3 u32, written by pass 2), from
-// which zstd_emit_kernel re-derives the offset values of the step
-enum : uint32_t { kWHanded = 0, kWP0, kWBlk, kWN, kWNseq, kWAls, kWSt0, kWSt1, kWSt2 };
-constexpr uint32_t kWTabs = 64, kWTr = kWTabs + 2 * 1284, kWWords = kWTr + 3 * 64 * 4;
+// Blocks per frame (oracle ZS_MAX_BLOCKS / ZS_MULTI_MIN): a frame with >= kMultiMin sequences
+// is kBlocks compressed blocks of equal sequence counts, sharing one literal code and one set
+// of sequence tables; block b holds sequences [b nseq / B, (b + 1) nseq / B).
+constexpr uint32_t kBlocks = 4, kMultiMin = 64;
+
+// walk scratch (zstd_entropy_kernel -> zstd_walk_kernel -> zstd_emit_kernel), per segment: a
+// record of kW* words; the Huffman codes (256 u32: code | length << 16); the FSE state tables
+// (u16, kTabDummy + 1) and transforms (3 x 64 u32); then per sequence its three codes (u32:
+// LL | OF << 6 | ML << 11, written by the entropy kernel) and each chain's state bits | their
+// count << 12 (u16, chains OF, ML, LL one array each); then per step of up to 64 sequences
+// (steps start at each block's first sequence) the repeat-offset history before it (3 u32),
+// from which zstd_emit_kernel re-derives the offset values of the step
+enum : uint32_t {
+  kWHanded = 0,  // 1: the emit kernel writes this segment's frame
+  kWN = 3,       // segment bytes
+  kWNseq,        // sequences
+  kWAls,         // accuracy logs LL | OF << 8 | ML << 16
+  kWNb = 9,      // blocks
+  kWLit,         // literal code: mode (0 raw, 1 RLE, 2 Huffman) | RLE byte << 8 | tree bytes << 16
+  kWNlit,        // literal bytes
+  kWTdesc,       // bytes of the modes byte + table descriptions (kWDescAt)
+  kWSb = 16,     // kBlocks + 1 words: first sequence of each block (then nseq)
+  kWLb = 21,     // kBlocks + 1 words: first literal of each block (then nlit)
+  kWStep = 26,   // kBlocks words: first history step of each block
+  kWFin = 32,    // kBlocks x 3 words: each block's final states (OF, ML, LL)
+  kWTreeAt = 48,  // the Huffman tree description (<= 130 bytes)
+  kWDescAt = 84,  // modes byte + sequence table descriptions (<= 256 bytes)
+  kWCodeAt = 160  // 256 words: literal codes
+};
+constexpr uint32_t kWTabs = 4 * 416, kWTr = kWTabs + 2 * 1284, kWWords = kWTr + 3 * 64 * 4;
+static_assert(kWCodeAt + 256 <= kWTabs / 4, "record words before the tables");
+static_assert(kWTabs % 16 == 0 && kWWords % 8 == 0, "aligned areas");
 __host__ __device__ constexpr uint32_t walk_cap(uint32_t seg) { return seg / 4u + 2u; }  // >= nseq
-__host__ __device__ constexpr uint32_t walk_steps(uint32_t seg) { return (walk_cap(seg) + 63u) / 64u; }
+__host__ __device__ constexpr uint32_t walk_steps(uint32_t seg) {
+  return (walk_cap(seg) + 63u) / 64u + kBlocks;  // (a block's steps start at its first sequence)
+}
 __host__ __device__ constexpr uint64_t walk_hist_at(uint32_t seg) {  // bytes, from the record (16-B aligned)
   return ((uint64_t)kWWords + 10ull * walk_cap(seg) + 15u) & ~15ull;
 }

@@ -21,11 +21,16 @@
 // written once, by a coalesced store.
 //
 // Records: u64 = L | M << 22 | off << 44, L / M = literal-length / match-length code << 16 |
-// its extra bits (the baseline is added by the executor), off <= 2^20 - 1 (saturated: a
-// segment <= 64 KiB has offsets <= 65536).
+// its extra bits (the baseline is added by the executor), off a 20-bit offset: an absolute
+// one <= 2^19 - 1 (saturated: a segment <= 64 KiB has offsets <= 65536), or -- blocks after
+// the first of a multi-block hand-off, whose chains run before the history at their start is
+// known -- a symbolic one, kSym | k << 17 | (2^17 - 1 - d) = "history slot k at the block's
+// start, minus d" (the repeat offset r0 - 1 of RFC 8878 3.1.2.5 is then the same subtraction
+// for both forms); zstd_exec_kernel resolves them block by block.
 #include "lane_copy.hip.h"
 #include "stream_ring.hip.h"
 #include "zstd_hand.hip.h"
+#include "order.hip.h"
 
 namespace bitar_hip {
 
@@ -34,6 +39,15 @@ namespace zsq {
 using namespace zhand;
 
 constexpr uint32_t kTab = 1280;          // cells per segment: LL 512 | OF 256 | ML 512
+constexpr uint32_t kSym = 0x80000u, kAbsMax = 0x7FFFFu;  // symbolic offsets, see above
+__device__ __forceinline__ uint32_t sym_slot(uint32_t k) { return kSym | (k << 17) | 0x1FFFFu; }
+// an offset field (record or history word) against the history r at the block's start:
+// absolute, or slot k minus d; 0 (invalid) for slot 3 or a negative result
+__device__ __forceinline__ uint32_t resolve_off(uint32_t v, uint32_t r0, uint32_t r1, uint32_t r2) {
+  const uint32_t k = (v >> 17) & 3u, d = 0x1FFFFu - (v & 0x1FFFFu);
+  const uint32_t base = k == 0 ? r0 : k == 1 ? r1 : k == 2 ? r2 : 0u;
+  return (v & kSym) ? (base > d ? base - d : 0u) : v;
+}
 constexpr uint32_t kOfAt = 512, kMlAt = 768;
 
 // Literal-length / match-length code -> baseline and extra-bit count (RFC 8878
@@ -127,37 +141,53 @@ __device__ __forceinline__ Step step_of(uint32_t cell, uint32_t al) {
 }  // namespace zsq
 
 // ---- phase A -----------------------------------------------------------------------------
-// L segments per wave (lane l < L owns segment blockIdx.x * L + l).  A segment is taken when
-// the wave decoder handed it over (produced == kHanded) and it has at most `rcap` sequences;
-// on success (the bitstream consumed exactly) produced = kRecs, else SEGMENT_ERROR and the
-// stream's error word; the sequence rules are checked by zstd_exec_kernel.  Others stay kHanded for zstd_handoff_kernel.
-template <uint32_t L>
+// L segments per wave (lane l < L owns segment blockIdx.x * L + l), B chains (blocks) per
+// segment: B = 1 takes the frames that handed their last block only (kNb == 1), B = 4 the
+// multi-block hand-offs (kNb >= 2), whose blocks' chains run side by side.  A segment is
+// taken when the wave decoder handed it over (produced == kHanded) and it has at most `rcap`
+// sequences; on success (every chain's bitstream consumed exactly) produced = kRecs, else
+// SEGMENT_ERROR and the stream's error word; the sequence rules are checked by
+// zstd_exec_kernel.  Single-block segments beyond rcap stay kHanded for zstd_handoff_kernel
+// (a multi-block one beyond rcap cannot be valid: rejected here).
+template <uint32_t L, uint32_t B = 1>
 __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint32_t* __restrict__ produced, uint8_t* __restrict__ hscr, uint64_t* __restrict__ recs,
-    uint32_t rcap, uint32_t* __restrict__ err, unsigned long long* __restrict__ stats) {
+    uint32_t rcap, uint32_t* __restrict__ err, unsigned long long* __restrict__ stats,
+    const uint32_t* __restrict__ order) {
   using namespace zsq;
   using lanes::ld8;
+  static_assert(L * B * 4 <= kWave, "a quad per chain");
   __shared__ __attribute__((aligned(16))) uint16_t cel[L * kTab];
   const uint32_t lane = lane_id();
   // stage the decode tables of the wave's segments, 4 cells per lane per step.  The headers
   // are loaded one lane per segment, together, and a segment's table loads are all issued
   // before the first is used: at about one wave per SIMD every serial load is exposed.
-  uint32_t p0 = 0, nq0 = 0, als0 = 0;
+  // (order: the segments by sequence count, most first, hand_key_kernel: slot x takes
+  // segment order[x], so a wave's chains are of similar length and the longest start first)
+  uint32_t p0 = 0, nq0 = 0, als0 = 0, nb0 = 0, il0 = 0;
   {
-    const uint32_t il = blockIdx.x * L + lane;
+    const uint32_t bl = blockIdx.x * L + lane;
+    const uint32_t il = bl < nseg ? (order ? order[bl] : bl) : bl;
+    il0 = il;
     if (lane < L && il < nseg) {
       const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
       p0 = produced[il];
-      nq0 = h[kNseq];
+      nq0 = h[kNseqAll];
       als0 = h[kAls];
+      nb0 = h[kNb];
     }
   }
-  const uint64_t tm = ballot(p0 == kHanded && nq0 <= rcap);
+  const bool mine = p0 == kHanded && (B == 1 ? nb0 == 1u : nb0 >= 2u);
+  if (B > 1 && lane < L && mine && nq0 > rcap) {  // (more sequences than a valid frame has)
+    produced[il0] = 0xFFFFFFFFu;
+    atomicOr(err, 1u);
+  }
+  const uint64_t tm = ballot(mine && nq0 <= rcap);
   for (uint64_t mm = tm; mm; mm &= mm - 1) {
     const uint32_t l = (uint32_t)__builtin_ctzll(mm);
-    const uint32_t il = blockIdx.x * L + l;
+    const uint32_t il = readlane(il0, l);
     const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
     const uint32_t als = readlane(als0, l);
     constexpr uint32_t kPer = (kCells / 4 + kWave - 1) / kWave;  // uint4 loads per lane per table
@@ -198,16 +228,21 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
   // extracts its two fields, and the quad exchanges the three values; the bit reader,
   // repeat offsets and records are replicated over the quad.  One wave instruction thus
   // advances all three FSE chains of 16 segments.
-  const uint32_t l = lane >> 2, j = lane & 3u;
-  const uint32_t i = blockIdx.x * L + l;
-  if (l >= L || i >= nseg || !((tm >> l) & 1u)) return;  // quad-uniform
-  GMEM uint32_t* h = global_ptr(reinterpret_cast<uint32_t*>(hscr + (uint64_t)i * kStride));
+  const uint32_t l = lane / (4 * B), bk = (lane >> 2) % B, j = lane & 3u;
+  // (fetched while every lane is active: a disabled source lane reads as 0)
+  const uint32_t i = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l < L ? l : 0u) << 2), (int)il0);
+  if (l >= L || blockIdx.x * L + l >= nseg || !((tm >> l) & 1u)) return;  // quad-uniform
+  GMEM uint32_t* h0 = global_ptr(reinterpret_cast<uint32_t*>(hscr + (uint64_t)i * kStride));
+  if (bk >= h0[kNb]) return;
+  const GMEM uint32_t* h = h0 + blk_at(bk);
   const uint32_t nseq = h[kNseq];
   const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
-  GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap);
+  GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap + h0[kX0 + kXW * bk + kXRec]);
   const uint32_t cs = csizes[i];
   const uint32_t q = h[kQ], end = h[kEnd], w3 = h[kAls];
-  uint32_t r0 = h[kRep0], r1 = h[kRep1], r2 = h[kRep2];
+  // the history at the block's start: known for the first, symbolic for the others
+  uint32_t r0 = bk ? sym_slot(0) : h0[kRep0], r1 = bk ? sym_slot(1) : h0[kRep1],
+           r2 = bk ? sym_slot(2) : h0[kRep2];
   const uint32_t al0 = w3 & 0xFFu, al1 = (w3 >> 8) & 0xFFu;
   const uint32_t t = j == 1 ? 2u : j == 2 ? 1u : 0u;  // table in the frame's LL, OF, ML order
   const uint32_t al = (w3 >> (8 * t)) & 0xFFu;
@@ -242,7 +277,8 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
     return (uint32_t)(C >> ((64u - p - n) & 63u)) & ((1u << n) - 1u);
   };
   const uint32_t lastb = (uint32_t)(C >> 56);
-  bool ok = (lastb != 0 || nseq == 0) && end == cs;
+  // (a multi-block hand-off ends at the frame's end: zstd_decompress_kernel checked it)
+  bool ok = (lastb != 0 || nseq == 0) && (B > 1 || end == cs);
   if (nseq == 0) {
     ok = ok && q == end;  // no sequences: no bitstream
   } else if (ok) {
@@ -280,16 +316,17 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
       // repeat offsets in select form (no exec-mask branches); literal length 0 = LL code 0
       // (which has no extra bits)
       const uint32_t idx = ofv + (lf == 0 ? 1u : 0u);
+      // (a new offset saturates below kSym: a valid one is <= 65536)
+      const uint32_t onew = ofv - 3 < kAbsMax ? ofv - 3 : kAbsMax;
       const uint32_t off =
-          sel(ofv > 3, ofv - 3, sel(idx == 1, r0, sel(idx == 2, r1, sel(idx == 3, r2, r0 - 1))));
+          sel(ofv > 3, onew, sel(idx == 1, r0, sel(idx == 2, r1, sel(idx == 3, r2, r0 - 1))));
       const bool shift2 = ofv > 3 || idx >= 3, shift1 = ofv > 3 || idx >= 2;
       const uint32_t c0 = r0, c1 = r1, c2 = r2;
       r2 = sel(shift2, c1, c2);
       r1 = sel(shift1, c0, c1);
       r0 = off;
-      // (an offset past 2^20 - 1 is out of range anyway: saturated, zstd_exec_kernel rejects)
-      const uint32_t os = off < 0xFFFFFu ? off : 0xFFFFFu;
-      return (uint64_t)lf | ((uint64_t)mf << 22) | ((uint64_t)os << 44);
+      // (r0 - 1 of an absolute 0 wraps: its low 20 bits read as slot 3, which resolves to 0)
+      return (uint64_t)lf | ((uint64_t)mf << 22) | ((uint64_t)(off & 0xFFFFFu) << 44);
     };
     // Groups of kG sequences: the records stay in registers and lane 0 of the quad stores
     // them at the group's end (the compiler waits for every outstanding store at the next
@@ -319,15 +356,22 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
   }
   if (j == 0) {
     if (ok) {
-      // (zstd_hlit_kernel may run alongside and mark the segment failed first)
+      // the history after the block (zstd_exec_kernel resolves the next block's offsets)
+      h0[kX0 + kXW * bk + kXFin0] = r0 & 0xFFFFFu;
+      h0[kX0 + kXW * bk + kXFin1] = r1 & 0xFFFFFu;
+      h0[kX0 + kXW * bk + kXFin2] = r2 & 0xFFFFFu;
+      // (zstd_hlit_kernel, or the segment's other chains, may mark the segment failed first:
+      // a failure overwrites kRecs and is never overwritten)
       atomicCAS(&produced[i], kHanded, kRecs);
-    } else {
-      produced[i] = 0xFFFFFFFFu;
+    }
+    uint32_t was = 0xFFFFFFFFu;
+    if (!ok) {
+      was = atomicExch(&produced[i], 0xFFFFFFFFu);
       atomicOr(err, 1u);
     }
-    if (stats) {
-      atomicAdd(stats + BITAR_HIP_PATH_ZSTD_SEQDEC, 1ull);
-      if (!ok) atomicAdd(stats + BITAR_HIP_PATH_ZSTD_SEQDEC_REJECT, 1ull);
+    if (stats) {  // (per segment: its first block's chain counts it, its first failure rejects it)
+      if (bk == 0) atomicAdd(stats + BITAR_HIP_PATH_ZSTD_SEQDEC, 1ull);
+      if (!ok && was != 0xFFFFFFFFu) atomicAdd(stats + BITAR_HIP_PATH_ZSTD_SEQDEC_REJECT, 1ull);
     }
   }
 }
@@ -358,10 +402,8 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   if (i >= nseg || uniform(produced[i]) != kRecs) return;
   const uint32_t lane = lane_id();
   const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
-  const uint32_t nseq = uniform(h[kNseq]), w3 = uniform(h[kAls]), litv = uniform(h[kLitV]);
-  const uint32_t regen = uniform(h[kRegen]), op0 = uniform(h[kOp]);
+  const uint32_t nbk = uniform(h[kNb]), lall = uniform(h[kLitAll]), op0 = uniform(h[kOp]);
   const uint32_t fsz = uniform(h[kFsz]), fcs = uniform(h[kFcs]);
-  const uint32_t lt = w3 >> 24;
   const uint32_t cap = seg;
   State s;
   s.dst = global_ptr(out + (uint64_t)i * seg);
@@ -370,15 +412,16 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   s.flushed = op0;
   s.fenced = op0;  // out[0, op0) was written by an earlier launch
   const GMEM uint8_t* src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
-  // literal index j -> byte: lsrc[j] (raw / Huffman) or the RLE byte
-  const GMEM uint8_t* lsrc = lt == 0 ? src + litv : s.dst + (cap - regen);
-  const uint32_t lbyte = litv & 0xFFu;
-  // (a literal-less segment's lsrc may lie past the buffer: index 0 of the output instead)
-  const GMEM uint8_t* lsafe = regen ? lsrc : s.dst;
+  // Huffman literals: the slot tail [cap - lall, cap), block b's at its kXLit
+  const GMEM uint8_t* tail = s.dst + (cap - lall);
   const uintptr_t base = (uintptr_t)s.dst;
-  const GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap);
-  uint32_t lp = 0;
+  // the history at the current block's start (block 0: the wave decoder's)
+  uint32_t R0 = uniform(h[kRep0]), R1 = uniform(h[kRep1]), R2 = uniform(h[kRep2]);
+  uint32_t lbase = 0;  // literals of the earlier blocks (for the room check)
   bool ok = true;
+  // per block: literal index j -> byte: lsrc[j] (raw / Huffman) or the RLE byte
+  uint32_t lt = 0, lbyte = 0;
+  const GMEM uint8_t* lsafe = s.dst;
   // one 64-byte step at output [xa, xa + 64) ∩ [.., xa + act): e = the run each lane lies in
   // (key << 24 | payload: odd key = literals, payload = output pos - literal index; even key
   // = match, payload = offset)
@@ -424,57 +467,83 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
     ring[act ? (uint32_t)((base + x) & kRingMask) : kRing + lane] = (uint8_t)v;
     lds_order();
   };
-  for (uint32_t kb = 0; kb < nseq; kb += kWave) {
-    const uint32_t n = nseq - kb < kWave ? nseq - kb : kWave;
-    const uint64_t r0 = rec[kb + (lane < n ? lane : n - 1)];
-    const uint64_t r = lane < n ? r0 : 0ull;
-    const uint32_t lf = (uint32_t)r & 0x3FFFFFu, mf = (uint32_t)(r >> 22) & 0x3FFFFFu;
-    uint32_t lb, lx, mb, mx;
-    ll_code(lf >> 16, lb, lx);
-    ml_code(mf >> 16, mb, mx);
-    const uint32_t ll = lb + (lf & 0xFFFFu), ml = lane < n ? mb + (mf & 0xFFFFu) : 0u,
-                   off = (uint32_t)(r >> 44);
-    const uint32_t inc = wave_incl_sum(ll + ml), ex = inc - (ll + ml);
-    const uint32_t linc = wave_incl_sum(ll), lex = linc - ll;
-    const uint32_t T = readlane(inc, kWave - 1), LT = readlane(linc, kWave - 1);
-    {
-      const uint32_t lpk = lp + lex, opk = s.op + ex;  // before sequence k
-      const bool bad = (lpk + ll > regen) | (opk + ml + (regen - lpk) > cap) | (off == 0) |
-                       (off > opk + ll);
-      if (ballot(lane < n && bad)) {
-        ok = false;
-        break;
+  for (uint32_t bk = 0; bk < nbk && ok; ++bk) {
+    const GMEM uint32_t* hb = h + blk_at(bk);
+    const uint32_t nseq = uniform(hb[kNseq]), w3 = uniform(hb[kAls]), litv = uniform(hb[kLitV]);
+    const uint32_t regen = uniform(hb[kRegen]);
+    const uint32_t xrec = uniform(h[kX0 + kXW * bk + kXRec]), xlit = uniform(h[kX0 + kXW * bk + kXLit]);
+    lt = w3 >> 24;
+    lbyte = litv & 0xFFu;
+    const GMEM uint8_t* lsrc = lt == 0 ? src + litv : tail + xlit;
+    // (a literal-less block's lsrc may lie past the buffer: index 0 of the output instead)
+    lsafe = regen ? lsrc : s.dst;
+    const GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap + xrec);
+    uint32_t lp = 0;
+    for (uint32_t kb = 0; kb < nseq; kb += kWave) {
+      const uint32_t n = nseq - kb < kWave ? nseq - kb : kWave;
+      const uint64_t r0 = rec[kb + (lane < n ? lane : n - 1)];
+      const uint64_t r = lane < n ? r0 : 0ull;
+      const uint32_t lf = (uint32_t)r & 0x3FFFFFu, mf = (uint32_t)(r >> 22) & 0x3FFFFFu;
+      uint32_t lb, lx, mb, mx;
+      ll_code(lf >> 16, lb, lx);
+      ml_code(mf >> 16, mb, mx);
+      const uint32_t ll = lb + (lf & 0xFFFFu), ml = lane < n ? mb + (mf & 0xFFFFu) : 0u;
+      // (blocks after the first: offsets relative to the history at the block's start)
+      const uint32_t off = resolve_off((uint32_t)(r >> 44), R0, R1, R2);
+      const uint32_t inc = wave_incl_sum(ll + ml), ex = inc - (ll + ml);
+      const uint32_t linc = wave_incl_sum(ll), lex = linc - ll;
+      const uint32_t T = readlane(inc, kWave - 1), LT = readlane(linc, kWave - 1);
+      {
+        const uint32_t lpk = lp + lex, opk = s.op + ex;  // before sequence k
+        // (room: the output of the match and every unread literal of this and later blocks,
+        // which the slot tail holds)
+        const bool bad = (lpk + ll > regen) | (opk + ml + (lall - lbase - lpk) > cap) |
+                         (off == 0) | (off > opk + ll);
+        if (ballot(lane < n && bad)) {
+          ok = false;
+          break;
+        }
       }
+      const uint32_t e_lit = ((2u * lane + 1u) << 24) | ((s.op + ex) - (lp + lex));
+      const uint32_t e_mat = ((2u * lane + 2u) << 24) | off;
+      uint32_t carry = 0;
+      for (uint32_t cb = 0; cb < T; cb += kWave) {
+        const uint32_t xa = s.op + cb;
+        if (xa + kWave - s.flushed > kFlushAt) flush(s, ring, xa, false);
+        lds_order();
+        ev[lane] = 0u;
+        lds_order();
+        const uint32_t p1 = ex - cb, p2 = ex + ll - cb;
+        ev[lane < n && ll && p1 < kWave ? p1 : kWave + lane] = e_lit;
+        ev[lane < n && p2 < kWave ? p2 : kWave + lane] = e_mat;
+        lds_order();
+        uint32_t e = ev[lane];
+        e = wave_incl_max(e > carry ? e : carry);
+        carry = readlane(e, kWave - 1);
+        chunk(xa, T - cb < kWave ? T - cb : kWave, e);
+      }
+      s.op += T;
+      lp += LT;
     }
-    const uint32_t e_lit = ((2u * lane + 1u) << 24) | ((s.op + ex) - (lp + lex));
-    const uint32_t e_mat = ((2u * lane + 2u) << 24) | off;
-    uint32_t carry = 0;
-    for (uint32_t cb = 0; cb < T; cb += kWave) {
+    // the literals after the block's last sequence
+    const uint32_t rest = ok ? regen - lp : 0u;
+    if (ok && (uint64_t)s.op + (lall - lbase - lp) > cap) ok = false;
+    for (uint32_t cb = 0; ok && cb < rest; cb += kWave) {
       const uint32_t xa = s.op + cb;
       if (xa + kWave - s.flushed > kFlushAt) flush(s, ring, xa, false);
-      lds_order();
-      ev[lane] = 0u;
-      lds_order();
-      const uint32_t p1 = ex - cb, p2 = ex + ll - cb;
-      ev[lane < n && ll && p1 < kWave ? p1 : kWave + lane] = e_lit;
-      ev[lane < n && p2 < kWave ? p2 : kWave + lane] = e_mat;
-      lds_order();
-      uint32_t e = ev[lane];
-      e = wave_incl_max(e > carry ? e : carry);
-      carry = readlane(e, kWave - 1);
-      chunk(xa, T - cb < kWave ? T - cb : kWave, e);
+      chunk(xa, rest - cb < kWave ? rest - cb : kWave, (1u << 24) | (s.op - lp));
     }
-    s.op += T;
-    lp += LT;
+    if (ok) s.op += rest;
+    lbase += regen;
+    // the history at the next block's start
+    const uint32_t f0 = uniform(h[kX0 + kXW * bk + kXFin0]), f1 = uniform(h[kX0 + kXW * bk + kXFin1]),
+                   f2 = uniform(h[kX0 + kXW * bk + kXFin2]);
+    const uint32_t n0 = resolve_off(f0, R0, R1, R2), n1 = resolve_off(f1, R0, R1, R2),
+                   n2 = resolve_off(f2, R0, R1, R2);
+    R0 = n0;
+    R1 = n1;
+    R2 = n2;
   }
-  // the literals after the last sequence
-  const uint32_t rest = ok ? regen - lp : 0u;
-  for (uint32_t cb = 0; cb < rest; cb += kWave) {
-    const uint32_t xa = s.op + cb;
-    if (xa + kWave - s.flushed > kFlushAt) flush(s, ring, xa, false);
-    chunk(xa, rest - cb < kWave ? rest - cb : kWave, (1u << 24) | (s.op - lp));
-  }
-  s.op += rest;
   flush(s, ring, s.op, true);
   ok = ok && (!fsz || fcs == s.op);
   if (lane == 0) {
@@ -491,14 +560,34 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   }
 }
 
-template __global__ void zstd_seqdec_kernel<16>(const uint8_t* const*, const uint8_t*, uint64_t,
-                                                const uint32_t*, uint32_t, uint32_t, uint32_t*,
-                                                uint8_t*, uint64_t*, uint32_t, uint32_t*, unsigned long long*);
-template __global__ void zstd_seqdec_kernel<4>(const uint8_t* const*, const uint8_t*, uint64_t,
-                                               const uint32_t*, uint32_t, uint32_t, uint32_t*,
-                                               uint8_t*, uint64_t*, uint32_t, uint32_t*, unsigned long long*);
-template __global__ void zstd_seqdec_kernel<8>(const uint8_t* const*, const uint8_t*, uint64_t,
-                                               const uint32_t*, uint32_t, uint32_t, uint32_t*,
-                                               uint8_t*, uint64_t*, uint32_t, uint32_t*, unsigned long long*);
+// Dispatch keys of the multi-block lane kernels (order.hip.h: lower keys first): which = 0
+// the segment's sequences (zstd_seqdec_kernel<4, 4>'s chains), 1 its literals
+// (zstd_hlit_kernel<4, 4>'s streams); segments they do not take sort last.
+__global__ __launch_bounds__(64) void hand_key_kernel(const uint32_t* __restrict__ produced,
+                                                      const uint8_t* __restrict__ hscr,
+                                                      uint32_t nseg, uint32_t which,
+                                                      uint32_t* __restrict__ keys) {
+  using namespace zhand;
+  const uint32_t i = blockIdx.x * kWave + lane_id();
+  if (i >= nseg) return;
+  uint32_t c = 0;
+  if (produced[i] == kHanded) {
+    const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
+    if (h[kNb] >= 2u) c = 1u + (which ? h[kLitAll] >> 8 : h[kNseqAll] >> 7);
+  }
+  keys[i] = kOrderBins - 1u - (c < kOrderBins - 1u ? c : kOrderBins - 1u);
+}
+
+#define BITAR_SEQDEC_INST(L, B)                                                              \
+  template __global__ void zstd_seqdec_kernel<L, B>(const uint8_t* const*, const uint8_t*,     \
+                                                    uint64_t, const uint32_t*, uint32_t,       \
+                                                    uint32_t, uint32_t*, uint8_t*, uint64_t*,  \
+                                                    uint32_t, uint32_t*, unsigned long long*,  \
+                                                    const uint32_t*);
+BITAR_SEQDEC_INST(16, 1)
+BITAR_SEQDEC_INST(8, 1)
+BITAR_SEQDEC_INST(4, 1)
+BITAR_SEQDEC_INST(4, 4)
+#undef BITAR_SEQDEC_INST
 
 }  // namespace bitar_hip

@@ -901,102 +901,129 @@ static uint32_t zs_weights_fse(const uint8_t* w, uint32_t nw, uint8_t* out) {
   return bw.pos + 1;
 }
 
-/* literals section of lit[0..n) into d; returns its size */
-static uint32_t zs_literals(const uint8_t* lit, uint32_t n, uint8_t* d, uint32_t cap, int* err) {
-  uint32_t hist[256] = {0}, distinct = 0, hsz;
+/* The literal code of a frame: built once from all of the segment's literals and shared by
+ * its blocks (the first Huffman-coded block carries the tree, later ones are Treeless). */
+typedef struct {
+  uint32_t mode;     /* 0 raw, 1 RLE (one distinct byte), 2 Huffman-capable */
+  uint8_t rle;
+  uint8_t len[256];
+  uint32_t code[256];
+  uint8_t desc[130];
+  uint32_t dsz;
+} zs_littab;
+
+static void zs_littab_build(const uint8_t* lit, uint32_t n, zs_littab* H) {
+  uint32_t hist[256] = {0}, distinct = 0;
   for (uint32_t i = 0; i < n; ++i)
     if (!hist[lit[i]]++) ++distinct;
-  if (n == 0 || distinct > 1) {
-    if (n > 0) {
-      /* ---- Huffman ---- */
-      uint8_t len[256];
-      bo_huff_lengths(hist, 256, 11, len);
-      uint32_t L = 0, max_sym = 0;
-      for (uint32_t s = 0; s < 256; ++s) {
-        if (len[s] > L) L = len[s];
-        if (len[s]) max_sym = s;
-      }
-      uint8_t w[256];
-      uint32_t rank_cnt[13] = {0};
-      for (uint32_t s = 0; s < 256; ++s) {
-        w[s] = len[s] ? (uint8_t)(L + 1 - len[s]) : 0;
-        if (len[s]) rank_cnt[w[s]]++;
-      }
-      /* codes: table index ranges by increasing weight, then symbol (HUF_readDTableX1) */
-      uint32_t start[13], next = 0, code[256];
-      for (uint32_t k = 1; k <= L; ++k) {
-        start[k] = next;
-        next += rank_cnt[k] << (k - 1);
-      }
-      for (uint32_t s = 0; s < 256; ++s) {
-        if (!len[s]) continue;
-        code[s] = start[w[s]] >> (w[s] - 1);
-        start[w[s]] += 1u << (w[s] - 1);
-      }
-      /* tree description */
-      uint8_t desc[130];
-      uint32_t dsz = 0;
-      const uint32_t nw = max_sym;
-      const uint32_t fsz = zs_weights_fse(w, nw, desc);
-      const uint32_t direct = nw <= 128 ? 1 + (nw + 1) / 2 : 0;
-      if (direct && (!fsz || direct <= fsz)) {
-        desc[0] = (uint8_t)(127 + nw);
-        for (uint32_t i = 0; i < nw; i += 2)
-          desc[1 + i / 2] = (uint8_t)((w[i] << 4) | (i + 1 < nw ? w[i + 1] : 0));
-        dsz = direct;
-      } else {
-        dsz = fsz;
-      }
-      if (dsz) {
-        const uint32_t ns = n < 256 ? 1 : 4, q = (n + 3) / 4;
-        uint32_t bytes[4] = {0}, total = dsz + (ns == 4 ? 6 : 0);
-        for (uint32_t k = 0; k < ns; ++k) {
-          const uint32_t a = ns == 1 ? 0 : k * q, b = ns == 1 ? n : (k == 3 ? n : (k + 1) * q);
-          uint64_t bits = 0;
-          for (uint32_t i = a; i < b; ++i) bits += len[lit[i]];
-          bytes[k] = (uint32_t)((bits + 1 + 7) / 8);
-          total += bytes[k];
-        }
-        const int32_t limit = (int32_t)n - (int32_t)((n >> 6) + 2);
-        if ((int32_t)total < limit) {
-          const uint32_t hs = ns == 1 || n < 1024 ? 3 : n < 16384 ? 4 : 5;
-          if (hs + total > cap) { *err = 1; return 0; }
-          const uint32_t sf = ns == 1 ? 0 : n < 1024 ? 1 : n < 16384 ? 2 : 3;
-          const uint64_t h = 2u | (sf << 2) |
-                             ((uint64_t)n << 4) | ((uint64_t)total << (hs == 3 ? 14 : hs == 4 ? 18 : 22));
-          for (uint32_t k = 0; k < hs; ++k) d[k] = (uint8_t)(h >> (8 * k));
-          uint32_t p = hs;
-          memcpy(d + p, desc, dsz);
-          p += dsz;
-          if (ns == 4) {
-            for (uint32_t k = 0; k < 3; ++k) {
-              d[p + 2 * k] = (uint8_t)bytes[k];
-              d[p + 2 * k + 1] = (uint8_t)(bytes[k] >> 8);
-            }
-            p += 6;
-          }
-          for (uint32_t k = 0; k < ns; ++k) {
-            const uint32_t a = ns == 1 ? 0 : k * q, b = ns == 1 ? n : (k == 3 ? n : (k + 1) * q);
-            zs_bw bw = {d, p, cap, 0, 0, 0};
-            for (uint32_t i = b; i-- > a;) zs_bw_add(&bw, code[lit[i]], len[lit[i]]);
-            zs_bw_close(&bw);
-            if (bw.err) { *err = 1; return 0; }
-            p = bw.pos;
-          }
-          return p;
-        }
-      }
-    }
-    /* ---- raw ---- */
-    zs_lit_header(d, 0, n, &hsz);
-    if (hsz + n > cap) { *err = 1; return 0; }
-    memcpy(d + hsz, lit, n);
-    return hsz + n;
+  H->mode = 0;
+  H->dsz = 0;
+  if (n == 0) return;
+  if (distinct == 1) {
+    H->mode = 1;
+    H->rle = lit[0];
+    return;
   }
-  /* ---- RLE ---- */
-  zs_lit_header(d, 1, n, &hsz);
-  d[hsz] = lit[0];
-  return hsz + 1;
+  /* ---- Huffman ---- */
+  bo_huff_lengths(hist, 256, 11, H->len);
+  uint32_t L = 0, max_sym = 0;
+  for (uint32_t s = 0; s < 256; ++s) {
+    if (H->len[s] > L) L = H->len[s];
+    if (H->len[s]) max_sym = s;
+  }
+  uint8_t w[256];
+  uint32_t rank_cnt[13] = {0};
+  for (uint32_t s = 0; s < 256; ++s) {
+    w[s] = H->len[s] ? (uint8_t)(L + 1 - H->len[s]) : 0;
+    if (H->len[s]) rank_cnt[w[s]]++;
+  }
+  /* codes: table index ranges by increasing weight, then symbol (HUF_readDTableX1) */
+  uint32_t start[13], next = 0;
+  for (uint32_t k = 1; k <= L; ++k) {
+    start[k] = next;
+    next += rank_cnt[k] << (k - 1);
+  }
+  for (uint32_t s = 0; s < 256; ++s) {
+    if (!H->len[s]) continue;
+    H->code[s] = start[w[s]] >> (w[s] - 1);
+    start[w[s]] += 1u << (w[s] - 1);
+  }
+  /* tree description: direct when possible and not larger than the FSE form */
+  const uint32_t nw = max_sym;
+  const uint32_t fsz = zs_weights_fse(w, nw, H->desc);
+  const uint32_t direct = nw <= 128 ? 1 + (nw + 1) / 2 : 0;
+  if (direct && (!fsz || direct <= fsz)) {
+    H->desc[0] = (uint8_t)(127 + nw);
+    for (uint32_t i = 0; i < nw; i += 2)
+      H->desc[1 + i / 2] = (uint8_t)((w[i] << 4) | (i + 1 < nw ? w[i + 1] : 0));
+    H->dsz = direct;
+  } else {
+    H->dsz = fsz;
+  }
+  if (H->dsz) H->mode = 2;
+}
+
+/* literals section of one block, lit[0..n), into d; returns its size.  Huffman when the
+ * block's section -- the tree included while *tree_sent is 0 -- is at least n/64 + 2 bytes
+ * smaller than n (then *tree_sent = 1; the block is Treeless when it already was 1); RLE for
+ * an RLE code and n > 0; raw otherwise.  With one block this is the single-block frame's
+ * rule exactly. */
+static uint32_t zs_literals_block(const uint8_t* lit, uint32_t n, const zs_littab* H,
+                                  int* tree_sent, uint8_t* d, uint32_t cap, int* err) {
+  uint32_t hsz;
+  if (H->mode == 1 && n > 0) {
+    if (cap < 4) { *err = 1; return 0; }
+    zs_lit_header(d, 1, n, &hsz);
+    d[hsz] = H->rle;
+    return hsz + 1;
+  }
+  if (H->mode == 2 && n > 0) {
+    const uint32_t ns = n < 256 ? 1 : 4, q = (n + 3) / 4;
+    const uint32_t dsz = *tree_sent ? 0u : H->dsz;
+    uint32_t bytes[4] = {0}, total = dsz + (ns == 4 ? 6 : 0);
+    for (uint32_t k = 0; k < ns; ++k) {
+      const uint32_t a = ns == 1 ? 0 : k * q, b = ns == 1 ? n : (k == 3 ? n : (k + 1) * q);
+      uint64_t bits = 0;
+      for (uint32_t i = a; i < b; ++i) bits += H->len[lit[i]];
+      bytes[k] = (uint32_t)((bits + 1 + 7) / 8);
+      total += bytes[k];
+    }
+    const int32_t limit = (int32_t)n - (int32_t)((n >> 6) + 2);
+    if ((int32_t)total < limit) {
+      const uint32_t hs = ns == 1 || n < 1024 ? 3 : n < 16384 ? 4 : 5;
+      if (hs + total > cap) { *err = 1; return 0; }
+      const uint32_t sf = ns == 1 ? 0 : n < 1024 ? 1 : n < 16384 ? 2 : 3;
+      const uint64_t type = *tree_sent ? 3u : 2u;  /* Treeless / Compressed_Literals */
+      const uint64_t h = type | (sf << 2) |
+                         ((uint64_t)n << 4) | ((uint64_t)total << (hs == 3 ? 14 : hs == 4 ? 18 : 22));
+      for (uint32_t k = 0; k < hs; ++k) d[k] = (uint8_t)(h >> (8 * k));
+      uint32_t p = hs;
+      memcpy(d + p, H->desc, dsz);
+      p += dsz;
+      if (ns == 4) {
+        for (uint32_t k = 0; k < 3; ++k) {
+          d[p + 2 * k] = (uint8_t)bytes[k];
+          d[p + 2 * k + 1] = (uint8_t)(bytes[k] >> 8);
+        }
+        p += 6;
+      }
+      for (uint32_t k = 0; k < ns; ++k) {
+        const uint32_t a = ns == 1 ? 0 : k * q, b = ns == 1 ? n : (k == 3 ? n : (k + 1) * q);
+        zs_bw bw = {d, p, cap, 0, 0, 0};
+        for (uint32_t i = b; i-- > a;) zs_bw_add(&bw, H->code[lit[i]], H->len[lit[i]]);
+        zs_bw_close(&bw);
+        if (bw.err) { *err = 1; return 0; }
+        p = bw.pos;
+      }
+      *tree_sent = 1;
+      return p;
+    }
+  }
+  /* ---- raw ---- */
+  zs_lit_header(d, 0, n, &hsz);
+  if (hsz + n > cap) { *err = 1; return 0; }
+  memcpy(d + hsz, lit, n);
+  return hsz + n;
 }
 
 /* ---- sequences section ---- */
@@ -1092,6 +1119,39 @@ uint32_t bo_zstd_bound(uint32_t n) {
   return n + 7 + 3 + 8 + 512;
 }
 
+/* Blocks of a frame (round 5): a frame with >= ZS_MULTI_MIN sequences is written as
+ * ZS_BLOCKS compressed blocks of equal sequence counts -- block b takes sequences
+ * [b nseq / B, (b + 1) nseq / B) and their literals, the last one the trailing literals too.
+ * The blocks share one literal code (the first Huffman-coded block carries the tree, the
+ * others are Treeless) and one set of sequence tables (described in the first block,
+ * Repeat_Mode in the others); repeat offsets run on across blocks (RFC 8878 3.1.2.5).  Each
+ * block's FSE state chains start from its own last sequence, so a decoder walks the blocks'
+ * chains -- and decodes their literal streams -- in parallel.  bo_set_zstd_blocks(1) writes
+ * the single-block frames of rounds 1-4. */
+#define ZS_MAX_BLOCKS 4u
+#define ZS_MULTI_MIN 64u
+static uint32_t g_zstd_blocks = ZS_MAX_BLOCKS;
+uint32_t bo_set_zstd_blocks(uint32_t b) {
+  const uint32_t old = g_zstd_blocks;
+  g_zstd_blocks = b < 1 ? 1 : b > ZS_MAX_BLOCKS ? ZS_MAX_BLOCKS : b;
+  return old;
+}
+static uint32_t zs_nblocks(uint32_t nseq, int drop) {
+  return (!drop && nseq >= ZS_MULTI_MIN) ? g_zstd_blocks : 1u;
+}
+/* sequence starts sb[0..nb] and literal starts lb[0..nb] of the blocks */
+static void zs_block_split(const uint32_t* ll, uint32_t nseq, uint32_t nlit, uint32_t nb,
+                           uint32_t* sb, uint32_t* lb) {
+  uint32_t acc = 0, k = 0;
+  for (uint32_t b = 0; b < nb; ++b) {
+    sb[b] = (uint32_t)((uint64_t)b * nseq / nb);
+    while (k < sb[b]) acc += ll[k++];
+    lb[b] = acc;
+  }
+  sb[nb] = nseq;
+  lb[nb] = nlit;
+}
+
 int bo_zstd_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_t cap,
                            uint32_t* csize) {
   if (n > 65536 || cap < bo_zstd_bound(n)) return BO_ERR_INVALID;
@@ -1166,87 +1226,106 @@ int bo_zstd_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_
     }
   }
   {
-    uint32_t op;
     /* frame header: magic, Single_Segment with the content size (1 byte below 256, else 2) */
     dst[0] = 0x28; dst[1] = 0xB5; dst[2] = 0x2F; dst[3] = 0xFD;
+    uint32_t fh;
     if (n < 256) {
       dst[4] = 0x20;
       dst[5] = (uint8_t)n;
-      op = 6;
+      fh = 6;
     } else {
       dst[4] = 0x60;
       dst[5] = (uint8_t)(n - 256);
       dst[6] = (uint8_t)((n - 256) >> 8);
-      op = 7;
+      fh = 7;
     }
-    const uint32_t blk = op;
-    int err = 0;
-    uint32_t p = blk + 3;
-    p += zs_literals(z.lit, z.nlit, dst + p, cap - p, &err);
-    if (!err && p + 4 <= cap) {
-      const uint32_t nseq = z.nseq;
-      if (nseq < 128) {
-        dst[p++] = (uint8_t)nseq;
+    const uint32_t nseq = z.nseq;
+    /* blocks: ZS_BLOCKS of equal sequence counts when the frame has >= ZS_MULTI_MIN
+     * sequences (each block's FSE state chains, and its literal streams, are then independent
+     * of the others': a decoder walks them in parallel), else one */
+    const uint32_t nb = zs_nblocks(nseq, z.drop != 0);
+    uint32_t sb[ZS_MAX_BLOCKS + 1], lb[ZS_MAX_BLOCKS + 1];
+    zs_block_split(z.ll, nseq, z.nlit, nb, sb, lb);
+    zs_littab H;
+    zs_littab_build(z.lit, z.nlit, &H);
+    int err = 0, tree_sent = 0;
+    uint32_t p = fh;
+    zs_seqtab* tll = NULL;
+    static __thread zs_seqtab tabs3[3];  /* (large: not on the stack; per thread) */
+    for (uint32_t b = 0; b < nb && !err; ++b) {
+      const uint32_t blk = p;
+      p = blk + 3;
+      if (p + 8 > cap) { err = 1; break; }
+      p += zs_literals_block(z.lit + lb[b], lb[b + 1] - lb[b], &H, &tree_sent, dst + p, cap - p,
+                             &err);
+      if (err || p + 4 > cap) { err = 1; break; }
+      const uint32_t s0 = sb[b], s1 = sb[b + 1], ns = s1 - s0;
+      if (ns < 128) {
+        dst[p++] = (uint8_t)ns;
       } else {
-        dst[p++] = (uint8_t)((nseq >> 8) + 128);
-        dst[p++] = (uint8_t)nseq;
+        dst[p++] = (uint8_t)((ns >> 8) + 128);
+        dst[p++] = (uint8_t)ns;
       }
-      if (nseq) {
+      if (ns) {
         uint8_t* llc = codes;
         uint8_t* mlc = codes + maxseq;
         uint8_t* ofc = codes + 2 * maxseq;
-        for (uint32_t i = 0; i < nseq; ++i) {
-          llc[i] = (uint8_t)bo_zstd_ll_code(z.ll[i]);
-          mlc[i] = (uint8_t)bo_zstd_ml_code(z.ml[i]);
-          ofc[i] = (uint8_t)zs_highbit(ov[i]);
+        zs_bw w = {dst, p + 1, cap, 0, 0, 0};
+        if (!tll) {
+          /* the tables: chosen over all of the frame's sequences, described in the first
+           * block; the later blocks repeat them (Repeat_Mode) */
+          for (uint32_t i = 0; i < nseq; ++i) {
+            llc[i] = (uint8_t)bo_zstd_ll_code(z.ll[i]);
+            mlc[i] = (uint8_t)bo_zstd_ml_code(z.ml[i]);
+            ofc[i] = (uint8_t)zs_highbit(ov[i]);
+          }
+          tll = tabs3;
+          zs_choose(&tabs3[0], llc, nseq, 35, 9, kLLDefault, 35, ZS_LL_AL, &w);
+          zs_choose(&tabs3[1], ofc, nseq, 31, 8, kOFDefault, 28, ZS_OF_AL, &w);
+          zs_choose(&tabs3[2], mlc, nseq, 52, 9, kMLDefault, 52, ZS_ML_AL, &w);
+          dst[p] = (uint8_t)((tabs3[0].mode << 6) | (tabs3[1].mode << 4) | (tabs3[2].mode << 2));
+        } else {
+          dst[p] = 0xFC;  /* Repeat_Mode for all three */
         }
-        const uint32_t mp = p++;  /* Symbol_Compression_Modes */
-        zs_bw w = {dst, p, cap, 0, 0, 0};
-        static __thread zs_seqtab tll, tof, tml;  /* (large: not on the stack; per thread) */
-        zs_choose(&tll, llc, nseq, 35, 9, kLLDefault, 35, ZS_LL_AL, &w);
-        zs_choose(&tof, ofc, nseq, 31, 8, kOFDefault, 28, ZS_OF_AL, &w);
-        zs_choose(&tml, mlc, nseq, 52, 9, kMLDefault, 52, ZS_ML_AL, &w);
-        dst[mp] = (uint8_t)((tll.mode << 6) | (tof.mode << 4) | (tml.mode << 2));
-        /* the bitstream: last sequence first */
+        const zs_seqtab *tl = &tabs3[0], *to = &tabs3[1], *tm = &tabs3[2];
+        /* the bitstream: the block's last sequence first */
         uint32_t sml = 0, sof = 0, sll = 0;
-        const uint32_t k = nseq - 1;
-        if (tml.mode != 1) zs_enc_init(&tml.ct, &sml, mlc[k]);
-        if (tof.mode != 1) zs_enc_init(&tof.ct, &sof, ofc[k]);
-        if (tll.mode != 1) zs_enc_init(&tll.ct, &sll, llc[k]);
+        const uint32_t k = s1 - 1;
+        if (tm->mode != 1) zs_enc_init(&tm->ct, &sml, mlc[k]);
+        if (to->mode != 1) zs_enc_init(&to->ct, &sof, ofc[k]);
+        if (tl->mode != 1) zs_enc_init(&tl->ct, &sll, llc[k]);
         zs_bw_add(&w, z.ll[k], kLLBits[llc[k]]);
         zs_bw_add(&w, z.ml[k] - 3, kMLBits[mlc[k]]);
         zs_bw_add(&w, ov[k], ofc[k]);
-        for (uint32_t j = nseq - 1; j-- > 0;) {
-          if (tof.mode != 1) zs_enc_sym(&w, &tof.ct, &sof, ofc[j]);
-          if (tml.mode != 1) zs_enc_sym(&w, &tml.ct, &sml, mlc[j]);
-          if (tll.mode != 1) zs_enc_sym(&w, &tll.ct, &sll, llc[j]);
+        for (uint32_t j = k; j-- > s0;) {
+          if (to->mode != 1) zs_enc_sym(&w, &to->ct, &sof, ofc[j]);
+          if (tm->mode != 1) zs_enc_sym(&w, &tm->ct, &sml, mlc[j]);
+          if (tl->mode != 1) zs_enc_sym(&w, &tl->ct, &sll, llc[j]);
           zs_bw_add(&w, z.ll[j], kLLBits[llc[j]]);
           zs_bw_add(&w, z.ml[j] - 3, kMLBits[mlc[j]]);
           zs_bw_add(&w, ov[j], ofc[j]);
         }
-        if (tml.mode != 1) zs_bw_add(&w, sml, tml.ct.al);
-        if (tof.mode != 1) zs_bw_add(&w, sof, tof.ct.al);
-        if (tll.mode != 1) zs_bw_add(&w, sll, tll.ct.al);
+        if (tm->mode != 1) zs_bw_add(&w, sml, tm->ct.al);
+        if (to->mode != 1) zs_bw_add(&w, sof, to->ct.al);
+        if (tl->mode != 1) zs_bw_add(&w, sll, tl->ct.al);
         zs_bw_close(&w);
         err |= w.err;
         p = w.pos;
       }
-    } else {
-      err = 1;
+      const uint32_t hdr = (b + 1 == nb ? 1u : 0u) | (2u << 1) | ((p - (blk + 3)) << 3);
+      dst[blk] = (uint8_t)hdr;
+      dst[blk + 1] = (uint8_t)(hdr >> 8);
+      dst[blk + 2] = (uint8_t)(hdr >> 16);
     }
-    if (err) { rc = BO_ERR_IO; goto out; }
-    const uint32_t csz = p - (blk + 3);
-    uint32_t hdr;
-    if (csz >= n) {  /* did not shrink: one raw block */
-      memcpy(dst + blk + 3, src, n);
-      hdr = 1u | (0u << 1) | (n << 3);
-      p = blk + 3 + n;
-    } else {
-      hdr = 1u | (2u << 1) | (csz << 3);
+    /* did not shrink (or outgrew the slot: the kernels' overflow): one raw block */
+    if (err || p - (fh + 3) >= n) {
+      memcpy(dst + fh + 3, src, n);
+      const uint32_t hdr = 1u | (0u << 1) | (n << 3);
+      dst[fh] = (uint8_t)hdr;
+      dst[fh + 1] = (uint8_t)(hdr >> 8);
+      dst[fh + 2] = (uint8_t)(hdr >> 16);
+      p = fh + 3 + n;
     }
-    dst[blk] = (uint8_t)hdr;
-    dst[blk + 1] = (uint8_t)(hdr >> 8);
-    dst[blk + 2] = (uint8_t)(hdr >> 16);
     *csize = p;
     rc = BO_OK;
   }

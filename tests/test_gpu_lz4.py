@@ -6,6 +6,8 @@ oracle's bytes (same window-scan parse) and those bytes must round-trip.  Full-s
 (1 GiB) runs are checked through size-independent properties (round trip equality,
 oracle agreement on sampled segments).
 """
+from contextlib import nullcontext
+
 import numpy as np
 import pytest
 
@@ -257,3 +259,79 @@ def test_wide_full_size_roundtrip_and_ratio(eng):
         del slab, out
     assert ratios[bitar_amd.CODEC_LZ4_WIDE] > 1.03 * ratios[bitar_amd.CODEC_LZ4], ratios
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("flags", [0, "plain"])
+def test_far_history_work_list(eng, flags):
+    """Large calls (>= 2048 segments, cost-ordered) hand the segments whose matches reach past
+    the decoder's LDS ring to the far kernel through a device work list; the far kernel is a
+    small grid that drains it.  A call mixing stock liblz4 segments (64 KiB history: they
+    defer), our own (never defer) and a few corrupted stock segments (rejected by the far
+    kernel) must decode exactly as the oracle does; plain-order calls take the full far grid."""
+    import bitar_amd
+    import stock_lib as S
+    seg, nseg = 65536, 3000
+    n = nseg * seg
+    host = O.fill(1, 77, n)
+    sslab, sstride, ssz = S.compress(S.LZ4, host, seg, 1)
+    stride = max(sstride, bitar_amd.slot_size(bitar_amd.CODEC_LZ4, seg))
+    e = eng if flags == 0 else bitar_amd.Engine(0, flags=bitar_amd.FLAG_PLAIN_ORDER | bitar_amd.FLAG_COUNT_PATHS)
+    try:
+        if flags == 0:
+            old = e.set_decoder_options(count_paths=1)
+        data = up(host)
+        gslab, gstride, gsz = e.compress(bitar_amd.CODEC_LZ4, data, seg)
+        gslab_h, gsz_h = down(gslab), down(gsz).astype(np.uint32)
+        slab = np.zeros(nseg * stride, np.uint8)
+        sizes = np.zeros(nseg, np.uint32)
+        rng = np.random.default_rng(5)
+        bad = set(rng.choice(np.arange(0, nseg, 2), 7, replace=False).tolist())
+        for i in range(nseg):
+            if i % 2 == 0:  # stock (far matches)
+                b = sslab[i * sstride:i * sstride + ssz[i]].copy()
+                if i in bad:
+                    b[len(b) // 2] ^= 0xA5
+            else:
+                b = gslab_h[i * gstride:i * gstride + gsz_h[i]]
+            slab[i * stride:i * stride + b.size] = b
+            sizes[i] = b.size
+        out = e.empty(n)
+        prod = e.empty(nseg, dtype=torch.int32)
+        e.decompress_slab_into(bitar_amd.CODEC_LZ4, up(slab), stride,
+                               up(sizes.view(np.uint8)).view(torch.int32), nseg, seg, out, prod,
+                               capacity=n)
+        blobs = [slab[i * stride:i * stride + sizes[i]] for i in range(nseg)]
+        # the oracle's verdicts: the intact segments decode to the input (checked for a
+        # sample here, all of them below); a corrupted one is decoded by the oracle alone
+        ref = host.copy()
+        verdict = np.full(nseg, seg, np.uint32)
+        for i in sorted(bad) + list(range(0, nseg, 97)):
+            r, dec = O.lz4_decompress(blobs[i], seg)
+            if i in bad:
+                verdict[i] = 0xFFFFFFFF if r != 0 else len(dec)
+                if r == 0:
+                    ref[i * seg:i * seg + len(dec)] = np.frombuffer(dec, np.uint8)
+            else:
+                assert r == 0 and dec == host[i * seg:(i + 1) * seg].tobytes(), i
+        rejected = int((verdict == 0xFFFFFFFF).sum())
+        try:
+            e.sync()
+            failed = False
+        except bitar_amd.BitarError:
+            failed = True
+        c = e.path_counters()
+        p = down(prod).view(np.uint32)
+        o = down(out)
+        diff = np.nonzero(p != verdict)[0]
+        assert diff.size == 0, (diff[:10].tolist(), p[diff[:10]].tolist(),
+                                verdict[diff[:10]].tolist(), sorted(bad), c)
+        assert failed == (rejected > 0)
+        assert c["lz4_far"] >= nseg // 4  # (stock segments of random data have no far match)
+        for i in range(nseg):
+            if verdict[i] != 0xFFFFFFFF:
+                assert np.array_equal(o[i * seg:i * seg + p[i]], ref[i * seg:i * seg + p[i]]), i
+    finally:
+        if flags == 0:
+            e.set_decoder_options(**old)
+        else:
+            e.close()

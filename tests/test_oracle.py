@@ -214,54 +214,72 @@ def test_oracle_zstd_rejects_malformed():
             break
 
 
-def _zstd_info(frame):
-    """Structure of a single-segment, single-block frame the oracle wrote: block type, and
-    for a compressed block the literal section (type, streams, sizes, Huffman description
+def _zstd_blocks(frame):
+    """Structure of a single-segment frame the oracle wrote, one dict per block: block type,
+    and for a compressed block the literal section (type, streams, sizes, Huffman description
     header byte) and the sequence section (count, table modes)."""
     fh = 6 if frame[4] == 0x20 else 7
     p = fh
-    h = frame[p] | (frame[p + 1] << 8) | (frame[p + 2] << 16)
-    last, btype, bsize = h & 1, (h >> 1) & 3, h >> 3
-    assert last == 1 and p + 3 + (bsize if btype != 1 else 1) == len(frame)
-    info = {"block": btype, "bsize": bsize}
-    if btype != 2:
-        return info
-    p += 3
-    b0 = frame[p]
-    lt, sf = b0 & 3, (b0 >> 2) & 3
-    if lt < 2:
-        if sf in (0, 2):
-            reg, hs = b0 >> 3, 1
-        elif sf == 1:
-            reg, hs = (b0 >> 4) + (frame[p + 1] << 4), 2
-        else:
-            reg, hs = (b0 >> 4) + (frame[p + 1] << 4) + (frame[p + 2] << 12), 3
-        lsz, streams, desc = hs + (reg if lt == 0 else 1), 0, None
-    else:
-        hs = 3 if sf <= 1 else 4 if sf == 2 else 5
-        c = int.from_bytes(frame[p:p + hs], "little")
-        bits = 10 if hs == 3 else 14 if hs == 4 else 18
-        reg, cs = (c >> 4) & ((1 << bits) - 1), c >> (4 + bits)
-        lsz, streams, desc = hs + cs, 1 if sf == 0 else 4, frame[p + hs]
-    q = p + lsz
-    nseq = frame[q]
-    if nseq >= 128:
-        nseq, q = ((nseq - 128) << 8) + frame[q + 1], q + 2
-    else:
-        q += 1
-    modes = None
-    if nseq:
-        m = frame[q]
-        modes = (m >> 6, (m >> 4) & 3, (m >> 2) & 3)
-    info.update(lit_type=lt, nlit=reg, lit_bytes=lsz, streams=streams, huf_desc=desc,
-                nseq=nseq, modes=modes)
-    return info
+    out = []
+    while True:
+        h = frame[p] | (frame[p + 1] << 8) | (frame[p + 2] << 16)
+        last, btype, bsize = h & 1, (h >> 1) & 3, h >> 3
+        info = {"block": btype, "bsize": bsize}
+        out.append(info)
+        end = p + 3 + (bsize if btype != 1 else 1)
+        if btype == 2:
+            q0 = p + 3
+            b0 = frame[q0]
+            lt, sf = b0 & 3, (b0 >> 2) & 3
+            if lt < 2:
+                if sf in (0, 2):
+                    reg, hs = b0 >> 3, 1
+                elif sf == 1:
+                    reg, hs = (b0 >> 4) + (frame[q0 + 1] << 4), 2
+                else:
+                    reg, hs = (b0 >> 4) + (frame[q0 + 1] << 4) + (frame[q0 + 2] << 12), 3
+                lsz, streams, desc = hs + (reg if lt == 0 else 1), 0, None
+            else:
+                hs = 3 if sf <= 1 else 4 if sf == 2 else 5
+                c = int.from_bytes(frame[q0:q0 + hs], "little")
+                bits = 10 if hs == 3 else 14 if hs == 4 else 18
+                reg, cs = (c >> 4) & ((1 << bits) - 1), c >> (4 + bits)
+                lsz, streams = hs + cs, 1 if sf == 0 else 4
+                desc = frame[q0 + hs] if lt == 2 else None
+            q = q0 + lsz
+            nseq = frame[q]
+            if nseq >= 128:
+                nseq, q = ((nseq - 128) << 8) + frame[q + 1], q + 2
+            else:
+                q += 1
+            modes = None
+            if nseq:
+                m = frame[q]
+                modes = (m >> 6, (m >> 4) & 3, (m >> 2) & 3)
+            info.update(lit_type=lt, nlit=reg, lit_bytes=lsz, streams=streams, huf_desc=desc,
+                        nseq=nseq, modes=modes)
+        p = end
+        if last:
+            break
+    assert p == len(frame)
+    return out
+
+
+def _zstd_info(frame):
+    """The first block's structure, with the frame's block count and total sequences."""
+    bl = _zstd_blocks(frame)
+    i = dict(bl[0])
+    i["nblocks"] = len(bl)
+    i["nseq_total"] = sum(b.get("nseq", 0) for b in bl)
+    return i
 
 
 def test_oracle_zstd_frame_structure():
-    """One block per segment (raw when it does not shrink); literals raw / RLE / Huffman with
-    1 stream below 256 literals, else 4; FSE-compressed Huffman weights when more than 128
-    would be sent directly; repeat-offset / FSE table modes on structured input."""
+    """One block per segment below 64 sequences, else 4 blocks of equal sequence counts (raw
+    when the frame does not shrink); literals raw / RLE / Huffman with 1 stream below 256
+    literals, else 4 (per block); the first Huffman block carries the tree and later ones are
+    Treeless; FSE-compressed Huffman weights when more than 128 would be sent directly;
+    table descriptions in the first block, Repeat_Mode in the others."""
     rnd = O.fill(0, 1, 65536).tobytes()
     r, f = O.zstd_compress(rnd)
     assert r == 0 and _zstd_info(f)["block"] == 0 and len(f) == 7 + 3 + 65536
@@ -269,9 +287,10 @@ def test_oracle_zstd_frame_structure():
     i = _zstd_info(O.zstd_compress(b"\x07" * 5000)[1])
     assert i["block"] == 2 and i["lit_type"] == 1
     # text: Huffman, 1 stream below 256 literals, else 4
-    text = O.fill(6, 3, 2000).tobytes()
+    text = O.fill(6, 3, 8000).tobytes()
     i = _zstd_info(O.zstd_compress(text[:600])[1])
     assert i["block"] == 2 and i["lit_type"] == 2 and i["streams"] == 1 and i["nlit"] < 256
+    assert i["nblocks"] == 1
     i = _zstd_info(O.zstd_compress(text)[1])
     assert i["lit_type"] == 2 and i["streams"] == 4 and i["nlit"] >= 256
     rng = np.random.default_rng(5)
@@ -285,8 +304,23 @@ def test_oracle_zstd_frame_structure():
     i = _zstd_info(O.zstd_compress(skew)[1])
     assert i["lit_type"] == 2 and i["huf_desc"] < 128
     col = O.fill(5, 1, 65536).tobytes()  # int64 column: sequences on FSE tables
-    i = _zstd_info(O.zstd_compress(col)[1])
-    assert i["block"] == 2 and i["nseq"] > 1000 and 2 in i["modes"]
+    bl = _zstd_blocks(O.zstd_compress(col)[1])
+    assert len(bl) == 4 and all(b["block"] == 2 for b in bl)
+    assert sum(b["nseq"] for b in bl) > 1000 and 2 in bl[0]["modes"]
+    counts = [b["nseq"] for b in bl]
+    assert max(counts) - min(counts) <= 1                     # equal sequence counts
+    assert all(b["modes"] == (3, 3, 3) for b in bl[1:])       # Repeat_Mode
+    huff = [b for b in bl if b["lit_type"] in (2, 3)]
+    assert huff and huff[0]["lit_type"] == 2 and all(b["lit_type"] == 3 for b in huff[1:])
+    # one block again with the single-block setting (rounds 1-4's frames)
+    L = O.lib()
+    L.bo_set_zstd_blocks.restype = ctypes.c_uint32
+    L.bo_set_zstd_blocks.argtypes = [ctypes.c_uint32]
+    old = L.bo_set_zstd_blocks(1)
+    try:
+        assert len(_zstd_blocks(O.zstd_compress(col)[1])) == 1
+    finally:
+        L.bo_set_zstd_blocks(old)
 
 
 def test_oracle_zstd_ratio_vs_libzstd1():
@@ -458,6 +492,10 @@ def test_zstd_dropped_gap_literals_are_rejected():
     acceptance is not looser than libzstd's on this class."""
     Z = _libzstd()
     seg = 65536
+    L = O.lib()
+    L.bo_set_zstd_blocks.restype = ctypes.c_uint32
+    L.bo_set_zstd_blocks.argtypes = [ctypes.c_uint32]
+    old_blocks = L.bo_set_zstd_blocks(1)  # (the round-3 frames: one block; DROP implies it)
     old = _set_zstd_flags(REP | SKIP | DROP)
     bad = 0
     try:
@@ -481,5 +519,6 @@ def test_zstd_dropped_gap_literals_are_rejected():
                 if r2 == 0:
                     assert back == out.raw[:rr]
     finally:
+        L.bo_set_zstd_blocks(old_blocks)
         _set_zstd_flags(old)
     assert bad >= 4
