@@ -394,6 +394,17 @@ __device__ __forceinline__ uint32_t word_raw(const GMEM uint8_t* s, int32_t a, i
   __builtin_memcpy(&v, s + (a < lo ? lo : a), 4);
   return v;
 }
+// 16 bytes {a, b} to d (any alignment)
+__device__ __forceinline__ void st16_raw(GMEM uint8_t* d, uint64_t a, uint64_t b) {
+  const uint4 v = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+  __builtin_memcpy(d, &v, 16);
+}
+// 16 stream bytes at s (any alignment)
+__device__ __forceinline__ uint4 ld16_raw(const GMEM uint8_t* s) {
+  uint4 v;
+  __builtin_memcpy(&v, s, 16);
+  return v;
+}
 }  // namespace zsh
 
 // The Huffman literal streams of handed-off blocks (kLitPend): 16 segments per wave, one lane
@@ -518,13 +529,20 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
 #define BITAR_HLIT_NW 8
 #endif
     constexpr uint32_t NW = BITAR_HLIT_NW;
+#ifndef BITAR_HLIT_X4
+#define BITAR_HLIT_X4 1
+#endif
+    constexpr bool X4 = BITAR_HLIT_X4 != 0 && NW == 8;
     uint32_t W[NW];
 #pragma unroll
     for (uint32_t w = 0; w < NW; ++w) W[w] = zsh::word_raw(src, top - 4 * (int32_t)(w + 1), lo);
     uint32_t used = 8 - (31u - (uint32_t)__builtin_clz(lastb));  // the end mark and zeros above it
     const uint32_t mask = (1u << log) - 1u;
-    uint64_t acc = 0;
-    uint32_t k = 0, ac = 0;
+    uint64_t acc = 0, prev = 0;
+    uint32_t k = 0, ac = 0, half = 0;
+#ifndef BITAR_HLIT_ST16
+#define BITAR_HLIT_ST16 1
+#endif
     auto phase = [&](uint32_t hi, uint32_t lo32, uint32_t& slot) __attribute__((always_inline)) {
       const uint64_t c = ((uint64_t)hi << 32) | lo32;
       auto emit = [&](uint32_t sym) __attribute__((always_inline)) {
@@ -532,7 +550,14 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
         acc |= (uint64_t)sym << (8 * ac);
         ++k;
         if (++ac == 8) {
-          lanes::st8(dst + k - 8, acc);
+          if constexpr (BITAR_HLIT_ST16 != 0) {
+            // 16 symbols per store: half the store addresses
+            if (half) zsh::st16_raw(dst + k - 16, prev, acc);
+            else prev = acc;
+            half ^= 1u;
+          } else {
+            lanes::st8(dst + k - 8, acc);
+          }
           acc = 0;
           ac = 0;
         }
@@ -552,19 +577,47 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
       }
       // (unconditional: a conditional load is a phi the compiler settles with vmcnt(0); when
       // the phase ended on k == n instead, the loop ends and the word is not read)
-      slot = zsh::word_raw(src, top - 4 * (int32_t)(NW + 1), lo);
+      if constexpr (!X4) slot = zsh::word_raw(src, top - 4 * (int32_t)(NW + 1), lo);
       if (used >= 32) {
         top -= 4;
         used -= 32;
       }
+    };
+    // X4: the four words a half-round consumed are reloaded by ONE 16-byte load (the
+    // addresser handles one address per lane either way, and the lanes' scattered loads bound
+    // this kernel: TA busy ~70 % of its cycles with a dword per phase).  The block [top - 32,
+    // top - 16) goes to W[h+3] .. W[h] (lowest address first).  Near the stream start the load
+    // is clamped to lo and the 128-bit value shifted back into place (the bytes below lo are
+    // below the stream and masked at the peek); it only runs after four full phases, so
+    // [lo, lo + 16) lies inside the stream.
+    auto reload4 = [&](uint32_t& wa, uint32_t& wb, uint32_t& wc, uint32_t& wd) __attribute__((always_inline)) {
+      const int32_t A = top - 32;
+      const int32_t a = A < lo ? lo : A;
+      const uint32_t sh = (uint32_t)(a - A) * 8u;  // 0 except near the start
+      const uint4 v = zsh::ld16_raw(src + a);
+      const uint64_t l64 = (uint64_t)v.x | ((uint64_t)v.y << 32);
+      const uint64_t h64 = (uint64_t)v.z | ((uint64_t)v.w << 32);
+      const uint32_t s1 = sh & 63u;
+      const uint64_t spill = s1 ? l64 >> (64u - s1) : 0ull;
+      const uint64_t rl = sh < 64 ? l64 << s1 : 0ull;
+      const uint64_t rh = sh < 64 ? (h64 << s1) | spill : sh < 128 ? l64 << s1 : 0ull;
+      wa = (uint32_t)rl;
+      wb = (uint32_t)(rl >> 32);
+      wc = (uint32_t)rh;
+      wd = (uint32_t)(rh >> 32);
     };
     while (k < n) {
 #pragma unroll
       for (uint32_t p = 0; p < NW; ++p) {
         phase(W[p], W[(p + 1) % NW], W[p]);
         if (k >= n) break;
+        if constexpr (X4) {
+          if (p == 3) reload4(W[3], W[2], W[1], W[0]);
+          if (p == 7) reload4(W[7], W[6], W[5], W[4]);
+        }
       }
     }
+    if (BITAR_HLIT_ST16 != 0 && half) lanes::st8(dst + k - ac - 8, prev);
     for (uint32_t r = 0; r < ac; ++r) dst[k - ac + r] = (uint8_t)(acc >> (8 * r));
     ok = 8 * (top - q) - (int32_t)used == 0;
   }

@@ -8,7 +8,8 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${TAG:-sq2}
 PROG=${PROG:-scripts/kernel_bench.py --codec zstd --kinds 2 --reps 1}
-timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+CTRS=${CTRS:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY}
+timeout -s KILL 300 rocprofv3 --pmc $CTRS \
   -d gpurun_out/$TAG -o pmc --output-format csv -- python3 $PROG \
   > gpurun_out/$TAG.log 2>&1 || { echo "sq pass failed"; tail -20 gpurun_out/$TAG.log; exit 1; }
 python3 - gpurun_out/$TAG/pmc_counter_collection.csv <<'PY'
