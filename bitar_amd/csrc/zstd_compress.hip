@@ -758,7 +758,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     distinct += (uint32_t)__builtin_popcountll(ballot(L.hist[s0 + lane] != 0));
   lds_order();
   ZSE_PHASE(1)
-  uint32_t lmode = 0, lrle = 0, dsz = 0;
+  uint32_t lmode = 0, lrle = 0, dsz = 0, tbits = 0;
   if (nlit > 0 && distinct == 1) {
     lmode = 1;
     lrle = lits[0];
@@ -833,6 +833,10 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     dsz = L.u[0];
     for (uint32_t k = lane; k < dsz; k += kWave) wbytes[4 * kWTreeAt + k] = L.desc[k];
     if (dsz) lmode = 2;
+    uint32_t tbl = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c) tbl += (uint32_t)L.len[64 * c + lane] * L.hist[64 * c + lane];
+    tbits = readlane(wave_incl_sum(tbl), kWave - 1);
   }
   ZSE_PHASE(2)
 
@@ -926,6 +930,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     wrec[kWLit] = lmode | (lrle << 8) | (dsz << 16);
     wrec[kWNlit] = nlit;
     wrec[kWTdesc] = tdesc;
+    wrec[kWTb] = tbits;
     wrec[kWSb + nb] = nseq;
     wrec[kWLb + nb] = nlit;
     wrec[kWHanded] = 1u;
@@ -1088,7 +1093,8 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
     reinterpret_cast<uint8_t*>(&sT)[k] = reinterpret_cast<const uint8_t*>(&kT)[k];
   const uint32_t n = uniform(w[kWN]), als = uniform(w[kWAls]);
   const uint32_t nb = uniform(w[kWNb]), litw = uniform(w[kWLit]);
-  const uint32_t tdesc = uniform(w[kWTdesc]);
+  const uint32_t tdesc = uniform(w[kWTdesc]), tbits = uniform(w[kWTb]);
+  const uint32_t nlit = uniform(w[kWNlit]);
   const uint32_t lmode = litw & 0xFFu, lrle = (litw >> 8) & 0xFFu, dsz = litw >> 16;
   const uint32_t al_ll = als & 0xFFu, al_of = (als >> 8) & 0xFFu, al_ml = als >> 16;
   if (lmode == 2) {
@@ -1120,6 +1126,12 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
     o.put(hb, fh);
   }
   uint32_t bpos[kBlocks], bhdr[kBlocks];
+  // per block, a Huffman literal section's header and jump table, written at the end (their
+  // sizes are known once the streams are): position (0: none), header size, header value,
+  // jump table position (0: none) and stream sizes
+  uint32_t ppos[kBlocks] = {0, 0, 0, 0}, phs[kBlocks] = {0, 0, 0, 0}, pjt[kBlocks] = {0, 0, 0, 0};
+  uint32_t pz[kBlocks] = {0, 0, 0, 0}, pz2[kBlocks] = {0, 0, 0, 0};
+  uint64_t ph[kBlocks] = {0, 0, 0, 0};
   bool tree_sent = false;
   // literals [a, a + m) of the segment's literal area as a Huffman stream (oracle
   // zs_literals_block): symbols from the last, 64 per step, from 1 KiB blocks of aligned
@@ -1173,52 +1185,56 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
       lit_header(1u, m);
       coded = true;
     } else if (lmode == 2 && m > 0) {
-      // the streams' sizes: code lengths summed per quarter (one pass over the literals)
+      // Huffman when an estimate from the frame's statistics (the block's share of all coded
+      // bits) and then the exact sizes both pass zs_literals_block's rule: the streams are
+      // encoded once, the header and jump table written at the end with their sizes, and a
+      // block the exact rule rejects is rewound and written raw
       const uint32_t ns = m < 256 ? 1u : 4u, q = (m + 3) / 4;
-      uint32_t bq[4] = {0, 0, 0, 0};
-      for (uint32_t g = a & ~15u; g < a + m; g += 16u * kWave) {
-        const uint32_t at = g + 16u * lane;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (at < a + m) v = *reinterpret_cast<const GMEM uint4*>(lits + at);
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (uint32_t jj = 0; jj < 16; ++jj) {
-          const uint32_t r = at + jj - a;  // (wraps for positions before a: >= m)
-          const uint32_t ln = hcode[(wv[jj >> 2] >> (8 * (jj & 3))) & 0xFFu] >> 16;
-          const uint32_t qi = ns == 1 ? 0u : r < q ? 0u : r < 2 * q ? 1u : r < 3 * q ? 2u : 3u;
-          const uint32_t add = r < m ? ln : 0u;
-          bq[0] += qi == 0 ? add : 0u;
-          bq[1] += qi == 1 ? add : 0u;
-          bq[2] += qi == 2 ? add : 0u;
-          bq[3] += qi == 3 ? add : 0u;
-        }
-      }
-      uint32_t sb[4];
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) sb[k] = (readlane(wave_incl_sum(bq[k]), kWave - 1) + 8) >> 3;
       const uint32_t tsz = tree_sent ? 0u : dsz;
-      const uint32_t total = tsz + (ns == 4 ? 6u + sb[0] + sb[1] + sb[2] + sb[3] : sb[0]);
       const int32_t limit = (int32_t)m - (int32_t)((m >> 6) + 2);
-      if ((int32_t)total < limit) {
+      const uint64_t est_bits = (uint64_t)m * tbits / nlit;
+      const uint32_t est = tsz + (ns == 4 ? 6u : 0u) + (uint32_t)((est_bits + 8u * ns) / 8u);
+      if ((int32_t)est < limit) {
         const uint32_t hs = ns == 1 || m < 1024 ? 3u : m < 16384 ? 4u : 5u;
         const uint32_t sf = ns == 1 ? 0u : m < 1024 ? 1u : m < 16384 ? 2u : 3u;
-        const uint64_t h = (tree_sent ? 3u : 2u) | (sf << 2) | ((uint64_t)m << 4) |
-                           ((uint64_t)total << (hs == 3 ? 14 : hs == 4 ? 18 : 22));
+        const uint32_t sec = o.op;
         o.room(hs);
-        o.put((uint32_t)(h >> (8 * (lane < 8 ? lane : 0u))) & 0xFFu, hs);
+        o.put(0u, hs);  // (the header, patched at the end)
         o.put_lds(bytes, tsz);
+        const uint32_t jt = o.op;
+        uint32_t z0 = 0, z1 = 0, z2 = 0;
         if (ns == 4) {
-          const uint32_t jj = lane >> 1;
-          const uint32_t sv = jj == 0 ? sb[0] : jj == 1 ? sb[1] : sb[2];
           o.room(6);
-          o.put((lane & 1) ? sv >> 8 : sv & 0xFFu, 6);
-          for (uint32_t k = 0; k < 4 && !o.overflow; ++k)
-            huff_stream(a + k * q, k == 3 ? a + m : a + (k + 1) * q);
+          o.put(0u, 6);  // (the jump table, patched at the end)
+          uint32_t pk = o.op;
+          huff_stream(a, a + q);
+          z0 = o.op - pk;
+          pk = o.op;
+          huff_stream(a + q, a + 2 * q);
+          z1 = o.op - pk;
+          pk = o.op;
+          huff_stream(a + 2 * q, a + 3 * q);
+          z2 = o.op - pk;
+          huff_stream(a + 3 * q, a + m);
         } else {
           huff_stream(a, a + m);
         }
-        tree_sent = true;
-        coded = true;
+        const uint32_t total = o.op - sec - hs;
+        if (!o.overflow && (int32_t)total < limit) {
+          const uint64_t h = (tree_sent ? 3u : 2u) | (sf << 2) | ((uint64_t)m << 4) |
+                             ((uint64_t)total << (hs == 3 ? 14 : hs == 4 ? 18 : 22));
+          ppos[b] = sec;
+          phs[b] = hs;
+          ph[b] = h;
+          pjt[b] = ns == 4 ? jt : 0u;
+          pz[b] = z0 | (z1 << 16);
+          pz2[b] = z2;
+          tree_sent = true;
+          coded = true;
+        } else if (!o.overflow) {  // rewind: raw after all
+          o.op = sec;
+          o.flushed = o.flushed > sec ? sec : o.flushed;
+        }
       }
     }
     if (!coded) {  // raw
@@ -1323,6 +1339,22 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
     const uint32_t at = bi == 0 ? bpos[0] : bi == 1 ? bpos[1] : bi == 2 ? bpos[2] : bpos[3];
     const uint32_t hv = bi == 0 ? bhdr[0] : bi == 1 ? bhdr[1] : bi == 2 ? bhdr[2] : bhdr[3];
     o.dst[at + byte] = (uint8_t)(hv >> (8 * byte));
+  }
+  if (!stored) {
+    // the Huffman literal sections' headers (lanes 16 b + k, k < 5) and jump tables (16 b + 8
+    // + k, k < 6)
+    const uint32_t bi = lane >> 4, k = lane & 15u;
+    const uint32_t pp = bi == 0 ? ppos[0] : bi == 1 ? ppos[1] : bi == 2 ? ppos[2] : ppos[3];
+    const uint32_t hs = bi == 0 ? phs[0] : bi == 1 ? phs[1] : bi == 2 ? phs[2] : phs[3];
+    const uint32_t jt = bi == 0 ? pjt[0] : bi == 1 ? pjt[1] : bi == 2 ? pjt[2] : pjt[3];
+    const uint32_t zz = bi == 0 ? pz[0] : bi == 1 ? pz[1] : bi == 2 ? pz[2] : pz[3];
+    const uint32_t z2 = bi == 0 ? pz2[0] : bi == 1 ? pz2[1] : bi == 2 ? pz2[2] : pz2[3];
+    const uint64_t hv = bi == 0 ? ph[0] : bi == 1 ? ph[1] : bi == 2 ? ph[2] : ph[3];
+    if (bi < nb && hs && k < hs) o.dst[pp + k] = (uint8_t)(hv >> (8 * k));
+    if (bi < nb && jt && k >= 8 && k < 14) {
+      const uint32_t e = k - 8, sv = e < 2 ? zz & 0xFFFFu : e < 4 ? zz >> 16 : z2;
+      o.dst[jt + e] = (uint8_t)((e & 1u) ? sv >> 8 : sv & 0xFFu);
+    }
   }
   if (lane == 0) sizes[i_seg] = o.op;
 }

@@ -34,6 +34,7 @@ enum : uint32_t {
   kWLit,         // literal code: mode (0 raw, 1 RLE, 2 Huffman) | RLE byte << 8 | tree bytes << 16
   kWNlit,        // literal bytes
   kWTdesc,       // bytes of the modes byte + table descriptions (kWDescAt)
+  kWTb,          // coded bits of all literals (sum of length x count): the blocks' estimate
   kWSb = 16,     // kBlocks + 1 words: first sequence of each block (then nseq)
   kWLb = 21,     // kBlocks + 1 words: first literal of each block (then nlit)
   kWStep = 26,   // kBlocks words: first history step of each block

@@ -905,6 +905,8 @@ static uint32_t zs_weights_fse(const uint8_t* w, uint32_t nw, uint8_t* out) {
  * its blocks (the first Huffman-coded block carries the tree, later ones are Treeless). */
 typedef struct {
   uint32_t mode;     /* 0 raw, 1 RLE (one distinct byte), 2 Huffman-capable */
+  uint32_t nlit;     /* all of the frame's literals */
+  uint64_t tb;       /* their Huffman-coded bits: sum of length x count */
   uint8_t rle;
   uint8_t len[256];
   uint32_t code[256];
@@ -918,6 +920,8 @@ static void zs_littab_build(const uint8_t* lit, uint32_t n, zs_littab* H) {
     if (!hist[lit[i]]++) ++distinct;
   H->mode = 0;
   H->dsz = 0;
+  H->nlit = n;
+  H->tb = 0;
   if (n == 0) return;
   if (distinct == 1) {
     H->mode = 1;
@@ -961,13 +965,16 @@ static void zs_littab_build(const uint8_t* lit, uint32_t n, zs_littab* H) {
     H->dsz = fsz;
   }
   if (H->dsz) H->mode = 2;
+  for (uint32_t s = 0; s < 256; ++s) H->tb += (uint64_t)H->len[s] * hist[s];
 }
 
 /* literals section of one block, lit[0..n), into d; returns its size.  Huffman when the
  * block's section -- the tree included while *tree_sent is 0 -- is at least n/64 + 2 bytes
- * smaller than n (then *tree_sent = 1; the block is Treeless when it already was 1); RLE for
- * an RLE code and n > 0; raw otherwise.  With one block this is the single-block frame's
- * rule exactly. */
+ * smaller than n, both by an estimate from the frame's statistics (the block's share of all
+ * coded bits, n tb / nlit) and exactly (then *tree_sent = 1; the block is Treeless when it
+ * already was 1); RLE for an RLE code and n > 0; raw otherwise.  (The estimate lets the
+ * kernel encode the streams once and write their sizes afterwards: it only encodes what the
+ * estimate admits and rewinds to raw when the exact rule fails.) */
 static uint32_t zs_literals_block(const uint8_t* lit, uint32_t n, const zs_littab* H,
                                   int* tree_sent, uint8_t* d, uint32_t cap, int* err) {
   uint32_t hsz;
@@ -980,6 +987,9 @@ static uint32_t zs_literals_block(const uint8_t* lit, uint32_t n, const zs_litta
   if (H->mode == 2 && n > 0) {
     const uint32_t ns = n < 256 ? 1 : 4, q = (n + 3) / 4;
     const uint32_t dsz = *tree_sent ? 0u : H->dsz;
+    const int32_t limit = (int32_t)n - (int32_t)((n >> 6) + 2);
+    const uint64_t est_bits = (uint64_t)n * H->tb / H->nlit;
+    const uint32_t est = dsz + (ns == 4 ? 6 : 0) + (uint32_t)((est_bits + 8u * ns) / 8u);
     uint32_t bytes[4] = {0}, total = dsz + (ns == 4 ? 6 : 0);
     for (uint32_t k = 0; k < ns; ++k) {
       const uint32_t a = ns == 1 ? 0 : k * q, b = ns == 1 ? n : (k == 3 ? n : (k + 1) * q);
@@ -988,8 +998,7 @@ static uint32_t zs_literals_block(const uint8_t* lit, uint32_t n, const zs_litta
       bytes[k] = (uint32_t)((bits + 1 + 7) / 8);
       total += bytes[k];
     }
-    const int32_t limit = (int32_t)n - (int32_t)((n >> 6) + 2);
-    if ((int32_t)total < limit) {
+    if ((int32_t)est < limit && (int32_t)total < limit) {
       const uint32_t hs = ns == 1 || n < 1024 ? 3 : n < 16384 ? 4 : 5;
       if (hs + total > cap) { *err = 1; return 0; }
       const uint32_t sf = ns == 1 ? 0 : n < 1024 ? 1 : n < 16384 ? 2 : 3;
