@@ -229,21 +229,22 @@ __device__ __forceinline__ uint32_t walk_tokens2h(uint32_t pw, uint32_t lim, uin
 // (measured: 4-8 % on our own streams when both share one kernel).
 constexpr uint32_t kDefer = 0xFFFFFFFEu;
 
-// defer (both kernels; null: the far kernel is a full grid that tests produced[i]): the
-// deferred-segment list the near kernel appends to, {count, (unused), list[nseg]}, count
-// zeroed by the call's order kernels.  The far kernel is then a bounded grid whose workgroups
-// stride over the list's entries, so a call
-// whose segments never reach past the ring (every stream of our encoders) costs a few
-// microseconds instead of a grid of nseg workgroups that queue behind concurrent launches.
 template <bool FARK>
-__device__ __forceinline__ void lz4_decode_segment(
-    uint32_t i, const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
-    uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t seg,
+__global__ __launch_bounds__(64) void lz4_decompress_kernel(
+    const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
+    uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
-    unsigned long long* __restrict__ stats, uint8_t* lds) {
+    unsigned long long* __restrict__ stats, const uint32_t* __restrict__ order) {
   using namespace lz4d;
+  // the ring at LDS address 0: a history source is then (address & mask), one add fewer
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing + kWin];
   uint8_t* ring = lds;
   uint8_t* win = lds + kRing;
+  if (blockIdx.x >= nseg) return;
+  // cost-ordered dispatch (seg_order_kernel): workgroup b decodes segment order[b]
+  const uint32_t i = order ? order[blockIdx.x] : blockIdx.x;
+  if (FARK && produced[i] != kDefer) return;
+
   State s;
   s.src = global_ptr(srcs ? srcs[i] : slab + (uint64_t)i * slot_stride);
   s.csize = csizes[i];
@@ -558,31 +559,6 @@ __device__ __forceinline__ void lz4_decode_segment(
   } else if (lane_id() == 0) {
     produced[i] = 0xFFFFFFFFu;
     atomicOr(err, 1u);
-  }
-}
-
-template <bool FARK>
-__global__ __launch_bounds__(64) void lz4_decompress_kernel(
-    const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
-    uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
-    uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,
-    unsigned long long* __restrict__ stats, const uint32_t* __restrict__ order) {
-  // the ring at LDS address 0: a history source is then (address & mask), one add fewer
-  __shared__ __attribute__((aligned(16))) uint8_t lds[lz4d::kRing + lz4d::kWin];
-  if constexpr (FARK) {
-    for (uint32_t b = blockIdx.x; b < nseg; b += gridDim.x) {
-      const uint32_t i = order ? order[b] : b;
-      if (produced[i] != kDefer) continue;
-      lz4_decode_segment<true>(i, srcs, slab, slot_stride, csizes, seg, out, produced, err,
-                               stats, lds);
-      lds_order();  // the next segment reuses the LDS ring / window
-    }
-  } else {
-    if (blockIdx.x >= nseg) return;
-    // cost-ordered dispatch (seg_order_kernel): workgroup b decodes segment order[b]
-    const uint32_t i = order ? order[blockIdx.x] : blockIdx.x;
-    lz4_decode_segment<false>(i, srcs, slab, slot_stride, csizes, seg, out, produced, err,
-                              stats, lds);
   }
 }
 

@@ -790,16 +790,9 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
     hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<false>, dim3(nseg), dim3(64), 0, s, srcs,
                        slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
                        stats, ord.order);
-    // the far kernel: at most kFarGrid workgroups, each striding over the dispatch slots for
-    // the segments the near kernel deferred.  A 1 GiB call keeps one workgroup per slot
-    // (stock liblz4 streams defer ~2/3 of their segments: 7168 workgroups striding over them,
-    // 28 waves per CU, decoded them 7 % slower); larger calls (the configs[3] record batch's
-    // 2 GiB parts) launch half the workgroups or fewer
-    constexpr uint32_t kFarGrid = 16384;
-    hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<true>,
-                       dim3(nseg > kFarGrid ? kFarGrid : nseg), dim3(64), 0, s, srcs, slab,
-                       stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s), stats,
-                       ord.order);
+    hipLaunchKernelGGL(bitar_hip::lz4_decompress_kernel<true>, dim3(nseg), dim3(64), 0, s, srcs,
+                       slab, stride, d_sizes, nseg, seg, out, d_produced, err_word(ctx, s),
+                       stats, ord.order);
     if (int r = ord.release()) return r;
   }
   else if (codec == BITAR_HIP_CODEC_DEFLATE) {

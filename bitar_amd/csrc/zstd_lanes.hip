@@ -532,7 +532,15 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
 #ifndef BITAR_HLIT_X4
 #define BITAR_HLIT_X4 1
 #endif
-    constexpr bool X4 = BITAR_HLIT_X4 != 0 && NW == 8;
+#ifndef BITAR_HLIT_ST16
+#define BITAR_HLIT_ST16 1
+#endif
+    // (multi-block hand-offs only: 16 waves per CU whose scattered lane loads and stores keep
+    // the addresser busy; at one wave per SIMD -- the single-block form, long streams -- the
+    // longer dependent chain of the 16-byte form costs more than the addresser time it saves:
+    // stock libzstd-1 decode 5.38 -> 6.35 ms in hlit with it)
+    constexpr bool X4 = BITAR_HLIT_X4 != 0 && NW == 8 && B > 1;
+    constexpr bool ST16 = BITAR_HLIT_ST16 != 0 && B > 1;
     uint32_t W[NW];
 #pragma unroll
     for (uint32_t w = 0; w < NW; ++w) W[w] = zsh::word_raw(src, top - 4 * (int32_t)(w + 1), lo);
@@ -540,9 +548,6 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     const uint32_t mask = (1u << log) - 1u;
     uint64_t acc = 0, prev = 0;
     uint32_t k = 0, ac = 0, half = 0;
-#ifndef BITAR_HLIT_ST16
-#define BITAR_HLIT_ST16 1
-#endif
     auto phase = [&](uint32_t hi, uint32_t lo32, uint32_t& slot) __attribute__((always_inline)) {
       const uint64_t c = ((uint64_t)hi << 32) | lo32;
       auto emit = [&](uint32_t sym) __attribute__((always_inline)) {
@@ -550,7 +555,7 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
         acc |= (uint64_t)sym << (8 * ac);
         ++k;
         if (++ac == 8) {
-          if constexpr (BITAR_HLIT_ST16 != 0) {
+          if constexpr (ST16) {
             // 16 symbols per store: half the store addresses
             if (half) zsh::st16_raw(dst + k - 16, prev, acc);
             else prev = acc;
@@ -617,7 +622,7 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
         }
       }
     }
-    if (BITAR_HLIT_ST16 != 0 && half) lanes::st8(dst + k - ac - 8, prev);
+    if (ST16 && half) lanes::st8(dst + k - ac - 8, prev);
     for (uint32_t r = 0; r < ac; ++r) dst[k - ac + r] = (uint8_t)(acc >> (8 * r));
     ok = 8 * (top - q) - (int32_t)used == 0;
   }

@@ -262,12 +262,11 @@ def test_wide_full_size_roundtrip_and_ratio(eng):
 
 
 @pytest.mark.parametrize("flags", [0, "plain"])
-def test_far_history_work_list(eng, flags):
-    """Large calls (>= 2048 segments, cost-ordered) hand the segments whose matches reach past
-    the decoder's LDS ring to the far kernel through a device work list; the far kernel is a
-    small grid that drains it.  A call mixing stock liblz4 segments (64 KiB history: they
-    defer), our own (never defer) and a few corrupted stock segments (rejected by the far
-    kernel) must decode exactly as the oracle does; plain-order calls take the full far grid."""
+def test_far_history_large_mixed_call(eng, flags):
+    """Large calls (>= 2048 segments, cost-ordered or plain) in which the near kernel defers the
+    segments whose matches reach past its LDS ring to the far kernel: a call mixing stock
+    liblz4 segments (64 KiB history: they defer), our own (never defer) and a few corrupted
+    stock segments (rejected by the far kernel) must decode exactly as the oracle does."""
     import bitar_amd
     import stock_lib as S
     seg, nseg = 65536, 3000
