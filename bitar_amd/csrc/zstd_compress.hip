@@ -952,8 +952,6 @@ __device__ __forceinline__ uint32_t zsq_qbcast(uint32_t v) {  // lane K of each 
 // record.  Same arithmetic as the oracle's per-block walk (bo_zstd_compress_block), bit for
 // bit.
 constexpr uint32_t kWalkSegs = 4;
-// 16 bytes to a 2-byte aligned address
-__device__ __forceinline__ void st16u(GMEM uint16_t* p, const uint4& v) { __builtin_memcpy(p, &v, 16); }
 __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict__ scratch,
                                                         uint64_t sstride, uint32_t seg,
                                                         uint32_t nseg, uint8_t* __restrict__ wscr,
@@ -1008,10 +1006,13 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
   GMEM uint32_t* w = global_ptr(reinterpret_cast<uint32_t*>(wscr + (uint64_t)i * wstride));
   if (blk >= w[kWNb]) return;  // quad-uniform
   const uint32_t s0 = w[kWSb + blk], s1 = w[kWSb + blk + 1];
-  const uint32_t cap = walk_cap(seg);
   const GMEM uint32_t* codes = w + kWWords / 4;
-  GMEM uint16_t* outs = reinterpret_cast<GMEM uint16_t*>(w + kWWords / 4 + cap) + (j < 3 ? j : 0u) * cap;
   const uint32_t c = j == 3 ? 0u : j;  // chain
+  // (walk_state_at: the quad's three chains store 48 contiguous bytes per group of 8)
+  GMEM uint16_t* outs =
+      reinterpret_cast<GMEM uint16_t*>(reinterpret_cast<GMEM uint8_t*>(w) + walk_state_bytes(seg)) +
+      c * 8u;
+  auto at = [](uint32_t k) __attribute__((always_inline)) { return (k >> 3) * 24u + (k & 7u); };
   const uint16_t* tb = tabs[l] + (c == 0 ? kTabOF : c == 1 ? kTabML : kTabLL);
   const uint32_t* tr = trs[l][c == 0 ? 1 : c == 1 ? 2 : 0];
   // this chain's code in the code word (LL 6 bits, OF 5, ML 6)
@@ -1035,11 +1036,16 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
     st = tb[(int32_t)(st >> nb) + tr_f(e)];
     return out;
   };
-  if (j < 3) outs[top] = 0;
+  if (j < 3) outs[at(top)] = 0;
   // k: sequences top - 1 .. s0, as offsets below top (kk = top - 1 - k')
   const int32_t lo = (int32_t)s0;
   int32_t k = (int32_t)top - 1;
   constexpr int32_t kG = 8;
+  // single steps down to a group boundary (k = 8 g + 7)
+  for (; k >= lo && (k & 7) != 7; --k) {
+    const uint32_t o = walk(tr[code(codes[k])]);
+    if (j < 3) outs[at((uint32_t)k)] = (uint16_t)o;
+  }
   // groups of 8: the transforms looked up together (independent of the states), then the
   // chain; the lane's 8 outputs stored together
   uint32_t r[kG];
@@ -1054,17 +1060,18 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
 #pragma unroll
     for (int32_t g = 0; g < kG; ++g) o[g] = walk(e[g]);
     if (j < 3) {
-      // the group's 8 outputs (sequences k - 7 .. k) as ONE 16-byte store: 16-bit stores
-      // scattered over 48 lanes' streams were written back as partial lines (3.0 GB of walk
-      // writes per GiB against 0.7 GB of state bits)
+      // the group's 8 outputs (sequences k - 7 .. k) as ONE 16-byte store, next to the quad's
+      // other two chains': one 48-byte run per quad and group (one stream per chain, 48
+      // streams per wave, were written back as partial lines: 3.0 GB of walk writes per GiB
+      // against 0.7 GB of state bits)
       const uint4 v = make_uint4(o[7] | (o[6] << 16), o[5] | (o[4] << 16), o[3] | (o[2] << 16),
                                  o[1] | (o[0] << 16));
-      st16u(outs + (k - kG + 1), v);
+      *reinterpret_cast<GMEM uint4*>(outs + at((uint32_t)(k - kG + 1))) = v;  // 16-B aligned
     }
   }
   for (; k >= lo; --k) {
     const uint32_t o = walk(tr[code(codes[k])]);
-    if (j < 3) outs[k] = (uint16_t)o;
+    if (j < 3) outs[at((uint32_t)k)] = (uint16_t)o;
   }
   if (j < 3) w[kWFin + 3 * blk + j] = st;
 }
@@ -1112,8 +1119,8 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
   const GMEM uint8_t* src = global_ptr(input + seg_off);
   const GMEM uint8_t* lits = global_ptr(scratch + (uint64_t)i_seg * sstride);
   const GMEM uint2* seqs = reinterpret_cast<const GMEM uint2*>(lits + lit_cap(seg));
-  const uint32_t cap = walk_cap(seg);
-  const GMEM uint16_t* outs = reinterpret_cast<const GMEM uint16_t*>(w + kWWords / 4 + cap);
+  const GMEM uint16_t* outs = reinterpret_cast<const GMEM uint16_t*>(
+      reinterpret_cast<const GMEM uint8_t*>(w) + walk_state_bytes(seg));
   const GMEM uint32_t* whist = w + walk_hist_at(seg) / 4;
   EntOut o;
   o.ring = obuf;
@@ -1274,7 +1281,8 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
       uint32_t bits = 0, zeroed = p0;
       const uint32_t st0 = uniform(w[kWStep + b]);
       auto word = [&](uint32_t j) __attribute__((always_inline)) {  // OF | ML | LL bits, counts
-        const uint32_t oo = outs[j], om = outs[cap + j], ol = outs[2 * cap + j];
+        const uint32_t sa = walk_state_at(j, 0);
+        const uint32_t oo = outs[sa], om = outs[sa + 8], ol = outs[sa + 16];
         const uint32_t nof = oo >> 12, nml = om >> 12, nll = ol >> 12;
         return (oo & 0xFFFu) | ((om & 0xFFFu) << nof) | ((ol & 0xFFFu) << (nof + nml)) |
                ((nof + nml + nll) << 26);

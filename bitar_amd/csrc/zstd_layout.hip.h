@@ -22,7 +22,8 @@ constexpr uint32_t kBlocks = 4, kMultiMin = 64;
 // record of kW* words; the Huffman codes (256 u32: code | length << 16); the FSE state tables
 // (u16, kTabDummy + 1) and transforms (3 x 64 u32); then per sequence its three codes (u32:
 // LL | OF << 6 | ML << 11, written by the entropy kernel) and each chain's state bits | their
-// count << 12 (u16, chains OF, ML, LL one array each); then per step of up to 64 sequences
+// count << 12 (u16) in groups of 8 sequences: group g holds the OF, ML and LL words of
+// sequences 8g .. 8g + 7, 8 of each chain (walk_state_at); then per step of up to 64 sequences
 // (steps start at each block's first sequence) the repeat-offset history before it (3 u32),
 // from which zstd_emit_kernel re-derives the offset values of the step
 enum : uint32_t {
@@ -50,8 +51,15 @@ __host__ __device__ constexpr uint32_t walk_cap(uint32_t seg) { return seg / 4u 
 __host__ __device__ constexpr uint32_t walk_steps(uint32_t seg) {
   return (walk_cap(seg) + 63u) / 64u + kBlocks;  // (a block's steps start at its first sequence)
 }
+// u16 index of chain c's state word of sequence k in the state area (chains 0 OF, 1 ML, 2 LL)
+__host__ __device__ constexpr uint32_t walk_state_at(uint32_t k, uint32_t c) {
+  return (k >> 3) * 24u + c * 8u + (k & 7u);
+}
+__host__ __device__ constexpr uint64_t walk_state_bytes(uint32_t seg) {  // bytes, from the record (16-B aligned)
+  return ((uint64_t)kWWords + 4ull * walk_cap(seg) + 15u) & ~15ull;
+}
 __host__ __device__ constexpr uint64_t walk_hist_at(uint32_t seg) {  // bytes, from the record (16-B aligned)
-  return ((uint64_t)kWWords + 10ull * walk_cap(seg) + 15u) & ~15ull;
+  return walk_state_bytes(seg) + 48ull * ((walk_cap(seg) + 7u) / 8u);
 }
 __host__ __device__ constexpr uint64_t walk_stride(uint32_t seg) {
   return (walk_hist_at(seg) + 12ull * walk_steps(seg) + 255u) & ~255ull;
