@@ -724,6 +724,11 @@ static uint32_t hlit_segs() {
   static const uint32_t v = pow2_knob("BITAR_HIP_HLIT_SEGS", 16);
   return v;
 }
+// (tuning knob: 1 puts the forked single-block literal kernel on the side stream after the
+// multi-block one instead of on the caller's stream after phase A)
+#ifndef BITAR_HLIT1_SIDE
+#define BITAR_HLIT1_SIDE 0
+#endif
 static uint32_t seqdec_segs() {
   static const uint32_t v = pow2_knob("BITAR_HIP_SEQDEC_SEGS", 16);
   return v;
@@ -898,12 +903,21 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
       hipStream_t a = fork ? side_stream_for(ctx, ctx->aux_streams, s) : nullptr;
       if (a && stream_after(a, s)) a = nullptr;
       // single-block hand-offs (16 segments x 4 streams / chains per wave) and, with the
-      // two-phase path, the multi-block ones (4 segments x 4 blocks x 4 per wave)
-      auto hlit = [&](hipStream_t s) {
+      // two-phase path, the multi-block ones (4 segments x 4 blocks x 4 per wave).  Forked
+      // (fork 1), the single-block literal kernel goes on the caller's stream after phase A:
+      // ahead of the multi-block literals on the side stream, its 36 KiB workgroups -- which
+      // exit at once on this engine's multi-block frames -- waited for CU room behind phase A,
+      // and the multi-block literals behind them (1 GiB kind 2: 1.3 ms on the call's path).
+      const bool split = a && fork == 1;
+      auto hlit1 = [&](hipStream_t s) {
         if (hs_n == 4) BITAR_HLIT(4, 1, nullptr);
         else if (hs_n == 8) BITAR_HLIT(8, 1, nullptr);
         else BITAR_HLIT(16, 1, nullptr);
+      };
+      auto hlit = [&](hipStream_t s) {
+        if (!split) hlit1(s);
         if (seq) BITAR_HLIT(4, 4, olit.order);
+        if (split && BITAR_HLIT1_SIDE) hlit1(s);
       };
       auto seqdec = [&](hipStream_t s) {
 #define BITAR_SEQDEC(N, B, O)                                                                 \
@@ -921,6 +935,7 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
       } else {
         hlit(a ? a : s);
         if (seq) seqdec(s);
+        if (split && !BITAR_HLIT1_SIDE) hlit1(s);
       }
       if (seq) {
         if (a && stream_after(s, a)) (void)hipStreamSynchronize(a);  // (join failed: wait here)

@@ -384,6 +384,19 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
 // literals, 1 <= offset <= output so far) from the batch's prefix sums -- and the frame's
 // content size at the end; a failure sets SEGMENT_ERROR and the error word.  The literal
 // tail is read ahead of every store: room for the unread literals was checked.
+// A block's literals (raw or Huffman) stream through an LDS ring of two 512-B rows, one
+// aligned 16-B block per lane of the first 32, the next row held in registers a row of
+// literals ahead: a step reads its literal bytes from LDS instead of waiting on HBM (the
+// prefetched rows lie at or past the next literal, which no output store has reached: the
+// room rule).  1 GiB decode against literal loads from HBM: kind 1 4.08 -> 3.96 ms, kinds
+// 2 / 5 equal; 1 KiB rows cost occupancy (6.7 KiB of LDS: 23 waves per CU) and were slower.
+#ifndef BITAR_EXEC_LRING
+#define BITAR_EXEC_LRING 1
+#endif
+#ifndef BITAR_EXEC_LROW
+#define BITAR_EXEC_LROW 512
+#endif
+constexpr uint32_t kLRow = BITAR_EXEC_LROW, kLRing = 2 * kLRow;
 __global__ __launch_bounds__(64) void zstd_exec_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, uint32_t nseg, uint32_t seg, uint8_t* __restrict__ out,
@@ -397,6 +410,7 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   // the scalar unit, shared by the CU's waves, bounds this kernel)
   __shared__ __attribute__((aligned(16))) uint8_t ring[kRing + kWave];
   __shared__ uint32_t ev[2 * kWave];
+  __shared__ __attribute__((aligned(16))) uint8_t lring[BITAR_EXEC_LRING ? kLRing : 16];
   if (blockIdx.x >= nseg) return;
   const uint32_t i = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   if (i >= nseg || uniform(produced[i]) != kRecs) return;
@@ -421,7 +435,23 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   bool ok = true;
   // per block: literal index j -> byte: lsrc[j] (raw / Huffman) or the RLE byte
   uint32_t lt = 0, lbyte = 0;
-  const GMEM uint8_t* lsafe = s.dst;
+  // the literal ring: literal index j of the block at lring[(la + j) & (kLRing - 1)] (absolute
+  // addressing: an aligned HBM block is an aligned ring block); indices [lF - kLRing, lF) are
+  // staged, lnx holds row lrow; lnext = the next literal index a step takes
+  uint64_t la = 0, lend = 0;
+  const GMEM uint8_t* lsafe = s.dst;  // (BITAR_EXEC_LRING 0: literals read from HBM)
+  uint32_t lF = 0, lrow = 0, lnext = 0;
+  uint4 lnx = make_uint4(0, 0, 0, 0);
+  auto lrow_load = [&](uint32_t r) __attribute__((always_inline)) -> uint4 {
+    const uint64_t a = (la & ~15ull) + (uint64_t)kLRow * r + 16u * lane;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (16u * lane < kLRow && a < lend) v = *reinterpret_cast<const GMEM uint4*>(a);
+    return v;
+  };
+  auto lrow_write = [&](uint32_t r, const uint4& v) __attribute__((always_inline)) {
+    const uint32_t a = (uint32_t)(la & ~15ull) + kLRow * r + 16u * lane;
+    if (16u * lane < kLRow) *reinterpret_cast<uint4*>(lring + (a & (kLRing - 1))) = v;
+  };
   // one 64-byte step at output [xa, xa + 64) ∩ [.., xa + act): e = the run each lane lies in
   // (key << 24 | payload: odd key = literals, payload = output pos - literal index; even key
   // = match, payload = offset)
@@ -442,8 +472,21 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
     // every lane loads both candidates (branch-free): its literal byte (index 0 for the
     // others) and its ring byte
     const bool lit = act && !ism;
-    const uint32_t vl = lt == 1 ? lbyte : (uint32_t)lsafe[lit ? from : 0u];
+    if (BITAR_EXEC_LRING && lt != 1 && lnext + kWave > lF) {  // stage the next row (it overwrites row lrow - 2)
+      lds_order();
+      lrow_write(lrow, lnx);
+      lF += kLRow;
+      ++lrow;
+      lnx = lrow_load(lrow);
+    }
     lds_order();
+    uint32_t vl;
+    if constexpr (BITAR_EXEC_LRING != 0) {
+      vl = lt == 1 ? lbyte : (uint32_t)lring[((uint32_t)la + from) & (kLRing - 1)];
+      lnext += (uint32_t)__builtin_popcountll(ballot(lit));
+    } else {
+      vl = lt == 1 ? lbyte : (uint32_t)lsafe[lit ? from : 0u];
+    }
     const uint32_t vr = ring[(base + from) & kRingMask];
     uint32_t v = lit ? vl : vr;
     if (ballot(far)) {  // (rare)
@@ -475,13 +518,31 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
     lt = w3 >> 24;
     lbyte = litv & 0xFFu;
     const GMEM uint8_t* lsrc = lt == 0 ? src + litv : tail + xlit;
-    // (a literal-less block's lsrc may lie past the buffer: index 0 of the output instead)
-    lsafe = regen ? lsrc : s.dst;
+    lnext = 0;
+    lsafe = regen ? lsrc : s.dst;  // (a literal-less block's lsrc may lie past the buffer)
+    if (BITAR_EXEC_LRING && lt != 1) {  // prime the ring with rows 0 and 1, row 2 in registers
+      la = (uint64_t)(uintptr_t)lsrc;
+      lend = la + regen;  // (no literals: nothing is loaded)
+      const uint4 v0 = lrow_load(0), v1 = lrow_load(1);
+      lnx = lrow_load(2);
+      lds_order();
+      lrow_write(0, v0);
+      lrow_write(1, v1);
+      lrow = 2;
+      lF = kLRing - (uint32_t)(la & 15u);
+    }
     const GMEM uint64_t* rec = global_ptr(recs + (uint64_t)i * rcap + xrec);
     uint32_t lp = 0;
+    // the records of the next 64 sequences are loaded while this batch runs
+    uint64_t rn = 0;
+    if (nseq) rn = rec[lane < nseq ? lane : nseq - 1];
     for (uint32_t kb = 0; kb < nseq; kb += kWave) {
       const uint32_t n = nseq - kb < kWave ? nseq - kb : kWave;
-      const uint64_t r0 = rec[kb + (lane < n ? lane : n - 1)];
+      const uint64_t r0 = rn;
+      if (kb + kWave < nseq) {
+        const uint32_t kn = kb + kWave + lane;
+        rn = rec[kn < nseq ? kn : nseq - 1];
+      }
       const uint64_t r = lane < n ? r0 : 0ull;
       const uint32_t lf = (uint32_t)r & 0x3FFFFFu, mf = (uint32_t)(r >> 22) & 0x3FFFFFu;
       uint32_t lb, lx, mb, mx;
