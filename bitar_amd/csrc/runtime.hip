@@ -880,9 +880,10 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
 #define BITAR_ZSTD_TAIL(K, N)                                                                 \
   hipLaunchKernelGGL(bitar_hip::K<N>, dim3((cn + N - 1) / N), dim3(64), 0, s, csrcs, cslab, stride, \
                      csz, cn, seg, cout, cprod, hs, ew)
+  // (the multi-block kernels (B > 1) take units of 4 blocks: 2 cn of them)
 #define BITAR_HLIT(N, B, O)                                                                   \
-  hipLaunchKernelGGL((bitar_hip::zstd_hlit_kernel<N, B>), dim3((cn + N - 1) / N), dim3(64), 0, s,  \
-                     csrcs, cslab, stride, csz, cn, seg, cout, cprod, hs, ew, O)
+  hipLaunchKernelGGL((bitar_hip::zstd_hlit_kernel<N, B>), dim3(((B > 1 ? 2 : 1) * cn + N - 1) / N), \
+                     dim3(64), 0, s, csrcs, cslab, stride, csz, cn, seg, cout, cprod, hs, ew, O)
       // the literal streams beside the sequences' phase A: one of the two on the aux stream
       // (zstd_fork 1: the literals there, launched first; 2: phase A there, first)
       // the multi-block lane kernels take their segments most expensive first (by sequences /
@@ -890,12 +891,12 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
       // index order would give whole CUs the same kind of segment)
       SegOrder oseq, olit;
       if (seq) {
-        (void)oseq.make(ctx, s, cn, nullptr, [&](uint32_t* keys) {
-          hipLaunchKernelGGL(bitar_hip::hand_key_kernel, dim3((cn + 63) / 64), dim3(64), 0, s,
+        (void)oseq.make(ctx, s, 2 * cn, nullptr, [&](uint32_t* keys) {
+          hipLaunchKernelGGL(bitar_hip::hand_key_kernel, dim3((2 * cn + 63) / 64), dim3(64), 0, s,
                              cprod, hs, cn, 0u, keys);
         }, 0, 1);
-        (void)olit.make(ctx, s, cn, nullptr, [&](uint32_t* keys) {
-          hipLaunchKernelGGL(bitar_hip::hand_key_kernel, dim3((cn + 63) / 64), dim3(64), 0, s,
+        (void)olit.make(ctx, s, 2 * cn, nullptr, [&](uint32_t* keys) {
+          hipLaunchKernelGGL(bitar_hip::hand_key_kernel, dim3((2 * cn + 63) / 64), dim3(64), 0, s,
                              cprod, hs, cn, 1u, keys);
         }, 0, 2);
       }
@@ -921,8 +922,9 @@ static int decompress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec,
       };
       auto seqdec = [&](hipStream_t s) {
 #define BITAR_SEQDEC(N, B, O)                                                                 \
-  hipLaunchKernelGGL((bitar_hip::zstd_seqdec_kernel<N, B>), dim3((cn + N - 1) / N), dim3(64), 0, s, \
-                     csrcs, cslab, stride, csz, cn, seg, cprod, hs, rp, rcap, ew, stats, O)
+  hipLaunchKernelGGL((bitar_hip::zstd_seqdec_kernel<N, B>), dim3(((B > 1 ? 2 : 1) * cn + N - 1) / N), \
+                     dim3(64), 0, s, csrcs, cslab, stride, csz, cn, seg, cprod, hs, rp, rcap, ew, \
+                     stats, O)
         if (sd == 4) BITAR_SEQDEC(4, 1, nullptr);
         else if (sd == 8) BITAR_SEQDEC(8, 1, nullptr);
         else BITAR_SEQDEC(16, 1, nullptr);

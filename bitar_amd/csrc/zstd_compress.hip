@@ -843,7 +843,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
   // ---- sequences: the blocks (equal sequence counts), repeat offsets (rep_scan), codes,
   // histograms, 64 sequences per step from each block's first; the history before each step
   // goes to the walk scratch (the records stay as the parse wrote them) ----
-  const uint32_t nb = nseq >= kMultiMin ? kBlocks : 1u;
+  const uint32_t nb = frame_blocks(nseq, nlit);
   uint32_t tdesc = 0;
   if (nseq) {
     for (uint32_t k = lane; k < 3 * 64; k += kWave) (&L.sh[0][0])[k] = 0;
@@ -944,7 +944,7 @@ __device__ __forceinline__ uint32_t zsq_qbcast(uint32_t v) {  // lane K of each 
 
 // ---- pass 3: the FSE state chains, four lanes per chain set --------------------------------
 // Lane 16 l + 4 b + j of the wave walks chain j (0 offsets, 1 match lengths, 2 literal
-// lengths; 3 repeats 0) of block b of segment blockIdx.x * 4 + l, the block's last sequence
+// lengths; 3 repeats 0) of block b (then b + 4) of segment blockIdx.x * 4 + l, the block's last sequence
 // first, with the segment's state table and transforms in LDS: the chains of a block are
 // independent of each other and of the other blocks' (each block's states start from its own
 // last sequence), so each is a lane's own loop.  Per sequence the lane stores its chain's
@@ -959,7 +959,7 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
                                                         const uint32_t* __restrict__ order) {
   using namespace cmp;
   using namespace zse;
-  static_assert(kWalkSegs * kBlocks * 4 == kWave, "a lane per chain");
+  static_assert(kWalkSegs * 4 * 4 == kWave && kBlocks <= 8, "a lane per chain of 4 blocks");
   __shared__ __attribute__((aligned(16))) uint16_t tabs[kWalkSegs][1284];
   __shared__ uint32_t trs[kWalkSegs][3][64];
   const uint32_t lane = lane_id();
@@ -998,14 +998,13 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
     for (uint32_t e = 0; e < 3; ++e) (&trs[l][0][0])[lane + e * kWave] = rv[e];
   }
   lds_order();
-  const uint32_t l = lane >> 4, blk = (lane >> 2) & 3u, j = lane & 3u;
+  const uint32_t l = lane >> 4, j = lane & 3u;
   const uint32_t b = blockIdx.x * kWalkSegs + l;
   // (fetched while every lane is active: a disabled source lane reads as 0)
   const uint32_t i = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(l << 2), (int)il0);
   if (b >= nseg || !((hm >> l) & 1u)) return;  // uniform over the segment's 16 lanes
   GMEM uint32_t* w = global_ptr(reinterpret_cast<uint32_t*>(wscr + (uint64_t)i * wstride));
-  if (blk >= w[kWNb]) return;  // quad-uniform
-  const uint32_t s0 = w[kWSb + blk], s1 = w[kWSb + blk + 1];
+  const uint32_t nbk = w[kWNb];
   const GMEM uint32_t* codes = w + kWWords / 4;
   const uint32_t c = j == 3 ? 0u : j;  // chain
   // (walk_state_at: the quad's three chains store 48 contiguous bytes per group of 8)
@@ -1018,6 +1017,9 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
   // this chain's code in the code word (LL 6 bits, OF 5, ML 6)
   const uint32_t csh = c == 0 ? 6u : c == 1 ? 11u : 0u, cmask = c == 0 ? 31u : 63u;
   auto code = [&](uint32_t cw) __attribute__((always_inline)) { return (cw >> csh) & cmask; };
+  // quad q walks blocks q and q + 4 (8-block frames), one after the other (quad-uniform)
+  for (uint32_t blk = (lane >> 2) & 3u; blk < nbk; blk += 4) {
+  const uint32_t s0 = w[kWSb + blk], s1 = w[kWSb + blk + 1];
   // the block's last sequence initialises the states (no state bits)
   const uint32_t top = s1 - 1;
   uint32_t st;
@@ -1074,6 +1076,7 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
     if (j < 3) outs[at((uint32_t)k)] = (uint16_t)o;
   }
   if (j < 3) w[kWFin + 3 * blk + j] = st;
+  }
 }
 
 // ---- pass 4: the frame -----------------------------------------------------------------------
@@ -1138,13 +1141,18 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
                         : lane == 5 ? fcs & 0xFFu : fcs >> 8;
     o.put(hb, fh);
   }
-  uint32_t bpos[kBlocks], bhdr[kBlocks];
-  // per block, a Huffman literal section's header and jump table, written at the end (their
-  // sizes are known once the streams are): position (0: none), header size, header value,
-  // jump table position (0: none) and stream sizes
-  uint32_t ppos[kBlocks] = {0, 0, 0, 0}, phs[kBlocks] = {0, 0, 0, 0}, pjt[kBlocks] = {0, 0, 0, 0};
-  uint32_t pz[kBlocks] = {0, 0, 0, 0}, pz2[kBlocks] = {0, 0, 0, 0};
-  uint64_t ph[kBlocks] = {0, 0, 0, 0};
+  // per block (LDS, uniform): its header's position and value, and a Huffman literal
+  // section's header and jump table, written at the end (their sizes are known once the
+  // streams are): position (0: none), header size, header value (2 words), jump table
+  // position (0: none) and stream sizes
+  enum : uint32_t { kBPos, kBHdr, kPPos, kPHs, kPH0, kPH1, kPJt, kPZ, kPZ2, kBW };
+  __shared__ uint32_t bm[kBlocks][kBW];
+  for (uint32_t k = lane; k < kBlocks * kBW; k += kWave) (&bm[0][0])[k] = 0;
+  auto bset = [&](uint32_t b, uint32_t f, uint32_t v) __attribute__((always_inline)) {
+    lds_order();
+    if (lane == 0) bm[b][f] = v;
+    lds_order();
+  };
   bool tree_sent = false;
   // literals [a, a + m) of the segment's literal area as a Huffman stream (oracle
   // zs_literals_block): symbols from the last, 64 per step, from 1 KiB blocks of aligned
@@ -1188,7 +1196,7 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
   };
   for (uint32_t b = 0; b < nb && !o.overflow; ++b) {
     const uint32_t blk = o.op;
-    bpos[b] = blk;
+    bset(b, kBPos, blk);
     o.room(3);
     o.op += 3;  // the block header, written last
     // ---- literal section ----
@@ -1236,12 +1244,13 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
         if (!o.overflow && (int32_t)total < limit) {
           const uint64_t h = (tree_sent ? 3u : 2u) | (sf << 2) | ((uint64_t)m << 4) |
                              ((uint64_t)total << (hs == 3 ? 14 : hs == 4 ? 18 : 22));
-          ppos[b] = sec;
-          phs[b] = hs;
-          ph[b] = h;
-          pjt[b] = ns == 4 ? jt : 0u;
-          pz[b] = z0 | (z1 << 16);
-          pz2[b] = z2;
+          bset(b, kPPos, sec);
+          bset(b, kPHs, hs);
+          bset(b, kPH0, (uint32_t)h);
+          bset(b, kPH1, (uint32_t)(h >> 32));
+          bset(b, kPJt, ns == 4 ? jt : 0u);
+          bset(b, kPZ, z0 | (z1 << 16));
+          bset(b, kPZ2, z2);
           tree_sent = true;
           coded = true;
         } else if (!o.overflow) {  // rewind: raw after all
@@ -1331,7 +1340,7 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
         o.op = p0 + ((bits + 7) >> 3);
       }
     }
-    bhdr[b] = (b + 1 == nb ? 1u : 0u) | (2u << 1) | ((o.op - (blk + 3)) << 3);
+    bset(b, kBHdr, (b + 1 == nb ? 1u : 0u) | (2u << 1) | ((o.op - (blk + 3)) << 3));
   }
   // the blocks, or one raw block when they are not smaller than the segment
   const bool stored = o.overflow || o.op - (fh + 3) >= n;
@@ -1341,33 +1350,31 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
     global_fence_wave();                     // earlier stores to this range land first
     wave_copy_global(o.dst + fh + 3, src, n);
     o.op = fh + 3 + n;
-    bpos[0] = fh;
-    bhdr[0] = 1u | (n << 3);
+    bset(0, kBPos, fh);
+    bset(0, kBHdr, 1u | (n << 3));
   } else {
     o.flush(o.op, true);
   }
   global_fence_wave();
   const uint32_t nh = stored ? 1u : nb;
+  lds_order();
   if (lane < 3 * nh) {
     const uint32_t bi = lane / 3, byte = lane - 3 * bi;
-    const uint32_t at = bi == 0 ? bpos[0] : bi == 1 ? bpos[1] : bi == 2 ? bpos[2] : bpos[3];
-    const uint32_t hv = bi == 0 ? bhdr[0] : bi == 1 ? bhdr[1] : bi == 2 ? bhdr[2] : bhdr[3];
-    o.dst[at + byte] = (uint8_t)(hv >> (8 * byte));
+    o.dst[bm[bi][kBPos] + byte] = (uint8_t)(bm[bi][kBHdr] >> (8 * byte));
   }
   if (!stored) {
-    // the Huffman literal sections' headers (lanes 16 b + k, k < 5) and jump tables (16 b + 8
-    // + k, k < 6)
-    const uint32_t bi = lane >> 4, k = lane & 15u;
-    const uint32_t pp = bi == 0 ? ppos[0] : bi == 1 ? ppos[1] : bi == 2 ? ppos[2] : ppos[3];
-    const uint32_t hs = bi == 0 ? phs[0] : bi == 1 ? phs[1] : bi == 2 ? phs[2] : phs[3];
-    const uint32_t jt = bi == 0 ? pjt[0] : bi == 1 ? pjt[1] : bi == 2 ? pjt[2] : pjt[3];
-    const uint32_t zz = bi == 0 ? pz[0] : bi == 1 ? pz[1] : bi == 2 ? pz[2] : pz[3];
-    const uint32_t z2 = bi == 0 ? pz2[0] : bi == 1 ? pz2[1] : bi == 2 ? pz2[2] : pz2[3];
-    const uint64_t hv = bi == 0 ? ph[0] : bi == 1 ? ph[1] : bi == 2 ? ph[2] : ph[3];
-    if (bi < nb && hs && k < hs) o.dst[pp + k] = (uint8_t)(hv >> (8 * k));
-    if (bi < nb && jt && k >= 8 && k < 14) {
-      const uint32_t e = k - 8, sv = e < 2 ? zz & 0xFFFFu : e < 4 ? zz >> 16 : z2;
-      o.dst[jt + e] = (uint8_t)((e & 1u) ? sv >> 8 : sv & 0xFFu);
+    // the Huffman literal sections' headers (lanes 16 b' + k, k < 5) and jump tables (16 b' +
+    // 8 + k, k < 6) of blocks b' and b' + 4
+    const uint32_t k = lane & 15u;
+    for (uint32_t bi = lane >> 4; bi < nb; bi += 4) {
+      const uint32_t pp = bm[bi][kPPos], hs = bm[bi][kPHs], jt = bm[bi][kPJt];
+      const uint32_t zz = bm[bi][kPZ], z2 = bm[bi][kPZ2];
+      const uint64_t hv = (uint64_t)bm[bi][kPH0] | ((uint64_t)bm[bi][kPH1] << 32);
+      if (hs && k < hs) o.dst[pp + k] = (uint8_t)(hv >> (8 * k));
+      if (jt && k >= 8 && k < 14) {
+        const uint32_t e = k - 8, sv = e < 2 ? zz & 0xFFFFu : e < 4 ? zz >> 16 : z2;
+        o.dst[jt + e] = (uint8_t)((e & 1u) ? sv >> 8 : sv & 0xFFu);
+      }
     }
   }
   if (lane == 0) sizes[i_seg] = o.op;

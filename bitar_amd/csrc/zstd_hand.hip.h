@@ -20,8 +20,8 @@ namespace bitar_hip {
 
 namespace zhand {
 
-constexpr uint32_t kMaxBlocks = 4;
-constexpr uint32_t kRec = 136, kCells = 512, kHufWords = 1024;
+constexpr uint32_t kMaxBlocks = 8;
+constexpr uint32_t kRec = 256, kCells = 512, kHufWords = 1024;
 constexpr uint32_t kCellsAt = kRec, kHufAt = kRec + 3 * kCells;
 constexpr uint64_t kStride = 4ull * (kRec + 3 * kCells + kHufWords);
 constexpr uint32_t kHanded = 0xFFFFFFFDu;  // produced[i] while the lane kernels own segment i
@@ -51,10 +51,13 @@ __host__ __device__ constexpr uint32_t blk_at(uint32_t b) { return b == 0 ? 0u :
 // kX0 + kXW b: its first record (zstd_seqdec_kernel's records, in block order), its literals'
 // offset in the slot tail [cap - kLitAll, cap), and its final repeat offsets (written by
 // zstd_seqdec_kernel: for b >= 1 in terms of the history before the block, see zstd_seq.hip)
-enum : uint32_t { kNb = 96, kNseqAll, kLitAll, kX0 = 100 };
+enum : uint32_t { kNb = 176, kNseqAll, kLitAll, kX0 = 180 };
 enum : uint32_t { kXRec = 0, kXLit, kXFin0, kXFin1, kXFin2 };
 constexpr uint32_t kXW = 8;
 static_assert(blk_at(kMaxBlocks - 1) + kBlkW <= kNb && kX0 + kXW * kMaxBlocks <= kRec, "layout");
+// The multi-block lane kernels take a frame's blocks in groups of 4 ("units": unit 2 i + g =
+// blocks 4 g .. 4 g + 3 of segment i); a frame of <= 4 blocks has one unit.
+constexpr uint32_t kUnitBlocks = 4;
 
 }  // namespace zhand
 

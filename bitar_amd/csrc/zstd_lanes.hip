@@ -421,7 +421,8 @@ __device__ __forceinline__ bool lits_pending(uint32_t p) {
 // B: the blocks of a segment in the wave (lane 4 B l + 4 b + j = stream j of block b of
 // segment l): B = 1 takes the frames that handed their last block only (kNb == 1), B = 4 the
 // multi-block hand-offs (kNb >= 2: the streams of all of a frame's blocks run at once, their
-// literals going to each block's place in the slot tail, zstd_hand.hip.h kXLit).
+// literals going to each block's place in the slot tail, zstd_hand.hip.h kXLit) by units of 4
+// blocks (slot l = unit blockIdx.x * S + l: blocks 4 g + b of segment unit >> 1, g = unit & 1).
 template <uint32_t S, uint32_t B>
 __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
@@ -444,20 +445,26 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
   // (pend: any block's streams pending; hlg: the table log, the same for every block)
   // (order: the segments by literal count, most first, hand_key_kernel: slot x takes
   // segment order[x])
-  uint32_t p0 = 0, pend = 0, hlg = 0, nbh = 0, il0 = 0;
+  static_assert(B == 1 || B == kUnitBlocks, "whole units");
+  const uint32_t nun = B > 1 ? 2 * nseg : nseg;  // units
+  uint32_t p0 = 0, pend = 0, hlg = 0, nbh = 0, il0 = 0, g0 = 0;
   {
     const uint32_t bl = blockIdx.x * S + lane;
-    const uint32_t il = bl < nseg ? (order ? order[bl] : bl) : bl;
+    const uint32_t u = bl < nun ? (order ? order[bl] : bl) : bl;
+    const uint32_t il = B > 1 ? u >> 1 : u;
     il0 = il;
-    if (lane < S && il < nseg) {
+    g0 = B > 1 ? u & 1u : 0u;
+    if (lane < S && bl < nun && il < nseg) {
       const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
       p0 = produced[il];
       nbh = h[kNb];
       uint32_t pd = 0, lg = 0;
 #pragma unroll
       for (uint32_t b = 0; b < B; ++b) {
-        const uint32_t pb = h[blk_at(b) + kLitPend], lb = h[blk_at(b) + kHufLog];
-        const bool in = b < nbh && pb == 1u;
+        const uint32_t bb = B * g0 + b;
+        const uint32_t pb = h[blk_at(bb < kMaxBlocks ? bb : 0u) + kLitPend];
+        const uint32_t lb = h[blk_at(bb < kMaxBlocks ? bb : 0u) + kHufLog];
+        const bool in = bb < nbh && pb == 1u;
         pd |= in ? 1u : 0u;
         lg = in ? lb : lg;
       }
@@ -488,10 +495,12 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     }
   }
   lds_order();
-  const uint32_t l = lane / (4 * B), bk = (lane >> 2) % B, j = lane & 3u;
+  const uint32_t l = lane / (4 * B), j = lane & 3u;
   // (fetched while every lane is active: a disabled source lane reads as 0)
   const uint32_t i = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l < S ? l : 0u) << 2), (int)il0);
-  if (l >= S || blockIdx.x * S + l >= nseg || !((tm >> l) & 1u)) return;
+  const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l < S ? l : 0u) << 2), (int)g0);
+  const uint32_t bk = B * g + (lane >> 2) % B;  // the block
+  if (l >= S || blockIdx.x * S + l >= nun || !((tm >> l) & 1u)) return;
   const GMEM uint32_t* h0 = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
   if (bk >= h0[kNb]) return;
   const GMEM uint32_t* h = h0 + blk_at(bk);

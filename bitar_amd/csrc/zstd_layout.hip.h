@@ -13,10 +13,14 @@ __host__ __device__ constexpr uint64_t scratch_stride(uint32_t seg) {
   return (lit_cap(seg) + 8ull * (seg / 4u + 2u) + 255u) & ~255ull;
 }
 
-// Blocks per frame (oracle ZS_MAX_BLOCKS / ZS_MULTI_MIN): a frame with >= kMultiMin sequences
-// is kBlocks compressed blocks of equal sequence counts, sharing one literal code and one set
-// of sequence tables; block b holds sequences [b nseq / B, (b + 1) nseq / B).
-constexpr uint32_t kBlocks = 4, kMultiMin = 64;
+// Blocks per frame (oracle zs_nblocks): a frame with >= kMultiMin sequences is 4 compressed
+// blocks of equal sequence counts -- 8 (kBlocks) with >= kWideLit literal bytes -- sharing one
+// literal code and one set of sequence tables; block b holds sequences [b nseq / B,
+// (b + 1) nseq / B).
+constexpr uint32_t kBlocks = 8, kMultiMin = 64, kWideLit = 32768;
+__host__ __device__ constexpr uint32_t frame_blocks(uint32_t nseq, uint32_t nlit) {
+  return nseq < kMultiMin ? 1u : nlit >= kWideLit ? 8u : 4u;
+}
 
 // walk scratch (zstd_entropy_kernel -> zstd_walk_kernel -> zstd_emit_kernel), per segment: a
 // record of kW* words; the Huffman codes (256 u32: code | length << 16); the FSE state tables
@@ -37,14 +41,18 @@ enum : uint32_t {
   kWTdesc,       // bytes of the modes byte + table descriptions (kWDescAt)
   kWTb,          // coded bits of all literals (sum of length x count): the blocks' estimate
   kWSb = 16,     // kBlocks + 1 words: first sequence of each block (then nseq)
-  kWLb = 21,     // kBlocks + 1 words: first literal of each block (then nlit)
-  kWStep = 26,   // kBlocks words: first history step of each block
-  kWFin = 32,    // kBlocks x 3 words: each block's final states (OF, ML, LL)
-  kWTreeAt = 48,  // the Huffman tree description (<= 130 bytes)
-  kWDescAt = 84,  // modes byte + sequence table descriptions (<= 256 bytes)
-  kWCodeAt = 160  // 256 words: literal codes
+  kWLb = 25,     // kBlocks + 1 words: first literal of each block (then nlit)
+  kWStep = 34,   // kBlocks words: first history step of each block
+  kWFin = 42,    // kBlocks x 3 words: each block's final states (OF, ML, LL)
+  kWTreeAt = 68,  // the Huffman tree description (<= 130 bytes)
+  kWDescAt = 104,  // modes byte + sequence table descriptions (<= 256 bytes)
+  kWCodeAt = 168   // 256 words: literal codes
 };
-constexpr uint32_t kWTabs = 4 * 416, kWTr = kWTabs + 2 * 1284, kWWords = kWTr + 3 * 64 * 4;
+static_assert(kWLb == kWSb + kBlocks + 1 && kWStep == kWLb + kBlocks + 1 &&
+                  kWFin == kWStep + kBlocks && kWTreeAt >= kWFin + 3 * kBlocks &&
+                  kWDescAt >= kWTreeAt + 33 && kWCodeAt >= kWDescAt + 64,
+              "record areas");
+constexpr uint32_t kWTabs = 4 * 424, kWTr = kWTabs + 2 * 1284, kWWords = kWTr + 3 * 64 * 4;
 static_assert(kWCodeAt + 256 <= kWTabs / 4, "record words before the tables");
 static_assert(kWTabs % 16 == 0 && kWWords % 8 == 0, "aligned areas");
 __host__ __device__ constexpr uint32_t walk_cap(uint32_t seg) { return seg / 4u + 2u; }  // >= nseq

@@ -143,7 +143,9 @@ __device__ __forceinline__ Step step_of(uint32_t cell, uint32_t al) {
 // ---- phase A -----------------------------------------------------------------------------
 // L segments per wave (lane l < L owns segment blockIdx.x * L + l), B chains (blocks) per
 // segment: B = 1 takes the frames that handed their last block only (kNb == 1), B = 4 the
-// multi-block hand-offs (kNb >= 2), whose blocks' chains run side by side.  A segment is
+// multi-block hand-offs (kNb >= 2), whose blocks' chains run side by side -- by units of 4
+// blocks (zstd_hand.hip.h kUnitBlocks: slot l owns unit blockIdx.x * L + l, blocks 4 g ..
+// 4 g + 3 of segment unit >> 1, g = unit & 1; 2 nseg units).  A segment is
 // taken when the wave decoder handed it over (produced == kHanded) and it has at most `rcap`
 // sequences; on success (every chain's bitstream consumed exactly) produced = kRecs, else
 // SEGMENT_ERROR and the stream's error word; the sequence rules are checked by
@@ -166,12 +168,16 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
   // before the first is used: at about one wave per SIMD every serial load is exposed.
   // (order: the segments by sequence count, most first, hand_key_kernel: slot x takes
   // segment order[x], so a wave's chains are of similar length and the longest start first)
-  uint32_t p0 = 0, nq0 = 0, als0 = 0, nb0 = 0, il0 = 0;
+  static_assert(B == 1 || B == kUnitBlocks, "whole units");
+  const uint32_t nun = B > 1 ? 2 * nseg : nseg;  // units
+  uint32_t p0 = 0, nq0 = 0, als0 = 0, nb0 = 0, il0 = 0, g0 = 0;
   {
     const uint32_t bl = blockIdx.x * L + lane;
-    const uint32_t il = bl < nseg ? (order ? order[bl] : bl) : bl;
+    const uint32_t u = bl < nun ? (order ? order[bl] : bl) : bl;
+    const uint32_t il = B > 1 ? u >> 1 : u;
     il0 = il;
-    if (lane < L && il < nseg) {
+    g0 = B > 1 ? u & 1u : 0u;
+    if (lane < L && bl < nun && il < nseg) {
       const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)il * kStride));
       p0 = produced[il];
       nq0 = h[kNseqAll];
@@ -179,7 +185,7 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
       nb0 = h[kNb];
     }
   }
-  const bool mine = p0 == kHanded && (B == 1 ? nb0 == 1u : nb0 >= 2u);
+  const bool mine = p0 == kHanded && (B == 1 ? nb0 == 1u : nb0 >= 2u && B * g0 < nb0);
   if (B > 1 && lane < L && mine && nq0 > rcap) {  // (more sequences than a valid frame has)
     produced[il0] = 0xFFFFFFFFu;
     atomicOr(err, 1u);
@@ -228,10 +234,12 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
   // extracts its two fields, and the quad exchanges the three values; the bit reader,
   // repeat offsets and records are replicated over the quad.  One wave instruction thus
   // advances all three FSE chains of 16 segments.
-  const uint32_t l = lane / (4 * B), bk = (lane >> 2) % B, j = lane & 3u;
+  const uint32_t l = lane / (4 * B), j = lane & 3u;
   // (fetched while every lane is active: a disabled source lane reads as 0)
   const uint32_t i = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l < L ? l : 0u) << 2), (int)il0);
-  if (l >= L || blockIdx.x * L + l >= nseg || !((tm >> l) & 1u)) return;  // quad-uniform
+  const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l < L ? l : 0u) << 2), (int)g0);
+  const uint32_t bk = B * g + (lane >> 2) % B;  // the block
+  if (l >= L || blockIdx.x * L + l >= nun || !((tm >> l) & 1u)) return;  // quad-uniform
   GMEM uint32_t* h0 = global_ptr(reinterpret_cast<uint32_t*>(hscr + (uint64_t)i * kStride));
   if (bk >= h0[kNb]) return;
   const GMEM uint32_t* h = h0 + blk_at(bk);
@@ -629,14 +637,18 @@ __global__ __launch_bounds__(64) void hand_key_kernel(const uint32_t* __restrict
                                                       uint32_t nseg, uint32_t which,
                                                       uint32_t* __restrict__ keys) {
   using namespace zhand;
-  const uint32_t i = blockIdx.x * kWave + lane_id();
-  if (i >= nseg) return;
+  // (keys of the 2 nseg units: unit u = blocks 4 (u & 1) .. of segment u >> 1, each unit of
+  // an 8-block frame about half of the frame's work)
+  const uint32_t u = blockIdx.x * kWave + lane_id(), i = u >> 1;
+  if (u >= 2 * nseg) return;
   uint32_t c = 0;
   if (produced[i] == kHanded) {
     const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
-    if (h[kNb] >= 2u) c = 1u + (which ? h[kLitAll] >> 8 : h[kNseqAll] >> 7);
+    const uint32_t nb = h[kNb], sh = nb > kUnitBlocks ? 1u : 0u;
+    if (nb >= 2u && kUnitBlocks * (u & 1u) < nb)
+      c = 1u + ((which ? h[kLitAll] >> 8 : h[kNseqAll] >> 7) >> sh);
   }
-  keys[i] = kOrderBins - 1u - (c < kOrderBins - 1u ? c : kOrderBins - 1u);
+  keys[u] = kOrderBins - 1u - (c < kOrderBins - 1u ? c : kOrderBins - 1u);
 }
 
 #define BITAR_SEQDEC_INST(L, B)                                                              \

@@ -129,9 +129,10 @@ uint32_t bo_set_lz4_parse_flags(uint32_t flags);
  * rejected by libzstd and by bo_zstd_decompress alike. */
 #define BO_ZSTD_DROP_GAP_LITERALS (1u << 17)
 uint32_t bo_set_zstd_parse_flags(uint32_t flags);
-/* Blocks per Zstd frame (default 4: frames with >= 64 sequences are written as 4 blocks of
- * equal sequence counts sharing one literal code and one set of tables; 1: the single-block
- * frames of rounds 1-4).  Returns the previous setting. */
+/* Blocks per Zstd frame.  Default (0): frames with >= 64 sequences are written as 4 blocks of
+ * equal sequence counts sharing one literal code and one set of tables, 8 when they also hold
+ * >= 32 KiB of literals; 1..8: that many for every frame with >= 64
+ * sequences (1: the single-block frames of rounds 1-4).  Returns the previous setting. */
 uint32_t bo_set_zstd_blocks(uint32_t blocks);
 void bo_window_parse_flags(const uint8_t* src, uint32_t n, uint32_t max_dist, uint32_t max_mlen,
                            uint32_t flags, bo_emit_fn emit, void* ctx);

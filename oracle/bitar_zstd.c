@@ -1129,24 +1129,31 @@ uint32_t bo_zstd_bound(uint32_t n) {
 }
 
 /* Blocks of a frame (round 5): a frame with >= ZS_MULTI_MIN sequences is written as
- * ZS_BLOCKS compressed blocks of equal sequence counts -- block b takes sequences
- * [b nseq / B, (b + 1) nseq / B) and their literals, the last one the trailing literals too.
+ * B = 4 compressed blocks of equal sequence counts -- block b takes sequences
+ * [b nseq / B, (b + 1) nseq / B) and their literals, the last one the trailing literals too --
+ * or B = 8 when it also has >= ZS_WIDE_LIT literal bytes (the near-incompressible columns of
+ * a record batch: ~64 KiB of literals whose Huffman streams, 4 per block, are a decoder's
+ * longest serial chains).
  * The blocks share one literal code (the first Huffman-coded block carries the tree, the
  * others are Treeless) and one set of sequence tables (described in the first block,
  * Repeat_Mode in the others); repeat offsets run on across blocks (RFC 8878 3.1.2.5).  Each
  * block's FSE state chains start from its own last sequence, so a decoder walks the blocks'
  * chains -- and decodes their literal streams -- in parallel.  bo_set_zstd_blocks(1) writes
  * the single-block frames of rounds 1-4. */
-#define ZS_MAX_BLOCKS 4u
+#define ZS_MAX_BLOCKS 8u
 #define ZS_MULTI_MIN 64u
-static uint32_t g_zstd_blocks = ZS_MAX_BLOCKS;
+#define ZS_WIDE_LIT 32768u
+/* 0: the rule above; else every frame with >= ZS_MULTI_MIN sequences has this many blocks */
+static uint32_t g_zstd_blocks = 0;
 uint32_t bo_set_zstd_blocks(uint32_t b) {
   const uint32_t old = g_zstd_blocks;
-  g_zstd_blocks = b < 1 ? 1 : b > ZS_MAX_BLOCKS ? ZS_MAX_BLOCKS : b;
+  g_zstd_blocks = b > ZS_MAX_BLOCKS ? ZS_MAX_BLOCKS : b;
   return old;
 }
-static uint32_t zs_nblocks(uint32_t nseq, int drop) {
-  return (!drop && nseq >= ZS_MULTI_MIN) ? g_zstd_blocks : 1u;
+static uint32_t zs_nblocks(uint32_t nseq, uint32_t nlit, int drop) {
+  if (drop || nseq < ZS_MULTI_MIN) return 1u;
+  if (g_zstd_blocks) return g_zstd_blocks;
+  return nlit >= ZS_WIDE_LIT ? 8u : 4u;
 }
 /* sequence starts sb[0..nb] and literal starts lb[0..nb] of the blocks */
 static void zs_block_split(const uint32_t* ll, uint32_t nseq, uint32_t nlit, uint32_t nb,
@@ -1249,10 +1256,10 @@ int bo_zstd_compress_block(const uint8_t* src, uint32_t n, uint8_t* dst, uint32_
       fh = 7;
     }
     const uint32_t nseq = z.nseq;
-    /* blocks: ZS_BLOCKS of equal sequence counts when the frame has >= ZS_MULTI_MIN
-     * sequences (each block's FSE state chains, and its literal streams, are then independent
-     * of the others': a decoder walks them in parallel), else one */
-    const uint32_t nb = zs_nblocks(nseq, z.drop != 0);
+    /* blocks: 4 or 8 of equal sequence counts when the frame has >= ZS_MULTI_MIN sequences
+     * (each block's FSE state chains, and its literal streams, are then independent of the
+     * others': a decoder walks them in parallel), else one */
+    const uint32_t nb = zs_nblocks(nseq, z.nlit, z.drop != 0);
     uint32_t sb[ZS_MAX_BLOCKS + 1], lb[ZS_MAX_BLOCKS + 1];
     zs_block_split(z.ll, nseq, z.nlit, nb, sb, lb);
     zs_littab H;

@@ -275,8 +275,8 @@ def _zstd_info(frame):
 
 
 def test_oracle_zstd_frame_structure():
-    """One block per segment below 64 sequences, else 4 blocks of equal sequence counts (raw
-    when the frame does not shrink); literals raw / RLE / Huffman with 1 stream below 256
+    """One block per segment below 64 sequences, else 4 blocks of equal sequence counts, 8
+    with >= 32 KiB of literals (raw when the frame does not shrink); literals raw / RLE / Huffman with 1 stream below 256
     literals, else 4 (per block); the first Huffman block carries the tree and later ones are
     Treeless; FSE-compressed Huffman weights when more than 128 would be sent directly;
     table descriptions in the first block, Repeat_Mode in the others."""
@@ -312,6 +312,15 @@ def test_oracle_zstd_frame_structure():
     assert all(b["modes"] == (3, 3, 3) for b in bl[1:])       # Repeat_Mode
     huff = [b for b in bl if b["lit_type"] in (2, 3)]
     assert huff and huff[0]["lit_type"] == 2 and all(b["lit_type"] == 3 for b in huff[1:])
+    # literal-heavy frames (a near-incompressible record-batch column): 8 blocks
+    rb = O.fill(2, 1000, 17 * 65536)[16 * 65536:].tobytes()
+    bl = _zstd_blocks(O.zstd_compress(rb)[1])
+    assert len(bl) == 8 and all(b["block"] == 2 for b in bl)
+    assert sum(b["nlit"] for b in bl) >= 32768 and sum(b["nseq"] for b in bl) >= 64
+    counts = [b["nseq"] for b in bl]
+    assert max(counts) - min(counts) <= 1
+    assert all(b["modes"] == (3, 3, 3) for b in bl[1:])
+    assert bl[0]["lit_type"] == 2 and all(b["lit_type"] == 3 for b in bl[1:])
     # one block again with the single-block setting (rounds 1-4's frames)
     L = O.lib()
     L.bo_set_zstd_blocks.restype = ctypes.c_uint32
