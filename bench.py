@@ -68,6 +68,8 @@ def parse():
                    help="skip the wide-parse LZ4 leg (the ratio operating point)")
     p.add_argument("--no-stock", action="store_true",
                    help="skip the stock-stream GPU decode legs")
+    p.add_argument("--no-qp2", action="store_true",
+                   help="skip the headline job over two queue-pair streams (informational)")
     p.add_argument("--only", default=None,
                    help="comma list of legs to run besides the headline (profiling runs)")
     p.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic.json"))
@@ -635,6 +637,13 @@ def main():
         # 1-GiB call per GPU (the harder, more representative LZ4 number)
         ka = run_job(eng, "lz4", 2, world * n, seg, 1, args.steps, args.warmup, world, rank,
                      seed=3)
+    qp2 = None
+    if args.codec == "lz4" and not args.no_qp2 and want(args, "qp2"):
+        # the headline job split over two queue-pair streams (reference EvaluateAsync,
+        # demo_app.cc:548-693): each half's decompress follows its compress on its stream, so
+        # one half's compress overlaps the other's decompress (informational, not `value`)
+        qp2 = run_job(eng, args.codec, args.kind, world * n, seg, 2, args.steps, args.warmup,
+                      world, rank)
     lw = None
     if args.codec == "lz4" and not args.no_lz4_wide and want(args, "lz4_wide"):
         # the ratio operating point: the same job through the wide LZ4 parse
@@ -705,6 +714,13 @@ def main():
         res["recordbatch"] = s
     if sec is not None:
         res["secondary"] = sec
+    if qp2 is not None:
+        s = leg_summary(args.codec, qp2, world, args.steps, args.traffic_json, leg="headline",
+                        workload="the headline job (same input, same work) split over 2 "
+                                 "queue-pair streams per GPU: each half compresses then "
+                                 "decompresses on its own stream, the halves overlapping")
+        s["streams_per_gpu"] = 2
+        res["headline_2qp"] = s
     if zs is not None:
         res["zstd"] = leg_summary(
             "zstd", zs, world, args.steps, args.traffic_json,
