@@ -743,10 +743,15 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
   // zstd_emit_kernel's (oracle zs_littab_build / zs_literals_block). ----
   for (uint32_t k = lane; k < 256; k += kWave) L.hist[k] = 0;
   lds_order();
+  // (the next 1 KiB is loaded before this one's 16 LDS atomics per lane: at one load per
+  // step the wave waited on every one of them)
+  uint4 vn = make_uint4(0, 0, 0, 0);
+  if (16u * lane < nlit) vn = *reinterpret_cast<const GMEM uint4*>(lits + 16u * lane);
   for (uint32_t b0 = 0; b0 < nlit; b0 += 16u * kWave) {
     const uint32_t at = b0 + 16u * lane;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (at < nlit) v = *reinterpret_cast<const GMEM uint4*>(lits + at);
+    const uint4 v = vn;
+    const uint32_t an = at + 16u * kWave;
+    if (an < nlit) vn = *reinterpret_cast<const GMEM uint4*>(lits + an);
     const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j)
@@ -1300,18 +1305,23 @@ __global__ __launch_bounds__(64) void zstd_emit_kernel(
       uint32_t jn = s0 + lastc * kWave + lane;
       uint2 prec = seqs[jn < s1 ? jn : s1 - 1];
       uint32_t pw = word(jn < s1 ? jn : s1 - 1);
+      // the step's history before it (zstd_entropy_kernel's scan), loaded a step ahead too
+      uint32_t ph0 = whist[3 * (st0 + lastc)], ph1 = whist[3 * (st0 + lastc) + 1],
+               ph2 = whist[3 * (st0 + lastc) + 2];
       for (int32_t c = (int32_t)lastc; c >= 0 && !o.overflow; --c) {
         const uint32_t j = s0 + (uint32_t)c * kWave + lane;
         const bool act = j < s1;
         const uint2 rec = prec;
         const uint32_t wd = pw;
+        uint32_t h0 = uniform(ph0), h1 = uniform(ph1), h2 = uniform(ph2);
         if (c > 0) {  // prefetch the next step
           prec = seqs[j - kWave];
           pw = word(j - kWave);
+          const uint32_t hn = 3 * (st0 + (uint32_t)c - 1);
+          ph0 = whist[hn];
+          ph1 = whist[hn + 1];
+          ph2 = whist[hn + 2];
         }
-        // the step's offset values from the history before it (zstd_entropy_kernel's scan)
-        const uint32_t hs = 3 * (st0 + (uint32_t)c);
-        uint32_t h0 = uniform(whist[hs]), h1 = uniform(whist[hs + 1]), h2 = uniform(whist[hs + 2]);
         const uint32_t cnt = s1 - (s0 + (uint32_t)c * kWave) < kWave ? s1 - (s0 + (uint32_t)c * kWave) : kWave;
         const uint32_t ll = rec.x & 0x1FFFFu, mlb = rec.y - 3u;
         const uint32_t ov = rep_scan(ll, rec.x >> 17, act, cnt, h0, h1, h2);

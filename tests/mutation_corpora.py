@@ -111,6 +111,11 @@ def zstd_sources():
             r = Z.ZSTD_compress(buf, n + 1024, plain, n, 1)
             assert not Z.ZSTD_isError(r)
             srcs.append((buf.raw[:r], plain))
+    # a literal-heavy record-batch column: our 8-block frame (>= 32 KiB of literals)
+    plain = O.fill(2, 1000, 17 * 65536)[16 * 65536:].tobytes()
+    r, ours = O.zstd_compress(plain)
+    assert r == 0
+    srcs.append((ours, plain))
     return srcs
 
 
