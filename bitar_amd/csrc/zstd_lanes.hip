@@ -537,7 +537,12 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
 #ifndef BITAR_HLIT_NW
 #define BITAR_HLIT_NW 8
 #endif
-    constexpr uint32_t NW = BITAR_HLIT_NW;
+#ifndef BITAR_HLIT_X8
+#define BITAR_HLIT_X8 1
+#endif
+    // X8 (multi-block hand-offs): a 16-word window reloaded 8 words (32 bytes) at a time
+    constexpr bool X8 = BITAR_HLIT_X8 != 0 && B > 1;
+    constexpr uint32_t NW = X8 ? 16u : BITAR_HLIT_NW;
 #ifndef BITAR_HLIT_X4
 #define BITAR_HLIT_X4 1
 #endif
@@ -548,14 +553,20 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
     // the addresser busy; at one wave per SIMD -- the single-block form, long streams -- the
     // longer dependent chain of the 16-byte form costs more than the addresser time it saves:
     // stock libzstd-1 decode 5.38 -> 6.35 ms in hlit with it)
-    constexpr bool X4 = BITAR_HLIT_X4 != 0 && NW == 8 && B > 1;
+    constexpr bool X4 = BITAR_HLIT_X4 != 0 && NW == 8 && B > 1 && !X8;
     constexpr bool ST16 = BITAR_HLIT_ST16 != 0 && B > 1;
+#ifndef BITAR_HLIT_ST32
+#define BITAR_HLIT_ST32 1
+#endif
+    // ST32: 32 symbols per pair of 16-byte stores (with X8: the line of a lane's output run is
+    // written in two halves instead of eight 16-byte pieces)
+    constexpr bool ST32 = ST16 && X8 && BITAR_HLIT_ST32 != 0;
     uint32_t W[NW];
 #pragma unroll
     for (uint32_t w = 0; w < NW; ++w) W[w] = zsh::word_raw(src, top - 4 * (int32_t)(w + 1), lo);
     uint32_t used = 8 - (31u - (uint32_t)__builtin_clz(lastb));  // the end mark and zeros above it
     const uint32_t mask = (1u << log) - 1u;
-    uint64_t acc = 0, prev = 0;
+    uint64_t acc = 0, prev = 0, pv1 = 0, pv2 = 0;
     uint32_t k = 0, ac = 0, half = 0;
     auto phase = [&](uint32_t hi, uint32_t lo32, uint32_t& slot) __attribute__((always_inline)) {
       const uint64_t c = ((uint64_t)hi << 32) | lo32;
@@ -564,7 +575,17 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
         acc |= (uint64_t)sym << (8 * ac);
         ++k;
         if (++ac == 8) {
-          if constexpr (ST16) {
+          if constexpr (ST32) {
+            // half counts the pending 8-symbol words (prev, pv1, pv2)
+            if (half == 3) {
+              zsh::st16_raw(dst + k - 32, prev, pv1);
+              zsh::st16_raw(dst + k - 16, pv2, acc);
+            }
+            prev = half == 0 ? acc : prev;
+            pv1 = half == 1 ? acc : pv1;
+            pv2 = half == 2 ? acc : pv2;
+            half = (half + 1) & 3u;
+          } else if constexpr (ST16) {
             // 16 symbols per store: half the store addresses
             if (half) zsh::st16_raw(dst + k - 16, prev, acc);
             else prev = acc;
@@ -591,7 +612,7 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
       }
       // (unconditional: a conditional load is a phi the compiler settles with vmcnt(0); when
       // the phase ended on k == n instead, the loop ends and the word is not read)
-      if constexpr (!X4) slot = zsh::word_raw(src, top - 4 * (int32_t)(NW + 1), lo);
+      if constexpr (!X4 && !X8) slot = zsh::word_raw(src, top - 4 * (int32_t)(NW + 1), lo);
       if (used >= 32) {
         top -= 4;
         used -= 32;
@@ -620,6 +641,28 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
       wc = (uint32_t)rh;
       wd = (uint32_t)(rh >> 32);
     };
+    // X8: the eight words a half-round consumed come back as the block [top - 64, top - 32),
+    // two 16-byte loads of one 32-byte run (its line is fetched once for both: the lanes'
+    // 16-byte reads missed L2 about every time, ~6x the stream bytes, once 8-block frames
+    // doubled the concurrent streams); near the stream start word by word (each clamped to
+    // lo like the initial fill: a word below lo lies below the stream, masked at the peek)
+    auto reload8 = [&](uint32_t h) __attribute__((always_inline)) {
+      const int32_t A = top - 64;
+      if (A >= lo) {
+        const uint4 v0 = zsh::ld16_raw(src + A), v1 = zsh::ld16_raw(src + A + 16);
+        W[h + 7] = v0.x;
+        W[h + 6] = v0.y;
+        W[h + 5] = v0.z;
+        W[h + 4] = v0.w;
+        W[h + 3] = v1.x;
+        W[h + 2] = v1.y;
+        W[h + 1] = v1.z;
+        W[h] = v1.w;
+      } else {
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u) W[h + 7 - u] = zsh::word_raw(src, A + 4 * (int32_t)u, lo);
+      }
+    };
     while (k < n) {
 #pragma unroll
       for (uint32_t p = 0; p < NW; ++p) {
@@ -629,9 +672,20 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
           if (p == 3) reload4(W[3], W[2], W[1], W[0]);
           if (p == 7) reload4(W[7], W[6], W[5], W[4]);
         }
+        if constexpr (X8) {
+          if (p == 7) reload8(0);
+          if (p == 15) reload8(8);
+        }
       }
     }
-    if (ST16 && half) lanes::st8(dst + k - ac - 8, prev);
+    if (ST32) {  // the pending words, oldest first
+      const uint32_t b0 = k - ac - 8 * half;
+      if (half >= 1) lanes::st8(dst + b0, prev);
+      if (half >= 2) lanes::st8(dst + b0 + 8, pv1);
+      if (half >= 3) lanes::st8(dst + b0 + 16, pv2);
+    } else if (ST16 && half) {
+      lanes::st8(dst + k - ac - 8, prev);
+    }
     for (uint32_t r = 0; r < ac; ++r) dst[k - ac + r] = (uint8_t)(acc >> (8 * r));
     ok = 8 * (top - q) - (int32_t)used == 0;
   }
