@@ -1329,7 +1329,15 @@ __device__ __forceinline__ uint32_t xxh64_low(const GMEM uint8_t* p, uint32_t n)
 
 }  // namespace zsd
 
-__global__ __launch_bounds__(64) void zstd_decompress_kernel(
+#ifndef BITAR_ZSD_WAVES
+#define BITAR_ZSD_WAVES 0
+#endif
+#if BITAR_ZSD_WAVES
+#define BITAR_ZSD_ATTR __attribute__((amdgpu_waves_per_eu(BITAR_ZSD_WAVES)))
+#else
+#define BITAR_ZSD_ATTR
+#endif
+__global__ __launch_bounds__(64) BITAR_ZSD_ATTR void zstd_decompress_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,

@@ -11,6 +11,9 @@ for f in runtime lz4_decompress inflate inflate_fixed compress util_kernels zstd
     lz4_decompress) extra="-mllvm -amdgpu-sched-strategy=max-ilp";;
     zstd_seq|zstd_lanes) extra="-mllvm -amdgpu-sched-strategy=max-memory-clause";;
     compress) extra="-mllvm -amdgpu-sched-strategy=iterative-maxocc";;
+    inflate) extra="-DBITAR_DEC_RING=2048";;
+    inflate_fixed) extra="-DBITAR_DEC_RING=1024";;
+    zstd_decompress) extra="-DBITAR_DEC_RING=2048 -DBITAR_ZSD_WAVES=3";;
   esac
   eval "extra=\${FLAGS_$f:-\$extra}"  # FLAGS_<file>="..." replaces a file's extra flags
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics $extra $defs -c csrc/$f.hip -o build_$name/$f.o &
