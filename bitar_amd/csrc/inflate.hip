@@ -644,7 +644,15 @@ __device__ __forceinline__ int inflate_codes(State& s, uint8_t* win, uint8_t* ri
 
 }  // namespace BITAR_INFL_NS
 
-__global__ __launch_bounds__(64) void BITAR_INFL_KERNEL(
+#ifndef BITAR_INFL_WAVES
+#define BITAR_INFL_WAVES 0
+#endif
+#if BITAR_INFL_WAVES
+#define BITAR_INFL_ATTR __attribute__((amdgpu_waves_per_eu(BITAR_INFL_WAVES)))
+#else
+#define BITAR_INFL_ATTR
+#endif
+__global__ __launch_bounds__(64) BITAR_INFL_ATTR void BITAR_INFL_KERNEL(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, const uint32_t* __restrict__ csizes, uint32_t nseg, uint32_t seg,
     uint8_t* __restrict__ out, uint32_t* __restrict__ produced, uint32_t* __restrict__ err,

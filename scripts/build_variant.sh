@@ -12,7 +12,7 @@ for f in runtime lz4_decompress inflate inflate_fixed compress util_kernels zstd
     zstd_seq|zstd_lanes) extra="-mllvm -amdgpu-sched-strategy=max-memory-clause";;
     compress) extra="-mllvm -amdgpu-sched-strategy=iterative-maxocc";;
     inflate) extra="-DBITAR_DEC_RING=2048";;
-    inflate_fixed) extra="-DBITAR_DEC_RING=1024";;
+    inflate_fixed) extra="-DBITAR_DEC_RING=1024 -DBITAR_INFL_WAVES=8";;
     zstd_decompress) extra="-DBITAR_DEC_RING=2048 -DBITAR_ZSD_WAVES=3";;
   esac
   eval "extra=\${FLAGS_$f:-\$extra}"  # FLAGS_<file>="..." replaces a file's extra flags
