@@ -1092,7 +1092,15 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
 // sequence bitstream: the fields of 64 sequences per step (highest first) with the state bits
 // from pass 3, the final states and the end mark.  Then the block headers, or one raw block
 // when the compressed blocks are not smaller than the segment.
-__global__ __launch_bounds__(64) void zstd_emit_kernel(
+#ifndef BITAR_EMIT_WAVES
+#define BITAR_EMIT_WAVES 0
+#endif
+#if BITAR_EMIT_WAVES
+#define BITAR_EMIT_ATTR __attribute__((amdgpu_waves_per_eu(BITAR_EMIT_WAVES)))
+#else
+#define BITAR_EMIT_ATTR
+#endif
+__global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     const uint8_t* __restrict__ scratch, uint64_t sstride, uint8_t* __restrict__ slab,
     uint64_t slot_stride, uint8_t* const* __restrict__ dsts, uint32_t* __restrict__ sizes,
