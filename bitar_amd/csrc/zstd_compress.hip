@@ -224,26 +224,17 @@ struct EntLds {
   uint8_t desc[192];       // Huffman tree description; then modes + table descriptions
   uint8_t tmp[256];        // serial bit writer output (weights FSE form, table descriptions)
   int16_t norm[64];
-  union {
-    // per-quarter literal counts ([0] quarters 0 | 1 << 16, [1] 2 | 3 << 16), dead once
-    // the stream sizes are known -- before the first FSE table is built
-    uint32_t hq[2][256];
-    struct {
+  uint32_t u[16];          // lane-0 results: sizes, modes, accuracy logs
+  uint32_t wk[32];         // lane-0 work: weight counts, code ranges
+  uint32_t sh[3][64];      // sequence code histograms: LL, OF, ML
+  union {                  // by phase (8.9 KiB of LDS in all: 17 waves per CU, was 13)
+    huf::TreeLds T;        // the literal code lengths (huff_lengths), dead once L.len is set
+    struct {               // then the FSE tables: the weights' (weights_fse), the sequences'
       uint16_t tabs[kTabDummy + 1];
       uint32_t tr[3][64];  // per symbol: deltaNbBits | deltaFindState << 20 (12-bit signed)
       uint8_t sym_at[512];
       uint16_t nxt[64];
     };
-  };
-  uint32_t u[16];          // lane-0 results: sizes, modes, accuracy logs
-  uint32_t wk[32];         // lane-0 work: weight counts, code ranges
-  union {                  // by phase
-    huf::TreeLds T;        // code lengths
-    struct {
-      uint32_t code[256];                 // code | length << 16
-      alignas(16) uint8_t lst[16 * kWave];  // literal block being encoded (16-B stores)
-    } E;
-    uint32_t sh[3][64];    // sequence code histograms: LL, OF, ML
   };
 };
 // 256 * log2(x), x >= 1
