@@ -62,7 +62,8 @@ __constant__ int16_t kOFDefault[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1,
                                        1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
 struct Tabs {  // LDS, per wave
-  uint32_t fse[4][512];  // decode cells (LL, OF, ML, Huffman weights): sym | nbits << 8 | base << 16
+  uint32_t fse[3][512];  // decode cells (LL, OF, ML): sym | nbits << 8 | base << 16
+  uint32_t wcells[64];   // the Huffman weights' cells (accuracy log <= 6)
   uint16_t huf[1u << kHufMaxLog];  // sym | nbits << 8
   int16_t norm[256];
   uint8_t wts[256];
@@ -354,7 +355,7 @@ __device__ __forceinline__ int huf_read(State& s, uint8_t* win, Tabs& t, uint32_
     uint32_t max_sym = 255, al;
     const int n = read_ncount(s, win, t, start + 1, hb, max_sym, al, 6);
     if (n < 0) return -1;
-    uint32_t* cells = t.fse[3];
+    uint32_t* cells = t.wcells;
     if (!fse_build(t, cells, max_sym, al)) return -1;
     Bwd b;
     if (!bwd_init(s, win, b, start + 1 + (uint32_t)n, hb - (uint32_t)n)) return -1;
