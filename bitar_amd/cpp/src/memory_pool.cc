@@ -42,12 +42,40 @@ thread_local int g_pool_device = 0;
 alignas(64) std::int64_t zero_size_area[1] = {0};
 std::uint8_t* const kZeroSizeArea = reinterpret_cast<std::uint8_t*>(&zero_size_area);
 
+#ifndef NDEBUG
+// Debug builds mark the first and last byte of a fresh allocation, of the grown part of a
+// reallocation and of a freed buffer, as the reference's pools do (memory_pool.cc:190-263),
+// so that reads of uninitialised or freed pool memory show a recognisable value.  HBM bytes
+// are written through the ABI's copy (both pools' memory is reachable by hipMemcpy).
+constexpr std::uint8_t kAllocPoison = 0xBC;
+constexpr std::uint8_t kReallocPoison = 0xBD;
+constexpr std::uint8_t kDeallocPoison = 0xBE;
+
+void PoisonByte(bitar_hip_ctx* ctx, bool device, std::uint8_t* at, std::uint8_t value) {
+  if (!device) {
+    *at = value;
+    return;
+  }
+  static const std::uint8_t kValues[3] = {kAllocPoison, kReallocPoison, kDeallocPoison};
+  const std::uint8_t* src = &kValues[value - kAllocPoison];
+  if (bitar_hip_memcpy(ctx, at, src, 1, nullptr) == 0) (void)bitar_hip_sync(ctx, nullptr);
+}
+
+void PoisonEnds(bitar_hip_ctx* ctx, bool device, std::uint8_t* lo, std::uint8_t* last,
+                std::uint8_t value) {
+  PoisonByte(ctx, device, lo, value);
+  if (last != lo) PoisonByte(ctx, device, last, value);
+}
+#endif
+
 template <bool kDevice>
 class HipPool : public arrow::MemoryPool {
  public:
   arrow::Status Allocate(int64_t size, int64_t /*alignment: HIP gives >= 256 B*/,
                          uint8_t** out) override {
     if (size < 0) return arrow::Status::Invalid("negative malloc size");
+    if (static_cast<std::uint64_t>(size) >= std::numeric_limits<std::size_t>::max())
+      return arrow::Status::OutOfMemory("malloc size overflows size_t");
     if (size == 0) {
       *out = kZeroSizeArea;
       return arrow::Status::OK();
@@ -59,6 +87,9 @@ class HipPool : public arrow::MemoryPool {
                            : bitar_hip_host_alloc(ctx, static_cast<uint64_t>(size), &p);
     if (rc != 0) return arrow::Status::OutOfMemory("allocation of size ", size, " failed");
     *out = static_cast<uint8_t*>(p);
+#ifndef NDEBUG
+    PoisonEnds(ctx, kDevice, *out, *out + size - 1, kAllocPoison);
+#endif
     HipAllocationTracker::Instance()->Emplace({*out, size, kDevice ? device : -1, kDevice});
     stats_.DidAllocateBytes(size);
     return arrow::Status::OK();
@@ -67,6 +98,8 @@ class HipPool : public arrow::MemoryPool {
   arrow::Status Reallocate(int64_t old_size, int64_t new_size, int64_t alignment,
                            uint8_t** ptr) override {
     if (new_size < 0) return arrow::Status::Invalid("negative realloc size");
+    if (static_cast<std::uint64_t>(new_size) >= std::numeric_limits<std::size_t>::max())
+      return arrow::Status::OutOfMemory("realloc overflows size_t");
     uint8_t* prev = *ptr;
     uint8_t* fresh = nullptr;
     ARROW_RETURN_NOT_OK(Allocate(new_size, alignment, &fresh));
@@ -79,6 +112,12 @@ class HipPool : public arrow::MemoryPool {
                 "realloc copy");
       BITAR_ABI(bitar_hip_sync(ctx, nullptr), "realloc sync");
     }
+#ifndef NDEBUG
+    if (new_size > old_size) {
+      ARROW_ASSIGN_OR_RAISE(auto* ctx, internal::HelperContext(kDevice ? g_pool_device : 0));
+      PoisonEnds(ctx, kDevice, fresh + old_size, fresh + new_size - 1, kReallocPoison);
+    }
+#endif
     Free(prev, old_size, alignment);
     *ptr = fresh;
     return arrow::Status::OK();
@@ -91,6 +130,9 @@ class HipPool : public arrow::MemoryPool {
     const int device = known && a.device >= 0 ? a.device : 0;
     auto ctx = internal::HelperContext(device);
     if (ctx.ok()) {
+#ifndef NDEBUG
+      if (size > 0) PoisonEnds(*ctx, kDevice, buffer, buffer + size - 1, kDeallocPoison);
+#endif
       if (kDevice) (void)bitar_hip_free(*ctx, buffer);
       else (void)bitar_hip_host_free(*ctx, buffer);
     }

@@ -673,9 +673,13 @@ struct EntOut : ByteOut {
 }  // namespace zse
 
 // The Zstd parse is the repeat-offset form with window skipping (oracle BO_PARSE_REP |
-// BO_PARSE_SKIP); BITAR_ZSTD_SKIP=0 builds the plain repeat-offset scan (tuning knob only).
+// BO_PARSE_SKIP); BITAR_ZSTD_SKIP=0 builds the plain repeat-offset scan, BITAR_ZSTD_REP=0 the
+// parse without repeat candidates (timing knobs only: not the oracle's output).
 #ifndef BITAR_ZSTD_SKIP
 #define BITAR_ZSTD_SKIP 1
+#endif
+#ifndef BITAR_ZSTD_REP
+#define BITAR_ZSTD_REP 1
 #endif
 __global__ __launch_bounds__(64) void zstd_parse_kernel(const uint8_t* __restrict__ input,
                                                         uint64_t n_total, uint32_t seg,
@@ -701,7 +705,7 @@ __global__ __launch_bounds__(64) void zstd_parse_kernel(const uint8_t* __restric
   o.seqs = reinterpret_cast<GMEM uint2*>(o.dst + zse::lit_cap(seg));
   o.nseq = 0;
   const GMEM uint8_t* in = global_ptr(input + seg_off);
-  parse<zse::SeqCollect, true, BITAR_ZSTD_SKIP != 0>(in, n, global_ptr(input + n_total), table, inring, kMaxDist,
+  parse<zse::SeqCollect, BITAR_ZSTD_REP != 0, BITAR_ZSTD_SKIP != 0>(in, n, global_ptr(input + n_total), table, inring, kMaxDist,
                                0xFFFFFFFFu, o);
   o.flush(o.op, true);
   if (lane_id() == 0) meta[i_seg] = make_uint2(o.op, o.nseq);

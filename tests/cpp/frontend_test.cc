@@ -465,6 +465,26 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
       if (st.ok()) CHECK(c->window_size() == (w.level >= 2 ? 14 : 12));
     }
   }
+#ifndef NDEBUG
+  // debug-build pool poisoning (reference memory_pool.cc:190-263): 0xBC at both ends of a
+  // fresh allocation, 0xBD at both ends of a reallocation's grown part, kept bytes intact
+  {
+    auto* pool = bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipHost);
+    uint8_t* p = nullptr;
+    CHECK_OK(pool->Allocate(100, 64, &p));
+    CHECK(p[0] == 0xBC && p[99] == 0xBC);
+    std::memset(p, 7, 100);
+    CHECK_OK(pool->Reallocate(100, 300, 64, &p));
+    CHECK(p[0] == 7 && p[99] == 7 && p[100] == 0xBD && p[299] == 0xBD);
+    pool->Free(p, 300, 64);
+    uint8_t* d = nullptr;  // the HBM pool poisons through the ABI's copy
+    auto* dpool = bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipDevice);
+    CHECK_OK(dpool->Allocate(1, 64, &d));
+    CHECK_OK(dpool->Reallocate(1, 4096, 64, &d));
+    dpool->Free(d, 4096, 64);
+    CHECK(pool->bytes_allocated() == 0);
+  }
+#endif
   // INTEGRATION.md's minimal program, run as written
   CHECK_OK(RoundTrip(data.data(), static_cast<std::int64_t>(data.size())));
   // empty input -> empty vector (device.cc:161-164); empty vector -> OK
