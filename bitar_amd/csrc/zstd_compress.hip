@@ -711,6 +711,26 @@ __global__ __launch_bounds__(64) void zstd_parse_kernel(const uint8_t* __restric
   if (lane_id() == 0) meta[i_seg] = make_uint2(o.op, o.nseq);
 }
 
+// first sequence of block b of nb (block nb: nseq), oracle zs_nblocks' split
+__device__ __forceinline__ uint32_t blk_start_of(uint32_t b, uint32_t nseq, uint32_t nb) {
+  return b >= nb ? nseq : (uint32_t)((uint64_t)b * nseq / nb);
+}
+
+#ifndef BITAR_ZSE_RUNS
+#define BITAR_ZSE_RUNS 1
+#endif
+// h[c] += 1 for each active lane's code c, as one LDS atomic per run of equal codes (lanes
+// [0, cnt) active): a run starts where the code differs from the previous lane's, and its
+// first lane adds the distance to the next run's start
+__device__ __forceinline__ void run_add(uint32_t* h, uint32_t c, bool act, uint32_t cnt) {
+  const uint32_t lane = lane_id();
+  const uint32_t prev = wave_shr1(c);
+  const uint64_t heads = ballot(act & ((lane == 0) | (c != prev)));
+  const uint64_t after = (heads >> lane) >> 1;
+  const uint32_t nxt = after ? lane + 1u + (uint32_t)__builtin_ctzll(after) : cnt;
+  if ((heads >> lane) & 1u) atomicAdd(&h[c], nxt - lane);
+}
+
 __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     uint8_t* __restrict__ scratch, uint64_t sstride, const uint2* __restrict__ meta,
@@ -853,34 +873,46 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     GMEM uint32_t* whist = reinterpret_cast<GMEM uint32_t*>(wbytes + walk_hist_at(seg));
     uint32_t st = 0, lsum = 0;
     uint2 nrec = lane < nseq ? seqs[lane] : make_uint2(0, 3);
+    uint32_t s0 = 0, s1 = blk_start_of(1u, nseq, nb);
     for (uint32_t b = 0; b < nb; ++b) {
-      const uint32_t s0 = (uint32_t)((uint64_t)b * nseq / nb);
-      const uint32_t s1 = (uint32_t)((uint64_t)(b + 1) * nseq / nb);
-      if (lane == 0) {
-        wrec[kWSb + b] = s0;
-        wrec[kWLb + b] = lsum;
-        wrec[kWStep + b] = st;
-      }
+      wrec[lane == 0 ? kWSb + b : kWTrash] = s0;
+      wrec[lane == 0 ? kWLb + b : kWTrash] = lsum;
+      wrec[lane == 0 ? kWStep + b : kWTrash] = st;
       for (uint32_t c0 = s0; c0 < s1; c0 += kWave, ++st) {
         const uint32_t j = c0 + lane;
         const uint32_t cnt = s1 - c0 < kWave ? s1 - c0 : kWave;
         const bool act = lane < cnt;
         const uint2 rec = nrec;
-        // prefetch the next step (it starts right after this one's last sequence)
-        if (c0 + cnt + lane < nseq) nrec = seqs[c0 + cnt + lane];
+        // prefetch the next step (it starts right after this one's last sequence).  The
+        // step's load and stores are issued on every lane (past the end: the last record, the
+        // record's trash word): their number per step is fixed, so the wait for this load
+        // does not have to wait for the stores issued after it.
+        const uint32_t jn = c0 + cnt + lane;
+        nrec = seqs[jn < nseq ? jn : nseq - 1u];
         const uint32_t ll = act ? rec.x & 0x1FFFFu : 0u, o = rec.x >> 17, ml = rec.y;
         // the history before this step, for zstd_emit_kernel's re-derivation of the step
-        if (lane < 3) whist[3 * st + lane] = lane == 0 ? c0r : lane == 1 ? c1r : c2r;
+        whist[3 * st + (lane < 2 ? lane : 2u)] = lane == 0 ? c0r : lane == 1 ? c1r : c2r;
         const uint32_t ov = rep_scan(ll, o, act, cnt, c0r, c1r, c2r);
+        const uint32_t llc = ll_code(ll), ofc = hb32(ov), mlc = ml_code(ml);
+#if BITAR_ZSE_RUNS
+        // histograms: LDS atomics cost about a cycle per lane, and a step holds few distinct
+        // codes in runs of equal ones (kind 2: ~30 runs of 64), so one lane per run adds the
+        // run's length
+        run_add(L.sh[0], llc, act, cnt);
+        run_add(L.sh[1], ofc, act, cnt);
+        run_add(L.sh[2], mlc, act, cnt);
+#else
         if (act) {
-          const uint32_t llc = ll_code(ll), ofc = hb32(ov), mlc = ml_code(ml);
           atomicAdd(&L.sh[0][llc], 1u);
           atomicAdd(&L.sh[1][ofc], 1u);
           atomicAdd(&L.sh[2][mlc], 1u);
-          wcodes[j] = llc | (ofc << 6) | (mlc << 11);  // for zstd_walk_kernel
         }
+#endif
+        *(act ? wcodes + j : wrec + kWTrash) = llc | (ofc << 6) | (mlc << 11);  // for zstd_walk_kernel
         lsum += readlane(wave_incl_sum(ll), kWave - 1);
       }
+      s0 = s1;
+      s1 = blk_start_of(b + 2u, nseq, nb);
     }
     lds_order();
     ZSE_PHASE(4)
@@ -1297,17 +1329,25 @@ __global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
       const uint32_t p0 = o.op;
       uint32_t bits = 0, zeroed = p0;
       const uint32_t st0 = uniform(w[kWStep + b]);
-      auto word = [&](uint32_t j) __attribute__((always_inline)) {  // OF | ML | LL bits, counts
+      // the state words of sequence j (OF, ML, LL: bits | count << 12), loaded a step ahead
+      // and combined at their use (combined right away, the loads were waited for at once)
+      auto load_words = [&](uint32_t j, uint32_t& oo, uint32_t& om, uint32_t& ol)
+          __attribute__((always_inline)) {
         const uint32_t sa = walk_state_at(j, 0);
-        const uint32_t oo = outs[sa], om = outs[sa + 8], ol = outs[sa + 16];
+        oo = outs[sa];
+        om = outs[sa + 8];
+        ol = outs[sa + 16];
+      };
+      auto word = [&](uint32_t oo, uint32_t om, uint32_t ol) __attribute__((always_inline)) {
         const uint32_t nof = oo >> 12, nml = om >> 12, nll = ol >> 12;
         return (oo & 0xFFFu) | ((om & 0xFFFu) << nof) | ((ol & 0xFFFu) << (nof + nml)) |
-               ((nof + nml + nll) << 26);
+               ((nof + nml + nll) << 26);  // OF | ML | LL bits, their count
       };
       const uint32_t lastc = (bn - 1) >> 6;
       uint32_t jn = s0 + lastc * kWave + lane;
       uint2 prec = seqs[jn < s1 ? jn : s1 - 1];
-      uint32_t pw = word(jn < s1 ? jn : s1 - 1);
+      uint32_t poo, pom, pol;
+      load_words(jn < s1 ? jn : s1 - 1, poo, pom, pol);
       // the step's history before it (zstd_entropy_kernel's scan), loaded a step ahead too
       uint32_t ph0 = whist[3 * (st0 + lastc)], ph1 = whist[3 * (st0 + lastc) + 1],
                ph2 = whist[3 * (st0 + lastc) + 2];
@@ -1315,12 +1355,13 @@ __global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
         const uint32_t j = s0 + (uint32_t)c * kWave + lane;
         const bool act = j < s1;
         const uint2 rec = prec;
-        const uint32_t wd = pw;
+        const uint32_t wd = word(poo, pom, pol);
         uint32_t h0 = uniform(ph0), h1 = uniform(ph1), h2 = uniform(ph2);
-        if (c > 0) {  // prefetch the next step
-          prec = seqs[j - kWave];
-          pw = word(j - kWave);
-          const uint32_t hn = 3 * (st0 + (uint32_t)c - 1);
+        {  // prefetch the next step (the last step reloads its own: fixed load counts)
+          const uint32_t jp = c > 0 ? j - kWave : (j < s1 ? j : s1 - 1);
+          prec = seqs[jp];
+          load_words(jp, poo, pom, pol);
+          const uint32_t hn = 3 * (st0 + (uint32_t)(c > 0 ? c - 1 : 0));
           ph0 = whist[hn];
           ph1 = whist[hn + 1];
           ph2 = whist[hn + 2];

@@ -32,6 +32,7 @@ __host__ __device__ constexpr uint32_t frame_blocks(uint32_t nseq, uint32_t nlit
 // from which zstd_emit_kernel re-derives the offset values of the step
 enum : uint32_t {
   kWHanded = 0,  // 1: the emit kernel writes this segment's frame
+  kWTrash = 1,   // the target of idle lanes' stores (fixed store counts in loops)
   kWN = 3,       // segment bytes
   kWNseq,        // sequences
   kWAls,         // accuracy logs LL | OF << 8 | ML << 16

@@ -20,8 +20,8 @@ def main():
     import bitar_amd
     eng = bitar_amd.Engine(0)
     codec = {"lz4": bitar_amd.CODEC_LZ4, "deflate": bitar_amd.CODEC_DEFLATE,
-             "zstd": bitar_amd.CODEC_ZSTD}[a.codec]
-    seg = 59460 if a.codec == "deflate" else 65536
+             "deflate_dyn": bitar_amd.CODEC_DEFLATE_DYNAMIC, "zstd": bitar_amd.CODEC_ZSTD}[a.codec]
+    seg = 59460 if a.codec.startswith("deflate") else 65536
     n = a.bytes
     nseg = (n + seg - 1) // seg
     stride = bitar_amd.slot_size(codec, seg)
