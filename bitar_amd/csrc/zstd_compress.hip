@@ -1119,6 +1119,9 @@ __global__ __launch_bounds__(64) void zstd_walk_kernel(const uint8_t* __restrict
 // sequence bitstream: the fields of 64 sequences per step (highest first) with the state bits
 // from pass 3, the final states and the end mark.  Then the block headers, or one raw block
 // when the compressed blocks are not smaller than the segment.
+#ifndef BITAR_HUF_PER_LANE
+#define BITAR_HUF_PER_LANE 8  // literals per lane and step in the Huffman streams (4 or 8)
+#endif
 #ifndef BITAR_EMIT_WAVES
 #define BITAR_EMIT_WAVES 0
 #endif
@@ -1195,7 +1198,7 @@ __global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
   };
   bool tree_sent = false;
   // literals [a, a + m) of the segment's literal area as a Huffman stream (oracle
-  // zs_literals_block): symbols from the last, 64 per step, from 1 KiB blocks of aligned
+  // zs_literals_block): symbols from the last, kPerLane x 64 per step, from 1 KiB blocks of aligned
   // 16-B groups staged in LDS, the next one loaded during the current one
   auto huff_stream = [&](uint32_t a, uint32_t b) __attribute__((always_inline)) {
     const uint32_t p0 = o.op;
@@ -1211,13 +1214,39 @@ __global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
       const int32_t g1 = g0 - (int32_t)kWave;
       if (g0 > gA && g1 + (int32_t)lane >= gA) blkv = l16[g1 + (int32_t)lane];
       const int32_t lo = max((int32_t)a, 16 * g0), hi = min((int32_t)b, 16 * (g0 + (int32_t)kWave));
-      for (int32_t e = hi; e > lo && !o.overflow; e -= (int32_t)kWave) {
-        const int32_t idx = e - (int32_t)kWave + (int32_t)lane;
-        const bool act = idx >= lo;
-        lds_order();
-        const uint32_t sym = act ? lst[idx - 16 * g0] : 0u;
-        const uint32_t cw = hcode[sym];
-        o.put_bits(act ? (cw & 0xFFFFu) : 0u, act ? cw >> 16 : 0u, 0, 0, p0, bits, zeroed);
+      // kPerLane x 64 symbols per step, lane l's are i0 .. i0 + kPerLane - 1, the highest
+      // first (the stream runs from the last symbol down; put_bits takes the lanes in
+      // descending order, each lane's v0 before its v1): v0 = the codes of the upper half,
+      // v1 = those of the lower half, each from its highest symbol (<= kPerLane / 2 x 11 bits).
+      // Per-step costs (the bit count's prefix sum, the room check, clearing the ring, the
+      // LDS ORs) are shared by kPerLane symbols: 1 -> 2 / 4 / 8 per lane, emit 1.38 -> 1.16 /
+      // 0.99 / 0.96 ms (kind 2)
+      constexpr int32_t kPerLane = BITAR_HUF_PER_LANE;
+      static_assert(kPerLane == 4 || kPerLane == 8, "4 or 8 literals per lane");
+      for (int32_t e = hi; e > lo && !o.overflow; e -= kPerLane * (int32_t)kWave) {
+        const int32_t i0 = e - kPerLane * (int32_t)kWave + kPerLane * (int32_t)lane;
+        // symbols i0 + k + 1 then i0 + k as one field (<= 22 bits)
+        auto pair = [&](int32_t k, uint32_t& p, uint32_t& np) __attribute__((always_inline)) {
+          const bool a1 = i0 + k + 1 >= lo, a0 = i0 + k >= lo;
+          lds_order();
+          const uint32_t w1 = hcode[a1 ? lst[i0 + k + 1 - 16 * g0] : 0u];
+          const uint32_t w0 = hcode[a0 ? lst[i0 + k - 16 * g0] : 0u];
+          const uint32_t n1 = a1 ? w1 >> 16 : 0u, n0 = a0 ? w0 >> 16 : 0u;
+          p = (a1 ? w1 & 0xFFFFu : 0u) | ((a0 ? w0 & 0xFFFFu : 0u) << n1);
+          np = n1 + n0;
+        };
+        uint32_t pa, na, pb, nb;
+        pair(kPerLane - 2, pa, na);
+        pair(kPerLane - 4, pb, nb);
+        if constexpr (kPerLane == 4) {
+          o.put_bits(pa, na, pb, nb, p0, bits, zeroed);
+        } else {
+          uint32_t pc, nc, pd, nd;
+          pair(2, pc, nc);
+          pair(0, pd, nd);
+          o.put_bits(pa | ((uint64_t)pb << na), na + nb, pc | ((uint64_t)pd << nc), nc + nd, p0,
+                     bits, zeroed);
+        }
       }
       if (g0 <= gA || o.overflow) break;
       g0 = g1;
