@@ -871,10 +871,11 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     uint32_t c0r = 1, c1r = 4, c2r = 8;  // the history before the step (uniform)
     GMEM uint32_t* wcodes = reinterpret_cast<GMEM uint32_t*>(wbytes + kWWords);
     GMEM uint32_t* whist = reinterpret_cast<GMEM uint32_t*>(wbytes + walk_hist_at(seg));
-    uint32_t st = 0, lsum = 0;
+    uint32_t st = 0, lacc = 0;  // literal bytes before the step, per lane (summed per block)
     uint2 nrec = lane < nseq ? seqs[lane] : make_uint2(0, 3);
     uint32_t s0 = 0, s1 = blk_start_of(1u, nseq, nb);
     for (uint32_t b = 0; b < nb; ++b) {
+      const uint32_t lsum = b ? readlane(wave_incl_sum(lacc), kWave - 1) : 0u;
       wrec[lane == 0 ? kWSb + b : kWTrash] = s0;
       wrec[lane == 0 ? kWLb + b : kWTrash] = lsum;
       wrec[lane == 0 ? kWStep + b : kWTrash] = st;
@@ -909,7 +910,7 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
         }
 #endif
         *(act ? wcodes + j : wrec + kWTrash) = llc | (ofc << 6) | (mlc << 11);  // for zstd_walk_kernel
-        lsum += readlane(wave_incl_sum(ll), kWave - 1);
+        lacc += ll;
       }
       s0 = s1;
       s1 = blk_start_of(b + 2u, nseq, nb);
