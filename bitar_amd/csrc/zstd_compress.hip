@@ -184,8 +184,8 @@ struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the lit
 // last j <= i that is not a plain repeat of r0 (ll_j > 0 && o_j == o_{j-1}); r2 = r1 before the
 // last k <= i that is neither such a repeat nor a repeat of r1 (prefix maxima + bpermute).
 // Every cross-lane op runs on all 64 lanes (a DPP or bpermute source lane that is off in
-// EXEC reads as 0).  Used by zstd_entropy_kernel (codes, histograms) and again by
-// zstd_emit_kernel (extra bits), so the records are never rewritten.
+// EXEC reads as 0).  zstd_entropy_kernel keeps each sequence's offset value beside its codes
+// (the walk scratch's code word), so zstd_emit_kernel reads it instead of scanning again.
 __device__ __forceinline__ uint32_t rep_scan(uint32_t ll, uint32_t o, bool act, uint32_t cnt,
                                              uint32_t& c0r, uint32_t& c1r, uint32_t& c2r) {
   const uint32_t lane = lane_id();
@@ -870,7 +870,6 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
     lds_order();
     uint32_t c0r = 1, c1r = 4, c2r = 8;  // the history before the step (uniform)
     GMEM uint32_t* wcodes = reinterpret_cast<GMEM uint32_t*>(wbytes + kWWords);
-    GMEM uint32_t* whist = reinterpret_cast<GMEM uint32_t*>(wbytes + walk_hist_at(seg));
     uint32_t st = 0, lacc = 0;  // literal bytes before the step, per lane (summed per block)
     uint2 nrec = lane < nseq ? seqs[lane] : make_uint2(0, 3);
     uint32_t s0 = 0, s1 = blk_start_of(1u, nseq, nb);
@@ -878,7 +877,6 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
       const uint32_t lsum = b ? readlane(wave_incl_sum(lacc), kWave - 1) : 0u;
       wrec[lane == 0 ? kWSb + b : kWTrash] = s0;
       wrec[lane == 0 ? kWLb + b : kWTrash] = lsum;
-      wrec[lane == 0 ? kWStep + b : kWTrash] = st;
       for (uint32_t c0 = s0; c0 < s1; c0 += kWave, ++st) {
         const uint32_t j = c0 + lane;
         const uint32_t cnt = s1 - c0 < kWave ? s1 - c0 : kWave;
@@ -891,8 +889,6 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
         const uint32_t jn = c0 + cnt + lane;
         nrec = seqs[jn < nseq ? jn : nseq - 1u];
         const uint32_t ll = act ? rec.x & 0x1FFFFu : 0u, o = rec.x >> 17, ml = rec.y;
-        // the history before this step, for zstd_emit_kernel's re-derivation of the step
-        whist[3 * st + (lane < 2 ? lane : 2u)] = lane == 0 ? c0r : lane == 1 ? c1r : c2r;
         const uint32_t ov = rep_scan(ll, o, act, cnt, c0r, c1r, c2r);
         const uint32_t llc = ll_code(ll), ofc = hb32(ov), mlc = ml_code(ml);
 #if BITAR_ZSE_RUNS
@@ -909,7 +905,10 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
           atomicAdd(&L.sh[2][mlc], 1u);
         }
 #endif
-        *(act ? wcodes + j : wrec + kWTrash) = llc | (ofc << 6) | (mlc << 11);  // for zstd_walk_kernel
+        // for zstd_walk_kernel (the codes) and zstd_emit_kernel (the codes, the offset value:
+        // <= kMaxDist + 3, 15 bits)
+        static_assert(cmp::kMaxDist + 3u < (1u << 15), "offset values in the code word");
+        *(act ? wcodes + j : wrec + kWTrash) = llc | (ofc << 6) | (mlc << 11) | (ov << 17);
         lacc += ll;
       }
       s0 = s1;
@@ -952,7 +951,6 @@ __global__ __launch_bounds__(64) void zstd_entropy_kernel(
   } else if (lane == 0) {
     wrec[kWSb] = 0;
     wrec[kWLb] = 0;
-    wrec[kWStep] = 0;
   }
   // the record: everything zstd_emit_kernel needs to write the frame
   if (lane == 0) {
@@ -1168,7 +1166,7 @@ __global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
   const GMEM uint2* seqs = reinterpret_cast<const GMEM uint2*>(lits + lit_cap(seg));
   const GMEM uint16_t* outs = reinterpret_cast<const GMEM uint16_t*>(
       reinterpret_cast<const GMEM uint8_t*>(w) + walk_state_bytes(seg));
-  const GMEM uint32_t* whist = w + walk_hist_at(seg) / 4;
+  const GMEM uint32_t* wcodes = w + kWWords / 4;
   EntOut o;
   o.ring = obuf;
   o.dst = global_ptr(dsts ? dsts[i_seg] : slab + (uint64_t)i_seg * slot_stride);
@@ -1358,7 +1356,6 @@ __global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
       }
       const uint32_t p0 = o.op;
       uint32_t bits = 0, zeroed = p0;
-      const uint32_t st0 = uniform(w[kWStep + b]);
       // the state words of sequence j (OF, ML, LL: bits | count << 12), loaded a step ahead
       // and combined at their use (combined right away, the loads were waited for at once)
       auto load_words = [&](uint32_t j, uint32_t& oo, uint32_t& om, uint32_t& ol)
@@ -1376,30 +1373,22 @@ __global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
       const uint32_t lastc = (bn - 1) >> 6;
       uint32_t jn = s0 + lastc * kWave + lane;
       uint2 prec = seqs[jn < s1 ? jn : s1 - 1];
+      uint32_t pwc = wcodes[jn < s1 ? jn : s1 - 1];  // codes | offset value << 17 (entropy)
       uint32_t poo, pom, pol;
       load_words(jn < s1 ? jn : s1 - 1, poo, pom, pol);
-      // the step's history before it (zstd_entropy_kernel's scan), loaded a step ahead too
-      uint32_t ph0 = whist[3 * (st0 + lastc)], ph1 = whist[3 * (st0 + lastc) + 1],
-               ph2 = whist[3 * (st0 + lastc) + 2];
       for (int32_t c = (int32_t)lastc; c >= 0 && !o.overflow; --c) {
         const uint32_t j = s0 + (uint32_t)c * kWave + lane;
         const bool act = j < s1;
         const uint2 rec = prec;
-        const uint32_t wd = word(poo, pom, pol);
-        uint32_t h0 = uniform(ph0), h1 = uniform(ph1), h2 = uniform(ph2);
+        const uint32_t wd = word(poo, pom, pol), wc = pwc;
         {  // prefetch the next step (the last step reloads its own: fixed load counts)
           const uint32_t jp = c > 0 ? j - kWave : (j < s1 ? j : s1 - 1);
           prec = seqs[jp];
+          pwc = wcodes[jp];
           load_words(jp, poo, pom, pol);
-          const uint32_t hn = 3 * (st0 + (uint32_t)(c > 0 ? c - 1 : 0));
-          ph0 = whist[hn];
-          ph1 = whist[hn + 1];
-          ph2 = whist[hn + 2];
         }
-        const uint32_t cnt = s1 - (s0 + (uint32_t)c * kWave) < kWave ? s1 - (s0 + (uint32_t)c * kWave) : kWave;
         const uint32_t ll = rec.x & 0x1FFFFu, mlb = rec.y - 3u;
-        const uint32_t ov = rep_scan(ll, rec.x >> 17, act, cnt, h0, h1, h2);
-        const uint32_t llc = ll_code(ll), mlc = ml_code(rec.y), ofc = hb32(ov);
+        const uint32_t llc = wc & 63u, ofc = (wc >> 6) & 31u, mlc = (wc >> 11) & 63u, ov = wc >> 17;
         const uint64_t stb = wd & 0x3FFFFFFu;
         const uint32_t stn = wd >> 26;
         const uint32_t llb = sT.ll_bits[llc], mlbits = sT.ml_bits[mlc];

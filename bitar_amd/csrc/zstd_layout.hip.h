@@ -25,11 +25,9 @@ __host__ __device__ constexpr uint32_t frame_blocks(uint32_t nseq, uint32_t nlit
 // walk scratch (zstd_entropy_kernel -> zstd_walk_kernel -> zstd_emit_kernel), per segment: a
 // record of kW* words; the Huffman codes (256 u32: code | length << 16); the FSE state tables
 // (u16, kTabDummy + 1) and transforms (3 x 64 u32); then per sequence its three codes (u32:
-// LL | OF << 6 | ML << 11, written by the entropy kernel) and each chain's state bits | their
-// count << 12 (u16) in groups of 8 sequences: group g holds the OF, ML and LL words of
-// sequences 8g .. 8g + 7, 8 of each chain (walk_state_at); then per step of up to 64 sequences
-// (steps start at each block's first sequence) the repeat-offset history before it (3 u32),
-// from which zstd_emit_kernel re-derives the offset values of the step
+// LL | OF << 6 | ML << 11 | the offset value << 17, written by the entropy kernel) and each
+// chain's state bits | their count << 12 (u16) in groups of 8 sequences: group g holds the
+// OF, ML and LL words of sequences 8g .. 8g + 7, 8 of each chain (walk_state_at)
 enum : uint32_t {
   kWHanded = 0,  // 1: the emit kernel writes this segment's frame
   kWTrash = 1,   // the target of idle lanes' stores (fixed store counts in loops)
@@ -43,7 +41,7 @@ enum : uint32_t {
   kWTb,          // coded bits of all literals (sum of length x count): the blocks' estimate
   kWSb = 16,     // kBlocks + 1 words: first sequence of each block (then nseq)
   kWLb = 25,     // kBlocks + 1 words: first literal of each block (then nlit)
-  kWStep = 34,   // kBlocks words: first history step of each block
+  kWStep = 34,   // kBlocks words (unused)
   kWFin = 42,    // kBlocks x 3 words: each block's final states (OF, ML, LL)
   kWTreeAt = 68,  // the Huffman tree description (<= 130 bytes)
   kWDescAt = 104,  // modes byte + sequence table descriptions (<= 256 bytes)
@@ -57,9 +55,6 @@ constexpr uint32_t kWTabs = 4 * 424, kWTr = kWTabs + 2 * 1284, kWWords = kWTr + 
 static_assert(kWCodeAt + 256 <= kWTabs / 4, "record words before the tables");
 static_assert(kWTabs % 16 == 0 && kWWords % 8 == 0, "aligned areas");
 __host__ __device__ constexpr uint32_t walk_cap(uint32_t seg) { return seg / 4u + 2u; }  // >= nseq
-__host__ __device__ constexpr uint32_t walk_steps(uint32_t seg) {
-  return (walk_cap(seg) + 63u) / 64u + kBlocks;  // (a block's steps start at its first sequence)
-}
 // u16 index of chain c's state word of sequence k in the state area (chains 0 OF, 1 ML, 2 LL)
 __host__ __device__ constexpr uint32_t walk_state_at(uint32_t k, uint32_t c) {
   return (k >> 3) * 24u + c * 8u + (k & 7u);
@@ -67,11 +62,8 @@ __host__ __device__ constexpr uint32_t walk_state_at(uint32_t k, uint32_t c) {
 __host__ __device__ constexpr uint64_t walk_state_bytes(uint32_t seg) {  // bytes, from the record (16-B aligned)
   return ((uint64_t)kWWords + 4ull * walk_cap(seg) + 15u) & ~15ull;
 }
-__host__ __device__ constexpr uint64_t walk_hist_at(uint32_t seg) {  // bytes, from the record (16-B aligned)
-  return walk_state_bytes(seg) + 48ull * ((walk_cap(seg) + 7u) / 8u);
-}
 __host__ __device__ constexpr uint64_t walk_stride(uint32_t seg) {
-  return (walk_hist_at(seg) + 12ull * walk_steps(seg) + 255u) & ~255ull;
+  return (walk_state_bytes(seg) + 48ull * ((walk_cap(seg) + 7u) / 8u) + 255u) & ~255ull;
 }
 
 }  // namespace zse
