@@ -160,7 +160,9 @@ struct Window {
 // ---- byte output staged in an LDS ring, flushed in aligned 16-B blocks ----------------
 constexpr uint32_t kObuf = BITAR_CMP_OBUF, kObufMask = kObuf - 1;
 
-template <uint32_t OB = kObuf>
+// ZERO: flushed ring bytes are cleared as they go out, so every ring byte at or past op is
+// zero (a bit writer ORs into them; the ring starts zeroed)
+template <uint32_t OB = kObuf, bool ZERO = false>
 struct ByteOutT {
   static constexpr uint32_t kSize = OB, kMask = OB - 1;
   uint8_t* ring;      // LDS, OB bytes + one trash byte per lane
@@ -180,17 +182,24 @@ struct ByteOutT {
     uint32_t head = (uint32_t)((16u - ((base + f) & 15u)) & 15u);
     if (head > upto - f) head = upto - f;
     if (head) {
-      if (lane < head) dst[f + lane] = ring[at(f + lane)];
+      if (lane < head) {
+        dst[f + lane] = ring[at(f + lane)];
+        if constexpr (ZERO) ring[at(f + lane)] = 0;
+      }
       f += head;
     }
     const uint32_t nb = (upto - f) >> 4;
     for (uint32_t b = lane; b < nb; b += kWave) {
       const uint32_t k = f + 16u * b;
       *reinterpret_cast<GMEM uint4*>(dst + k) = *reinterpret_cast<const uint4*>(ring + at(k));
+      if constexpr (ZERO) *reinterpret_cast<uint4*>(ring + at(k)) = make_uint4(0, 0, 0, 0);
     }
     f += nb << 4;
     if (final && f < upto) {
-      if (lane < upto - f) dst[f + lane] = ring[at(f + lane)];
+      if (lane < upto - f) {
+        dst[f + lane] = ring[at(f + lane)];
+        if constexpr (ZERO) ring[at(f + lane)] = 0;
+      }
       f = upto;
     }
     flushed = f;

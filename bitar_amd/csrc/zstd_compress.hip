@@ -621,22 +621,18 @@ __device__ uint32_t choose_table(EntLds& L, uint32_t t, uint32_t nseq, SBits& w)
   return 0u | (def_al << 8) | (def_max << 16);
 }
 
-struct EntOut : ByteOut {
+struct EntOut : ByteOutT<kObuf, true> {
   // OR the lanes' bit fields (v0 of n0 bits, then v1 of n1 bits; n0 + n1 <= 96), in
   // DESCENDING lane order, into the bitstream that starts at output byte p0; bits = bits
-  // written so far; zeroed = first ring byte not yet cleared for the bitstream
+  // written so far (zeroed: unused, the ring is cleared as it is flushed)
   __device__ __forceinline__ void put_bits(uint64_t v0, uint32_t n0, uint64_t v1, uint32_t n1,
                                            uint32_t p0, uint32_t& bits, uint32_t& zeroed) {
-    const uint32_t lane = lane_id();
     const uint32_t nb = n0 + n1;
     const uint32_t incl = wave_incl_sum(nb);
     const uint32_t total = readlane(incl, 63);
     op = p0 + (bits >> 3);
     if (!room((total >> 3) + 16)) return;
-    const uint32_t end = p0 + ((bits + total + 7) >> 3);
-    lds_order();
-    for (uint32_t b = zeroed + lane; b < end; b += kWave) ring[at(b)] = 0;
-    if (end > zeroed) zeroed = end;
+    (void)zeroed;  // (the ring bytes at and past op are zero: cleared as they are flushed)
     const uint32_t pos = bits + total - incl;  // lanes above come first
     const uint32_t base = (((uint32_t)(uintptr_t)dst + p0) & kObufMask) << 3;
     const uint32_t wmask = kObufMask >> 2;
@@ -1174,6 +1170,10 @@ __global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
   o.op = 0;
   o.flushed = 0;
   o.overflow = false;
+  // the ring starts zeroed (EntOut clears what it flushes: the bit writer ORs into it)
+  for (uint32_t k = lane; k < kObuf / 16; k += kWave)
+    reinterpret_cast<uint4*>(obuf)[k] = make_uint4(0, 0, 0, 0);
+  lds_order();
   // frame header: magic, Single_Segment with the content size (1 byte below 256, else 2)
   const uint32_t fh = n < 256 ? 6u : 7u;
   {
