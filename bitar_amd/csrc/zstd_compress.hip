@@ -1222,14 +1222,29 @@ __global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
       // 0.99 / 0.96 ms (kind 2)
       constexpr int32_t kPerLane = BITAR_HUF_PER_LANE;
       static_assert(kPerLane == 4 || kPerLane == 8, "4 or 8 literals per lane");
-      for (int32_t e = hi; e > lo && !o.overflow; e -= kPerLane * (int32_t)kWave) {
+      // (steps end at multiples of 8, so a lane's 8 symbol bytes are ONE aligned 8-byte LDS
+      // read; symbols outside [lo, hi) are masked)
+      static_assert(kPerLane == 8 || kPerLane == 4, "");
+      for (int32_t e = (hi + 7) & ~7; e > lo && !o.overflow; e -= kPerLane * (int32_t)kWave) {
         const int32_t i0 = e - kPerLane * (int32_t)kWave + kPerLane * (int32_t)lane;
+        const int32_t r0 = i0 - 16 * g0;  // in lst (a multiple of kPerLane)
+        lds_order();
+        uint32_t sw[2];
+        if constexpr (kPerLane == 8) {
+          const uint2 v8 = *reinterpret_cast<const uint2*>(lst + (r0 > 0 ? r0 : 0));
+          sw[0] = v8.x;
+          sw[1] = v8.y;
+        } else {
+          sw[0] = *reinterpret_cast<const uint32_t*>(lst + (r0 > 0 ? r0 : 0));
+          sw[1] = 0;
+        }
         // symbols i0 + k + 1 then i0 + k as one field (<= 22 bits)
         auto pair = [&](int32_t k, uint32_t& p, uint32_t& np) __attribute__((always_inline)) {
-          const bool a1 = i0 + k + 1 >= lo, a0 = i0 + k >= lo;
-          lds_order();
-          const uint32_t w1 = hcode[a1 ? lst[i0 + k + 1 - 16 * g0] : 0u];
-          const uint32_t w0 = hcode[a0 ? lst[i0 + k - 16 * g0] : 0u];
+          const bool a1 = (i0 + k + 1 >= lo) & (i0 + k + 1 < hi);
+          const bool a0 = (i0 + k >= lo) & (i0 + k < hi);
+          const uint32_t s1 = (sw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
+          const uint32_t s0 = (sw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+          const uint32_t w1 = hcode[s1], w0 = hcode[s0];
           const uint32_t n1 = a1 ? w1 >> 16 : 0u, n0 = a0 ? w0 >> 16 : 0u;
           p = (a1 ? w1 & 0xFFFFu : 0u) | ((a0 ? w0 & 0xFFFFu : 0u) << n1);
           np = n1 + n0;
