@@ -185,7 +185,12 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
       nb0 = h[kNb];
     }
   }
-  const bool mine = p0 == kHanded && (B == 1 ? nb0 == 1u : nb0 >= 2u && B * g0 < nb0);
+  // (B > 1: the other unit of an 8-block frame may already have finished and moved the
+  // segment to kRecs -- its units can sit in different workgroups under the cost order -- so
+  // kRecs is taken too; exec runs after this whole launch, and a failure's 0xFFFFFFFF, which
+  // is never overwritten, still excludes the segment)
+  const bool handed = p0 == kHanded || (B > 1 && p0 == kRecs);
+  const bool mine = handed && (B == 1 ? nb0 == 1u : nb0 >= 2u && B * g0 < nb0);
   if (B > 1 && lane < L && mine && nq0 > rcap) {  // (more sequences than a valid frame has)
     produced[il0] = 0xFFFFFFFFu;
     atomicOr(err, 1u);

@@ -204,6 +204,53 @@ def test_libzstd_decodes_gpu_frames(eng):
             assert not Z.ZSTD_isError(r) and buf.raw[:r] == plain, (kind, i)
 
 
+def _zstd_blocks(frame):
+    """number of blocks in one RFC 8878 frame (header fields per RFC 8878 3.1.1.1)"""
+    fhd = frame[4]
+    single = (fhd >> 5) & 1
+    p = 5 + (0 if single else 1) + (0, 1, 2, 4)[fhd & 3]
+    p += (1 if single else 0, 2, 4, 8)[fhd >> 6]
+    nb = 0
+    while True:
+        h = frame[p] | frame[p + 1] << 8 | frame[p + 2] << 16
+        nb += 1
+        p += 3 + (1 if (h >> 1) & 3 == 1 else h >> 3)
+        if h & 1:
+            return nb
+
+
+def test_zstd_multiblock_units_in_different_waves(eng):
+    """4-block and 8-block frames mixed in one call of >= 2048 units: the cost-ordered
+    dispatch of zstd_seqdec_kernel<4, 4> puts the two 4-block units of an 8-block frame in
+    different workgroups, and one of them may start after the other finished and moved the
+    segment to kRecs (it must still take its blocks).  Every byte checked, and
+    phase A must have run on every multi-block frame."""
+    import bitar_amd
+    seg, nseg = 65536, 6144
+    n = seg * nseg
+    data = eng.empty(n)
+    eng.fill(2, 11, data)  # the Arrow record batch: literal-heavy columns get 8 blocks
+    slab, stride, sizes = eng.compress(bitar_amd.CODEC_ZSTD, data, seg)
+    eng.sync()
+    gs, g = down(sizes).astype(np.uint32), down(slab)
+    nb = np.array([_zstd_blocks(g[i * stride:i * stride + gs[i]]) for i in range(nseg)])
+    assert (nb == 8).sum() >= 64 and (nb == 4).sum() >= 64, np.bincount(nb)
+    old = eng.set_decoder_options(count_paths=1)
+    try:
+        for rep in range(2):
+            out, prod = eng.decompress(bitar_amd.CODEC_ZSTD, slab, stride, sizes, seg)
+            eng.sync()
+            assert torch.equal(out[:n], data), rep
+            assert int(prod.to(torch.int64).sum().item()) == n
+        pc = eng.path_counters()
+    finally:
+        eng.set_decoder_options(**old)
+    if eng.decoder_options()["zstd_seq"]:
+        assert pc["zstd_seqdec"] >= 2 * int((nb >= 2).sum()), pc
+    del data, slab, out
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("kind", [1, 2])
 def test_zstd_full_size_roundtrip_1gib(eng, kind):
     """BASELINE configs[5] per GPU: 1 GiB, 64 KiB segments, round trip + oracle samples."""
