@@ -84,6 +84,10 @@ class CompressDevice {
   /// HIP extras: bytes per output slot, and the hipStream_t of a queue pair.
   [[nodiscard]] std::uint64_t slot_size() const noexcept { return slot_size_; }
   [[nodiscard]] void* stream(std::uint16_t queue_pair_id) const;
+  /// log2 of the farthest match distance the configured encoder emits (12; 14 for the wide
+  /// LZ4 parse), set by Initialize.  configuration's window_size() is what was requested (or
+  /// this value when 0 was), as in the reference.
+  [[nodiscard]] std::uint8_t encoder_window() const noexcept { return encoder_window_; }
 
   /// \brief Per-segment checksums of the last Compress (over its input) or Decompress (over
   /// its output) on \p queue_pair_id, when the configuration asks for a checksum type: the
@@ -125,6 +129,7 @@ class CompressDevice {
 
   bitar_hip_ctx* ctx_ = nullptr;
   std::uint64_t slot_size_ = 0;
+  std::uint8_t encoder_window_ = 0;
   std::unique_ptr<internal::DeviceMemory> device_memory_;
   std::vector<std::unique_ptr<internal::QueuePairMemory>> qp_memory_;
 };

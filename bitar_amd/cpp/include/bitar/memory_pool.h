@@ -65,4 +65,9 @@ arrow::MemoryPool* GetMemoryPool(MemoryPoolBackend backend);
 void SetHipPoolDevice(int device);
 int HipPoolDevice();
 
+/// Whether this build of the pools writes the debug poison bytes (reference
+/// memory_pool.cc:190-263 under `#ifndef NDEBUG`): false for the shipped release libbitar.so,
+/// true for the debug variant (lib/debug/libbitar.so).
+bool PoolPoisons();
+
 }  // namespace bitar

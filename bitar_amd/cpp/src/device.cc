@@ -734,22 +734,24 @@ arrow::Status CompressDevice<Class, Enable>::ValidateConfiguration() {
     return arrow::Status::Invalid("level is not in the range of [1, 9]");
   if (configuration_->codec() != Codec::LZ4 && configuration_->level() != 1)
     return arrow::Status::Invalid("level is not in the range of [1, 1] for this codec");
-  // window log: the reach of the encoder this configuration runs (bitar_hip_max_distance:
-  // 2560 B -> 2^12, the wide LZ4 parse 14848 B -> 2^14).  The reference sets the device
-  // maximum (device.cc:389-393); here the configured value reports what the encoder actually
-  // uses.  A caller may ask for any window from that up to the format's maximum (DEFLATE 2^15,
-  // LZ4 / single-segment Zstd 2^16): the streams are valid for it, and window_size() then
-  // reports the reach.  A smaller window cannot be honoured and is refused.
+  // window log (reference device.cc:389-393): 0 asks for the device's maximum, which here is
+  // the reach of the encoder this configuration runs (bitar_hip_max_distance: 2560 B -> 2^12,
+  // the wide LZ4 parse 14848 B -> 2^14); a requested window is validated and kept as the
+  // reference keeps it.  Any window from the reach up to the format's maximum (DEFLATE 2^15,
+  // LZ4 / single-segment Zstd 2^16) is honoured -- every stream the encoder writes is valid for
+  // it, and the decoders take the format's full window -- a smaller one is refused.
+  // encoder_window() reports the reach whatever was requested.
   const std::uint32_t reach = bitar_hip_max_distance(internal::AbiCodec(*configuration_));
   std::uint8_t window = 1;
   while ((1u << window) < reach) ++window;
+  encoder_window_ = window;
   const std::uint8_t max_window = configuration_->codec() == Codec::DEFLATE ? 15 : 16;
-  if (configuration_->window_size() != 0 &&
-      (configuration_->window_size() < window || configuration_->window_size() > max_window)) {
+  if (configuration_->window_size() == 0) {
+    configuration_->set_window_size(window);
+  } else if (configuration_->window_size() < window || configuration_->window_size() > max_window) {
     return arrow::Status::Invalid("window_size is not in the range of [", +window, ", ",
                                   +max_window, "]");
   }
-  configuration_->set_window_size(window);
   if (configuration_->max_preallocate_memzones() < internal::kMinPreallocateSlots) {
     return arrow::Status::Invalid("max_preallocate_memzones (",
                                   configuration_->max_preallocate_memzones(),

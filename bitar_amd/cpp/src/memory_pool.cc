@@ -44,9 +44,11 @@ std::uint8_t* const kZeroSizeArea = reinterpret_cast<std::uint8_t*>(&zero_size_a
 
 #ifndef NDEBUG
 // Debug builds mark the first and last byte of a fresh allocation, of the grown part of a
-// reallocation and of a freed buffer, as the reference's pools do (memory_pool.cc:190-263),
-// so that reads of uninitialised or freed pool memory show a recognisable value.  HBM bytes
-// are written through the ABI's copy (both pools' memory is reachable by hipMemcpy).
+// reallocation and (host pool) of a freed buffer, as the reference's pools do
+// (memory_pool.cc:190-263), so that reads of uninitialised or freed pool memory show a
+// recognisable value.  HBM bytes are written through the ABI's copy on the helper context,
+// which no other user of a fresh allocation can race with.  Release builds (-DNDEBUG, the
+// shipped libbitar.so) do none of it.
 constexpr std::uint8_t kAllocPoison = 0xBC;
 constexpr std::uint8_t kReallocPoison = 0xBD;
 constexpr std::uint8_t kDeallocPoison = 0xBE;
@@ -131,7 +133,10 @@ class HipPool : public arrow::MemoryPool {
     auto ctx = internal::HelperContext(device);
     if (ctx.ok()) {
 #ifndef NDEBUG
-      if (size > 0) PoisonEnds(*ctx, kDevice, buffer, buffer + size - 1, kDeallocPoison);
+      // (host memory only: HBM is returned to the driver right away, and a copy on the helper
+      // context's stream would not be ordered after work still queued on a queue pair's
+      // stream that reads the buffer)
+      if (!kDevice && size > 0) PoisonEnds(*ctx, kDevice, buffer, buffer + size - 1, kDeallocPoison);
 #endif
       if (kDevice) (void)bitar_hip_free(*ctx, buffer);
       else (void)bitar_hip_host_free(*ctx, buffer);
@@ -178,6 +183,14 @@ void HipAllocationTracker::Emplace(const HipAllocation& a) {
 void HipAllocationTracker::Release(const std::uint8_t* addr) {
   const std::lock_guard<std::mutex> lock(mutex_);
   allocations_.erase(addr);
+}
+
+bool PoolPoisons() {
+#ifndef NDEBUG
+  return true;
+#else
+  return false;
+#endif
 }
 
 void SetHipPoolDevice(int device) { g_pool_device = device; }

@@ -1,8 +1,12 @@
 // frontend_test.cc -- tests of the bitar C++ front-end (namespace bitar) on MI355X.
 //
-// Modes: `cpu` (no GPU needed: configuration rules, discovery errors) and `gpu <in> <outdir>`
+// Modes: `cpu` (no GPU needed: configuration rules, discovery errors), `gpu <in> <outdir>`
 // (Compress/Decompress/Recycle/async through real devices; compressed segments are written
-// to <outdir> so the Python side can check them with zlib / liblz4).  Mirrors the reference's
+// to <outdir> so the Python side can check them with zlib / liblz4), `arrow <in> <outdir>`
+// (the util::Codec adapters) and `pool <0|1> <in>` (the pools' debug poisoning, expected on
+// or off, and buffers the front-end did not allocate: hipHostRegister'd host memory and HBM
+// owned by another context).  Built twice: against the release libbitar.so (-DNDEBUG) and
+// the debug variant (lib/debug/libbitar.so).  Mirrors the reference's
 // only behavioural checks (apps/demo_app.cc:288-290, 500-501, 534-543, 671-686).
 #include <arrow/api.h>
 #include <arrow/buffer.h>
@@ -11,7 +15,10 @@
 #include <arrow/memory_pool.h>
 #include <arrow/util/compression.h>
 
+#include <hip/hip_runtime_api.h>  // (hipHostRegister: a caller-pinned buffer, PoolTests)
+
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -19,6 +26,7 @@
 #include <vector>
 
 #include "bitar/bitar.h"
+#include "bitar_hip.h"
 
 namespace {
 
@@ -462,29 +470,13 @@ void GpuTests(const std::string& input_path, const std::string& outdir) {
       const auto* c = cfg.get();
       const auto st = d->Initialize(std::move(cfg));
       CHECK(st.ok() == w.ok);
-      if (st.ok()) CHECK(c->window_size() == (w.level >= 2 ? 14 : 12));
+      // (a requested window is kept, 0 is answered with the reach; encoder_window() is the
+      // reach either way)
+      const int reach = w.level >= 2 ? 14 : 12;
+      if (st.ok()) CHECK(c->window_size() == (w.window ? w.window : reach));
+      if (st.ok()) CHECK(d->encoder_window() == reach);
     }
   }
-#ifndef NDEBUG
-  // debug-build pool poisoning (reference memory_pool.cc:190-263): 0xBC at both ends of a
-  // fresh allocation, 0xBD at both ends of a reallocation's grown part, kept bytes intact
-  {
-    auto* pool = bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipHost);
-    uint8_t* p = nullptr;
-    CHECK_OK(pool->Allocate(100, 64, &p));
-    CHECK(p[0] == 0xBC && p[99] == 0xBC);
-    std::memset(p, 7, 100);
-    CHECK_OK(pool->Reallocate(100, 300, 64, &p));
-    CHECK(p[0] == 7 && p[99] == 7 && p[100] == 0xBD && p[299] == 0xBD);
-    pool->Free(p, 300, 64);
-    uint8_t* d = nullptr;  // the HBM pool poisons through the ABI's copy
-    auto* dpool = bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipDevice);
-    CHECK_OK(dpool->Allocate(1, 64, &d));
-    CHECK_OK(dpool->Reallocate(1, 4096, 64, &d));
-    dpool->Free(d, 4096, 64);
-    CHECK(pool->bytes_allocated() == 0);
-  }
-#endif
   // INTEGRATION.md's minimal program, run as written
   CHECK_OK(RoundTrip(data.data(), static_cast<std::int64_t>(data.size())));
   // empty input -> empty vector (device.cc:161-164); empty vector -> OK
@@ -621,6 +613,173 @@ void ArrowCodecTests(const std::string& input_path, const std::string& outdir) {
   }
 }
 
+
+// arrow pools over memory the front-end did not allocate: (a) malloc'd host memory pinned by
+// hipHostRegister (its device address may differ from the host one, so the device must stage
+// it by copy, runtime.hip bitar_hip_pointer_info); (b) HBM of another bitar context
+class RegisteredPool : public arrow::MemoryPool {
+ public:
+  arrow::Status Allocate(int64_t size, int64_t, uint8_t** out) override {
+    void* p = nullptr;
+    if (posix_memalign(&p, 4096, static_cast<std::size_t>(size ? size : 1)) != 0)
+      return arrow::Status::OutOfMemory("posix_memalign");
+    if (hipHostRegister(p, static_cast<std::size_t>(size ? size : 1), hipHostRegisterDefault) != hipSuccess) {
+      std::free(p);
+      return arrow::Status::IOError("hipHostRegister");
+    }
+    *out = static_cast<uint8_t*>(p);
+    bytes_ += size;
+    return arrow::Status::OK();
+  }
+  arrow::Status Reallocate(int64_t old_size, int64_t new_size, int64_t a, uint8_t** ptr) override {
+    uint8_t* fresh = nullptr;
+    ARROW_RETURN_NOT_OK(Allocate(new_size, a, &fresh));
+    std::memcpy(fresh, *ptr, static_cast<std::size_t>(std::min(old_size, new_size)));
+    Free(*ptr, old_size, a);
+    *ptr = fresh;
+    return arrow::Status::OK();
+  }
+  void Free(uint8_t* p, int64_t size, int64_t) override {
+    (void)hipHostUnregister(p);
+    std::free(p);
+    bytes_ -= size;
+  }
+  int64_t bytes_allocated() const override { return bytes_; }
+  std::string backend_name() const override { return "host_registered"; }
+  int64_t max_memory() const override { return -1; }
+  int64_t total_bytes_allocated() const override { return 0; }
+  int64_t num_allocations() const override { return 0; }
+
+ private:
+  int64_t bytes_ = 0;
+};
+
+class OtherContextPool : public arrow::MemoryPool {
+ public:
+  explicit OtherContextPool(bitar_hip_ctx* ctx) : ctx_(ctx) {}
+  arrow::Status Allocate(int64_t size, int64_t, uint8_t** out) override {
+    void* p = nullptr;
+    if (bitar_hip_alloc(ctx_, static_cast<uint64_t>(size ? size : 1), &p) != 0)
+      return arrow::Status::OutOfMemory("bitar_hip_alloc");
+    *out = static_cast<uint8_t*>(p);
+    bytes_ += size;
+    return arrow::Status::OK();
+  }
+  arrow::Status Reallocate(int64_t, int64_t, int64_t, uint8_t**) override {
+    return arrow::Status::NotImplemented("fixed-size test pool");
+  }
+  void Free(uint8_t* p, int64_t size, int64_t) override {
+    (void)bitar_hip_free(ctx_, p);
+    bytes_ -= size;
+  }
+  int64_t bytes_allocated() const override { return bytes_; }
+  std::string backend_name() const override { return "other_context"; }
+  int64_t max_memory() const override { return -1; }
+  int64_t total_bytes_allocated() const override { return 0; }
+  int64_t num_allocations() const override { return 0; }
+
+ private:
+  bitar_hip_ctx* ctx_;
+  int64_t bytes_ = 0;
+};
+
+// one HBM byte back to the host
+uint8_t DeviceByte(bitar_hip_ctx* ctx, const uint8_t* at) {
+  uint8_t v = 0;
+  CHECK(bitar_hip_memcpy(ctx, &v, at, 1, nullptr) == 0);
+  CHECK(bitar_hip_sync(ctx, nullptr) == 0);
+  return v;
+}
+
+void PoolTests(bool expect_poison, const std::string& input_path) {
+  CHECK(bitar::PoolPoisons() == expect_poison);
+  bitar_hip_config cfg{1, 0};
+  bitar_hip_ctx* other = nullptr;
+  CHECK(bitar_hip_open(0, &cfg, &other) == 0);
+  if (!other) return;
+  if (expect_poison) {
+    // debug-build pool poisoning (reference memory_pool.cc:190-263): 0xBC at both ends of a
+    // fresh allocation, 0xBD at both ends of a reallocation's grown part, kept bytes intact;
+    // 0xBE at both ends of a freed host buffer (HBM is returned to the driver unpoisoned)
+    auto* pool = bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipHost);
+    uint8_t* p = nullptr;
+    CHECK_OK(pool->Allocate(100, 64, &p));
+    CHECK(p[0] == 0xBC && p[99] == 0xBC);
+    std::memset(p, 7, 100);
+    CHECK_OK(pool->Reallocate(100, 300, 64, &p));
+    CHECK(p[0] == 7 && p[99] == 7 && p[100] == 0xBD && p[299] == 0xBD);
+    pool->Free(p, 300, 64);
+    // the HBM pool, read back through the ABI's copy
+    auto* dpool = bitar::GetMemoryPool(bitar::MemoryPoolBackend::HipDevice);
+    uint8_t* d = nullptr;
+    CHECK_OK(dpool->Allocate(4096, 64, &d));
+    CHECK(DeviceByte(other, d) == 0xBC && DeviceByte(other, d + 4095) == 0xBC);
+    static const uint8_t k7[2] = {7, 7};
+    CHECK(bitar_hip_memcpy(other, d, k7, 1, nullptr) == 0 &&
+          bitar_hip_memcpy(other, d + 4095, k7, 1, nullptr) == 0 &&
+          bitar_hip_sync(other, nullptr) == 0);
+    CHECK_OK(dpool->Reallocate(4096, 10000, 64, &d));
+    CHECK(DeviceByte(other, d) == 7 && DeviceByte(other, d + 4095) == 7);
+    CHECK(DeviceByte(other, d + 4096) == 0xBD && DeviceByte(other, d + 9999) == 0xBD);
+    dpool->Free(d, 10000, 64);
+    CHECK(pool->bytes_allocated() == 0 && dpool->bytes_allocated() == 0);
+  }
+  // buffers the front-end did not allocate, through Compress and Decompress
+  const auto data = ReadFile(input_path);
+  CHECK(data.size() > 100000);
+  auto* driver = bitar::CompressDriver<bitar::Class_HIP_GFX950>::Instance();
+  auto ids = driver->ListAvailableDeviceIds();
+  CHECK_OK(ids.status());
+  if (!ids.ok()) return;
+  RegisteredPool registered;
+  OtherContextPool foreign(other);
+  for (const auto codec : {bitar::Codec::LZ4, bitar::Codec::DEFLATE, bitar::Codec::ZSTD}) {
+    const std::uint32_t seg = codec == bitar::Codec::DEFLATE ? 59460 : 65536;
+    const auto nseg = (data.size() + seg - 1) / seg;
+    auto devs = driver->GetDevices({(*ids)[0]});
+    CHECK_OK(devs.status());
+    if (!devs.ok()) return;
+    auto& d = (*devs)[0];
+    CHECK_OK(d->Initialize(MakeConfig(codec, seg)));
+    for (arrow::MemoryPool* pool : {static_cast<arrow::MemoryPool*>(&registered),
+                                    static_cast<arrow::MemoryPool*>(&foreign)}) {
+      const bool host = pool == &registered;
+      auto in = arrow::AllocateBuffer(static_cast<int64_t>(data.size()), pool);
+      CHECK_OK(in.status());
+      if (!in.ok()) continue;
+      std::shared_ptr<arrow::Buffer> input = std::move(*in);
+      if (host) {
+        std::memcpy(input->mutable_data(), data.data(), data.size());
+      } else {
+        CHECK(bitar_hip_memcpy(other, input->mutable_data(), data.data(), data.size(), nullptr) == 0);
+        CHECK(bitar_hip_sync(other, nullptr) == 0);
+      }
+      auto comp = d->Compress(0, input);
+      CHECK_OK(comp.status());
+      if (!comp.ok()) continue;
+      CHECK(comp->size() == nseg);
+      auto o = arrow::AllocateResizableBuffer(static_cast<int64_t>(nseg * seg), pool);
+      CHECK_OK(o.status());
+      if (!o.ok()) continue;
+      std::unique_ptr<arrow::ResizableBuffer> out = std::move(*o);
+      // (the foreign pool cannot grow a buffer: the output is allocated at full capacity)
+      CHECK_OK(d->Decompress(0, *comp, out));
+      CHECK(out->size() == static_cast<int64_t>(data.size()));
+      std::vector<uint8_t> back(data.size());
+      if (host) {
+        std::memcpy(back.data(), out->data(), data.size());
+      } else {
+        CHECK(bitar_hip_memcpy(other, back.data(), out->data(), data.size(), nullptr) == 0);
+        CHECK(bitar_hip_sync(other, nullptr) == 0);
+      }
+      CHECK(std::memcmp(back.data(), data.data(), data.size()) == 0);
+      CHECK(d->Recycle(*comp) == comp->size());
+    }
+  }
+  CHECK(registered.bytes_allocated() == 0 && foreign.bytes_allocated() == 0);
+  CHECK(bitar_hip_close(other) == 0);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -630,12 +789,14 @@ int main(int argc, char** argv) {
     // no GPU in the build container: discovery must fail cleanly, not crash
     auto ids = bitar::CompressDriver<bitar::Class_HIP_GFX950>::Instance()->ListAvailableDeviceIds();
     if (!ids.ok()) CHECK(ids.status().IsInvalid());
+  } else if (argc >= 4 && mode == "pool") {
+    PoolTests(std::string(argv[2]) == "1", argv[3]);
   } else if (argc >= 4 && mode == "arrow") {
     ArrowCodecTests(argv[2], argv[3]);
   } else if (argc >= 4) {
     GpuTests(argv[2], argv[3]);
   } else {
-    std::cerr << "usage: frontend_test cpu | gpu <input> <outdir> | arrow <input> <outdir>\n";
+    std::cerr << "usage: frontend_test cpu | gpu <input> <outdir> | arrow <input> <outdir> | pool <0|1> <input>\n";
     return 2;
   }
   std::cout << (g_failures ? "FAILED " : "PASSED ") << g_failures << " failures\n";

@@ -34,6 +34,21 @@ def test_frontend_builds_and_cpu_rules():
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_release_and_debug_builds():
+    """The shipped libbitar.so is the release build (-DNDEBUG): its pools do not poison memory
+    (the reference poisons only without NDEBUG, memory_pool.cc:190-263); lib/debug/libbitar.so
+    is the debug variant that does."""
+    _build()
+    for path, want in ((os.path.join(CPP, "lib", "libbitar.so"), False),
+                       (os.path.join(CPP, "lib", "debug", "libbitar.so"), True)):
+        L = ctypes.CDLL(path)
+        f = L._ZN5bitar11PoolPoisonsEv
+        f.restype = ctypes.c_bool
+        assert f() is want, path
+    r = subprocess.run([BIN + "_debug", "cpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_integration_example_is_the_tested_code():
     """INTEGRATION.md's minimal program is the function frontend_test runs in GPU mode, word
     for word (so the documented flow is the tested one)."""
@@ -124,6 +139,23 @@ def test_frontend_on_gpu(tmp_path):
                 rc, got = dec(stream, k * seg)
                 assert rc == 0 and got == plain, (name, j)
             assert enc(plain) == (0, stream), (name, j)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["release", "debug"])
+def test_frontend_pools_on_gpu(tmp_path, variant):
+    """Pool poisoning read back (debug: 0xBC / 0xBD at the ends of fresh and grown HBM and host
+    allocations; release: none), and Compress / Decompress of LZ4, DEFLATE and Zstd over
+    buffers the front-end did not allocate: hipHostRegister'd host memory (staged by copy:
+    its device address may differ) and HBM owned by another bitar context."""
+    binary = BIN + ("_debug" if variant == "debug" else "")
+    if not os.path.exists(binary):
+        _build()
+    inp = tmp_path / "input.bin"
+    inp.write_bytes(O.fill(O.KIND_ARROW, 17, 5 * 65536 + 4321).tobytes())
+    r = subprocess.run([binary, "pool", "1" if variant == "debug" else "0", str(inp)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 def _lz4f_compress(plain, independent, block_checksum, content_checksum, content_size):
