@@ -186,9 +186,18 @@ def run_job(eng, codec_name, kind, job_bytes, seg, nstreams, steps, warmup, worl
              "parts": len(job.layout.parts)}
     total_c = int(job.index[-1].item())
     job.free()
-    (elapsed, bad), (csum,) = reduce_max_sum([elapsed, 0.0 if ok else 1.0], [float(csize)], world)
+    t_comp, t_dec = sum(comp_ms) / len(comp_ms) / 1e3, sum(dec_ms) / len(dec_ms) / 1e3
+    # max over ranks, and the per-rank spread (min through the max of the negation), so the
+    # first multi-GPU run can be diagnosed from its line: a slow rank shows as max/min > 1
+    (elapsed, bad, tc_max, td_max, n_el, n_tc, n_td), (csum,) = reduce_max_sum(
+        [elapsed, 0.0 if ok else 1.0, t_comp, t_dec, -elapsed, -t_comp, -t_dec], [float(csize)], world)
+    spread = {"elapsed_s": [round(-n_el, 6), round(elapsed, 6)],
+              "compress_launch_ms": [round(-n_tc * 1e3, 4), round(tc_max * 1e3, 4)],
+              "decompress_launch_ms": [round(-n_td * 1e3, 4), round(td_max * 1e3, 4)],
+              "elapsed_max_over_min": round(elapsed / -n_el, 4) if n_el else None}
     return {"elapsed": elapsed, "ok": bad == 0.0, "csize_local": csize, "csize_total": total_c,
-            "t_comp": sum(comp_ms) / len(comp_ms) / 1e3, "t_dec": sum(dec_ms) / len(dec_ms) / 1e3,
+            "rank_spread": spread,
+            "t_comp": t_comp, "t_dec": t_dec,
             "t_comp_span": sum(comp_span) / len(comp_span) / 1e3,
             "t_dec_span": sum(dec_span) / len(dec_span) / 1e3,
             "local": local, "job_bytes": job_bytes}
@@ -250,7 +259,8 @@ def leg_summary(name, r, world, steps, traffic_json, workload, leg=None):
             "compression_ratio": round(U / r["csize_total"], 4) if r["csize_total"] else None,
             "compress_gibs_per_launch": round(r["local"]["nbytes"] / r["local"]["parts"] / r["t_comp"] / GIB, 3),
             "decompress_gibs_per_launch": round(r["local"]["nbytes"] / r["local"]["parts"] / r["t_dec"] / GIB, 3),
-            "roundtrip_ok": r["ok"], "roofline": roof, "kernels": kern}
+            "roundtrip_ok": r["ok"], "roofline": roof, "kernels": kern,
+            **({"rank_spread": r["rank_spread"]} if world > 1 else {})}
 
 
 def random_decompress(eng, n, seg, args):
@@ -696,6 +706,8 @@ def main():
         "roofline": roof,
         "kernels": kernels,
     }
+    if world > 1:
+        res["rank_spread"] = r["rank_spread"]
     if stock is not None:
         res["stock_ratio"] = {
             "ours_lz4": res["compression_ratio"] if std else None,

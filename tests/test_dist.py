@@ -127,3 +127,81 @@ def test_assign_covers_every_segment_once():
 def test_frame_index_single_rank():
     sizes = torch.tensor([5, 0, 7, 0xFFFF], dtype=torch.int64)
     assert bd.frame_index(sizes).tolist() == [0, 5, 5, 12, 12 + 0xFFFF]
+
+
+# ---- world size 8 rehearsal (the 8-GPU node's rank count) ----------------------------------
+# BASELINE configs[3]: an 8 GiB record batch in 64 KiB chunks (131072 segments, 4 queue-pair
+# streams per rank); configs[4]: 8 GiB of Zstd column buffers in 64 KiB segments over 2
+# streams.  Each rank builds its Layout, makes up deterministic per-segment sizes for the
+# segments it owns (a hash of the global id: no compression here, the bookkeeping is under
+# test), all-gathers them with SizeGather over gloo and builds the frame index; every rank
+# must hold the same global sizes and index as a single-process computation, and the ranks'
+# runs must cover every segment and byte of the job exactly once.
+JOBS8 = {"configs3": (8 << 30, 65536, 4), "configs4": (8 << 30, 65536, 2),
+         "ragged": ((8 << 30) - 12345, 59460, 3)}
+
+
+def _fake_sizes(gids):
+    return ((gids * 2654435761) >> 7) % 70000 + 1  # (some above 65535: uint32 values)
+
+
+def _rank8_main(rank, world, port, q):
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        out = {}
+        for name, (job, seg, nstreams) in JOBS8.items():
+            lay = bd.Layout(job, seg, world, rank, nstreams=nstreams)
+            gids = lay.shard.segments
+            local = _fake_sizes(gids).to(torch.int32)
+            sizes = bd.SizeGather(lay.nseg, world)(local)
+            index = bd.frame_index(sizes)
+            runs = [(r.gseg, r.lseg, r.count, r.goff, r.loff, r.nbytes) for r in lay.runs]
+            parts = [(p.stream, p.lseg, p.count, p.loff, p.nbytes) for p in lay.parts]
+            out[name] = (int(sizes.sum()), int(index[-1]), int((index[:-1] * 7 % 1000003).sum()),
+                         runs, parts, lay.local_nseg, lay.local_bytes)
+        q.put((rank, out))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as ex:  # pragma: no cover - reported to the parent
+        q.put((rank, "error: " + repr(ex)))
+
+
+def test_world8_layout_gather_and_index():
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank8_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r, v in res.items():
+        assert not isinstance(v, str), (r, v)
+    for name, (job, seg, nstreams) in JOBS8.items():
+        nseg = (job + seg - 1) // seg
+        ref = _fake_sizes(torch.arange(nseg, dtype=torch.int64))
+        ref_index = bd.frame_index(ref)
+        want = (int(ref.sum()), int(ref_index[-1]), int((ref_index[:-1] * 7 % 1000003).sum()))
+        seg_cover = torch.zeros(nseg, dtype=torch.int32)
+        nbytes = 0
+        for r in range(world):
+            total, last, chk, runs, parts, lnseg, lbytes = res[r][name]
+            assert (total, last, chk) == want, (name, r)
+            # runs: round-robin batches of 256, stored contiguously in ascending order
+            lseg = loff = 0
+            for gseg, rl, count, goff, rloff, nb in runs:
+                assert (rl, rloff) == (lseg, loff) and gseg % 256 == 0 and (gseg // 256) % world == r
+                assert goff == gseg * seg and nb == min(count * seg, job - goff)
+                seg_cover[gseg:gseg + count] += 1
+                lseg += count
+                loff += nb
+            assert (lseg, loff) == (lnseg, lbytes)
+            nbytes += lbytes
+            # parts: nstreams near-equal runs of whole local segments covering the rank's share
+            assert sum(p[2] for p in parts) == lnseg and sum(p[4] for p in parts) == lbytes
+            assert max(p[2] for p in parts) - min(p[2] for p in parts) <= 1
+            assert len(parts) == min(nstreams, lnseg)
+        assert bool((seg_cover == 1).all()) and nbytes == job, name

@@ -31,6 +31,10 @@ def test_bench_two_ranks_share_one_gpu():
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["roundtrip_ok"] and r["value"] > 0
     assert r["config"]["segments_per_gpu"] == 1024  # 128 MiB job, batches of 256 segments
+    # per-rank spread of the timed region and launch durations (min, max over ranks)
+    sp = r["rank_spread"]
+    assert sp["elapsed_s"][0] <= sp["elapsed_s"][1] and sp["elapsed_max_over_min"] >= 1.0
+    assert sp["compress_launch_ms"][0] <= sp["compress_launch_ms"][1]
     for leg in ("recordbatch", "zstd", "deflate"):
         assert r[leg]["roundtrip_ok"], leg
 
