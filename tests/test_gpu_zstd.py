@@ -206,6 +206,7 @@ def test_libzstd_decodes_gpu_frames(eng):
 
 def _zstd_blocks(frame):
     """number of blocks in one RFC 8878 frame (header fields per RFC 8878 3.1.1.1)"""
+    frame = bytes(frame)  # (python ints: numpy uint8 shifts would wrap)
     fhd = frame[4]
     single = (fhd >> 5) & 1
     p = 5 + (0 if single else 1) + (0, 1, 2, 4)[fhd & 3]
