@@ -56,7 +56,10 @@ constexpr uint32_t kIn = BITAR_CMP_RING, kInMask = kIn - 1;  // LDS input ring
 constexpr uint32_t kMaxDist = kIn - 1536;
 constexpr uint32_t kInPad = 64;  // mirror of ring[0, 64) after its end: probes never wrap
 constexpr uint32_t kRow = 1024;                   // prefetch row: one 16-B block per lane
-constexpr uint32_t kPreExt = 32;                  // parallel per-lane match extension limit
+#ifndef BITAR_CMP_PREEXT
+#define BITAR_CMP_PREEXT 32
+#endif
+constexpr uint32_t kPreExt = BITAR_CMP_PREEXT;    // parallel per-lane match extension limit
 
 template <uint32_t HLOG = kHashLog>
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - HLOG); }
@@ -261,7 +264,7 @@ __device__ __forceinline__ uint32_t chain_fast(uint64_t& m, uint64_t extm, uint3
 // folds into the chain-end compare and runs once per window: 7 SALU + 1 VALU per match.
 // The lane's chain bit is set here (the caller sets it again after the extension).
 #ifndef BITAR_CMP_CHAIN
-#define BITAR_CMP_CHAIN 2
+#define BITAR_CMP_CHAIN 3
 #endif
 constexpr uint32_t kExtLen = 128;
 __device__ __forceinline__ uint32_t chain_fast2(uint64_t& m, uint32_t lenw, uint64_t& chain,
@@ -292,6 +295,43 @@ __device__ __forceinline__ uint32_t chain_fast2(uint64_t& m, uint32_t lenw, uint
       : [len] "v"(lenw)
       : "scc");
   return l;
+}
+
+// Form 3 (BITAR_CMP_CHAIN == 3): the successor of every lane is computed once per window on
+// the VALU -- nx[j] = the first valid lane at or past j + len[j] (64: the chain leaves the
+// window; 128 + j: lane j needs the cooperative extension, whose length is not known yet) --
+// so the scalar loop per match is one v_readlane (the next lane is the next lane select),
+// one s_bitset1, one compare and one branch (unrolled twice).  Matches per window: 6.6 on
+// kind 1, up to 8.6 on kind 5 (oracle counts), so the chain was ~half of the parse's scalar
+// instructions.  Returns the lane that stopped the walk (64, or 128 + an extension lane),
+// every chain lane before it set in `chain`.  (A VALU-written SGPR needs 4 wait states before
+// it is a lane select: s_nop 1 + the compare + the branch + the bitset.)
+__device__ __forceinline__ uint32_t chain_succ(uint32_t l, uint32_t nx, uint64_t& chain) {
+  __asm__ volatile(
+      "L_cs_%=:\n"
+      "s_bitset1_b64 %[ch], %[l]\n"
+      "v_readlane_b32 %[l], %[nx], %[l]\n"
+      "s_nop 1\n"
+      "s_cmp_gt_u32 %[l], 63\n"
+      "s_cbranch_scc1 L_co_%=\n"
+      "s_bitset1_b64 %[ch], %[l]\n"
+      "v_readlane_b32 %[l], %[nx], %[l]\n"
+      "s_nop 1\n"
+      "s_cmp_lt_u32 %[l], 64\n"
+      "s_cbranch_scc1 L_cs_%=\n"
+      "L_co_%=:\n"
+      : [l] "+s"(l), [ch] "+s"(chain)
+      : [nx] "v"(nx)
+      : "scc");
+  return l;
+}
+// per lane: nx as above, from e = lane + lenw (lenw = 128 on extension lanes)
+__device__ __forceinline__ uint32_t chain_next(uint64_t valid, uint32_t e) {
+  const uint64_t t = ~0ull << (e & 63u);
+  const uint32_t lo = (uint32_t)t & (uint32_t)valid, hi = (uint32_t)(t >> 32) & (uint32_t)(valid >> 32);
+  const uint32_t f = min(min(ffbl(lo), __builtin_elementwise_add_sat(ffbl(hi), 32u)), 64u);
+  const uint32_t far = e >= 128u ? e : 64u;
+  return e >= 64u ? far : f;
 }
 
 // The window-scan parse over one segment; hands each window to E::window and the tail to
@@ -417,7 +457,69 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       uint32_t mlen_v = len;
       uint64_t m = valid;
       uint32_t e = 0;
-#if BITAR_CMP_CHAIN == 2
+#if BITAR_CMP_CHAIN == 3
+      uint32_t lenw;
+      __asm__("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(lenw) : "v"(len), "v"(kExtLen), "s"(extm));
+      if (valid) {
+        const uint32_t nx = chain_next(valid, lane + lenw);
+        uint32_t l = lowbit(valid);
+        for (;;) {
+          l = chain_succ(l, nx, chain);
+          if (l < 128u) break;
+          l -= 128u;  // an extension lane (its chain bit is set): extend it cooperatively
+          const uint32_t i = x + l;
+          uint32_t li = match_limit - i;
+          if (li > max_mlen) li = max_mlen;
+          const uint32_t c = readlane(cand, l);
+          const uint32_t lr = li < F - i ? li : F - i;
+          uint32_t k = kPreExt;
+          bool more = true;
+          for (;;) {
+            const uint32_t kk = k + 4u * lane;
+            uint32_t cl = 4;
+            if (kk < lr) {
+              cl = common4(I.dword(i + kk), I.dword(c + kk));
+              if (cl > lr - kk) cl = lr - kk;
+            }
+            const uint64_t stop = ballot(kk >= lr || cl < 4);
+            if (stop) {
+              const uint32_t sl = (uint32_t)__builtin_ctzll(stop);
+              const uint32_t ks = k + 4u * sl;
+              k = ks >= lr ? lr : ks + readlane(cl, sl);
+              more = k == lr && lr < li;
+              break;
+            }
+            k += 4u * kWave;
+          }
+          while (more) {
+            const uint32_t kk = k + 16u * lane;
+            uint32_t cl = 16;
+            if (kk < li) {
+              const uint4 a = ld16u(in + i + kk, in_end);
+              const uint4 b = ld16u(in + c + kk, in_end);
+              cl = common16(a, b);
+              if (cl > li - kk) cl = li - kk;
+            }
+            const uint64_t stop = ballot(kk >= li || cl < 16);
+            if (stop) {
+              const uint32_t sl = (uint32_t)__builtin_ctzll(stop);
+              const uint32_t ks = k + 16u * sl;
+              k = ks >= li ? li : ks + readlane(cl, sl);
+              break;
+            }
+            k += 16u * kWave;
+          }
+          if (lane == l) mlen_v = k;
+          const uint32_t ee = l + k;
+          const uint64_t rest = ee < kWave ? valid & (~0ull << ee) : 0ull;
+          if (!rest) break;
+          l = lowbit(rest);
+        }
+        const uint32_t last = highbit(chain);
+        e = last + readlane(mlen_v, last);
+      }
+      if (false) {
+#elif BITAR_CMP_CHAIN == 2
       uint32_t lenw;
       __asm__("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(lenw) : "v"(len), "v"(kExtLen), "s"(extm));
 #endif
@@ -482,6 +584,9 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
         e = l + mlen;
         m = e < kWave ? valid & (~0ull << e) : 0ull;
       }
+#if BITAR_CMP_CHAIN == 3
+      }
+#endif
       if (chain) pos = x + e;
       if constexpr (REP) {
         // the history after this window's matches: the 3 most recently used distinct
