@@ -114,6 +114,88 @@ struct Lz4Out : ByteOutT<kLz4Obuf> {
     if (ml >= 15) put_ext(ml - 15);
   }
 
+#ifndef BITAR_LZ4_GATHER
+#define BITAR_LZ4_GATHER 2
+#endif
+#if BITAR_LZ4_GATHER == 2
+  // records of lanes [lo, hi) (all ordinary) as LZ4 sequences, gathered 64 output bytes per
+  // step; false (nothing written) if they would overrun the slot.
+  // Per step (u = output byte + 1, vs op; lane t holds byte R + t):
+  //  * the sequence of each byte: every token in the step marks its byte (LDS, the mark is
+  //    the token's u and is cleared once read), one compare turns the marks into the step's
+  //    start mask S, and the byte's sequence lane is lo - 1 + (tokens before the step) +
+  //    (tokens at bytes R .. R + t): S & 1 on the scalar unit, the rest one v_mbcnt pair;
+  //  * the byte itself: one ds_bpermute each of three packed words -- pA = A | T1 << 16
+  //    (A = u of the token less the literal-length byte's presence, so r = u - A is 0 / 1 for
+  //    the header bytes and >= 2 for literals whether or not that byte exists; T1 = u of the
+  //    first offset byte), pH = the two header bytes | (the literal's ring index - u) << 16,
+  //    pT = offset | match-length byte << 16 -- then sel = min(u - T1, r + 4, 6) indexes
+  //    {pT bytes 0..3, hb0, hb1, literal}: one v_perm builds the upper word, one picks.
+  // 18 VALU per 64 output bytes (the mark-tag / prefix-max form: ~50).
+  __device__ __forceinline__ bool bulk(const InRing& I, uint32_t lo, uint32_t hi, uint32_t q,
+                                       uint32_t lit_start, uint32_t off, uint32_t mlen) {
+    const uint32_t lane = lane_id();
+    const bool in = (lane >= lo) & (lane < hi);
+    const uint32_t lit_len = q - lit_start, ml = mlen - kMinMatch;
+    const uint32_t nlx = lit_len >= 15 ? 1u : 0u, nmx = ml >= 15 ? 1u : 0u;
+    const uint32_t e = in ? 3u + nlx + nmx + lit_len : 0u;
+    const uint32_t incl = wave_incl_sum(e);
+    const uint32_t total = readlane(incl, kWave - 1);
+    if ((uint64_t)op + total > cap) return false;
+    const uint32_t a = incl - e;  // output offset of the sequence's token
+    const uint32_t tok = ((lit_len < 15 ? lit_len : 15) << 4) | (ml < 15 ? ml : 15);
+    const uint32_t A = a + nlx;
+    const uint32_t T1 = a + 2u + nlx + lit_len;
+    const uint32_t hb = nlx ? tok | (((lit_len - 15u) & 0xFFu) << 8) : tok << 8;
+    const uint32_t D = I.in_lo + lit_start - A - 2u;  // ring index of a literal byte = D + u
+    const uint32_t pA = A | (T1 << 16);
+    const uint32_t pH = hb | (D << 16);
+    const uint32_t pT = (off & 0xFFFFu) | (((ml - 15u) & 0xFFu) << 16);
+    // mark slot x4 (lanes outside [lo, hi): the trash slot), and the mark: the token's u
+    const uint32_t a4 = in ? a << 2 : 0x7FFFFF00u;
+    const uint32_t mark = a + 1u;
+    const uint32_t zero = 0;
+    const uint32_t rbase = (uint32_t)(uintptr_t)dst + op - 1u;  // ring index = rbase + u
+    uint32_t u = lane + 1u;
+    uint32_t before = lo - 1u;  // lo - 1 + tokens before the step
+    for (uint32_t R = 0; R < total; R += kWave) {
+      // (the slot's capacity was checked for the whole batch: only the staging ring's room)
+      if (op + kWave - flushed > kLz4Obuf - 64) flush(op, false);
+      lds_order();
+      const uint32_t slot = min(a4 - (R << 2), (uint32_t)kWave << 2);
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(L->marks) + slot) = mark;
+      lds_order();
+      const uint32_t mk = L->marks[lane];
+      L->marks[lane] = zero;
+      const uint64_t S = ballot(mk == u);
+      const uint32_t base = before + (uint32_t)(S & 1u);
+      const uint64_t S1 = S >> 1;
+      // (the scalar base added after the shift: one v_lshl_add, no v_mov into the mbcnt)
+      const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(S1 >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)S1, 0u));
+      before += (uint32_t)__builtin_popcountll(S);
+      const int src = (int)((idx << 2) + (base << 2));
+      const uint32_t qA = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pA);
+      const uint32_t qH = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pH);
+      const uint32_t qT = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pT);
+      const uint32_t r = u - (qA & 0xFFFFu);
+      const uint32_t t = u - (qA >> 16);
+      const uint32_t sel = min(min(t, r + 4u), 6u);
+      const uint32_t litb = I.ring[(((u << 16) + qH) >> 16) & I.mask];
+      // [hb0, hb1, literal, 0] then {pT bytes, that}[sel]
+      const uint32_t hi4 = __builtin_amdgcn_perm(litb, qH, 0x0C040100u);
+      const uint32_t b = __builtin_amdgcn_perm(hi4, qT, sel);
+      const uint32_t nb = total - R < kWave ? total - R : kWave;
+      // all 64 bytes are written: those past nb lie at or past the new op, inside the room
+      // just made, and are rewritten before they are flushed
+      ring[(rbase + u) & kMask] = (uint8_t)b;
+      lds_order();
+      op += nb;
+      u += kWave;
+    }
+    return true;
+  }
+#else
   // records of lanes [lo, hi) (all ordinary) as LZ4 sequences, gathered 64 output bytes per
   // step; false (nothing written) if they would overrun the slot
   __device__ __forceinline__ bool bulk(const InRing& I, uint32_t lo, uint32_t hi, uint32_t q,
@@ -166,6 +248,7 @@ struct Lz4Out : ByteOutT<kLz4Obuf> {
     }
     return true;
   }
+#endif
 
   // every pending record as LZ4 sequences
   __device__ __forceinline__ void flush_seqs(const GMEM uint8_t* in, const InRing& I) {

@@ -402,6 +402,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
     auto window = [&](uint32_t x) __attribute__((always_inline)) {
       const uint32_t p = x + lane;
       const bool act = p <= last_start;
+      const uint64_t actm = ballot(p <= last_start);  // (a single compare: see the read-back)
       const uint4 v = vp;
       const uint32_t h = hash4<HLOG>(v.x);
       // Table and ring accesses are issued on all lanes (no exec-mask branches: the scalar
@@ -442,7 +443,11 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       // lanes at or past the parse position holding a match, and those of them whose match
       // reached kPreExt bytes and may go on (cooperative extension during the walk)
       const uint32_t pos_in = pos;
-      const uint32_t start = pos > x ? pos - x : 0u;
+      // (pos > x ? pos - x : 0 as a uniform max: the compiler's saturating subtract is a VALU
+      // clamp plus a readfirstlane)
+      uint32_t start;
+      __asm__("s_max_u32 %0, %1, %2" : "=s"(start) : "s"(pos), "s"(x));
+      start -= x;
       // (len >= kMinMatch implies pre; ballots of single compares, see wave.hip.h)
       uint64_t valid = ballot(len >= kMinMatch) & (start < kWave ? ~0ull << start : 0ull);
       if constexpr (REP) {  // a hash-only match gives way to a repeat match just ahead
@@ -624,7 +629,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       // (the empty asm pins the read-back's use, and so its wait, here)
       uint32_t bk = back;
       __asm__ volatile("" : "+v"(bk));
-      if (ballot(bk < p) & ballot(act)) {  // rare: only on same-slot collisions
+      if (ballot(bk < p) & actm) {  // rare: only on same-slot collisions
         bool redo = act && bk < p;
         while (ballot(redo)) {
           lds_order();
