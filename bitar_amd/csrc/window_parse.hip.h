@@ -674,7 +674,10 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       if constexpr (SKIP) {
         if (x - g + (kWave - 1) >= kSkipProbe + kWave - 1) {  // g >= x + 64, or x >= g + 128
           if (pos >= x + kWave) {  // inside the current match
-            x += kWave;
+            // every window lying wholly inside it at once (skipped windows do nothing else),
+            // but not past the next row load, which the loop's top must see
+            const uint32_t xs = x + ((pos - x) & ~(kWave - 1));
+            x = xs < next_load ? xs : next_load;
             lds_order();
             vp = I.bytes16(x + lane);
             continue;
