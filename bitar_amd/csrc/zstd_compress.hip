@@ -111,6 +111,162 @@ __device__ __forceinline__ uint32_t ml_code(uint32_t ml) {  // ml >= 3
 // ---- scratch layout: zstd_layout.hip.h ------------------------------------------------------
 
 // ---- pass 1: the parse, literals + sequence records ---------------------------------------
+#ifndef BITAR_ZSTD_BULK
+#define BITAR_ZSTD_BULK 1
+#endif
+#if BITAR_ZSTD_BULK
+// Batched (as the LZ4 emitter, compress.hip): each window only appends its matches {start |
+// distance << 16, length} to an LDS list; every <= 48 records (and before the tail) one flush
+// writes their 8-byte records with one coalesced store and gathers their literal runs
+// [previous match end, match start) into the literal area, 64 literal bytes per step: every
+// non-empty run marks its first byte (its u = offset + 1 in the batch's literals), one compare
+// gives the step's start mask, a v_mbcnt pair the run (counted over the non-empty runs, whose
+// ring offsets are compacted to their rank once per batch), one ds_bpermute its offset, one
+// LDS read the byte.  Runs that start before the input ring's low end (probe-skipped stretches,
+// long random runs) take the per-run path (HBM -> HBM beyond 256 bytes).
+constexpr uint32_t kZsCap = 64;      // records per flush (a window adds <= 16)
+constexpr uint32_t kZsObuf = 512;    // literal staging ring
+struct ZsLds {
+  uint8_t ring[kZsObuf];
+  uint2 recs[kZsCap + 1];            // + a trash record
+  uint32_t marks[kWave + 1];         // zero between steps; + trash
+};
+struct SeqCollect : ByteOutT<kZsObuf> {
+  ZsLds* L;
+  GMEM uint2* seqs;
+  uint32_t nseq;      // records written
+  uint32_t npend;     // records pending in L->recs
+  uint32_t last_end;  // end of the last match (the next literal run's start)
+
+  // literal bytes [s, s + len) of the input, appended to the literal area
+  __device__ __forceinline__ void literals(const GMEM uint8_t* in, const InRing& I, uint32_t s,
+                                           uint32_t len) {
+    if (!len) return;
+    const uint32_t lane = lane_id();
+    if (len <= 256 && s >= I.lo) {
+      for (uint32_t k = 0; k < len; k += kWave) {
+        const uint32_t step = len - k < kWave ? len - k : kWave;
+        room(step);
+        lds_order();
+        const uint32_t b = I.byte(s + k + (lane < step ? lane : 0u));
+        put(b, step);
+      }
+    } else {  // long run (or not in the input ring): drain the ring, then HBM -> HBM
+      flush(op, true);
+      wave_copy_global(dst + op, in + s, len);
+      op += len;
+      flushed = op;
+    }
+  }
+  // the literal runs of lanes [lo, hi) (all in the input ring), gathered 64 bytes per step
+  __device__ __forceinline__ void gather(const InRing& I, uint32_t lo, uint32_t hi,
+                                         uint32_t lit_start, uint32_t ll) {
+    const uint32_t lane = lane_id();
+    const bool ne = (lane >= lo) & (lane < hi) & (ll != 0u);
+    const uint32_t e = ne ? ll : 0u;
+    const uint32_t incl = wave_incl_sum(e);
+    const uint32_t total = readlane(incl, kWave - 1);
+    if (!total) return;
+    const uint32_t a = incl - e;  // the run's first literal, in the batch's literals
+    // the non-empty runs' ring offsets (ring index of a literal = D + u), compacted by rank
+    const uint64_t nem = ballot(ne);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(nem >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)nem, 0u));
+    const uint32_t D = I.in_lo + lit_start - a - 1u;
+    lds_order();
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(L->recs);  // (the records are in registers)
+    tmp[ne ? rank : kWave] = D;
+    lds_order();
+    const uint32_t Dc = tmp[lane];
+    const uint32_t a4 = ne ? a << 2 : 0x7FFFFF00u;  // mark slot x4 (others: the trash slot)
+    const uint32_t mark = a + 1u;
+    const uint32_t zero = 0;
+    const uint32_t rbase = (uint32_t)(uintptr_t)dst + op - 1u;  // ring index = rbase + u
+    uint32_t u = lane + 1u;
+    uint32_t before = 0;  // non-empty runs starting before the step
+    lds_order();
+    for (uint32_t R = 0; R < total; R += kWave) {
+      if (op + kWave - flushed > kZsObuf - 64) flush(op, false);
+      lds_order();
+      const uint32_t slot = min(a4 - (R << 2), (uint32_t)kWave << 2);
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(L->marks) + slot) = mark;
+      lds_order();
+      const uint32_t mk = L->marks[lane];
+      L->marks[lane] = zero;
+      const uint64_t S = ballot(mk == u);
+      const uint32_t base = before - 1u + (uint32_t)(S & 1u);
+      const uint64_t S1 = S >> 1;
+      const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(S1 >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)S1, 0u));
+      before += (uint32_t)__builtin_popcountll(S);
+      const uint32_t d = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((k << 2) + (base << 2)),
+                                                                (int)Dc);
+      const uint32_t b = I.ring[(d + u) & I.mask];
+      const uint32_t nb = total - R < kWave ? total - R : kWave;
+      // all 64 bytes are written: those past nb lie at or past the new op, inside the room
+      // just made, and are rewritten before they are flushed
+      ring[(rbase + u) & kMask] = (uint8_t)b;
+      lds_order();
+      op += nb;
+      u += kWave;
+    }
+  }
+  // every pending record: to HBM, and its literal run to the literal area
+  __device__ __forceinline__ void flush_seqs(const GMEM uint8_t* in, const InRing& I) {
+    const uint32_t cnt = npend;
+    npend = 0;
+    if (!cnt) return;
+    const uint32_t lane = lane_id();
+    lds_order();
+    const uint2 rec = L->recs[lane < cnt ? lane : kZsCap];
+    const uint32_t q = rec.x & 0xFFFFu, off = rec.x >> 16, mlen = rec.y;
+    const uint32_t end = q + mlen;
+    const uint32_t prev = wave_shr1(end);
+    const uint32_t lit_start = lane == 0 ? last_end : prev;
+    const uint32_t ll = q - lit_start;
+    last_end = readlane(end, cnt - 1);
+    if (lane < cnt) seqs[nseq + lane] = make_uint2(ll | (off << 17), mlen);
+    nseq += cnt;
+    const uint64_t live = cnt < kWave ? (1ull << cnt) - 1 : ~0ull;
+    uint64_t special = ballot(lit_start < I.lo) & ballot(ll != 0u) & live;
+    uint32_t lo = 0;
+    for (;;) {
+      const uint32_t k = special ? (uint32_t)__builtin_ctzll(special) : cnt;
+      if (k > lo) gather(I, lo, k, lit_start, ll);
+      if (k >= cnt) break;
+      literals(in, I, readlane(lit_start, k), readlane(ll, k));
+      special &= special - 1;
+      lo = k + 1;
+    }
+  }
+  // the tail literals (after whatever is pending)
+  __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I, uint32_t s,
+                                           uint32_t len, uint32_t, uint32_t) {
+    flush_seqs(in, I);
+    literals(in, I, s, len);
+  }
+  __device__ __forceinline__ void between(const GMEM uint8_t* in, const InRing& I) {
+    if (npend > kZsCap - 16) flush_seqs(in, I);
+  }
+  // the tail starts at the last match's end
+  __device__ __forceinline__ uint32_t pending_from(uint32_t anchor, uint32_t) const {
+    return anchor;
+  }
+  __device__ __forceinline__ void window(const GMEM uint8_t*, const InRing&, const Window& W,
+                                         uint32_t, uint32_t) {
+    if (!W.chain) return;
+    const uint64_t chain = W.chain;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)chain, 0u));
+    const uint32_t lane = lane_id();
+    lds_order();
+    L->recs[(chain >> lane) & 1u ? npend + rank : kZsCap] =
+        make_uint2((W.x + lane) | (W.off << 16), W.mlen);
+    lds_order();
+    npend += (uint32_t)__builtin_popcountll(chain);
+  }
+};
+#else
 struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the literal area
   GMEM uint2* seqs;
   uint32_t nseq;
@@ -176,6 +332,7 @@ struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the lit
     }
   }
 };
+#endif
 
 // ---- repeat offsets (RFC 8878 3.1.2.5), 64 sequences per step ------------------------------
 // The offset value of each lane's sequence (distance o, literal length ll) from the history
@@ -686,13 +843,26 @@ __global__ __launch_bounds__(64) void zstd_parse_kernel(const uint8_t* __restric
   // (+ one trash entry: probe lanes past the segment insert there, see parse)
   __shared__ __attribute__((aligned(16))) uint16_t table[(1u << kHashLog) + 8];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
+#if BITAR_ZSTD_BULK
+  __shared__ __attribute__((aligned(16))) zse::ZsLds zl;
+#else
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kObuf + kWave];  // + trash bytes
+#endif
   const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
   zse::SeqCollect o;
+#if BITAR_ZSTD_BULK
+  o.L = &zl;
+  o.ring = zl.ring;
+  o.npend = 0;
+  o.last_end = 0;
+  zl.marks[lane_id()] = 0;
+  lds_order();
+#else
   o.ring = obuf;
+#endif
   o.dst = global_ptr(scratch + (uint64_t)i_seg * sstride);
   o.cap = zse::lit_cap(seg);
   o.op = 0;
