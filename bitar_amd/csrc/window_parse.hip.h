@@ -12,7 +12,8 @@
 //
 // Per fixed window of 64 positions (one per lane):
 //   1. hash the 4 bytes at every position (from the ring), look up a 1024-entry LDS table of
-//      u16 positions, then insert every position (the largest position wins a slot);
+//      u16 positions, then insert every position with one ds_write_b16 (the largest position
+//      wins a slot: the hardware keeps the highest lane's write, see BITAR_CMP_NOREDO);
 //   2. lanes with a candidate verify + measure the match on 16 bytes from the ring, and
 //      lanes still matching extend in parallel up to 32 bytes;
 //   3. a scalar chain walk picks the greedy matches in lane order (one ctz per match,
@@ -56,6 +57,17 @@ constexpr uint32_t kIn = BITAR_CMP_RING, kInMask = kIn - 1;  // LDS input ring
 constexpr uint32_t kMaxDist = kIn - 1536;
 constexpr uint32_t kInPad = 64;  // mirror of ring[0, 64) after its end: probes never wrap
 constexpr uint32_t kRow = 1024;                   // prefetch row: one 16-B block per lane
+// Same-slot inserts of one window (or probe) resolve by the hardware: lanes of ONE
+// ds_write_b16 that hit the same address leave the highest lane's value, i.e. the largest
+// position -- the oracle's ascending-insert rule -- so no read-back is needed (measured on
+// gfx950: every segment of the 1 GiB LZ4 / LZ4_WIDE / DEFLATE / Zstd parity tests bit-exact
+// without it, LZ4 compress 2.89 -> 2.74 ms/GiB).  BITAR_CMP_NOREDO=0 builds the read-back
+// and re-write loop that enforces the rule independently of that ordering.  Either way only
+// the candidate choice could differ, never the validity of a match (every candidate is
+// verified against the input).
+#ifndef BITAR_CMP_NOREDO
+#define BITAR_CMP_NOREDO 1
+#endif
 #ifndef BITAR_CMP_PREEXT
 #define BITAR_CMP_PREEXT 32
 #endif
@@ -424,7 +436,9 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       table[h] = (uint16_t)p;
       lds_order();
       // read back now, settle same-slot writes at the end of the window
+#if !BITAR_CMP_NOREDO
       const uint32_t back = table[h];
+#endif
       vp = I.bytes16(p + kWave);  // next window's bytes
       const bool pre = act && cand < p && p - cand <= max_dist;
       uint32_t lim = match_limit - p;
@@ -627,6 +641,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       emitted = pos > x + kWave ? pos : x + kWave;
       // same-slot writes of this window: re-write until the largest position holds the slot
       // (the empty asm pins the read-back's use, and so its wait, here)
+#if !BITAR_CMP_NOREDO
       uint32_t bk = back;
       __asm__ volatile("" : "+v"(bk));
       if (ballot(bk < p) & actm) {  // rare: only on same-slot collisions
@@ -638,6 +653,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
           redo = redo && table[h] < p;
         }
       }
+#endif
     };
     // Row k+1 goes into the ring at x = 1024 k + 512 (the ring then runs 576..1536 B ahead
     // of the scan); right after, the row register block is reloaded with row k+2, which
@@ -697,6 +713,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
               lds_order();
               table[act ? h : (1u << HLOG)] = (uint16_t)p;
               lds_order();
+#if !BITAR_CMP_NOREDO
               bool redo = act && table[h] < p;
               while (ballot(redo)) {
                 lds_order();
@@ -704,6 +721,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
                 lds_order();
                 redo = redo && table[h] < p;
               }
+#endif
               x += st * kWave;
               continue;
             }
