@@ -1507,6 +1507,13 @@ __global__ __launch_bounds__(64) BITAR_EMIT_ATTR void zstd_emit_kernel(
           tree_sent = true;
           coded = true;
         } else if (!o.overflow) {  // rewind: raw after all
+          // the abandoned streams' bits not yet flushed are still in the ring, whose bytes at
+          // and past op must be zero for the bit writer (it ORs): clear them (positions
+          // [max(sec, flushed), op), fewer than the ring's size); and the streams' bytes
+          // already stored to HBM land before the header and the raw copy overwrite them
+          for (uint32_t k = max(sec, o.flushed) + lane; k < o.op; k += kWave) obuf[o.at(k)] = 0;
+          lds_order();
+          global_fence_wave();
           o.op = sec;
           o.flushed = o.flushed > sec ? sec : o.flushed;
         }
