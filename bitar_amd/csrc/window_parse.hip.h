@@ -494,13 +494,12 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
           uint32_t k = kPreExt;
           bool more = true;
           for (;;) {
+            // every lane compares (ring reads stay in bounds by the mask; a lane at or past lr
+            // stops the scan whatever it read), and the stop mask is two single-compare
+            // ballots: no exec-mask branch, no bool re-materialised for the ballot
             const uint32_t kk = k + 4u * lane;
-            uint32_t cl = 4;
-            if (kk < lr) {
-              cl = common4(I.dword(i + kk), I.dword(c + kk));
-              if (cl > lr - kk) cl = lr - kk;
-            }
-            const uint64_t stop = ballot(kk >= lr || cl < 4);
+            const uint32_t cl = min(common4(I.dword(i + kk), I.dword(c + kk)), lr - kk);
+            const uint64_t stop = ballot(kk >= lr) | ballot(cl < 4u);
             if (stop) {
               const uint32_t sl = (uint32_t)__builtin_ctzll(stop);
               const uint32_t ks = k + 4u * sl;
@@ -513,13 +512,13 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
           while (more) {
             const uint32_t kk = k + 16u * lane;
             uint32_t cl = 16;
-            if (kk < li) {
+            if (kk < li) {  // (HBM: no load past the candidate's or the position's end)
               const uint4 a = ld16u(in + i + kk, in_end);
               const uint4 b = ld16u(in + c + kk, in_end);
               cl = common16(a, b);
               if (cl > li - kk) cl = li - kk;
             }
-            const uint64_t stop = ballot(kk >= li || cl < 16);
+            const uint64_t stop = ballot(kk >= li) | ballot(cl < 16u);
             if (stop) {
               const uint32_t sl = (uint32_t)__builtin_ctzll(stop);
               const uint32_t ks = k + 16u * sl;

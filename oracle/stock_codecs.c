@@ -75,11 +75,13 @@ static void* worker(void* arg) {
       }
       j->sizes[i] = (uint32_t)c;
     } else {
+      /* capacity: this segment's own length (the last one may be short; libzstd >= 1.5
+       * may stage literals in the tail of dst up to the capacity it is given) */
       uint8_t* dst = j->out + off;
       const uint32_t csz = j->sizes[i];
       uint64_t p = 0;
       if (j->codec == SC_LZ4) {
-        int r = LZ4_decompress_safe((const char*)slot, (char*)dst, (int)csz, (int)j->seg);
+        int r = LZ4_decompress_safe((const char*)slot, (char*)dst, (int)csz, (int)len);
         if (r < 0) { j->err = -1; break; }
         p = (uint64_t)r;
       } else if (j->codec == SC_DEFLATE) {
@@ -87,11 +89,11 @@ static void* worker(void* arg) {
         zs.next_in = slot;
         zs.avail_in = csz;
         zs.next_out = dst;
-        zs.avail_out = j->seg;
+        zs.avail_out = (uInt)len;
         if (inflate(&zs, Z_FINISH) != Z_STREAM_END) { j->err = -1; break; }
         p = zs.total_out;
       } else {
-        size_t r = ZSTD_decompressDCtx(dc, dst, j->seg, slot, csz);
+        size_t r = ZSTD_decompressDCtx(dc, dst, len, slot, csz);
         if (ZSTD_isError(r)) { j->err = -1; break; }
         p = r;
       }

@@ -64,13 +64,14 @@ def slots_per_window(host):
     return float(np.mean([64.0 / np.unique(r).size for r in w]))
 
 
+@pytest.mark.parametrize("seed", [7, 11, 23])
 @pytest.mark.parametrize("name,seg", [("LZ4", 65536), ("LZ4_WIDE", 65536), ("ZSTD", 65536),
                                       ("DEFLATE", 59460), ("DEFLATE_DYNAMIC", 59460)])
-def test_same_slot_windows_vs_oracle(eng, name, seg):
+def test_same_slot_windows_vs_oracle(eng, name, seg, seed):
     import bitar_amd
     codec = getattr(bitar_amd, "CODEC_" + name)
     n = (16 << 16) + 777
-    host = same_slot_stream(n, 7)
+    host = same_slot_stream(n, seed)
     assert slots_per_window(host) > 2.5  # (positions per distinct slot in a window)
     data = torch.from_numpy(host).cuda()
     slab, stride, sizes = eng.compress(codec, data, seg)
@@ -78,3 +79,82 @@ def test_same_slot_windows_vs_oracle(eng, name, seg):
     eng.sync()
     assert torch.equal(out[:n], data)
     P.assert_every_segment_matches_oracle(codec, data, n, seg, slab, stride, sizes)
+
+
+def structured_stream(n, seed):
+    """n bytes of randomly chosen stretches: runs of one byte, small-alphabet strings, periodic
+    bursts, random bytes, copies from 1 B .. 60 KiB back (near, far and overlapping), zero
+    pages and word-like text -- shapes whose boundaries the synthetic kinds rarely put side by
+    side."""
+    rng = np.random.default_rng(seed)
+    out = bytearray(rng.bytes(16))
+    words = [bytes(rng.integers(97, 123, int(rng.integers(2, 9)), dtype=np.uint8)) for _ in range(64)]
+    while len(out) < n:
+        k = int(rng.integers(0, 7))
+        if k == 0:
+            out += bytes([int(rng.integers(0, 256))]) * int(rng.integers(1, 600))
+        elif k == 1:
+            al = np.frombuffer(rng.bytes(int(rng.integers(2, 9))), np.uint8)
+            out += rng.choice(al, int(rng.integers(20, 2000))).tobytes()
+        elif k == 2:
+            per = rng.bytes(int(rng.integers(1, 40)))
+            out += (per * 200)[:int(rng.integers(8, 3000))]
+        elif k == 3:
+            out += rng.bytes(int(rng.integers(1, 1500)))
+        elif k == 4:
+            back = int(rng.integers(1, min(len(out), 61440) + 1))
+            m = int(rng.integers(4, 700))
+            s = len(out) - back
+            for j in range(m):  # byte by byte: the copy may overlap itself
+                out.append(out[s + j])
+        elif k == 5:
+            out += bytes(int(rng.integers(64, 5000)))
+        else:
+            out += b" ".join(words[int(i)] for i in rng.integers(0, 64, int(rng.integers(5, 300))))
+    return np.frombuffer(bytes(out[:n]), np.uint8).copy()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("name,seg", [("LZ4", 65536), ("LZ4_WIDE", 65536), ("ZSTD", 65536),
+                                      ("DEFLATE", 59460), ("DEFLATE_DYNAMIC", 59460)])
+def test_structured_fuzz_vs_oracle_and_stock(eng, name, seg, seed):
+    """our frames: bit-exact against the oracle, decoded by the GPU and by the stock library"""
+    import bitar_amd
+    import stock_lib as S
+    codec = getattr(bitar_amd, "CODEC_" + name)
+    n = (24 << 16) + 12345
+    host = structured_stream(n, seed)
+    data = torch.from_numpy(host).cuda()
+    slab, stride, sizes = eng.compress(codec, data, seg)
+    out, prod = eng.decompress(codec, slab, stride, sizes, seg)
+    eng.sync()
+    assert torch.equal(out[:n], data)
+    P.assert_every_segment_matches_oracle(codec, data, n, seg, slab, stride, sizes)
+    stock = {"LZ4": S.LZ4, "LZ4_WIDE": S.LZ4, "ZSTD": S.ZSTD}.get(name, S.DEFLATE)
+    P.stock_decodes_every_frame(stock, slab, stride, sizes, data, n, seg)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+@pytest.mark.parametrize("name,levels", [("LZ4", [1]), ("DEFLATE_DYNAMIC", [1, 6, 9]),
+                                         ("ZSTD", [1, 3, 9, 19])])
+def test_structured_fuzz_stock_streams_decode(eng, name, levels, seed):
+    """streams the stock libraries write from the same shapes, at several levels: the GPU
+    decoders reproduce the input"""
+    import bitar_amd
+    import stock_lib as S
+    codec = getattr(bitar_amd, "CODEC_" + name)
+    sc = {"LZ4": S.LZ4, "ZSTD": S.ZSTD}.get(name, S.DEFLATE)
+    seg = 59460 if name.startswith("DEFLATE") else 65536
+    n = (12 << 16) + 999
+    host = structured_stream(n, 100 + seed)
+    for level in levels:
+        slab_h, stride, sizes_h = S.compress(sc, host, seg, level, P.THREADS)
+        nseg = sizes_h.size
+        slab = torch.from_numpy(slab_h).cuda()
+        sizes = torch.from_numpy(sizes_h.view(np.int32)).cuda()
+        out = eng.empty(nseg * seg)
+        prod = eng.empty(nseg, dtype=torch.int32)
+        eng.decompress_slab_into(codec, slab, stride, sizes, nseg, seg, out, prod,
+                                 capacity=nseg * seg)
+        eng.sync()
+        assert np.array_equal(out[:n].cpu().numpy(), host), f"level {level}"
