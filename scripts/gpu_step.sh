@@ -1,4 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_collisions.py -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/fuzz.log 2>&1 && echo "fuzz ok" && grep -E "passed|failed" gpurun_out/fuzz.log | tail -2 && bash scripts/gpu_tests.sh > /dev/null && tail -2 gpurun_out/pytest_gpu.log
+for r in 1 2; do for v in far4k far8k cur far32k; do
+  if [ $v = cur ]; then lib=bitar_amd/lib/libbitar_hip.so; else lib=bitar_amd/lib/variants/libbitar_hip_$v.so; fi
+  echo -n "$v "; BITAR_HIP_LIB=$lib timeout -k 10 200 python scripts/stock_bench.py --codec lz4 --kind 1 2>/dev/null | grep codec || exit 1
+done; done
