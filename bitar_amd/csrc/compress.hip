@@ -44,10 +44,20 @@ __device__ __forceinline__ uint32_t lane_sel(uint64_t m, uint32_t a, uint32_t b)
 // offset, literal; trash bytes for the rest) after two prefix scans per window; with the
 // emitter removed the parse ran 30 % faster (1 GiB kinds 1 / 5 / 6), so that is what this
 // batching takes aim at.  The output bytes are the same.
-constexpr uint32_t kLz4Obuf = 512;  // output ring (flushed to HBM in 16-B blocks)
+#ifndef BITAR_LZ4_GATHER
+#define BITAR_LZ4_GATHER 2
+#endif
+#ifndef BITAR_LZ4_OBUF
+#define BITAR_LZ4_OBUF 512
+#endif
+constexpr uint32_t kLz4Obuf = BITAR_LZ4_OBUF;  // output ring (flushed to HBM in 16-B blocks)
 constexpr uint32_t kSeqCap = 64;    // records per flush (a window adds <= 16)
 struct Lz4Lds {
+#if BITAR_LZ4_GATHER == 2
+  uint8_t ring[kLz4Obuf];          // (the gather writes every lane's byte inside the room)
+#else
   uint8_t ring[kLz4Obuf + kWave];  // + one trash byte per lane
+#endif
   uint2 seqs[kSeqCap + 1];         // + a trash record
   uint32_t marks[kWave + 1];       // sequence starts of the current output step; + trash
 };
@@ -114,9 +124,6 @@ struct Lz4Out : ByteOutT<kLz4Obuf> {
     if (ml >= 15) put_ext(ml - 15);
   }
 
-#ifndef BITAR_LZ4_GATHER
-#define BITAR_LZ4_GATHER 2
-#endif
 #if BITAR_LZ4_GATHER == 2
   // records of lanes [lo, hi) (all ordinary) as LZ4 sequences, gathered 64 output bytes per
   // step; false (nothing written) if they would overrun the slot.
@@ -438,8 +445,16 @@ struct DflOut {
 // RING / HLOG: the parse's input ring and hash table -- 4 KiB / 1024 entries (distance cap
 // 2560: BITAR_HIP_CODEC_LZ4, 21 waves per CU), or 16 KiB / 4096 entries (cap 14848:
 // BITAR_HIP_CODEC_LZ4_WIDE, the ratio operating point; 27.3 KiB of LDS, 5 waves per CU)
+#ifndef BITAR_LZ4C_WAVES
+#define BITAR_LZ4C_WAVES 0  // tuning knob: waves per SIMD the register allocation must allow
+#endif
+#if BITAR_LZ4C_WAVES
+#define BITAR_LZ4C_ATTR __attribute__((amdgpu_waves_per_eu(BITAR_LZ4C_WAVES)))
+#else
+#define BITAR_LZ4C_ATTR
+#endif
 template <uint32_t RING, uint32_t HLOG>
-__global__ __launch_bounds__(64) void lz4_compress_kernel(
+__global__ __launch_bounds__(64) BITAR_LZ4C_ATTR void lz4_compress_kernel(
     const uint8_t* __restrict__ input, uint64_t n_total, uint32_t seg,
     uint8_t* __restrict__ slab, uint64_t slot_stride, uint8_t* const* __restrict__ dsts,
     uint32_t* __restrict__ sizes, uint32_t* __restrict__ err, const uint32_t* __restrict__ order) {
