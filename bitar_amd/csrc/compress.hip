@@ -355,6 +355,13 @@ __device__ __forceinline__ uint32_t match_code(uint32_t mlen, uint32_t off, uint
   return code | (lx << ln) | (rev(dc, 5) << (ln + le)) | (dx << (ln + le + 5));
 }
 
+#ifndef BITAR_DFL_BULK
+#define BITAR_DFL_BULK 1
+#endif
+struct DflLds {
+  uint2 recs[kSeqCap + 1];    // + a trash record
+  uint32_t marks[kWave + 1];  // zero between steps; + trash
+};
 struct DflOut {
   uint32_t* stage;     // LDS, kBitWords dwords, zero outside the pending range
   GMEM uint32_t* dst;  // slot (16-B aligned)
@@ -402,8 +409,8 @@ struct DflOut {
     put_lanes(lane_id() == 0 ? val : 0u, lane_id() == 0 ? nb : 0u);
   }
   // literal codes of [s, s+n) (from the input ring when it holds them, else from HBM)
-  __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I, uint32_t s,
-                                           uint32_t n, uint32_t, uint32_t) {
+  __device__ __forceinline__ void literals(const GMEM uint8_t* in, const InRing& I, uint32_t s,
+                                           uint32_t n) {
     const uint32_t lane = lane_id();
     const bool ring_ok = s >= I.lo;
     for (uint32_t k = 0; k < n; k += kWave) {
@@ -419,9 +426,121 @@ struct DflOut {
       if (overflow) return;
     }
   }
+#if BITAR_DFL_BULK
+  // Batched (as the LZ4 emitter): a window appends its matches {start | distance << 16,
+  // length} to an LDS list; every <= 48 records (and before the tail) one flush codes their
+  // symbols -- each record's literal run [previous match end, start), then its match --
+  // 64 symbols per step: every run marks its first symbol (the run's u = symbol offset + 1),
+  // one compare gives the step's start mask, a v_mbcnt pair the run, three ds_bpermute its
+  // literal ring offset, match-symbol position + code length and match code (coded once per
+  // record); a literal lane codes its byte from the input ring.  Only real symbols are coded
+  // (the per-window form coded all 64 positions, the ones inside matches too).  Runs starting
+  // below the input ring take the per-run path.  Same bitstream.
+  DflLds* L;
+  uint32_t npend, last_end;
+
+  __device__ __forceinline__ void bulk(const InRing& I, uint32_t lo, uint32_t hi,
+                                       uint32_t lit_start, uint32_t ll, uint32_t mv, uint32_t mb) {
+    const uint32_t lane = lane_id();
+    const bool in = (lane >= lo) & (lane < hi);
+    const uint32_t e = in ? ll + 1u : 0u;
+    const uint32_t incl = wave_incl_sum(e);
+    const uint32_t total = readlane(incl, kWave - 1);
+    const uint32_t a = incl - e;  // the run's first symbol
+    const uint32_t D = I.in_lo + lit_start - a - 1u;  // ring index of a literal = D + u
+    const uint32_t pX = ((a + ll + 1u) << 16) | mb;   // u of the match symbol | its length
+    const uint32_t a4 = in ? a << 2 : 0x7FFFFF00u;
+    const uint32_t mark = a + 1u;
+    const uint32_t zero = 0;
+    uint32_t u = lane + 1u;
+    uint32_t before = lo - 1u;
+    for (uint32_t R = 0; R < total && !overflow; R += kWave) {
+      lds_order();
+      const uint32_t slot = min(a4 - (R << 2), (uint32_t)kWave << 2);
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(L->marks) + slot) = mark;
+      lds_order();
+      const uint32_t mk = L->marks[lane];
+      L->marks[lane] = zero;
+      const uint64_t S = ballot(mk == u);
+      const uint32_t base = before + (uint32_t)(S & 1u);
+      const uint64_t S1 = S >> 1;
+      const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(S1 >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)S1, 0u));
+      before += (uint32_t)__builtin_popcountll(S);
+      const int src = (int)((k << 2) + (base << 2));
+      const uint32_t qD = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)D);
+      const uint32_t qX = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pX);
+      const uint32_t qM = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)mv);
+      const uint32_t b = I.ring[(qD + u) & I.mask];
+      uint32_t lb;
+      const uint32_t lv = fixed_code(b, lb);
+      const bool ism = u == (qX >> 16);
+      const bool live = u <= total;
+      put_lanes(ism ? qM : lv, live ? (ism ? (qX & 63u) : lb) : 0u);
+      u += kWave;
+    }
+  }
+  // every pending record's literal run and match
+  __device__ __forceinline__ void flush_seqs(const GMEM uint8_t* in, const InRing& I) {
+    const uint32_t cnt = npend;
+    npend = 0;
+    if (!cnt || overflow) return;
+    const uint32_t lane = lane_id();
+    lds_order();
+    const uint2 rec = L->recs[lane < cnt ? lane : kSeqCap];
+    const uint32_t q = rec.x & 0xFFFFu, off = rec.x >> 16, mlen = rec.y;
+    const uint32_t end = q + mlen;
+    const uint32_t prev = wave_shr1(end);
+    const uint32_t lit_start = lane == 0 ? last_end : prev;
+    const uint32_t ll = q - lit_start;
+    last_end = readlane(end, cnt - 1);
+    uint32_t mb;
+    const uint32_t mv = match_code(lane < cnt ? mlen : 3u, lane < cnt ? off : 1u, mb);
+    const uint64_t live = cnt < kWave ? (1ull << cnt) - 1 : ~0ull;
+    uint64_t special = ballot(lit_start < I.lo) & ballot(ll != 0u) & live;
+    uint32_t lo = 0;
+    for (;;) {
+      const uint32_t k = special ? (uint32_t)__builtin_ctzll(special) : cnt;
+      if (k > lo) bulk(I, lo, k, lit_start, ll, mv, mb);
+      if (k >= cnt || overflow) break;
+      literals(in, I, readlane(lit_start, k), readlane(ll, k));
+      put_one(readlane(mv, k), readlane(mb, k));
+      special &= special - 1;
+      lo = k + 1;
+    }
+  }
+  // the tail literals start at the last match's end (after whatever is pending)
+  __device__ __forceinline__ uint32_t pending_from(uint32_t anchor, uint32_t) const { return anchor; }
+  __device__ __forceinline__ void between(const GMEM uint8_t* in, const InRing& I) {
+    if (npend > kSeqCap - 16) flush_seqs(in, I);
+  }
+  // the tail literals (matches end >= 5 bytes before the segment end, so this always runs)
+  __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I, uint32_t s,
+                                           uint32_t n, uint32_t, uint32_t) {
+    flush_seqs(in, I);
+    literals(in, I, s, n);
+  }
+  __device__ __forceinline__ void window(const GMEM uint8_t*, const InRing&, const Window& W,
+                                         uint32_t, uint32_t) {
+    if (!W.chain) return;
+    const uint64_t chain = W.chain;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)chain, 0u));
+    const uint32_t lane = lane_id();
+    lds_order();
+    L->recs[lane_sel(chain, npend + rank, kSeqCap)] =
+        make_uint2((W.x + lane) | (W.off << 16), W.mlen);
+    lds_order();
+    npend += (uint32_t)__builtin_popcountll(chain);
+  }
+#else
   // literals are emitted window by window: the tail starts where output stopped
   __device__ __forceinline__ uint32_t pending_from(uint32_t, uint32_t emitted) const { return emitted; }
   __device__ __forceinline__ void between(const GMEM uint8_t*, const InRing&) {}
+  __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I, uint32_t s,
+                                           uint32_t n, uint32_t, uint32_t) {
+    literals(in, I, s, n);
+  }
 
   // One window: each position contributes its literal code, its match symbol (a selected
   // match starts there) or nothing (inside a match); one prefix sum places them all.
@@ -438,6 +557,7 @@ struct DflOut {
     const bool lit = !cl && !covered && q < n;
     put_lanes(cl ? mv : lit ? lv : 0u, cl ? mb : lit ? lb : 0u);
   }
+#endif
 };
 
 }  // namespace cmp
@@ -498,6 +618,9 @@ __global__ __launch_bounds__(64) void deflate_compress_kernel(
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
   __shared__ __attribute__((aligned(16))) uint32_t stage[kBitWords];
+#if BITAR_DFL_BULK
+  __shared__ __attribute__((aligned(16))) DflLds dl;
+#endif
   const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
@@ -511,6 +634,13 @@ __global__ __launch_bounds__(64) void deflate_compress_kernel(
   o.bits = 0;
   o.wflushed = 0;
   o.overflow = false;
+#if BITAR_DFL_BULK
+  o.L = &dl;
+  o.npend = 0;
+  o.last_end = 0;
+  dl.marks[lane_id()] = 0;
+  lds_order();
+#endif
   o.put_one(1u | (1u << 1), 3);  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
   parse(global_ptr(input + seg_off), n, global_ptr(input + n_total), table, inring, kMaxDist,
         258u, o);
