@@ -265,7 +265,7 @@ struct Lz4Out : ByteOutT<kLz4Obuf> {
     const uint32_t lane = lane_id();
     lds_order();
     const uint2 rec = L->seqs[lane < cnt ? lane : kSeqCap];
-    const uint32_t q = rec.x & 0xFFFFu, off = rec.x >> 16, mlen = rec.y;
+    const uint32_t q = rec.x & 0xFFFFu, off = (rec.x >> 16) + 1u, mlen = rec.y;
     const uint32_t end = q + mlen;
     const uint32_t prev = wave_shr1(end);
     const uint32_t lit_start = lane == 0 ? last_end : prev;
@@ -315,7 +315,7 @@ struct Lz4Out : ByteOutT<kLz4Obuf> {
     const uint32_t lane = lane_id();
     lds_order();
     L->seqs[lane_sel(chain, nseq + rank, kSeqCap)] =
-        make_uint2((W.x + lane) | (W.off << 16), W.mlen);
+        make_uint2((W.x + lane) | (W.dm1 << 16), W.mlen);
     lds_order();
     nseq += (uint32_t)__builtin_popcountll(chain);
   }
@@ -488,7 +488,7 @@ struct DflOut {
     const uint32_t lane = lane_id();
     lds_order();
     const uint2 rec = L->recs[lane < cnt ? lane : kSeqCap];
-    const uint32_t q = rec.x & 0xFFFFu, off = rec.x >> 16, mlen = rec.y;
+    const uint32_t q = rec.x & 0xFFFFu, off = (rec.x >> 16) + 1u, mlen = rec.y;
     const uint32_t end = q + mlen;
     const uint32_t prev = wave_shr1(end);
     const uint32_t lit_start = lane == 0 ? last_end : prev;
@@ -529,7 +529,7 @@ struct DflOut {
     const uint32_t lane = lane_id();
     lds_order();
     L->recs[lane_sel(chain, npend + rank, kSeqCap)] =
-        make_uint2((W.x + lane) | (W.off << 16), W.mlen);
+        make_uint2((W.x + lane) | (W.dm1 << 16), W.mlen);
     lds_order();
     npend += (uint32_t)__builtin_popcountll(chain);
   }
@@ -552,7 +552,7 @@ struct DflOut {
     const uint32_t pend = wave_incl_max(cl ? q + W.mlen : 0u);  // end of the last match <= q
     const bool covered = q < W.pos_in || (!cl && q < pend);
     uint32_t mb, lb;
-    const uint32_t mv = match_code(cl ? W.mlen : 3u, cl ? W.off : 1u, mb);
+    const uint32_t mv = match_code(cl ? W.mlen : 3u, cl ? W.off() : 1u, mb);
     const uint32_t lv = fixed_code(W.byte, lb);
     const bool lit = !cl && !covered && q < n;
     put_lanes(cl ? mv : lit ? lv : 0u, cl ? mb : lit ? lb : 0u);

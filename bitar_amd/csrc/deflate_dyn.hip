@@ -95,7 +95,7 @@ struct RecOut : ByteOutT<kRecBuf> {  // the byte ring carries the match records
     const uint64_t litm = ballot(lit);
     uint32_t lnx, lxv, dnx, dxv;
     const uint32_t ls = len_sym(cl ? W.mlen : 3u, lnx, lxv);
-    const uint32_t ds = dist_sym(cl ? W.off : 1u, dnx, dxv);
+    const uint32_t ds = dist_sym(cl ? W.off() : 1u, dnx, dxv);
     lds_order();
     if (lit) atomicAdd(&lh[W.byte], 1u);
     if (cl) {

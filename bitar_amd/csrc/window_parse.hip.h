@@ -165,11 +165,12 @@ struct Window {
   uint32_t x;       // window start
   uint64_t chain;   // lanes where a selected match starts
   uint32_t mlen;    // per lane: match length (chain lanes)
-  uint32_t off;     // per lane: match distance (chain lanes)
+  uint32_t dm1;     // per lane: match distance - 1 (chain lanes)
   uint32_t byte;    // per lane: input byte at x + lane
   uint32_t pos_in;  // parse position at window start: [x, pos_in) is covered by a match
   uint32_t done;    // end of the positions earlier windows handed over (SKIP: positions in
                     // [done, x) lay in skipped probe windows and are all literals)
+  __device__ __forceinline__ uint32_t off() const { return dm1 + 1u; }  // match distance
 };
 
 // ---- byte output staged in an LDS ring, flushed in aligned 16-B blocks ----------------
@@ -411,10 +412,18 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
     // one window of 64 positions at x; vp = the 16 bytes at x + lane, read during the
     // previous window (the ring already holds them then)
     uint4 vp = make_uint4(0, 0, 0, 0);
+    // windows starting at or past x_edge hold a position past last_start, or one whose limit
+    // (match_limit - p) does not exceed kPreExt
+    const uint32_t int_end = min(last_start + 1u, match_limit > kPreExt ? match_limit - kPreExt : 0u);
+    // (readfirstlane: kept in an SGPR, so the per-window test is a scalar compare)
+    const uint32_t x_edge =
+        __builtin_amdgcn_readfirstlane(int_end >= kWave ? int_end - (kWave - 1) : 0u);
     auto window = [&](uint32_t x) __attribute__((always_inline)) {
       const uint32_t p = x + lane;
       const bool act = p <= last_start;
+#if !BITAR_CMP_NOREDO
       const uint64_t actm = ballot(p <= last_start);  // (a single compare: see the read-back)
+#endif
       const uint4 v = vp;
       const uint32_t h = hash4<HLOG>(v.x);
       // Table and ring accesses are issued on all lanes (no exec-mask branches: the scalar
@@ -440,19 +449,28 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       const uint32_t back = table[h];
 #endif
       vp = I.bytes16(p + kWave);  // next window's bytes
-      const bool pre = act && cand < p && p - cand <= max_dist;
-      uint32_t lim = match_limit - p;
-      if (lim > max_mlen) lim = max_mlen;
+      // distance - 1: 1 <= p - cand <= max_dist is one unsigned compare (cand >= p wraps)
+      const uint32_t dm1 = p + ~cand;
+      const bool pre = dm1 < max_dist;
       // verify the 4 bytes and measure up to 16, from the input ring
       const uint32_t c16 = common16(v, I.bytes16(cand));
-      uint32_t len = pre ? (c16 < lim ? c16 : lim) : 0u;
+      uint32_t len = pre ? c16 : 0u;
       // lanes still matching after 16 bytes extend in parallel, up to kPreExt
       for (uint32_t k = 16; k < kPreExt; k += 16) {
-        const bool go = pre && len == k && lim > k;
-        // (len == k >= 16 implies pre: two single-compare ballots, see wave.hip.h)
-        if (!(ballot(len == k) & ballot(lim > k))) break;
+        const bool go = len == k;  // (implies pre)
+        if (!ballot(len == k)) break;
         const uint32_t l2 = k + common16(I.bytes16(p + k), I.bytes16(cand + k));
-        len = go ? (l2 < lim ? l2 : lim) : len;
+        len = go ? l2 : len;
+      }
+      // The segment's last windows: positions past last_start find nothing, matches stop at
+      // match_limit (and max_mlen).  Elsewhere neither binds (every lane's limit exceeds
+      // kPreExt), so those checks -- 6 VALU per window -- run only here, after the
+      // pre-extension (clamping its result is the same as clamping each step).
+      if (x >= x_edge) {
+        __asm__ volatile("");  // (keeps this a branch: if-converted, every window paid it)
+        const uint32_t l = match_limit - p;
+        const uint32_t lim = act ? (l < max_mlen ? l : max_mlen) : 0u;
+        len = len < lim ? len : lim;
       }
       // lanes at or past the parse position holding a match, and those of them whose match
       // reached kPreExt bytes and may go on (cooperative extension during the walk)
@@ -471,7 +489,8 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
         for (uint32_t k = 1; k <= kRepAhead; ++k) ahead |= repm >> k;
         valid &= ~(~repm & ahead);
       }
-      const uint64_t extm = valid & ballot(len == kPreExt) & ballot(lim > kPreExt);
+      // (a lane at its limit may be included: its cooperative extension stops at once)
+      const uint64_t extm = valid & ballot(len == kPreExt);
       uint64_t chain = 0;
       uint32_t mlen_v = len;
       uint64_t m = valid;
@@ -611,7 +630,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
         // distances (move-to-front) of [h2, h1, h0, the chain's distances in lane order],
         // found by ballots instead of a per-match scalar loop
         if (chain) {
-          const uint32_t offv = p - cand;
+          const uint32_t offv = dm1 + 1u;
           const uint32_t n0 = readlane(offv, highbit(chain));
           const uint64_t m1 = chain & ballot(offv != n0);
           const uint32_t o1 = h0 != n0 ? h0 : h1;  // first old distance unlike n0
@@ -629,7 +648,7 @@ __device__ __forceinline__ uint32_t parse(const GMEM uint8_t* in, uint32_t n, co
       W.x = x;
       W.chain = chain;
       W.mlen = mlen_v;
-      W.off = p - cand;
+      W.dm1 = dm1;
       W.byte = v.x & 0xFFu;
       W.pos_in = pos_in;
       W.done = emitted;

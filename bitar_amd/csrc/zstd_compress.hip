@@ -219,7 +219,7 @@ struct SeqCollect : ByteOutT<kZsObuf> {
     const uint32_t lane = lane_id();
     lds_order();
     const uint2 rec = L->recs[lane < cnt ? lane : kZsCap];
-    const uint32_t q = rec.x & 0xFFFFu, off = rec.x >> 16, mlen = rec.y;
+    const uint32_t q = rec.x & 0xFFFFu, off = (rec.x >> 16) + 1u, mlen = rec.y;
     const uint32_t end = q + mlen;
     const uint32_t prev = wave_shr1(end);
     const uint32_t lit_start = lane == 0 ? last_end : prev;
@@ -261,7 +261,7 @@ struct SeqCollect : ByteOutT<kZsObuf> {
     const uint32_t lane = lane_id();
     lds_order();
     L->recs[(chain >> lane) & 1u ? npend + rank : kZsCap] =
-        make_uint2((W.x + lane) | (W.off << 16), W.mlen);
+        make_uint2((W.x + lane) | (W.dm1 << 16), W.mlen);
     lds_order();
     npend += (uint32_t)__builtin_popcountll(chain);
   }
@@ -327,7 +327,7 @@ struct SeqCollect : ByteOut {  // the byte ring carries literal bytes to the lit
     if (W.chain) {
       const uint32_t si = __builtin_amdgcn_mbcnt_hi((uint32_t)(W.chain >> 32),
                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)W.chain, 0u));
-      if (cl) seqs[nseq + si] = make_uint2(ll | (W.off << 17), W.mlen);
+      if (cl) seqs[nseq + si] = make_uint2(ll | (W.off() << 17), W.mlen);
       nseq += (uint32_t)__builtin_popcountll(W.chain);
     }
   }
