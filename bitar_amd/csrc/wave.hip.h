@@ -71,7 +71,8 @@ __device__ __forceinline__ uint32_t shfl_down1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)v);
 }
 
-// byte-shift funnel: bytes [r, r+4) of the little-endian pair (lo, hi)
+// byte-shift funnel: bytes [r, r+4) of the little-endian pair (lo, hi); only r's low 2 bits
+// count (v_alignbyte_b32), so callers may pass an unmasked byte address
 __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t r) {
   return __builtin_amdgcn_alignbyte(hi, lo, r);
 }

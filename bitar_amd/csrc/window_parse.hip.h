@@ -110,7 +110,8 @@ __device__ __forceinline__ uint32_t common16(uint4 a, uint4 b) {
   const uint32_t c1 = __builtin_elementwise_add_sat(ffbl(d1), 32u);
   const uint32_t c2 = __builtin_elementwise_add_sat(ffbl(d2), 64u);
   const uint32_t c3 = __builtin_elementwise_add_sat(ffbl(d3), 96u);
-  return min(min(min(c0, c1), min(c2, c3)), 128u) >> 3;
+  // (two v_min3: the 128 cap rides in the second's third operand)
+  return min(min(min(min(c0, c1), c2), c3), 128u) >> 3;
 }
 
 // number of equal leading bytes of two little-endian values
@@ -145,14 +146,14 @@ struct InRing {
   // 4 / 16 bytes at position q (little-endian); the pad lets the dword reads run past the
   // ring's end without wrapping
   __device__ __forceinline__ uint32_t dword(uint32_t q) const {
-    const uint32_t a = (in_lo + q) & mask;
-    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring) + (a >> 2);
-    return funnel(r32[0], r32[1], a & 3u);
+    const uint32_t u = in_lo + q;
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring) + ((u & mask) >> 2);
+    return funnel(r32[0], r32[1], u);  // (v_alignbyte_b32 reads the shift's low 2 bits)
   }
   __device__ __forceinline__ uint4 bytes16(uint32_t q) const {
-    const uint32_t a = (in_lo + q) & mask;
-    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring) + (a >> 2);
-    const uint32_t sh = a & 3u;
+    const uint32_t u = in_lo + q;
+    const uint32_t* r32 = reinterpret_cast<const uint32_t*>(ring) + ((u & mask) >> 2);
+    const uint32_t sh = u;  // (v_alignbyte_b32 reads the shift's low 2 bits only)
     const uint32_t w0 = r32[0], w1 = r32[1], w2 = r32[2], w3 = r32[3], w4 = r32[4];
     return make_uint4(funnel(w0, w1, sh), funnel(w1, w2, sh), funnel(w2, w3, sh),
                       funnel(w3, w4, sh));
