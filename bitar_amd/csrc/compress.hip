@@ -310,11 +310,12 @@ struct Lz4Out : ByteOutT<kLz4Obuf> {
                                          uint32_t, uint32_t) {
     if (!W.chain) return;
     const uint64_t chain = W.chain;
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)chain, 0u));
+    // (the record index: v_mbcnt adds its second operand, so no separate add)
+    const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)chain, nseq));
     const uint32_t lane = lane_id();
     lds_order();
-    L->seqs[lane_sel(chain, nseq + rank, kSeqCap)] =
+    L->seqs[lane_sel(chain, idx, kSeqCap)] =
         make_uint2((W.x + lane) | (W.dm1 << 16), W.mlen);
     lds_order();
     nseq += (uint32_t)__builtin_popcountll(chain);
@@ -524,11 +525,12 @@ struct DflOut {
                                          uint32_t, uint32_t) {
     if (!W.chain) return;
     const uint64_t chain = W.chain;
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)chain, 0u));
+    // (the record index: v_mbcnt adds its second operand, so no separate add)
+    const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)chain, npend));
     const uint32_t lane = lane_id();
     lds_order();
-    L->recs[lane_sel(chain, npend + rank, kSeqCap)] =
+    L->recs[lane_sel(chain, idx, kSeqCap)] =
         make_uint2((W.x + lane) | (W.dm1 << 16), W.mlen);
     lds_order();
     npend += (uint32_t)__builtin_popcountll(chain);

@@ -312,12 +312,12 @@ __device__ __forceinline__ uint32_t chain_fast2(uint64_t& m, uint32_t lenw, uint
 }
 
 // Form 3 (BITAR_CMP_CHAIN == 3): the successor of every lane is computed once per window on
-// the VALU -- nx[j] = the first valid lane at or past j + len[j] (64: the chain leaves the
-// window; 128 + j: lane j needs the cooperative extension, whose length is not known yet) --
+// the VALU -- nx[j] = the first valid lane at or past j + len[j] (64..127: the chain leaves
+// the window; 128 + j: lane j needs the cooperative extension, whose length is not known yet) --
 // so the scalar loop per match is one v_readlane (the next lane is the next lane select),
 // one s_bitset1, one compare and one branch (unrolled twice).  Matches per window: 6.6 on
 // kind 1, up to 8.6 on kind 5 (oracle counts), so the chain was ~half of the parse's scalar
-// instructions.  Returns the lane that stopped the walk (64, or 128 + an extension lane),
+// instructions.  Returns the lane that stopped the walk (64..127, or 128 + an extension lane),
 // every chain lane before it set in `chain`.  (A VALU-written SGPR needs 4 wait states before
 // it is a lane select: s_nop 1 + the compare + the branch + the bitset.)
 __device__ __forceinline__ uint32_t chain_succ(uint32_t l, uint32_t nx, uint64_t& chain) {
@@ -339,13 +339,15 @@ __device__ __forceinline__ uint32_t chain_succ(uint32_t l, uint32_t nx, uint64_t
       : "scc");
   return l;
 }
-// per lane: nx as above, from e = lane + lenw (lenw = 128 on extension lanes)
+// per lane: nx as above, from e = lane + lenw (lenw = 128 on extension lanes).  f = the first
+// valid lane at or past e (64: none) is >= e whenever e < 64, so max(f, e) is f there and e
+// for e >= 64 (f <= 64 then, whatever the masked shift made of it): a lane leaving the window
+// returns e in [64, 128), an extension lane 128 + lane -- one v_max instead of two selects.
 __device__ __forceinline__ uint32_t chain_next(uint64_t valid, uint32_t e) {
   const uint64_t t = ~0ull << (e & 63u);
   const uint32_t lo = (uint32_t)t & (uint32_t)valid, hi = (uint32_t)(t >> 32) & (uint32_t)(valid >> 32);
   const uint32_t f = min(min(ffbl(lo), __builtin_elementwise_add_sat(ffbl(hi), 32u)), 64u);
-  const uint32_t far = e >= 128u ? e : 64u;
-  return e >= 64u ? far : f;
+  return max(f, e);
 }
 
 // The window-scan parse over one segment; hands each window to E::window and the tail to

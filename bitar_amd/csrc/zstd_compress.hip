@@ -256,11 +256,12 @@ struct SeqCollect : ByteOutT<kZsObuf> {
                                          uint32_t, uint32_t) {
     if (!W.chain) return;
     const uint64_t chain = W.chain;
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)chain, 0u));
+    // (the record index: v_mbcnt adds its second operand, so no separate add)
+    const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)chain, npend));
     const uint32_t lane = lane_id();
     lds_order();
-    L->recs[(chain >> lane) & 1u ? npend + rank : kZsCap] =
+    L->recs[(chain >> lane) & 1u ? idx : kZsCap] =
         make_uint2((W.x + lane) | (W.dm1 << 16), W.mlen);
     lds_order();
     npend += (uint32_t)__builtin_popcountll(chain);
