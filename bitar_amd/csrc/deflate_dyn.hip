@@ -70,7 +70,7 @@ __device__ __forceinline__ uint32_t fixed_len(uint32_t s) {
 // literal (u64); match k of the segment: one u32 = length symbol - 257 (5 bits) | its extra
 // bits (5) | distance symbol (5) | its extra bits (<= 10) -- the emit pass needs neither the
 // parse's coverage rule nor the symbol arithmetic again.
-constexpr uint32_t kMaskBytes = 16384;  // <= 1024 windows (n <= 65536)
+[[maybe_unused]] constexpr uint32_t kMaskBytes = 16384;  // <= 1024 windows (n <= 65536)
 constexpr uint32_t kPlanWindows = kPlanRecBytes + 1;  // word index of the window count
 constexpr uint32_t kPlanTail = kPlanRecBytes + 2;     // word index of the tail start
 
@@ -145,6 +145,180 @@ struct RecOut : ByteOutT<kRecBuf> {  // the byte ring carries the match records
   __device__ __forceinline__ void between(const GMEM uint8_t*, const InRing&) {}
   __device__ __forceinline__ uint32_t pending_from(uint32_t, uint32_t emitted) const { return emitted; }
 };
+
+#ifndef BITAR_DYN_BULK
+#define BITAR_DYN_BULK 1
+#endif
+#if BITAR_DYN_BULK
+// Batched pass 1 (as the LZ4 / Zstd collectors): a window only appends its matches {start |
+// distance - 1 << 16, length} to an LDS list (~6 VALU instead of the per-window symbol
+// arithmetic, prefix max and mask pair); every <= 48 records -- and whenever the oldest pending
+// literal is 1 KiB behind the scan, so literal runs stay in the input ring -- one flush writes
+// the records to the record area with one coalesced store, counts their length and distance
+// symbols (one lane per record), and gathers their literal runs 64 bytes per step (the LZ4
+// gather: start marks, one compare, v_mbcnt) into the literal histogram AND the literal area,
+// in position order.  Pass 2 then reads records and a contiguous literal stream, never the
+// input.  Scratch per segment: [plan kPlanBytes][literals: lit_cap(seg)][records: 8 B each].
+constexpr uint32_t kDynCap = 64;     // records per flush (a window adds <= 16)
+constexpr uint32_t kDynObuf = 512;   // literal staging ring
+constexpr uint32_t kDynGap = 1024;   // flush once the oldest pending literal is this far behind
+__host__ __device__ constexpr uint32_t lit_cap(uint32_t seg) { return (seg + 15u) & ~15u; }
+struct DynLds {
+  uint8_t ring[kDynObuf];
+  uint2 recs[kDynCap + 1];     // + a trash record
+  uint32_t marks[kWave + 1];   // zero between steps; + trash
+};
+struct DynCollect : ByteOutT<kDynObuf> {
+  DynLds* L;
+  uint32_t* lh;          // LDS literal/length histogram (286)
+  uint32_t* dh;          // LDS distance histogram (30)
+  GMEM uint2* seqs;      // record area
+  uint32_t nseq, rec_cap, npend;
+  uint32_t last_end;     // literals before it are in the literal area
+  uint32_t x_seen;       // positions below it are decided (literal or inside a match)
+
+  // literal bytes [s, s + len): counted and appended, 64 per step (from the input ring when
+  // it holds them, else from HBM)
+  __device__ __forceinline__ void lit_run(const GMEM uint8_t* in, const InRing& I, uint32_t s,
+                                          uint32_t len) {
+    const uint32_t lane = lane_id();
+    for (uint32_t k = 0; k < len && !overflow; k += kWave) {
+      const uint32_t step = len - k < kWave ? len - k : kWave;
+      if (!room(step)) return;
+      const uint32_t q = s + k + (lane < step ? lane : 0u);
+      lds_order();
+      const uint32_t b = s + k >= I.lo ? I.byte(q) : (uint32_t)in[q];
+      if (lane < step) atomicAdd(&lh[b], 1u);
+      put(b, step);
+    }
+  }
+  // the literal runs of record lanes [lo, hi) (all in the input ring), 64 bytes per step
+  __device__ __forceinline__ void gather(const InRing& I, uint32_t lo, uint32_t hi,
+                                         uint32_t lit_start, uint32_t ll) {
+    const uint32_t lane = lane_id();
+    const bool ne = (lane >= lo) & (lane < hi) & (ll != 0u);
+    const uint32_t e = ne ? ll : 0u;
+    const uint32_t incl = wave_incl_sum(e);
+    const uint32_t total = readlane(incl, kWave - 1);
+    if (!total) return;
+    if ((uint64_t)op + total > cap) { overflow = true; return; }
+    const uint32_t a = incl - e;  // the run's first literal, in the batch's literals
+    // the non-empty runs' ring offsets (ring index of a literal = D + u), compacted by rank
+    const uint64_t nem = ballot(ne);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(nem >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)nem, 0u));
+    const uint32_t D = I.in_lo + lit_start - a - 1u;
+    lds_order();
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(L->recs);  // (the records are in registers)
+    tmp[ne ? rank : kWave] = D;
+    lds_order();
+    const uint32_t Dc = tmp[lane];
+    const uint32_t a4 = ne ? a << 2 : 0x7FFFFF00u;  // mark slot x4 (others: the trash slot)
+    const uint32_t mark = a + 1u;
+    const uint32_t zero = 0;
+    const uint32_t rbase = (uint32_t)(uintptr_t)dst + op - 1u;  // ring index = rbase + u
+    uint32_t u = lane + 1u;
+    uint32_t before = 0;  // non-empty runs starting before the step
+    lds_order();
+    for (uint32_t R = 0; R < total; R += kWave) {
+      if (op + kWave - flushed > kDynObuf - 64) flush(op, false);
+      lds_order();
+      const uint32_t slot = min(a4 - (R << 2), (uint32_t)kWave << 2);
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(L->marks) + slot) = mark;
+      lds_order();
+      const uint32_t mk = L->marks[lane];
+      L->marks[lane] = zero;
+      const uint64_t S = ballot(mk == u);
+      const uint32_t base = before - 1u + (uint32_t)(S & 1u);
+      const uint64_t S1 = S >> 1;
+      const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(S1 >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)S1, 0u));
+      before += (uint32_t)__builtin_popcountll(S);
+      const uint32_t d = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((k << 2) + (base << 2)),
+                                                                (int)Dc);
+      const uint32_t b = I.ring[(d + u) & I.mask];
+      const uint32_t nb = total - R < kWave ? total - R : kWave;
+      if (lane < nb) atomicAdd(&lh[b], 1u);
+      // all 64 bytes are written: those past nb lie at or past the new op, inside the room
+      // just made, and are rewritten before they are flushed
+      ring[(rbase + u) & kMask] = (uint8_t)b;
+      lds_order();
+      op += nb;
+      u += kWave;
+    }
+  }
+  // every pending record: to the record area, its symbols counted, its literal run gathered;
+  // then the literals up to x_seen
+  __device__ __forceinline__ void flush_seqs(const GMEM uint8_t* in, const InRing& I) {
+    const uint32_t cnt = npend;
+    npend = 0;
+    if (overflow) return;
+    const uint32_t lane = lane_id();
+    if (cnt) {
+      lds_order();
+      const uint2 rec = L->recs[lane < cnt ? lane : kDynCap];
+      const uint32_t q = rec.x & 0xFFFFu, off = (rec.x >> 16) + 1u, mlen = rec.y;
+      const uint32_t end = q + mlen;
+      const uint32_t prev = wave_shr1(end);
+      const uint32_t lit_start = lane == 0 ? last_end : prev;
+      const uint32_t ll = q - lit_start;
+      last_end = readlane(end, cnt - 1);
+      if (nseq + cnt > rec_cap) { overflow = true; return; }
+      if (lane < cnt) seqs[nseq + lane] = rec;
+      nseq += cnt;
+      uint32_t lnx, lxv, dnx, dxv;
+      const uint32_t ls = len_sym(lane < cnt ? mlen : 3u, lnx, lxv);
+      const uint32_t ds = dist_sym(lane < cnt ? off : 1u, dnx, dxv);
+      lds_order();
+      if (lane < cnt) {
+        atomicAdd(&lh[257 + ls], 1u);
+        atomicAdd(&dh[ds], 1u);
+      }
+      lds_order();
+      const uint64_t live = cnt < kWave ? (1ull << cnt) - 1 : ~0ull;
+      uint64_t special = ballot(lit_start < I.lo) & ballot(ll != 0u) & live;
+      uint32_t lo = 0;
+      for (;;) {
+        const uint32_t k = special ? (uint32_t)__builtin_ctzll(special) : cnt;
+        if (k > lo) gather(I, lo, k, lit_start, ll);
+        if (k >= cnt || overflow) break;
+        lit_run(in, I, readlane(lit_start, k), readlane(ll, k));
+        special &= special - 1;
+        lo = k + 1;
+      }
+    }
+    if (x_seen > last_end && !overflow) {
+      lit_run(in, I, last_end, x_seen - last_end);
+      last_end = x_seen;
+    }
+  }
+  __device__ __forceinline__ void between(const GMEM uint8_t* in, const InRing& I) {
+    if (npend > kDynCap - 16 || x_seen > last_end + kDynGap) flush_seqs(in, I);
+  }
+  // the tail: everything pending, then the literals to the segment's end (matches end >= 5
+  // bytes before it, so this always runs)
+  __device__ __forceinline__ void sequence(const GMEM uint8_t* in, const InRing& I, uint32_t s,
+                                           uint32_t len, uint32_t, uint32_t) {
+    x_seen = s + len;  // (the segment's end)
+    flush_seqs(in, I);
+  }
+  __device__ __forceinline__ uint32_t pending_from(uint32_t anchor, uint32_t) const { return anchor; }
+  __device__ __forceinline__ void window(const GMEM uint8_t*, const InRing&, const Window& W,
+                                         uint32_t, uint32_t n) {
+    x_seen = W.x + kWave < n ? W.x + kWave : n;
+    if (!W.chain) return;
+    const uint64_t chain = W.chain;
+    const uint32_t lane = lane_id();
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(chain >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)chain, 0u));
+    lds_order();
+    L->recs[(chain >> lane) & 1u ? npend + rank : kDynCap] =
+        make_uint2((W.x + lane) | (W.dm1 << 16), W.mlen);
+    lds_order();
+    npend += (uint32_t)__builtin_popcountll(chain);
+  }
+};
+#endif
 
 // ---- code construction (restated by oracle/bitar_deflate_dyn.c) --------------------------
 using huf::TreeLds;
@@ -345,15 +519,51 @@ __global__ __launch_bounds__(64) void deflate_dyn_parse_kernel(
   using namespace dyn;
   __shared__ __attribute__((aligned(16))) uint16_t table[1u << kHashLog];
   __shared__ __attribute__((aligned(16))) uint8_t inring[kIn + kInPad];
+  __shared__ uint32_t hist[kNLit + kNDist];
+#if BITAR_DYN_BULK
+  __shared__ __attribute__((aligned(16))) DynLds dl;
+#else
   __shared__ __attribute__((aligned(16))) uint8_t obuf[kRecBuf + kWave];
   __shared__ __attribute__((aligned(16))) uint4 cst[kMaskRing];
-  __shared__ uint32_t hist[kNLit + kNDist];
+#endif
   const uint32_t i_seg = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   const uint64_t seg_off = (uint64_t)i_seg * seg;
   if (seg_off >= n_total) return;
   const uint32_t n = (uint32_t)((n_total - seg_off) < seg ? (n_total - seg_off) : seg);
   for (uint32_t k = lane_id(); k < kNLit + kNDist; k += kWave) hist[k] = 0;
   GMEM uint8_t* scr = global_ptr(scratch + (uint64_t)i_seg * scr_stride);
+#if BITAR_DYN_BULK
+  DynCollect o;
+  o.L = &dl;
+  o.ring = dl.ring;
+  o.dst = scr + kPlanBytes;
+  o.cap = lit_cap(seg);
+  o.op = 0;
+  o.flushed = 0;
+  o.overflow = false;
+  o.lh = hist;
+  o.dh = hist + kNLit;
+  o.seqs = reinterpret_cast<GMEM uint2*>(scr + kPlanBytes + lit_cap(seg));
+  o.rec_cap = (uint32_t)((scr_stride - kPlanBytes - lit_cap(seg)) / 8u);
+  o.nseq = 0;
+  o.npend = 0;
+  o.last_end = 0;
+  o.x_seen = 0;
+  dl.marks[lane_id()] = 0;
+  lds_order();
+  parse(global_ptr(input + seg_off), n, global_ptr(input + n_total), table, inring, kMaxDist,
+        258u, o);
+  o.flush(o.op, true);
+  lds_order();
+  GMEM uint32_t* plan = reinterpret_cast<GMEM uint32_t*>(scr);
+  for (uint32_t k = lane_id(); k < kNLit + kNDist; k += kWave) plan[k] = hist[k];
+  if (lane_id() == 0) {
+    plan[kPlanRecBytes] = o.overflow ? 0xFFFFFFFFu : o.nseq;  // (bulk: the record count)
+    plan[kPlanWindows] = o.op;                                  // (bulk: the literal count)
+    plan[kPlanTail] = o.last_end;
+  }
+  if (o.overflow && lane_id() == 0) atomicOr(err, 2u);
+#else
   RecOut o;
   o.ring = obuf;
   o.dst = scr + kPlanBytes + kMaskBytes;
@@ -380,6 +590,7 @@ __global__ __launch_bounds__(64) void deflate_dyn_parse_kernel(
     plan[kPlanTail] = tail;
   }
   if (o.overflow && lane_id() == 0) atomicOr(err, 2u);
+#endif
 }
 
 __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
@@ -555,6 +766,97 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
   lds_order();
   o.bits = readlane(hbits, 0);  // < kStageWords * 32 - the flush margin: no flush needed yet
 
+#if BITAR_DYN_BULK
+  // Symbols from the records and the literal stream, 64 per step.  Per chunk of 64 records
+  // (one 8-B load per lane, the next chunk's issued a chunk ahead): each record's literal run
+  // [previous match end, start) and its match symbol (codes + extra bits, <= 45 bits, built
+  // once per record); then the chunk's symbols 64 per step -- every run marks its first
+  // symbol, one compare gives the step's start mask, v_mbcnt the run k, two ds_bpermute the
+  // match code and one its position | length; a literal symbol u of run k is literal number
+  // lit_base + u - 1 - k of the stream, read from an LDS ring the stream flows through.
+  {
+    const uint32_t nrec = plan[kPlanRecBytes], nlit = plan[kPlanWindows];
+    uint8_t* rings = pool + kStageWords * 4;
+    RowRing<1024> Lr;
+    Lr.init(reinterpret_cast<const GMEM uint4*>(scr + kPlanBytes), (nlit + 15u) & ~15u, rings);
+    uint32_t* marks = reinterpret_cast<uint32_t*>(rings + 2048);  // kWave + 1
+    marks[lane] = 0;
+    const GMEM uint2* recs = reinterpret_cast<const GMEM uint2*>(scr + kPlanBytes + lit_cap(seg));
+    uint2 nxt = make_uint2(0, 0);
+    if (lane < nrec) nxt = recs[lane];
+    uint32_t last_end = 0, lit_base = 0;
+    for (uint32_t c0 = 0; c0 < nrec && !o.overflow; c0 += kWave) {
+      const uint2 rec = nxt;
+      nxt = make_uint2(0, 0);
+      if (c0 + kWave + lane < nrec) nxt = recs[c0 + kWave + lane];
+      const uint32_t cnt = nrec - c0 < kWave ? nrec - c0 : kWave;
+      const bool live = lane < cnt;
+      const uint32_t q = rec.x & 0xFFFFu, off = (rec.x >> 16) + 1u, mlen = rec.y;
+      const uint32_t end = q + mlen;
+      const uint32_t prev = wave_shr1(end);
+      const uint32_t ll = q - (lane == 0 ? last_end : prev);
+      last_end = readlane(end, cnt - 1);
+      uint32_t lnx, lxv, dnx, dxv;
+      const uint32_t ls = len_sym(live ? mlen : 3u, lnx, lxv);
+      const uint32_t ds = dist_sym(live ? off : 1u, dnx, dxv);
+      lds_order();
+      const uint32_t lt_ = ltab[257 + ls];
+      const uint32_t dt = dtab[ds];
+      const uint32_t ln = lt_ >> 16, dn = dt >> 16;
+      const uint32_t lo = (lt_ & 0xFFFFu) | (lxv << ln);  // <= 20 bits
+      const uint64_t mv = (uint64_t)lo | ((uint64_t)((dt & 0xFFFFu) | (dxv << dn)) << (ln + lnx));
+      const uint32_t mb = ln + lnx + dn + dnx;
+      const uint32_t e = live ? ll + 1u : 0u;
+      const uint32_t incl = wave_incl_sum(e);
+      const uint32_t total = readlane(incl, kWave - 1);
+      const uint32_t a = incl - e;                    // the run's first symbol
+      const uint32_t pX = ((a + ll + 1u) << 8) | mb;  // u of the match symbol | its bit count
+      const uint32_t mlo = (uint32_t)mv, mhi = (uint32_t)(mv >> 32);
+      const uint32_t a4 = live ? a << 2 : 0x7FFFFF00u;
+      const uint32_t mark = a + 1u;
+      const uint32_t zero = 0;
+      uint32_t u = lane + 1u;
+      uint32_t before = 0xFFFFFFFFu;  // runs started before the step, less one
+      for (uint32_t R = 0; R < total && !o.overflow; R += kWave) {
+        Lr.ensure(lit_base + R + kWave);
+        lds_order();
+        const uint32_t slot = min(a4 - (R << 2), (uint32_t)kWave << 2);
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(marks) + slot) = mark;
+        lds_order();
+        const uint32_t mk = marks[lane];
+        marks[lane] = zero;
+        const uint64_t S = ballot(mk == u);
+        const uint32_t base = before + (uint32_t)(S & 1u);
+        const uint64_t S1 = S >> 1;
+        const uint32_t k = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(S1 >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)S1, 0u));
+        before += (uint32_t)__builtin_popcountll(S);
+        const int src = (int)(k << 2);
+        const uint32_t qX = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pX);
+        const uint32_t qlo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)mlo);
+        const uint32_t qhi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)mhi);
+        const uint32_t b = Lr.byte(lit_base + u - 1u - k);
+        const uint32_t lt = ltab[b];
+        const bool ism = u == (qX >> 8);
+        const bool act = u <= total;
+        const uint64_t val = ism ? ((uint64_t)qhi << 32 | qlo) : (uint64_t)(lt & 0xFFFFu);
+        o.put(act ? val : 0ull, act ? (ism ? (qX & 0xFFu) : (lt >> 16)) : 0u);
+        u += kWave;
+      }
+      lit_base += total - cnt;
+    }
+    // the tail literals (after the last match): the rest of the stream
+    for (uint32_t k = lit_base; k < nlit && !o.overflow; k += kWave) {
+      const bool act = k + lane < nlit;
+      Lr.ensure(k + kWave);
+      lds_order();
+      const uint32_t b = act ? Lr.byte(k + lane) : 0u;
+      lds_order();
+      const uint32_t lt = ltab[b];
+      o.put(act ? (uint64_t)(lt & 0xFFFFu) : 0ull, act ? (lt >> 16) : 0u);
+    }
+  }
+#else
   // symbols, kB windows per step (independent LDS reads and prefix sums across the
   // windows of a step); window masks, match records and input bytes stream through LDS rings
   RowRing<512> C, I;
@@ -618,6 +920,7 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
     const uint32_t lt = ltab[b];
     o.put(act ? (uint64_t)(lt & 0xFFFFu) : 0ull, act ? (lt >> 16) : 0u);
   }
+#endif
   {
     lds_order();
     const uint32_t eob = ltab[256];

@@ -524,10 +524,14 @@ static int compress_impl(bitar_hip_ctx* ctx, void* stream, uint32_t codec, const
   }
   else if (codec == BITAR_HIP_CODEC_DEFLATE_DYNAMIC) {
     // pass 1 (parse -> records + histograms) and pass 2 (codes + emit) through a
-    // stream-ordered scratch per segment (deflate_dyn.hip): 2 KiB plan + 16 KiB of window
-    // masks + match records (<= one slot).  Large calls run in chunks of <= kChunkSegs
+    // stream-ordered scratch per segment (deflate_dyn.hip): 2 KiB plan + the literal stream
+    // (<= seg bytes, 16-B aligned) + 8-byte match records (<= seg / 4: matches are >= 4
+    // bytes); the per-window form (BITAR_DYN_BULK 0) needs 2 KiB + 16 KiB of window masks +
+    // 4-byte records, within the same stride.  Large calls run in chunks of <= kChunkSegs
     // segments over one scratch allocation, so scratch is bounded whatever the call's size.
-    const uint64_t scr_stride = bitar_hip_slot_size(BITAR_HIP_CODEC_DEFLATE, seg) + 2048u + 16384u;
+    const uint64_t scr_old = bitar_hip_slot_size(BITAR_HIP_CODEC_DEFLATE, seg) + 2048u + 16384u;
+    const uint64_t scr_bulk = 2048u + ((seg + 15u) & ~15ull) + 8u * ((uint64_t)seg / 4u + 64u);
+    const uint64_t scr_stride = ((scr_old > scr_bulk ? scr_old : scr_bulk) + 15u) & ~15ull;
     const Chunks ch(nseg);
     void* scratch = nullptr;
     HIP_TRY(hipMallocAsync(&scratch, ch.size * scr_stride, s), "scratch allocation");
