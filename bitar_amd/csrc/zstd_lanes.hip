@@ -438,6 +438,12 @@ __global__ __launch_bounds__(64) void zstd_hlit_kernel(
   // symbol, the second a tiny table)
   __shared__ uint16_t tab[S][kHufWords];  // two symbol bytes per entry pair
   __shared__ uint8_t len8[S][256];
+#ifndef BITAR_HLIT_PRIO
+#define BITAR_HLIT_PRIO 3
+#endif
+  // It runs beside zstd_seqdec_kernel (another stream) and ends after it: its streams are
+  // the decode's critical path, so its waves take the issue arbiter first (seqdec has slack)
+  if (BITAR_HLIT_PRIO) __builtin_amdgcn_s_setprio(BITAR_HLIT_PRIO);
   const uint32_t lane = lane_id();
   // The wave's segment headers, one lane per segment, loaded together, and each table's
   // words issued before any is used: at about one wave per SIMD every serial load is
