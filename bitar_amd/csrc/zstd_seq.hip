@@ -410,6 +410,9 @@ __global__ __launch_bounds__(64) void zstd_seqdec_kernel(
 #define BITAR_EXEC_LROW 512
 #endif
 constexpr uint32_t kLRow = BITAR_EXEC_LROW, kLRing = 2 * kLRow;
+#ifndef BITAR_EXEC_MARKS
+#define BITAR_EXEC_MARKS 1
+#endif
 __global__ __launch_bounds__(64) void zstd_exec_kernel(
     const uint8_t* const* __restrict__ srcs, const uint8_t* __restrict__ slab,
     uint64_t slot_stride, uint32_t nseg, uint32_t seg, uint8_t* __restrict__ out,
@@ -428,6 +431,10 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   const uint32_t i = order ? order[blockIdx.x] : blockIdx.x;  // (cost-ordered dispatch)
   if (i >= nseg || uniform(produced[i]) != kRecs) return;
   const uint32_t lane = lane_id();
+  if (BITAR_EXEC_MARKS) {  // the sequence marks: zero between steps
+    ev[lane] = 0u;
+    lds_order();
+  }
   const GMEM uint32_t* h = global_ptr(reinterpret_cast<const uint32_t*>(hscr + (uint64_t)i * kStride));
   const uint32_t nbk = uniform(h[kNb]), lall = uniform(h[kLitAll]), op0 = uniform(h[kOp]);
   const uint32_t fsz = uniform(h[kFsz]), fcs = uniform(h[kFcs]);
@@ -468,12 +475,10 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
   // one 64-byte step at output [xa, xa + 64) ∩ [.., xa + act): e = the run each lane lies in
   // (key << 24 | payload: odd key = literals, payload = output pos - literal index; even key
   // = match, payload = offset)
-  auto chunk = [&](uint32_t xa, uint32_t nact, uint32_t e) __attribute__((always_inline)) {
+  // (ism: a match byte, from = its source position; else a literal, from = its index)
+  auto chunk = [&](uint32_t xa, uint32_t nact, bool ism, uint32_t from) __attribute__((always_inline)) {
     const uint32_t x = xa + lane;
     const bool act = lane < nact;
-    const bool ism = ((e >> 24) & 1u) == 0;
-    const uint32_t pay = e & 0xFFFFFFu;
-    const uint32_t from = x - pay;  // literal index, or match source position
     // far history (before the ring's reach, or written by the wave decoder): HBM, after a
     // fence over what this wave flushed
     const bool far = act && ism && from < xa && (from < op0 || from + kNearOff < x);
@@ -578,6 +583,44 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
           break;
         }
       }
+#if BITAR_EXEC_MARKS
+      // Each output byte finds its sequence as the compressors' gathers do: every sequence
+      // (>= 3 bytes: its first byte is its own) stores its u (batch byte index + 1) into the
+      // mark of its first byte, the byte's lane reads and clears its mark, one compare gives
+      // the step's start mask, the sequence is a scalar base + v_mbcnt, and three ds_bpermute
+      // fetch its first match byte, literal-index delta and offset.  (Was: the starts of its
+      // literal run and its match scattered to LDS events, a DPP prefix max, a carry.)
+      const bool live = lane < n;
+      const uint32_t a4 = live ? ex << 2 : 0x7FFFFF00u;  // mark slot x4 (others: the trash)
+      const uint32_t mark = ex + 1u;
+      const uint32_t T1 = ex + ll;                         // first match byte (batch index)
+      const uint32_t D = (lp + lex) - ex;                  // literal index = batch index + D
+      const uint32_t zero = 0;
+      uint32_t before = 0xFFFFFFFFu;  // sequences started before the step, less one
+      for (uint32_t cb = 0; cb < T; cb += kWave) {
+        const uint32_t xa = s.op + cb;
+        if (xa + kWave - s.flushed > kFlushAt) flush(s, ring, xa, false);
+        lds_order();
+        const uint32_t slot = min(a4 - (cb << 2), (uint32_t)kWave << 2);
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(ev) + slot) = mark;
+        lds_order();
+        const uint32_t b = cb + lane;  // batch byte index
+        const uint32_t mk = ev[lane];
+        ev[lane] = zero;
+        const uint64_t S = ballot(mk == b + 1u);
+        const uint32_t base = before + (uint32_t)(S & 1u);
+        const uint64_t S1 = S >> 1;
+        const uint32_t k = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(S1 >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)S1, 0u));
+        before += (uint32_t)__builtin_popcountll(S);
+        const int src4 = (int)(k << 2);
+        const uint32_t qT1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src4, (int)T1);
+        const uint32_t qD = (uint32_t)__builtin_amdgcn_ds_bpermute(src4, (int)D);
+        const uint32_t qoff = (uint32_t)__builtin_amdgcn_ds_bpermute(src4, (int)off);
+        const bool ism = b >= qT1;
+        chunk(xa, T - cb < kWave ? T - cb : kWave, ism, ism ? xa + lane - qoff : b + qD);
+      }
+#else
       const uint32_t e_lit = ((2u * lane + 1u) << 24) | ((s.op + ex) - (lp + lex));
       const uint32_t e_mat = ((2u * lane + 2u) << 24) | off;
       uint32_t carry = 0;
@@ -594,8 +637,9 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
         uint32_t e = ev[lane];
         e = wave_incl_max(e > carry ? e : carry);
         carry = readlane(e, kWave - 1);
-        chunk(xa, T - cb < kWave ? T - cb : kWave, e);
+        chunk(xa, T - cb < kWave ? T - cb : kWave, ((e >> 24) & 1u) == 0, xa + lane - (e & 0xFFFFFFu));
       }
+#endif
       s.op += T;
       lp += LT;
     }
@@ -605,7 +649,7 @@ __global__ __launch_bounds__(64) void zstd_exec_kernel(
     for (uint32_t cb = 0; ok && cb < rest; cb += kWave) {
       const uint32_t xa = s.op + cb;
       if (xa + kWave - s.flushed > kFlushAt) flush(s, ring, xa, false);
-      chunk(xa, rest - cb < kWave ? rest - cb : kWave, (1u << 24) | (s.op - lp));
+      chunk(xa, rest - cb < kWave ? rest - cb : kWave, false, xa + lane - (s.op - lp));
     }
     if (ok) s.op += rest;
     lbase += regen;
