@@ -12,7 +12,7 @@ for f in runtime lz4_decompress inflate inflate_fixed compress util_kernels zstd
     zstd_seq) extra="-mllvm -amdgpu-sched-strategy=max-memory-clause -DBITAR_DEC_RING=2048";;
     zstd_lanes) extra="-mllvm -amdgpu-sched-strategy=max-memory-clause";;
     zstd_compress) extra="-DBITAR_EMIT_WAVES=8";;
-    compress) extra="-mllvm -amdgpu-sched-strategy=iterative-maxocc";;
+    compress) extra="-mllvm -amdgpu-sched-strategy=max-ilp";;
     inflate) extra="-DBITAR_DEC_RING=2048";;
     inflate_fixed) extra="-DBITAR_DEC_RING=1024 -DBITAR_INFL_WAVES=8";;
     zstd_decompress) extra="-DBITAR_DEC_RING=2048 -DBITAR_ZSD_WAVES=3";;
