@@ -9,9 +9,10 @@ for f in runtime lz4_decompress inflate inflate_fixed compress util_kernels zstd
   extra=""
   case $f in  # (the Makefile's per-file scheduler; FLAGS_<file> below overrides)
     lz4_decompress) extra="-mllvm -amdgpu-sched-strategy=max-ilp";;
-    zstd_seq) extra="-mllvm -amdgpu-sched-strategy=max-memory-clause -DBITAR_DEC_RING=2048";;
+    zstd_seq) extra="-mllvm -amdgpu-sched-strategy=max-ilp -DBITAR_DEC_RING=2048";;
     zstd_lanes) extra="-mllvm -amdgpu-sched-strategy=max-memory-clause";;
-    zstd_compress) extra="-DBITAR_EMIT_WAVES=8";;
+    zstd_compress) extra="-DBITAR_EMIT_WAVES=8 -mllvm -amdgpu-sched-strategy=max-ilp";;
+    deflate_dyn) extra="-mllvm -amdgpu-sched-strategy=max-ilp";;
     compress) extra="-mllvm -amdgpu-sched-strategy=max-ilp";;
     inflate) extra="-DBITAR_DEC_RING=2048";;
     inflate_fixed) extra="-DBITAR_DEC_RING=1024 -DBITAR_INFL_WAVES=8";;
