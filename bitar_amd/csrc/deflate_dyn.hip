@@ -160,7 +160,10 @@ struct RecOut : ByteOutT<kRecBuf> {  // the byte ring carries the match records
 // in position order.  Pass 2 then reads records and a contiguous literal stream, never the
 // input.  Scratch per segment: [plan kPlanBytes][literals: lit_cap(seg)][records: 8 B each].
 constexpr uint32_t kDynCap = 64;     // records per flush (a window adds <= 16)
-constexpr uint32_t kDynObuf = 512;   // literal staging ring
+#ifndef BITAR_DYN_OBUF
+#define BITAR_DYN_OBUF 512
+#endif
+constexpr uint32_t kDynObuf = BITAR_DYN_OBUF;   // literal staging ring
 constexpr uint32_t kDynGap = 1024;   // flush once the oldest pending literal is this far behind
 __host__ __device__ constexpr uint32_t lit_cap(uint32_t seg) { return (seg + 15u) & ~15u; }
 struct DynLds {
@@ -610,7 +613,13 @@ __global__ __launch_bounds__(64) void deflate_dyn_emit_kernel(
   // (codes first; then the 2-KiB bit ring + the window-mask and input rings, 1 KiB each,
   // and the record ring, 2 KiB: a step may read 1 KiB of records).  6 KiB instead of 10:
   // 16 workgroups per CU instead of 11 (the pass is latency-bound: 8 cost it 10 %)
+#if BITAR_DYN_BULK
+  // (batched: the bit ring, the literal stream's 2-KiB ring and the marks -- the pool is then
+  // the tree scratch's size: 16 -> 18 workgroups per CU)
+  constexpr uint32_t kEmitLds = kStageWords * 4 + 2048 + 4 * (kWave + 4);
+#else
   constexpr uint32_t kEmitLds = kStageWords * 4 + 1024 + 2048 + 1024;
+#endif
   __shared__ __attribute__((aligned(16))) uint8_t pool[sizeof(TreeLds) > kEmitLds
                                                            ? sizeof(TreeLds) : kEmitLds];
   TreeLds& T = *reinterpret_cast<TreeLds*>(pool);
