@@ -437,13 +437,24 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       // every output byte takes the record of the latest sequence starting at or before it
       // (a written word has bit 31 clear, so its key is >= 0; the first sequence's, at lane
       // 0, is 0, so every half-0 key ends >= 0)
+#ifndef BITAR_LZ4D_KEYS2
+#define BITAR_LZ4D_KEYS2 1
+#endif
       const uint32_t key0 =
           (uint32_t)wave_incl_max_i((int32_t)((vrec0 & 0x8000003Fu) | (lane << 24)));
+#if BITAR_LZ4D_KEYS2
+      // (both halves' scans side by side: each DPP step's two wait states filled by the
+      // other scan's; the second is wasted on a batch of <= 64 bytes)
+      const int32_t key1 =
+          wave_incl_max_i((int32_t)((vrec1 & 0x8000003Fu) | ((lane + kWave) << 24)));
+#endif
       half(std::integral_constant<uint32_t, 0>{}, key0);
       if (out > kWave) {
         // second half: its own starts (all past byte 64), else the first half's last record
+#if !BITAR_LZ4D_KEYS2
         const int32_t key1 =
             wave_incl_max_i((int32_t)((vrec1 & 0x8000003Fu) | ((lane + kWave) << 24)));
+#endif
         const int32_t carry = (int32_t)readlane(key0, kWave - 1);
         half(std::integral_constant<uint32_t, 1>{}, (uint32_t)(key1 > carry ? key1 : carry));
       }
