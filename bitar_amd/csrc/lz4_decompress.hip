@@ -356,7 +356,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       if (big) stay_far = false;
       // (3)+(4) for the output bytes 64h .. 64h+63 (lane t: byte 64h + t); `key` is the
       // byte's sequence: its token lane (bits 0..5) and output start (bits 24..30)
-      auto half = [&](auto h_tag, uint32_t key) __attribute__((always_inline)) {
+      auto prep = [&](auto h_tag, uint32_t key) __attribute__((always_inline)) -> uint32_t {
         constexpr uint32_t H = decltype(h_tag)::value;
         const uint32_t q = lane + H * kWave;  // output byte of this lane (vs op)
         // sources: window literal / ring history / HBM history (far) / alias of an earlier
@@ -396,6 +396,12 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         st = is_lit ? lit_a : st;
         if (big && srel < -(int32_t)kNearOff && !is_lit)
           st = (s.op + (uint32_t)srel) | 0x40000000u;  // far: the output position
+        return st;
+      };
+      // pointer doubling, the gather and the store of a half whose sources prep gave
+      auto finish = [&](auto h_tag, uint32_t st) __attribute__((always_inline)) {
+        constexpr uint32_t H = decltype(h_tag)::value;
+        const uint32_t q = lane + H * kWave;  // output byte of this lane (vs op)
         // pointer doubling until no byte of the half aliases another: every alias chain
         // strictly descends (srel <= q - 1, past-the-end bytes included), so <= 6 rounds
         // (written out: the compiler's form of this loop spends three branches on the
@@ -434,6 +440,9 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         ring[(base + s.op + q) & kRingMask] = (uint8_t)g;
         lds_order();
       };
+      auto half = [&](auto h_tag, uint32_t key) __attribute__((always_inline)) {
+        finish(h_tag, prep(h_tag, key));
+      };
       // every output byte takes the record of the latest sequence starting at or before it
       // (a written word has bit 31 clear, so its key is >= 0; the first sequence's, at lane
       // 0, is 0, so every half-0 key ends >= 0)
@@ -448,7 +457,25 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       const int32_t key1 =
           wave_incl_max_i((int32_t)((vrec1 & 0x8000003Fu) | ((lane + kWave) << 24)));
 #endif
+#ifndef BITAR_LZ4D_SPLIT
+#define BITAR_LZ4D_SPLIT 1
+#endif
+#if BITAR_LZ4D_KEYS2 && BITAR_LZ4D_SPLIT
+      // both halves' sources worked out before either gathers (independent work side by
+      // side; the second half's is wasted on a batch of <= 64 bytes), then half 0's gather and
+      // store, then half 1's, which may read half 0's bytes from the ring
+      {
+        const uint32_t st0 = prep(std::integral_constant<uint32_t, 0>{}, key0);
+        const int32_t carry = (int32_t)readlane(key0, kWave - 1);
+        const uint32_t st1 = prep(std::integral_constant<uint32_t, 1>{},
+                                  (uint32_t)(key1 > carry ? key1 : carry));
+        finish(std::integral_constant<uint32_t, 0>{}, st0);
+        if (out > kWave) finish(std::integral_constant<uint32_t, 1>{}, st1);
+      }
+      if (false) {
+#else
       half(std::integral_constant<uint32_t, 0>{}, key0);
+#endif
       if (out > kWave) {
         // second half: its own starts (all past byte 64), else the first half's last record
 #if !BITAR_LZ4D_KEYS2
@@ -458,6 +485,9 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
         const int32_t carry = (int32_t)readlane(key0, kWave - 1);
         half(std::integral_constant<uint32_t, 1>{}, (uint32_t)(key1 > carry ? key1 : carry));
       }
+#if BITAR_LZ4D_KEYS2 && BITAR_LZ4D_SPLIT
+      }
+#endif
       if constexpr (BITAR_LZ4D_ENDRULES == 1 || BITAR_LZ4D_ENDRULES == 2) {
         bip = s.ip;
         last_ml = 0;
