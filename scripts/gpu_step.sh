@@ -1,5 +1,14 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 && tail -1 gpurun_out/smoke.log && \
-timeout -k 10 700 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > gpurun_out/gpu_tests.txt 2>&1 && tail -1 gpurun_out/gpu_tests.txt
+VARIANTS="cur i_ilp i_mmc" CODEC=deflate KINDS=1,2,5 ROUNDS=2 bash scripts/ab.sh > gpurun_out/ab_isched.txt 2>&1 && \
+VARIANTS="cur i_ilp i_mmc" CODEC=deflate_dyn KINDS=1,2 ROUNDS=1 bash scripts/ab.sh >> gpurun_out/ab_isched.txt 2>&1 && \
+python3 - <<'PY'
+import json,collections
+cur=None; d=collections.defaultdict(list)
+for l in open('gpurun_out/ab_isched.txt'):
+    if l.startswith('=='): cur=l.split()[1]; continue
+    if l.startswith('{'):
+        j=json.loads(l); d[(j['codec'],j['kind'],cur)].append(j['decompress_ms'])
+for k,v in sorted(d.items()): print(k, [round(x,3) for x in v])
+PY
